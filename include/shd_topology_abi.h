@@ -1,0 +1,184 @@
+/*
+ * shd_topology_abi.h -- C ABI of libshdtopo.so, the MI355X-native routing engine that replaces
+ * Shadow's topology subsystem (src/topology/shd-topology.c + shd-path.c, Shadow v1.11.1).
+ *
+ * Part 1 is exactly the reference header src/topology/shd-topology.h:12-22 with the GLib
+ * typedefs written as plain C (gchar=char, gboolean=int, gdouble=double, guint64=uint64_t), so
+ * Shadow's callers link against it unchanged:
+ *   runnable/action/shd-load-topology.c:50,79  topology_new
+ *   engine/shd-slave.c:147                     topology_free
+ *   host/shd-host.c:97 / :172 / :1082          topology_attach / topology_detach / isRoutable
+ *   engine/shd-worker.c:352,360                topology_getReliability / topology_getLatency
+ *   engine/shd-slave.c:261-268                 topology_getLatency (TCP autotune)
+ *
+ * Imports resolved from the Shadow executable at load time (weak: a standalone process loads
+ * libshdtopo_shim.so, a restatement of these four functions, first):
+ *   uint32_t address_toNetworkIP(Address*)       src/topology/shd-address.c:114
+ *   double   random_nextDouble(Random*)          src/utility/shd-random.c:34
+ *   void     worker_updateMinTimeJump(double)    src/engine/shd-worker.c:459
+ *
+ * Part 2 adds the two entry points the north star names: the global minimum
+ * latency (absent in the reference: it is pushed from shd-topology.c:500-511, K2) and the
+ * per-window packet batch (engine-side adapter of src/engine/shd-worker.c:332-370).
+ *
+ * Part 3 is the device-level boundary used by multi-GPU drivers (one process per GPU): shard
+ * rows into caller-owned HBM buffers, install an all-gathered table, route packets already
+ * resident in HBM.  Device pointers are plain `void*` / typed pointers into HBM; `stream` is a
+ * hipStream_t passed as void* (NULL = the library's own stream).  No torch types anywhere.
+ *
+ * Errors follow the reference: getters return -1.0 for an unattached address
+ * (shd-topology.c:882-892, logs "critical"); an attached-but-unroutable pair is a fatal
+ * error() in the reference (shd-topology.c:917-928) -- here it aborts too unless the
+ * "abort_on_error" option is set to 0, in which case the getter returns -1.0.
+ */
+#ifndef SHD_TOPOLOGY_ABI_H_
+#define SHD_TOPOLOGY_ABI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct _Topology Topology;
+typedef struct _Address Address; /* Shadow's, opaque here */
+typedef struct _Random Random;   /* Shadow's, opaque here */
+
+/* ---------------- Part 1: src/topology/shd-topology.h:14-22 ---------------- */
+/* shd-topology.c:1237  NULL on failure (parse error, not strongly connected, latency <= 0) */
+Topology* topology_new(const char* graphPath);
+/* shd-topology.c:1199 */
+void topology_free(Topology* top);
+/* shd-topology.c:1154  consumes exactly one random_nextDouble(randomSourcePool) unless LPM */
+void topology_attach(Topology* top, Address* address, Random* randomSourcePool, char* ipHint,
+                     char* geocodeHint, char* typeHint, uint64_t* bwDownOut, uint64_t* bwUpOut);
+/* shd-topology.c:1190 */
+void topology_detach(Topology* top, Address* address);
+/* shd-topology.c:960 */
+int topology_isRoutable(Topology* top, Address* srcAddress, Address* dstAddress);
+/* shd-topology.c:940  ms, -1.0 on failure */
+double topology_getLatency(Topology* top, Address* srcAddress, Address* dstAddress);
+/* shd-topology.c:950  [0,1], -1.0 on failure */
+double topology_getReliability(Topology* top, Address* srcAddress, Address* dstAddress);
+
+/* ---------------- Part 2: north-star additions ---------------- */
+/* Global min latency (ms) over all attached pairs incl. self pairs; replaces the lazily
+ * pushed minimum of shd-topology.c:500-511.  Builds the table if needed.  -1.0 on failure. */
+double topology_getMinimumLatency(Topology* top);
+
+typedef struct {
+    uint32_t srcIP;         /* network order, as address_toNetworkIP */
+    uint32_t dstIP;
+    uint32_t payloadLength; /* packet_getPayloadLength: 0 = control packet, never dropped */
+    uint32_t rngState;      /* sender host's rand_r state BEFORE the draw */
+    uint64_t now;           /* worker clock at emit, ns */
+} TopoPacketIn;
+
+typedef struct {
+    uint64_t time;          /* delivery event time, ns (0 if dropped) */
+    uint32_t rngState;      /* sender's rand_r state after the draw */
+    uint8_t delivered;      /* PDS_INET_SENT (1) / PDS_INET_DROPPED (0) */
+    uint8_t _pad[3];
+} TopoPacketOut;
+
+/* worker_schedulePacket (shd-worker.c:332-370) for n packets of one scheduler window, host
+ * buffers (includes the PCIe copies).  jumpNs/clampInterHost: shd-worker.c:310-324.
+ * Returns 0, or a negative error (unattached address: -2). */
+int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketOut* out, size_t n,
+                              uint64_t jumpNs, int clampInterHost);
+
+/* ---------------- Part 3: device-level boundary / library extras ---------------- */
+int shdtopo_version(void);
+/* CDATA topologies (shd-load-topology.c:57-82) without the temp file */
+Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
+
+/* options: "abort_on_error" (1), "lazy" (1 = K3 first-rooted-wins emulation, 0 = eager
+ * forward rows), "delta" (near-far bucket width, ms), "slots" (concurrent SSSP workgroups),
+ * "device" (HIP device ordinal).  Returns 0 or -1 for an unknown key. */
+int shdtopo_set_option(Topology* top, const char* key, double value);
+
+/* attach by raw IP and a rand_r state (same algorithm and RNG use as topology_attach) */
+int32_t shdtopo_attach_ip(Topology* top, uint32_t ip, uint32_t* rngState, const char* ipHint,
+                          const char* geocodeHint, const char* typeHint, uint64_t* bwDownOut,
+                          uint64_t* bwUpOut);
+double shdtopo_get_latency_ip(Topology* top, uint32_t srcIP, uint32_t dstIP);
+double shdtopo_get_reliability_ip(Topology* top, uint32_t srcIP, uint32_t dstIP);
+
+/* graph facts */
+int64_t shdtopo_num_vertices(Topology* top);
+int64_t shdtopo_num_edges(Topology* top);
+int shdtopo_is_complete(Topology* top);
+int shdtopo_is_directed(Topology* top);
+
+/* attached-vertex table geometry: A distinct attached vertices, ascending vertex index */
+int64_t shdtopo_num_attached(Topology* top);
+int64_t shdtopo_attached_vertices(Topology* top, int32_t* out, int64_t cap);
+int32_t shdtopo_column_of_ip(Topology* top, uint32_t ip);          /* -1 if unattached */
+int32_t shdtopo_vertex_of_ip(Topology* top, uint32_t ip);          /* -1 if unattached */
+
+/* Build the whole A x A table on this process's GPU (SSSP or complete-pair kernel). */
+int shdtopo_build(Topology* top);
+/* Build rows [row0,row1) into caller-owned HBM: lr = {f64 lat, f64 rel}[rows][A],
+ * hops = u16[rows][A], rowmin = f64[rows] (may be NULL).  Enqueued on `stream`. */
+int shdtopo_build_rows(Topology* top, int64_t row0, int64_t row1, void* d_lr, void* d_hops,
+                       void* d_rowmin, void* stream);
+/* Install an assembled A x A table (e.g. after an RCCL all-gather) as the routing table.
+ * The library copies it into its own buffers (same device). */
+int shdtopo_bind_table(Topology* top, const void* d_lr, const void* d_hops, double globalMin,
+                       void* stream);
+/* Copy the current table to host memory (lat, rel: f64[A*A]; hops: u16[A*A]; any may be NULL) */
+int shdtopo_table_to_host(Topology* top, double* lat, double* rel, uint16_t* hops);
+
+/* Route n packets whose inputs are resident in HBM (SoA, attached-column indices). */
+int shdtopo_route_batch_device(Topology* top, const int32_t* d_srcCol, const int32_t* d_dstCol,
+                               const uint32_t* d_payload, const uint32_t* d_stateIn,
+                               const uint64_t* d_now, int64_t n, uint64_t jumpNs, int clamp,
+                               uint64_t* d_time, uint32_t* d_stateOut, uint8_t* d_delivered,
+                               void* stream);
+
+/* lazily tracked minimum (reference trajectory, shd-topology.c:500-511) */
+double shdtopo_get_lazy_minimum_latency(Topology* top);
+
+typedef struct {
+    double build_ms;          /* wall time of the last table build (device, event timed) */
+    double sssp_kernel_ms;    /* event-timed duration of the last SSSP / pair kernel launch */
+    double route_kernel_ms;   /* event-timed duration of the last packet-route launch */
+    int64_t sources;          /* rows computed by the last build */
+    int64_t targets;          /* A */
+    int64_t ambiguous_pairs;  /* pairs whose path crosses a d-tied parent (heap order decides) */
+    int64_t relaxations;      /* edge relaxations attempted by the last SSSP launch */
+    int64_t long_paths;       /* pairs with more hops than the in-register path buffer */
+    int64_t errors;           /* pairs with a missing edge (no self loop etc.) */
+} ShdStats;
+int shdtopo_get_stats(Topology* top, ShdStats* out);
+
+/* Write the loaded graph back out as GraphML (same key schema as the bundled resource files). */
+int shdtopo_write_graphml(Topology* top, const char* path);
+
+/* ---- synthetic workloads (BASELINE.json configs 4/5; tools, not on the routing path) ---- */
+typedef struct {
+    uint64_t seed;
+    int64_t n_routers;   /* 990000 */
+    int64_t n_poi;       /* 10000 */
+    int64_t n_edges;     /* 10000000 undirected edges in total, incl. poi uplinks + self loops */
+    int integer_latency; /* 1: latency ~ U{1..100} (heavy ties) */
+    double alpha;        /* Chung-Lu endpoint weight ~ rank^(-alpha); 1/1.1 */
+} ShdSynthParams;
+Topology* shdtopo_new_synthetic(const ShdSynthParams* p);
+
+/* Attach n_hosts hosts with Tor-like type hints (94 % client, 5 % relay, 1 % server) following
+ * Shadow's seed chain (master --seed -> slave seed -> per-host nodeSeed), IPs
+ * 11.0.0.1 + k; then emit n_packets packets of one window: src uniform over hosts, dst by role,
+ * payload 1448 w.p. 0.8 else 0, pre-draw rand_r state from each host's stream, now ~
+ * U[t0, t0 + jump).  Output arrays are host memory of length n_packets (hostState: n_hosts,
+ * the hosts' states after attach). */
+int shdtopo_synth_packets(Topology* top, uint64_t seed, int64_t n_hosts, int64_t n_packets,
+                          uint64_t t0, uint64_t jump, int32_t* srcCol, int32_t* dstCol,
+                          uint32_t* payload, uint32_t* stateIn, uint64_t* now,
+                          uint32_t* srcIP, uint32_t* dstIP);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHD_TOPOLOGY_ABI_H_ */

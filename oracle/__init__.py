@@ -1,0 +1,473 @@
+"""CPU oracle for the Shadow routing hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import this
+package, and only as the checker.  The product (``shadow_amd``) never imports it; its HIP path
+fails loudly when its extension is missing instead of falling back here.
+
+Pieces (each cites the reference behaviour it restates, paths relative to /root/reference):
+
+* ``read_graphml``      -- igraph 0.7.1 ``igraph_read_graph_graphml`` semantics as used by
+                          ``_topology_loadGraph`` (src/topology/shd-topology.c:95-123): vertex
+                          index = node order, edge id = edge order, numeric data -> f64 (NaN if
+                          missing), strings -> "" if missing.  Written with ElementTree, i.e.
+                          independent of the product's hand-written C++ reader.
+* ``OGraph``            -- the graph + igraph incidence lists / oi index (oracle.c).
+* ``attach_vertex``     -- ``_topology_findAttachmentVertex`` + hook + LPM
+                          (shd-topology.c:965-1152).
+* ``OracleTopology``    -- the reference ``Topology`` object: two-level path cache, reverse
+                          lookup for undirected graphs, complete/SSSP dispatch and the running
+                          minimum latency (shd-topology.c:434-512, 876-963).
+* ``route_packets``     -- ``worker_schedulePacket`` (src/engine/shd-worker.c:332-370).
+* ``rand_r`` / ``next_double`` -- glibc rand_r behind src/utility/shd-random.c:30-37.
+
+SSSP-branch parity is *unpinned* against igraph itself (igraph is absent and the reference holds
+no golden vectors); see DESIGN.md "Oracle and parity".
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import socket
+import struct
+import subprocess
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+INADDR_NONE = 0xFFFFFFFF
+INADDR_ANY = 0
+RAND_MAX = 2147483647.0
+
+
+def build():
+    """Compile oracle.c with gcc (the checker, not the product)."""
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        i32, i64 = ctypes.c_int32, ctypes.c_int64
+        L.orc_rand_r.argtypes = [P]
+        L.orc_rand_r.restype = i32
+        L.orc_next_double.argtypes = [P]
+        L.orc_next_double.restype = ctypes.c_double
+        L.orc_build_incidence.argtypes = [i32, i64, ctypes.c_int, P, P, P, P, P, P, P, P]
+        L.orc_get_eid.argtypes = [ctypes.c_int, P, P, P, P, i32, i32]
+        L.orc_get_eid.restype = i64
+        L.orc_dijkstra.argtypes = [i32, P, P, P, P, P, i32, P, i64, P, P, P, P]
+        L.orc_source_rows.argtypes = [i32, ctypes.c_int, P, P, P, P, P, P, P, P, P, i32, P, i64,
+                                      P, P, P]
+        L.orc_table_rows.argtypes = [i32, ctypes.c_int, P, P, P, P, P, P, P, P, P, P, i64, P, i64,
+                                     P, P, P, ctypes.c_int]
+        L.orc_parent_ties.argtypes = [i32, P, P, P, P, P, P, i32, P]
+        L.orc_complete_pairs.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, P, P, i64, P, P]
+        L.orc_route_packets.argtypes = [i64, P, P, P, P, P, ctypes.c_uint64, ctypes.c_int, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ------------------------------------------------------------------------------------------
+# RNG (glibc rand_r; src/utility/shd-random.c:30-37)
+# ------------------------------------------------------------------------------------------
+def rand_r(state: int):
+    """Return (value, new_state)."""
+    s = np.array([state & 0xFFFFFFFF], dtype=np.uint32)
+    r = lib().orc_rand_r(_p(s))
+    return int(r), int(s[0])
+
+
+def next_double(state: int):
+    """random_nextDouble: rand_r / RAND_MAX.  Returns (value, new_state)."""
+    r, s = rand_r(state)
+    return float(r) / RAND_MAX, s
+
+
+def c_round(x: float) -> int:
+    """C99 round() (half away from zero) for x >= 0, exact for every double."""
+    f = math.floor(x)
+    return int(f + 1) if (x - f) >= 0.5 else int(f)
+
+
+# ------------------------------------------------------------------------------------------
+# Address helpers (src/topology/shd-address.c:137-144 address_stringToIP)
+# ------------------------------------------------------------------------------------------
+def string_to_ip(s):
+    """inet_pton(AF_INET) -> in_addr_t as the host sees it (network-order bytes, little-endian
+    integer on x86); INADDR_NONE on failure."""
+    if s is None:
+        return INADDR_NONE
+    try:
+        b = socket.inet_pton(socket.AF_INET, s)
+    except (OSError, ValueError):
+        return INADDR_NONE
+    return struct.unpack("<I", b)[0]
+
+
+# ------------------------------------------------------------------------------------------
+# GraphML (igraph 0.7.1 reader semantics)
+# ------------------------------------------------------------------------------------------
+_NUMERIC = {"double", "float", "int", "long", "integer"}
+
+
+def _strip_ns(tag):
+    return tag.rsplit("}", 1)[-1]
+
+
+def read_graphml(path_or_bytes):
+    """Parse GraphML into plain arrays.  Returns dict with V, E, directed, eu, ev (document
+    order endpoints), vertex attrs (dict name -> list/array) and edge attrs."""
+    if isinstance(path_or_bytes, (bytes, bytearray)):
+        import io
+        src = io.BytesIO(path_or_bytes)
+    else:
+        src = path_or_bytes
+    keys = {}
+    node_ids = {}
+    vattr_rows = []
+    eu, ev, eattr_rows = [], [], []
+    directed = False
+    for event, elem in ET.iterparse(src, events=("end", "start")):
+        tag = _strip_ns(elem.tag)
+        if event == "start":
+            if tag == "graph":
+                directed = elem.get("edgedefault", "directed") == "directed"
+            continue
+        if tag == "key":
+            default = None
+            for ch in elem:
+                if _strip_ns(ch.tag) == "default":
+                    default = ch.text or ""
+            keys[elem.get("id")] = (elem.get("attr.name"), elem.get("attr.type", "string"),
+                                    elem.get("for", "all"), default)
+        elif tag == "node":
+            nid = elem.get("id")
+            data = {ch.get("key"): (ch.text or "") for ch in elem if _strip_ns(ch.tag) == "data"}
+            if nid not in node_ids:
+                node_ids[nid] = len(vattr_rows)
+                vattr_rows.append((nid, data))
+            elem.clear()
+        elif tag == "edge":
+            s, t = elem.get("source"), elem.get("target")
+            for x in (s, t):
+                if x not in node_ids:
+                    node_ids[x] = len(vattr_rows)
+                    vattr_rows.append((x, {}))
+            eu.append(node_ids[s])
+            ev.append(node_ids[t])
+            eattr_rows.append({ch.get("key"): (ch.text or "") for ch in elem
+                               if _strip_ns(ch.tag) == "data"})
+            elem.clear()
+
+    def conv(kid, raw):
+        name, typ, _, default = keys[kid]
+        if raw is None:
+            raw = default
+        if typ in _NUMERIC:
+            if raw is None:
+                return float("nan")
+            try:
+                return float(raw)
+            except ValueError:
+                return float("nan")
+        return raw if raw is not None else ""
+
+    vkeys = [k for k, (_, _, f, _) in keys.items() if f in ("node", "all")]
+    ekeys = [k for k, (_, _, f, _) in keys.items() if f in ("edge", "all")]
+    vattrs = {"id": [nid for nid, _ in vattr_rows]}
+    for k in vkeys:
+        vattrs[keys[k][0]] = [conv(k, d.get(k)) for _, d in vattr_rows]
+    eattrs = {}
+    for k in ekeys:
+        eattrs[keys[k][0]] = [conv(k, d.get(k)) for d in eattr_rows]
+    return dict(V=len(vattr_rows), E=len(eu), directed=directed,
+                eu=np.asarray(eu, dtype=np.int32), ev=np.asarray(ev, dtype=np.int32),
+                vattrs=vattrs, eattrs=eattrs)
+
+
+class OGraph:
+    """The topology graph as the reference's igraph_t + attribute table sees it."""
+
+    def __init__(self, V, eu, ev, elat, eloss, vloss, directed=False, vattrs=None):
+        self.V = int(V)
+        self.E = int(len(eu))
+        self.directed = bool(directed)
+        self.eu = np.ascontiguousarray(eu, dtype=np.int32)
+        self.ev = np.ascontiguousarray(ev, dtype=np.int32)
+        self.elat = np.ascontiguousarray(elat, dtype=np.float64)
+        self.eloss = np.ascontiguousarray(eloss, dtype=np.float64)
+        self.vloss = np.ascontiguousarray(vloss, dtype=np.float64)
+        self.vattrs = vattrs or {}
+        L = lib()
+        V, E = self.V, self.E
+        self.efrom = np.empty(E, np.int32)
+        self.eto = np.empty(E, np.int32)
+        self.inc_ptr = np.empty(V + 1, np.int64)
+        self.inc_eid = np.empty(E * (1 if directed else 2), np.int32)
+        self.oi = np.empty(E, np.int32)
+        self.os = np.empty(V + 1, np.int64)
+        r = L.orc_build_incidence(V, E, int(directed), _p(self.eu), _p(self.ev), _p(self.efrom),
+                                  _p(self.eto), _p(self.inc_ptr), _p(self.inc_eid), _p(self.oi),
+                                  _p(self.os))
+        if r != 0:
+            raise ValueError("bad edge list (%d)" % r)
+
+    @classmethod
+    def from_graphml(cls, path_or_bytes):
+        g = read_graphml(path_or_bytes)
+        ea, va = g["eattrs"], g["vattrs"]
+        nan = float("nan")
+        elat = np.asarray(ea.get("latency", [nan] * g["E"]), dtype=np.float64)
+        eloss = np.asarray(ea.get("packetloss", [nan] * g["E"]), dtype=np.float64)
+        vloss = np.asarray(va.get("packetloss", [nan] * g["V"]), dtype=np.float64)
+        return cls(g["V"], g["eu"], g["ev"], elat, eloss, vloss, g["directed"], va)
+
+    # -- properties (shd-topology.c:125-218) --
+    def is_complete(self):
+        """igraph_clique_number == V (direction, loops and multi-edges ignored)."""
+        a = np.minimum(self.eu, self.ev).astype(np.int64)
+        b = np.maximum(self.eu, self.ev).astype(np.int64)
+        m = a != b
+        pairs = np.unique(a[m] * self.V + b[m])
+        return len(pairs) == self.V * (self.V - 1) // 2
+
+    def is_strongly_connected(self):
+        import scipy.sparse as sp
+        from scipy.sparse.csgraph import connected_components
+        A = sp.coo_matrix((np.ones(self.E), (self.eu, self.ev)), shape=(self.V, self.V)).tocsr()
+        n, _ = connected_components(A, directed=self.directed, connection="strong")
+        return n == 1
+
+    def get_eid(self, a, b):
+        return int(lib().orc_get_eid(int(self.directed), _p(self.efrom), _p(self.eto),
+                                     _p(self.oi), _p(self.os), int(a), int(b)))
+
+    # -- SSSP --
+    def dijkstra(self, src, targets=None):
+        if targets is None:
+            targets = np.arange(self.V, dtype=np.int32)
+        targets = np.ascontiguousarray(targets, dtype=np.int32)
+        V = self.V
+        dist = np.empty(V, np.float64)
+        pv = np.empty(V, np.int32)
+        pe = np.empty(V, np.int32)
+        rank = np.empty(V, np.int64)
+        lib().orc_dijkstra(V, _p(self.inc_ptr), _p(self.inc_eid), _p(self.efrom), _p(self.eto),
+                           _p(self.elat), int(src), _p(targets), len(targets), _p(dist), _p(pv),
+                           _p(pe), _p(rank))
+        return dist, pv, pe, rank
+
+    def parent_ties(self, dist, src):
+        out = np.empty(self.V, np.int32)
+        lib().orc_parent_ties(self.V, _p(self.inc_ptr), _p(self.inc_eid), _p(self.efrom),
+                              _p(self.eto), _p(self.elat), _p(dist), int(src), _p(out))
+        return out
+
+    def source_rows(self, srcs, targets, nthreads=1):
+        """Rows of the attached-pair table: (lat, rel, hops) [len(srcs)][len(targets)]."""
+        srcs = np.ascontiguousarray(srcs, dtype=np.int32)
+        targets = np.ascontiguousarray(targets, dtype=np.int32)
+        n, m = len(srcs), len(targets)
+        lat = np.empty((n, m), np.float64)
+        rel = np.empty((n, m), np.float64)
+        hops = np.empty((n, m), np.int32)
+        r = lib().orc_table_rows(self.V, int(self.directed), _p(self.inc_ptr), _p(self.inc_eid),
+                                 _p(self.efrom), _p(self.eto), _p(self.oi), _p(self.os),
+                                 _p(self.elat), _p(self.eloss), _p(self.vloss), _p(srcs), n,
+                                 _p(targets), m, _p(lat), _p(rel), _p(hops), int(nthreads))
+        if r != 0:
+            raise RuntimeError("helper failed (missing edge, e.g. no self loop): %d" % r)
+        return lat, rel, hops
+
+    def complete_pairs(self, srcs, dsts):
+        srcs = np.ascontiguousarray(srcs, dtype=np.int32)
+        dsts = np.ascontiguousarray(dsts, dtype=np.int32)
+        n = len(srcs)
+        lat = np.empty(n, np.float64)
+        rel = np.empty(n, np.float64)
+        r = lib().orc_complete_pairs(int(self.directed), _p(self.efrom), _p(self.eto),
+                                     _p(self.oi), _p(self.os), _p(self.elat), _p(self.eloss),
+                                     _p(self.vloss), _p(srcs), _p(dsts), n, _p(lat), _p(rel))
+        if r != 0:
+            raise RuntimeError("lookupPath failed: no edge for pair %d" % (-r - 1))
+        return lat, rel
+
+    def table(self, attached, nthreads=1):
+        """Eager attached-vertex table T[i][j] for attached vertices (sorted distinct)."""
+        a = np.asarray(sorted(set(int(x) for x in attached)), dtype=np.int32)
+        if self.is_complete():
+            S, D = np.meshgrid(a, a, indexing="ij")
+            lat, rel = self.complete_pairs(S.ravel(), D.ravel())
+            hops = np.ones(len(a) * len(a), np.int32)
+            k = len(a)
+            return a, lat.reshape(k, k), rel.reshape(k, k), hops.reshape(k, k)
+        lat, rel, hops = self.source_rows(a, a, nthreads)
+        return a, lat, rel, hops
+
+
+# ------------------------------------------------------------------------------------------
+# attach (shd-topology.c:965-1152)
+# ------------------------------------------------------------------------------------------
+def attach_vertex(vattrs, state, ip_hint=None, geocode_hint=None, type_hint=None):
+    """Return (vertex, new_state, draws).  `state` is the host Random's rand_r state."""
+    ids = vattrs["id"]
+    ips = vattrs.get("ip", [""] * len(ids))
+    types = vattrs.get("type", [""] * len(ids))
+    codes = vattrs.get("geocode", [""] * len(ids))
+    requested = string_to_ip(ip_hint) if ip_hint is not None else INADDR_NONE
+    cand = {"all": [], "type": [], "code": [], "tc": []}
+    nips = {"all": 0, "type": 0, "code": 0, "tc": 0}
+    exact = False
+    for v in range(len(ids)):
+        if "poi" not in ids[v]:
+            continue
+        vip = string_to_ip(ips[v])
+        usable = vip != INADDR_NONE and vip != INADDR_ANY
+        if ip_hint is not None and requested != INADDR_NONE and requested != INADDR_ANY:
+            if vip == requested:
+                if not exact:
+                    for k in cand:
+                        cand[k] = []
+                exact = True
+                cand["all"].append(v)
+                if usable:
+                    nips["all"] += 1
+        if exact:
+            continue
+        tm = type_hint is not None and types[v].lower() == type_hint.lower()
+        cm = geocode_hint is not None and codes[v].lower() == geocode_hint.lower()
+        cand["all"].append(v)
+        if usable:
+            nips["all"] += 1
+        if tm:
+            cand["type"].append(v)
+            nips["type"] += usable
+        if cm:
+            cand["code"].append(v)
+            nips["code"] += usable
+        if tm and cm:
+            cand["tc"].append(v)
+            nips["tc"] += usable
+    for k in ("tc", "type", "code", "all"):
+        if cand[k] or k == "all":
+            chosen = k
+            break
+    cands = cand[chosen]
+    use_lpm = ip_hint is not None and nips[chosen] > 0
+    if not cands:
+        raise RuntimeError("no attachment candidates")
+    if use_lpm and not exact:
+        best_match, best = 0, -1
+        for v in cands:
+            m = string_to_ip(ips[v]) & requested
+            if m > best_match:
+                best_match, best = m, v
+        return best, state, 0
+    r, state = next_double(state)
+    idx = c_round(float(len(cands) - 1) * r)
+    return cands[idx], state, 1
+
+
+# ------------------------------------------------------------------------------------------
+# The reference Topology object with its lazy cache (shd-topology.c:434-512, 876-963)
+# ------------------------------------------------------------------------------------------
+class OracleTopology:
+    def __init__(self, graph: OGraph):
+        self.g = graph
+        self.is_complete = graph.is_complete()
+        self.is_directed = graph.directed
+        self.virtual_ip = {}          # ip -> vertex
+        self.cache = {}               # src -> {dst: (lat, rel)}
+        self.minimum_path_latency = 0.0
+        self.min_updates = []         # worker_updateMinTimeJump trajectory
+        self.shortest_path_count = 0
+
+    def attach(self, ip, state, ip_hint=None, geocode_hint=None, type_hint=None):
+        v, state, _ = attach_vertex(self.g.vattrs, state, ip_hint, geocode_hint, type_hint)
+        self.virtual_ip[ip] = v
+        return v, state
+
+    def detach(self, ip):
+        self.virtual_ip.pop(ip, None)
+
+    def _store(self, s, d, lat, rel):
+        self.cache.setdefault(s, {})[d] = (lat, rel)
+        if self.minimum_path_latency == 0 or lat < self.minimum_path_latency:
+            self.minimum_path_latency = lat
+            self.min_updates.append(lat)
+
+    def _lookup(self, s, d):
+        return self.cache.get(s, {}).get(d)
+
+    def get_path_entry(self, src_ip, dst_ip):
+        s = self.virtual_ip.get(src_ip, -1)
+        d = self.virtual_ip.get(dst_ip, -1)
+        if s < 0 or d < 0:
+            return None
+        p = self._lookup(s, d)
+        if p is None and not self.is_directed:
+            p = self._lookup(d, s)
+        if p is None:
+            if self.is_complete:
+                lat, rel = self.g.complete_pairs([s], [d])
+                self._store(s, d, float(lat[0]), float(rel[0]))
+            else:
+                targets = np.asarray(list(self.virtual_ip.values()), dtype=np.int32)
+                lat, rel, _ = self.g.source_rows([s], targets)
+                self.shortest_path_count += 1
+                for k, t in enumerate(targets):
+                    self._store(s, int(t), float(lat[0, k]), float(rel[0, k]))
+            p = self._lookup(s, d)
+        return p
+
+    def get_latency(self, src_ip, dst_ip):
+        p = self.get_path_entry(src_ip, dst_ip)
+        return -1.0 if p is None else p[0]
+
+    def get_reliability(self, src_ip, dst_ip):
+        p = self.get_path_entry(src_ip, dst_ip)
+        return -1.0 if p is None else p[1]
+
+    def is_routable(self, src_ip, dst_ip):
+        return self.get_latency(src_ip, dst_ip) > -1
+
+
+def master_min_jump(min_path_latency_ms, runahead_ms=0):
+    """shd-master.c:98-124: (u64)minLat * 1e6 ns, default 10 ms, --runahead lower bound."""
+    nxt = int(min_path_latency_ms) * 1000000 if min_path_latency_ms > 0 else 0
+    jump = nxt if nxt > 0 else 10 * 1000000
+    cfg = int(runahead_ms) * 1000000
+    if cfg > 0 and jump < cfg:
+        jump = cfg
+    return jump
+
+
+# ------------------------------------------------------------------------------------------
+# packet route (shd-worker.c:332-370)
+# ------------------------------------------------------------------------------------------
+def route_packets(lat, rel, payload, state, now, jump, clamp):
+    """Returns (time u64[n], delivered u8[n], new_state u32[n])."""
+    n = len(lat)
+    lat = np.ascontiguousarray(lat, np.float64)
+    rel = np.ascontiguousarray(rel, np.float64)
+    payload = np.ascontiguousarray(payload, np.uint32)
+    st = np.array(state, dtype=np.uint32, copy=True)
+    now = np.ascontiguousarray(now, np.uint64)
+    t = np.empty(n, np.uint64)
+    dl = np.empty(n, np.uint8)
+    lib().orc_route_packets(n, _p(lat), _p(rel), _p(payload), _p(st), _p(now),
+                            ctypes.c_uint64(int(jump)), int(clamp), _p(t), _p(dl))
+    return t, dl, st

@@ -1,0 +1,522 @@
+/*
+ * oracle.c -- TEST INFRASTRUCTURE ONLY (never linked into, loaded by, or called from the
+ * product library shadow_amd/libshdtopo.so).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this file's shared object, and only as the checker.
+ *
+ * A plain-C CPU restatement of the Shadow v1.11.1 routing hot path:
+ *
+ *   reference (read as text, never compiled -- igraph is absent):
+ *     src/topology/shd-topology.c:561-671   _topology_computeSourcePathsHelper  -> orc_source_rows()
+ *     src/topology/shd-topology.c:673-833   _topology_computeSourcePaths        -> orc_source_rows()
+ *     src/topology/shd-topology.c:835-873   _topology_lookupPath (complete)     -> orc_complete_pairs()
+ *     src/topology/shd-topology.c:534-559   _topology_getEdgeHelper             -> orc_get_eid() + callers
+ *     src/engine/shd-worker.c:332-370       worker_schedulePacket               -> orc_route_packets()
+ *     src/engine/shd-worker.c:310-324       inter-host clamp                    -> orc_route_packets()
+ *     src/utility/shd-random.c:30-37        random_nextInt/nextDouble (rand_r)  -> orc_rand_r()
+ *
+ *   third-party dependency restated (NOT in /root/reference): igraph C library, version
+ *   unpinned by the reference (cmake/FindIGRAPH.cmake:12-49); API usage pins it to 0.7.x,
+ *   this file follows igraph 0.7.1's published algorithms:
+ *     - type_indexededgelist.c: undirected edges stored from=max(u,v), to=min(u,v);
+ *       igraph_incident(mode=ALL) = out-list (from==u, ascending to) then in-list
+ *       (to==u, ascending from); self loops therefore appear twice      -> orc_build_incidence()
+ *     - indheap.c: igraph_2wheap_t (indexed max-heap on -dist; shift_up swaps while
+ *       data[x] >= data[parent]; sink prefers left on >=)              -> struct wheap
+ *     - structural_properties.c: igraph_get_shortest_paths_dijkstra (dist=-1 init,
+ *       first-finite / strict-improvement relax, early exit on targets)  -> orc_dijkstra()
+ *     - igraph_get_eid (binary search in the from/to index)             -> orc_get_eid()
+ *
+ * Parity status: the SSSP branch is "parity unpinned" against igraph itself (no igraph in the
+ * container, no reference golden vectors -- SURVEY.md 8(c)).  Distances are cross-checked in
+ * tests against scipy.sparse.csgraph.dijkstra (left-to-right f64 sums => unique fixpoint).
+ * rand_r is pinned against glibc's own rand_r (the reference's dependency) in tests.
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_RAND_MAX 2147483647.0
+
+/* ------------------------------------------------------------------------------------------ */
+/* glibc rand_r restatement (stdlib/rand_r.c), the generator behind shd-random.c:30-37.        */
+/* ------------------------------------------------------------------------------------------ */
+int32_t orc_rand_r(uint32_t* seed) {
+    uint32_t next = *seed;
+    int32_t result;
+    next *= 1103515245u;
+    next += 12345u;
+    result = (int32_t)((next / 65536u) % 2048u);
+    next *= 1103515245u;
+    next += 12345u;
+    result <<= 10;
+    result ^= (int32_t)((next / 65536u) % 1024u);
+    next *= 1103515245u;
+    next += 12345u;
+    result <<= 10;
+    result ^= (int32_t)((next / 65536u) % 1024u);
+    *seed = next;
+    return result;
+}
+
+/* shd-random.c:34-37 random_nextDouble */
+double orc_next_double(uint32_t* seed) {
+    return ((double)orc_rand_r(seed)) / ORC_RAND_MAX;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* igraph 0.7.1 indexed edge list                                                             */
+/* ------------------------------------------------------------------------------------------ */
+
+/* stable counting sort of the permutation `perm` (length E) by key[perm[i]] in [0, K) */
+static void counting_sort(int64_t E, int32_t K, const int32_t* key, const int32_t* perm_in,
+                          int32_t* perm_out, int64_t* cnt /* K+1 scratch */) {
+    memset(cnt, 0, sizeof(int64_t) * (size_t)(K + 1));
+    for (int64_t i = 0; i < E; i++) cnt[key[perm_in[i]] + 1]++;
+    for (int32_t k = 0; k < K; k++) cnt[k + 1] += cnt[k];
+    for (int64_t i = 0; i < E; i++) perm_out[cnt[key[perm_in[i]]]++] = perm_in[i];
+}
+
+/*
+ * Normalise endpoints (undirected: from=max, to=min -- igraph_add_edges) and build the
+ * incidence lists igraph_lazy_inclist_get() returns for mode OUT (directed) / ALL (undirected).
+ * Also returns the oi order (edges sorted by (from, to, eid)) used by orc_get_eid.
+ *   inc_ptr: V+1, inc_eid: 2E (undirected) or E (directed), oi: E, os: V+1
+ */
+int orc_build_incidence(int32_t V, int64_t E, int directed, const int32_t* u, const int32_t* v,
+                        int32_t* efrom, int32_t* eto, int64_t* inc_ptr, int32_t* inc_eid,
+                        int32_t* oi, int64_t* os) {
+    int32_t* id = (int32_t*)calloc((size_t)(E > 0 ? E : 1), sizeof(int32_t));
+    int32_t* tmp = (int32_t*)malloc(sizeof(int32_t) * (size_t)(E > 0 ? E : 1));
+    int32_t* ii = (int32_t*)malloc(sizeof(int32_t) * (size_t)(E > 0 ? E : 1));
+    int64_t* cnt = (int64_t*)malloc(sizeof(int64_t) * (size_t)(V + 1));
+    int64_t* is = (int64_t*)malloc(sizeof(int64_t) * (size_t)(V + 1));
+    if (!id || !tmp || !ii || !cnt || !is) return -1;
+    for (int64_t e = 0; e < E; e++) {
+        if (u[e] < 0 || u[e] >= V || v[e] < 0 || v[e] >= V) return -2;
+        if (directed || u[e] > v[e]) { efrom[e] = u[e]; eto[e] = v[e]; }
+        else { efrom[e] = v[e]; eto[e] = u[e]; }
+        id[e] = (int32_t)e;
+    }
+    /* oi: order by from, then to, then eid (igraph_vector_order on (from, to)) */
+    counting_sort(E, V, eto, id, tmp, cnt);
+    counting_sort(E, V, efrom, tmp, oi, cnt);
+    /* ii: order by to, then from, then eid */
+    counting_sort(E, V, efrom, id, tmp, cnt);
+    counting_sort(E, V, eto, tmp, ii, cnt);
+    /* os / is: start offsets */
+    memset(os, 0, sizeof(int64_t) * (size_t)(V + 1));
+    memset(is, 0, sizeof(int64_t) * (size_t)(V + 1));
+    for (int64_t e = 0; e < E; e++) { os[efrom[e] + 1]++; is[eto[e] + 1]++; }
+    for (int32_t k = 0; k < V; k++) { os[k + 1] += os[k]; is[k + 1] += is[k]; }
+    /* incidence lists */
+    int64_t p = 0;
+    for (int32_t x = 0; x < V; x++) {
+        inc_ptr[x] = p;
+        for (int64_t i = os[x]; i < os[x + 1]; i++) inc_eid[p++] = oi[i];
+        if (!directed)
+            for (int64_t i = is[x]; i < is[x + 1]; i++) inc_eid[p++] = ii[i];
+    }
+    inc_ptr[V] = p;
+    free(id); free(tmp); free(ii); free(cnt); free(is);
+    return 0;
+}
+
+/*
+ * igraph_get_eid(graph, &eid, pfrom, pto, directed=TRUE, error=TRUE) restated: binary search
+ * in the oi index.  For an undirected graph the endpoints are normalised first.  Parallel edges:
+ * igraph returns whichever its binary search lands on (implementation-defined); this restatement
+ * returns the lowest eid, and the synthetic generators never emit parallel edges.
+ * Returns -1 when no such edge exists (the reference then logs critical and fails).
+ */
+int64_t orc_get_eid(int directed, const int32_t* efrom, const int32_t* eto, const int32_t* oi,
+                    const int64_t* os, int32_t from, int32_t to) {
+    int32_t xf = from, xt = to;
+    if (!directed && xf < xt) { xf = to; xt = from; }
+    int64_t lo = os[xf], hi = os[xf + 1];
+    while (lo < hi) {            /* first position with eto >= xt */
+        int64_t mid = lo + (hi - lo) / 2;
+        if (eto[oi[mid]] < xt) lo = mid + 1; else hi = mid;
+    }
+    if (lo < os[xf + 1] && eto[oi[lo]] == xt) return oi[lo];
+    return -1;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* igraph 0.7.1 two-way indexed heap (indheap.c igraph_2wheap_t), max-heap on -dist            */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    double* data;     /* heap keys */
+    int32_t* index;   /* heap position -> vertex */
+    int64_t* index2;  /* vertex -> position+2 (0 = not in heap) */
+    int64_t size;
+} wheap;
+
+#define W_PARENT(x) ((((x) + 1) / 2) - 1)
+#define W_LEFT(x) ((((x) + 1) * 2) - 1)
+#define W_RIGHT(x) (((x) + 1) * 2)
+
+static void wheap_switch(wheap* h, int64_t e1, int64_t e2) {
+    if (e1 != e2) {
+        double t3 = h->data[e1];
+        h->data[e1] = h->data[e2];
+        h->data[e2] = t3;
+        int32_t t1 = h->index[e1], t2 = h->index[e2];
+        h->index2[t1] = e2 + 2;
+        h->index2[t2] = e1 + 2;
+        h->index[e1] = t2;
+        h->index[e2] = t1;
+    }
+}
+
+static void wheap_shift_up(wheap* h, int64_t elem) {
+    while (!(elem == 0 || h->data[elem] < h->data[W_PARENT(elem)])) {
+        wheap_switch(h, elem, W_PARENT(elem));
+        elem = W_PARENT(elem);
+    }
+}
+
+static void wheap_sink(wheap* h, int64_t head) {
+    for (;;) {
+        int64_t size = h->size;
+        if (W_LEFT(head) >= size) return;
+        if (W_RIGHT(head) == size || h->data[W_LEFT(head)] >= h->data[W_RIGHT(head)]) {
+            if (h->data[head] < h->data[W_LEFT(head)]) {
+                wheap_switch(h, head, W_LEFT(head));
+                head = W_LEFT(head);
+            } else return;
+        } else {
+            if (h->data[head] < h->data[W_RIGHT(head)]) {
+                wheap_switch(h, head, W_RIGHT(head));
+                head = W_RIGHT(head);
+            } else return;
+        }
+    }
+}
+
+static void wheap_push(wheap* h, int32_t idx, double elem) {
+    int64_t size = h->size;
+    h->data[size] = elem;
+    h->index[size] = idx;
+    h->size = size + 1;
+    h->index2[idx] = size + 2;
+    wheap_shift_up(h, size);
+}
+
+static double wheap_delete_max(wheap* h, int32_t* idx_out) {
+    double tmp = h->data[0];
+    int32_t tmpidx = h->index[0];
+    wheap_switch(h, 0, h->size - 1);
+    h->size--;
+    h->index2[tmpidx] = 0;
+    wheap_sink(h, 0);
+    *idx_out = tmpidx;
+    return tmp;
+}
+
+static void wheap_modify(wheap* h, int32_t idx, double elem) {
+    int64_t pos = h->index2[idx] - 2;
+    h->data[pos] = elem;
+    wheap_sink(h, pos);
+    wheap_shift_up(h, pos);
+}
+
+/* per-thread scratch for one SSSP */
+typedef struct {
+    int32_t V;
+    double* dist;
+    int64_t* parent_eid1; /* igraph parent_eids: eid+1, 0 = none */
+    char* is_target;
+    wheap h;
+    int32_t* path;        /* scratch for path reconstruction */
+} orc_ws;
+
+static int ws_init(orc_ws* w, int32_t V) {
+    w->V = V;
+    w->dist = (double*)malloc(sizeof(double) * (size_t)V);
+    w->parent_eid1 = (int64_t*)malloc(sizeof(int64_t) * (size_t)V);
+    w->is_target = (char*)malloc((size_t)V);
+    w->h.data = (double*)malloc(sizeof(double) * (size_t)V);
+    w->h.index = (int32_t*)malloc(sizeof(int32_t) * (size_t)V);
+    w->h.index2 = (int64_t*)malloc(sizeof(int64_t) * (size_t)V);
+    w->path = (int32_t*)malloc(sizeof(int32_t) * (size_t)(V + 1));
+    return (w->dist && w->parent_eid1 && w->is_target && w->h.data && w->h.index && w->h.index2 &&
+            w->path) ? 0 : -1;
+}
+
+static void ws_free(orc_ws* w) {
+    free(w->dist); free(w->parent_eid1); free(w->is_target);
+    free(w->h.data); free(w->h.index); free(w->h.index2); free(w->path);
+}
+
+#define OTHER(efrom, eto, e, x) ((efrom)[e] == (x) ? (eto)[e] : (efrom)[e])
+
+/*
+ * igraph_get_shortest_paths_dijkstra(graph, vertices, NULL, from, to=targets, weights, OUT)
+ * restated (igraph 0.7.1).  Leaves dist[] (-1 = unreached) and parent_eid1[] in ws.
+ * pop_rank (optional, V): order in which vertices were popped (-1 = never popped).
+ */
+static void dijkstra_ws(orc_ws* ws, const int64_t* inc_ptr, const int32_t* inc_eid,
+                        const int32_t* efrom, const int32_t* eto, const double* w, int32_t src,
+                        const int32_t* targets, int64_t ntargets, int64_t* pop_rank) {
+    int32_t V = ws->V;
+    for (int32_t i = 0; i < V; i++) {
+        ws->dist[i] = -1.0;
+        ws->parent_eid1[i] = 0;
+        ws->is_target[i] = 0;
+        ws->h.index2[i] = 0;
+        if (pop_rank) pop_rank[i] = -1;
+    }
+    int64_t to_reach = ntargets;
+    for (int64_t k = 0; k < ntargets; k++) {
+        if (!ws->is_target[targets[k]]) ws->is_target[targets[k]] = 1;
+        else to_reach--;
+    }
+    ws->h.size = 0;
+    ws->dist[src] = 0.0;
+    wheap_push(&ws->h, src, 0.0);
+    int64_t rank = 0;
+    while (ws->h.size > 0 && to_reach > 0) {
+        int32_t minnei;
+        double mindist = -wheap_delete_max(&ws->h, &minnei);
+        if (pop_rank) pop_rank[minnei] = rank;
+        rank++;
+        if (ws->is_target[minnei]) {
+            ws->is_target[minnei] = 0;
+            to_reach--;
+        }
+        for (int64_t i = inc_ptr[minnei]; i < inc_ptr[minnei + 1]; i++) {
+            int32_t edge = inc_eid[i];
+            int32_t tto = OTHER(efrom, eto, edge, minnei);
+            double altdist = mindist + w[edge];
+            double curdist = ws->dist[tto];
+            if (curdist < 0) {
+                ws->dist[tto] = altdist;
+                ws->parent_eid1[tto] = (int64_t)edge + 1;
+                wheap_push(&ws->h, tto, -altdist);
+            } else if (altdist < curdist) {
+                ws->dist[tto] = altdist;
+                ws->parent_eid1[tto] = (int64_t)edge + 1;
+                wheap_modify(&ws->h, tto, -altdist);
+            }
+        }
+    }
+}
+
+/* standalone SSSP entry used by tests: dist (-1 unreached), parent vertex (-1 none), pop rank */
+int orc_dijkstra(int32_t V, const int64_t* inc_ptr, const int32_t* inc_eid, const int32_t* efrom,
+                 const int32_t* eto, const double* w, int32_t src, const int32_t* targets,
+                 int64_t ntargets, double* dist, int32_t* parent_v, int32_t* parent_e,
+                 int64_t* pop_rank) {
+    orc_ws ws;
+    if (ws_init(&ws, V)) return -1;
+    dijkstra_ws(&ws, inc_ptr, inc_eid, efrom, eto, w, src, targets, ntargets, pop_rank);
+    for (int32_t i = 0; i < V; i++) {
+        dist[i] = ws.dist[i];
+        if (ws.parent_eid1[i]) {
+            int32_t e = (int32_t)(ws.parent_eid1[i] - 1);
+            parent_e[i] = e;
+            parent_v[i] = OTHER(efrom, eto, e, i);
+        } else {
+            parent_e[i] = -1;
+            parent_v[i] = -1;
+        }
+    }
+    ws_free(&ws);
+    return 0;
+}
+
+/*
+ * Per-target helper (shd-topology.c:561-671) applied to every target after one Dijkstra from
+ * src (shd-topology.c:753-823).  Path reconstruction as igraph 0.7.1: walk parent_eids back
+ * from the target; the path of target==src is [src].
+ * Outputs per target k: lat[k], rel[k], hops[k] (loop iterations of the helper).
+ * Returns 0, or -(k+1) if the helper failed for target k (missing edge, e.g. no self loop).
+ */
+static int source_rows_ws(orc_ws* ws, int directed, const int64_t* inc_ptr, const int32_t* inc_eid,
+                          const int32_t* efrom, const int32_t* eto, const int32_t* oi,
+                          const int64_t* os, const double* elat, const double* eloss,
+                          const double* vloss, int32_t src, const int32_t* targets,
+                          int64_t ntargets, double* lat, double* rel, int32_t* hops) {
+    dijkstra_ws(ws, inc_ptr, inc_eid, efrom, eto, elat, src, targets, ntargets, NULL);
+    for (int64_t k = 0; k < ntargets; k++) {
+        int32_t node = targets[k];
+        /* vertex path [src, ..., node] */
+        int64_t size = 0;
+        int32_t act = node;
+        while (ws->parent_eid1[act]) {
+            size++;
+            int32_t e = (int32_t)(ws->parent_eid1[act] - 1);
+            act = OTHER(efrom, eto, e, act);
+        }
+        int32_t* path = ws->path;
+        path[size] = node;
+        act = node;
+        int64_t s2 = size;
+        while (ws->parent_eid1[act]) {
+            int32_t e = (int32_t)(ws->parent_eid1[act] - 1);
+            act = OTHER(efrom, eto, e, act);
+            s2--;
+            path[s2] = act;
+        }
+        int64_t n = size + 1;
+        double totalLatency = 0.0, totalReliability = 1.0;
+        totalReliability *= (1.0 - vloss[src]);
+        int32_t dstv = path[n - 1];
+        if ((src != dstv) || (src == dstv && n > 2)) totalReliability *= (1.0 - vloss[dstv]);
+        int64_t start = (n == 1) ? 0 : 1;
+        int32_t from = src;
+        int32_t h = 0;
+        for (int64_t i = start; i < n; i++) {
+            int32_t to = path[i];
+            int64_t e = orc_get_eid(directed, efrom, eto, oi, os, from, to);
+            if (e < 0) return (int)(-(k + 1));
+            totalLatency += elat[e];
+            totalReliability *= (1.0 - eloss[e]);
+            from = to;
+            h++;
+        }
+        if (totalLatency == 0.0) totalLatency = 1.0;
+        lat[k] = totalLatency;
+        rel[k] = totalReliability;
+        hops[k] = h;
+    }
+    return 0;
+}
+
+int orc_source_rows(int32_t V, int directed, const int64_t* inc_ptr, const int32_t* inc_eid,
+                    const int32_t* efrom, const int32_t* eto, const int32_t* oi, const int64_t* os,
+                    const double* elat, const double* eloss, const double* vloss, int32_t src,
+                    const int32_t* targets, int64_t ntargets, double* lat, double* rel,
+                    int32_t* hops) {
+    orc_ws ws;
+    if (ws_init(&ws, V)) return -1000000;
+    int r = source_rows_ws(&ws, directed, inc_ptr, inc_eid, efrom, eto, oi, os, elat, eloss, vloss,
+                           src, targets, ntargets, lat, rel, hops);
+    ws_free(&ws);
+    return r;
+}
+
+/* multi-source table: rows for srcs[0..nsrc) x targets, nthreads pthreads (1 = the reference's
+ * serialised graphLock behaviour).  Output row-major [nsrc][ntargets]. */
+typedef struct {
+    int32_t V; int directed;
+    const int64_t* inc_ptr; const int32_t* inc_eid; const int32_t* efrom; const int32_t* eto;
+    const int32_t* oi; const int64_t* os; const double* elat; const double* eloss;
+    const double* vloss; const int32_t* srcs; int64_t nsrc; const int32_t* targets;
+    int64_t ntargets; double* lat; double* rel; int32_t* hops;
+    int64_t next; pthread_mutex_t mu; int err;
+} rows_job;
+
+static void* rows_worker(void* arg) {
+    rows_job* j = (rows_job*)arg;
+    orc_ws ws;
+    if (ws_init(&ws, j->V)) { j->err = -1; return NULL; }
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        int64_t i = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (i >= j->nsrc) break;
+        int r = source_rows_ws(&ws, j->directed, j->inc_ptr, j->inc_eid, j->efrom, j->eto, j->oi,
+                               j->os, j->elat, j->eloss, j->vloss, j->srcs[i], j->targets,
+                               j->ntargets, j->lat + i * j->ntargets, j->rel + i * j->ntargets,
+                               j->hops + i * j->ntargets);
+        if (r) j->err = r;
+    }
+    ws_free(&ws);
+    return NULL;
+}
+
+int orc_table_rows(int32_t V, int directed, const int64_t* inc_ptr, const int32_t* inc_eid,
+                   const int32_t* efrom, const int32_t* eto, const int32_t* oi, const int64_t* os,
+                   const double* elat, const double* eloss, const double* vloss,
+                   const int32_t* srcs, int64_t nsrc, const int32_t* targets, int64_t ntargets,
+                   double* lat, double* rel, int32_t* hops, int nthreads) {
+    rows_job j = {V, directed, inc_ptr, inc_eid, efrom, eto, oi, os, elat, eloss, vloss, srcs,
+                  nsrc, targets, ntargets, lat, rel, hops, 0, PTHREAD_MUTEX_INITIALIZER, 0};
+    if (nthreads < 1) nthreads = 1;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, rows_worker, &j);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th);
+    return j.err;
+}
+
+/*
+ * Parent-tie analysis: for every reached v != src, the candidates are the
+ * incident u != v with fl(d[u] + w) == d[v]; parent(v) = argmin (d[u], popRank(u)).  flags[v] =
+ * number of candidates sharing the minimum d[u] (0 for src/unreached, 1 = unambiguous).
+ * Used by tests to show where heap pop order decides the parent.
+ */
+int orc_parent_ties(int32_t V, const int64_t* inc_ptr, const int32_t* inc_eid,
+                    const int32_t* efrom, const int32_t* eto, const double* w, const double* dist,
+                    int32_t src, int32_t* ncand_min) {
+    for (int32_t x = 0; x < V; x++) {
+        ncand_min[x] = 0;
+        if (x == src || dist[x] < 0) continue;
+        double best = INFINITY;
+        int32_t cnt = 0;
+        for (int64_t i = inc_ptr[x]; i < inc_ptr[x + 1]; i++) {
+            int32_t e = inc_eid[i];
+            int32_t y = OTHER(efrom, eto, e, x);
+            if (y == x || dist[y] < 0) continue;
+            if (dist[y] + w[e] == dist[x]) {
+                if (dist[y] < best) { best = dist[y]; cnt = 1; }
+                else if (dist[y] == best) cnt++;
+            }
+        }
+        ncand_min[x] = cnt;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* complete-graph branch: _topology_lookupPath (shd-topology.c:835-873)                        */
+/* ------------------------------------------------------------------------------------------ */
+int orc_complete_pairs(int directed, const int32_t* efrom, const int32_t* eto, const int32_t* oi,
+                       const int64_t* os, const double* elat, const double* eloss,
+                       const double* vloss, const int32_t* srcs, const int32_t* dsts, int64_t n,
+                       double* lat, double* rel) {
+    for (int64_t k = 0; k < n; k++) {
+        int32_t s = srcs[k], d = dsts[k];
+        double totalLatency = 0.0, totalReliability = 1.0;
+        totalReliability *= (1.0 - vloss[s]);
+        totalReliability *= (1.0 - vloss[d]);
+        int64_t e = orc_get_eid(directed, efrom, eto, oi, os, s, d);
+        if (e < 0) return (int)(-(k + 1));
+        double edgeLatency = elat[e];
+        double edgeReliability = 1.0 - eloss[e];
+        totalLatency += edgeLatency;
+        totalReliability *= edgeReliability;
+        lat[k] = totalLatency;
+        rel[k] = totalReliability;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* packet route: worker_schedulePacket (shd-worker.c:332-370) + clamp (shd-worker.c:310-324)   */
+/* ------------------------------------------------------------------------------------------ */
+void orc_route_packets(int64_t n, const double* lat, const double* rel, const uint32_t* payload,
+                       uint32_t* state, const uint64_t* now, uint64_t jump, int clamp,
+                       uint64_t* out_time, uint8_t* out_delivered) {
+    for (int64_t k = 0; k < n; k++) {
+        double reliability = rel[k];
+        double chance = orc_next_double(&state[k]);
+        if (chance <= reliability || payload[k] == 0) {
+            double latency = lat[k];
+            uint64_t delay = (uint64_t)ceil(latency * 1000000.0);
+            uint64_t t = now[k] + delay;
+            if (clamp) {
+                uint64_t minTime = now[k] + jump;
+                if (t < minTime) t = minTime;
+            }
+            out_time[k] = t;
+            out_delivered[k] = 1;
+        } else {
+            out_time[k] = 0;
+            out_delivered[k] = 0;
+        }
+    }
+}

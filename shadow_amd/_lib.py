@@ -1,0 +1,125 @@
+"""ctypes binding of libshdtopo.so (include/shd_topology_abi.h).
+
+The shared objects are built in-tree by ``make -C shadow_amd/csrc`` (``__graft_entry__.build``).
+There is no fallback: if the library is missing, importing the product raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libshdtopo.so")
+SHIM_PATH = os.path.join(HERE, "libshdtopo_shim.so")
+
+P = ctypes.c_void_p
+i32, i64, u32, u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64
+dbl = ctypes.c_double
+cstr = ctypes.c_char_p
+
+
+class TopoPacketIn(ctypes.Structure):
+    _fields_ = [("srcIP", u32), ("dstIP", u32), ("payloadLength", u32), ("rngState", u32),
+                ("now", u64)]
+
+
+class TopoPacketOut(ctypes.Structure):
+    _fields_ = [("time", u64), ("rngState", u32), ("delivered", ctypes.c_uint8),
+                ("_pad", ctypes.c_uint8 * 3)]
+
+
+class ShdStats(ctypes.Structure):
+    _fields_ = [("build_ms", dbl), ("sssp_kernel_ms", dbl), ("route_kernel_ms", dbl),
+                ("sources", i64), ("targets", i64), ("ambiguous_pairs", i64),
+                ("relaxations", i64), ("long_paths", i64), ("errors", i64)]
+
+
+class ShdSynthParams(ctypes.Structure):
+    _fields_ = [("seed", u64), ("n_routers", i64), ("n_poi", i64), ("n_edges", i64),
+                ("integer_latency", ctypes.c_int), ("alpha", dbl)]
+
+
+# every symbol include/shd_topology_abi.h declares: name -> (restype, argtypes)
+SIGNATURES = {
+    "topology_new": (P, [cstr]),
+    "topology_free": (None, [P]),
+    "topology_attach": (None, [P, P, P, cstr, cstr, cstr, P, P]),
+    "topology_detach": (None, [P, P]),
+    "topology_isRoutable": (ctypes.c_int, [P, P, P]),
+    "topology_getLatency": (dbl, [P, P, P]),
+    "topology_getReliability": (dbl, [P, P, P]),
+    "topology_getMinimumLatency": (dbl, [P]),
+    "topology_routePacketBatch": (ctypes.c_int, [P, P, P, ctypes.c_size_t, u64, ctypes.c_int]),
+    "shdtopo_version": (ctypes.c_int, []),
+    "shdtopo_new_from_buffer": (P, [cstr, ctypes.c_size_t]),
+    "shdtopo_set_option": (ctypes.c_int, [P, cstr, dbl]),
+    "shdtopo_attach_ip": (i32, [P, u32, P, cstr, cstr, cstr, P, P]),
+    "shdtopo_get_latency_ip": (dbl, [P, u32, u32]),
+    "shdtopo_get_reliability_ip": (dbl, [P, u32, u32]),
+    "shdtopo_num_vertices": (i64, [P]),
+    "shdtopo_num_edges": (i64, [P]),
+    "shdtopo_is_complete": (ctypes.c_int, [P]),
+    "shdtopo_is_directed": (ctypes.c_int, [P]),
+    "shdtopo_num_attached": (i64, [P]),
+    "shdtopo_attached_vertices": (i64, [P, P, i64]),
+    "shdtopo_column_of_ip": (i32, [P, u32]),
+    "shdtopo_vertex_of_ip": (i32, [P, u32]),
+    "shdtopo_build": (ctypes.c_int, [P]),
+    "shdtopo_build_rows": (ctypes.c_int, [P, i64, i64, P, P, P, P]),
+    "shdtopo_bind_table": (ctypes.c_int, [P, P, P, dbl, P]),
+    "shdtopo_table_to_host": (ctypes.c_int, [P, P, P, P]),
+    "shdtopo_route_batch_device": (ctypes.c_int, [P, P, P, P, P, P, i64, u64, ctypes.c_int, P,
+                                                  P, P, P]),
+    "shdtopo_get_lazy_minimum_latency": (dbl, [P]),
+    "shdtopo_get_stats": (ctypes.c_int, [P, P]),
+    "shdtopo_write_graphml": (ctypes.c_int, [P, cstr]),
+    "shdtopo_new_synthetic": (P, [P]),
+    "shdtopo_synth_packets": (ctypes.c_int, [P, u64, i64, i64, u64, u64, P, P, P, P, P, P, P]),
+}
+
+SHIM_SIGNATURES = {
+    "shim_address_new": (P, [u32]),
+    "shim_address_free": (None, [P]),
+    "address_toNetworkIP": (u32, [P]),
+    "random_new": (P, [ctypes.c_uint]),
+    "random_free": (None, [P]),
+    "random_nextDouble": (dbl, [P]),
+    "random_nextInt": (ctypes.c_int, [P]),
+    "shim_random_state": (ctypes.c_uint, [P]),
+    "worker_updateMinTimeJump": (None, [dbl]),
+    "shim_last_min_latency": (dbl, []),
+    "shim_next_min_jump": (u64, []),
+    "shim_min_updates": (ctypes.c_int, []),
+    "shim_reset": (None, []),
+}
+
+_lib = None
+_shim = None
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def _bind(L, sigs):
+    for name, (res, args) in sigs.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def load():
+    """Load the shim (RTLD_GLOBAL, so libshdtopo's weak Shadow imports resolve) and the engine."""
+    global _lib, _shim
+    if _lib is not None:
+        return _lib, _shim
+    for p in (SHIM_PATH, LIB_PATH):
+        if not os.path.exists(p):
+            raise LibraryMissing(
+                "%s is not built: run `make -C shadow_amd/csrc` (or __graft_entry__.build()); "
+                "the routing engine has no CPU fallback" % p)
+    _shim = ctypes.CDLL(SHIM_PATH, mode=ctypes.RTLD_GLOBAL)
+    _bind(_shim, SHIM_SIGNATURES)
+    _lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    _bind(_lib, SIGNATURES)
+    return _lib, _shim

@@ -1,0 +1,1123 @@
+// topo_core.cpp -- the Topology object behind the C ABI of include/shd_topology_abi.h.
+//
+// Reference: src/topology/shd-topology.c (Shadow v1.11.1).  What changes against the reference:
+//   * paths are not computed lazily one igraph Dijkstra at a time under a global lock
+//     (shd-topology.c:673-833); the whole attached-vertex table is built on the
+//     GPU on first use after the attach set settles (sssp_rows_kernel / pair_table_complete);
+//   * getters read an immutable table; the reference's first-rooted-wins cache behaviour
+//     (shd-topology.c:894-915) is reproduced with per-source "materialised"
+//     flags (lazy mode, default) so answers and the min-latency trajectory are bit-identical
+//     for the same query sequence;
+//   * attach uses a candidate index built once instead of an O(V) scan per host.
+#include <arpa/inet.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <vector>
+
+#include "../../include/shd_topology_abi.h"
+#include "topo_internal.h"
+
+// ---- imports from the Shadow executable (weak: absent in a standalone process) ----
+extern "C" {
+__attribute__((weak)) uint32_t address_toNetworkIP(Address* address);
+__attribute__((weak)) double random_nextDouble(Random* random);
+__attribute__((weak)) void worker_updateMinTimeJump(double minPathLatency);
+}
+
+using namespace shdtopo;
+
+namespace {
+
+int log_level() {
+    static int lvl = [] {
+        const char* e = getenv("SHDTOPO_LOG");
+        return e ? atoi(e) : 1;
+    }();
+    return lvl;
+}
+
+void logf(int lvl, const char* tag, const char* fmt, ...) {
+    if (lvl > log_level()) return;
+    va_list ap;
+    va_start(ap, fmt);
+    fprintf(stderr, "[shdtopo] %s: ", tag);
+    vfprintf(stderr, fmt, ap);
+    fputc('\n', stderr);
+    va_end(ap);
+}
+#define CRITICAL(...) logf(1, "critical", __VA_ARGS__)
+#define WARNING(...) logf(1, "warning", __VA_ARGS__)
+#define MESSAGE(...) logf(2, "message", __VA_ARGS__)
+
+#define HIPCHK(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) {                                                             \
+            CRITICAL("HIP error %s at %s:%d (%s)", hipGetErrorString(_e), __FILE__, __LINE__, \
+                     #expr);                                                                \
+            return -100 - (int)_e;                                                          \
+        }                                                                                   \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t ensure(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        release();
+        hipError_t e = hipMalloc(&p, sizeof(T) * (count ? count : 1));
+        if (e == hipSuccess) n = count;
+        else p = nullptr;
+        return e;
+    }
+};
+
+}  // namespace
+
+struct _Topology {
+    HostGraph g;
+    bool isComplete = false;
+    bool isDirected = false;
+    bool hasMultiEdges = false;
+
+    // options
+    bool abortOnError = true;
+    bool lazy = true;
+    double delta = 0.0;  // 0 = auto
+    int slotsOpt = 0;
+    int device = 0;
+
+    // attach state (shd-topology.c:20-24 virtualIP)
+    std::shared_mutex ipMu;
+    std::unordered_map<uint32_t, int32_t> virtualIP;
+    AttachIndex aidx;
+
+    // table geometry
+    std::mutex buildMu;
+    std::atomic<bool> tableValid{false};
+    std::atomic<bool> hostValid{false};
+    std::vector<int32_t> attached;  // columns: distinct attached vertices, ascending
+    std::vector<int32_t> colOf;     // vertex -> column
+    int64_t A = 0;
+
+    // device state
+    bool devInit = false;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+    bool csrUploaded = false;
+    std::vector<int32_t> perm;  // new -> old
+    std::vector<int32_t> inv;   // old -> new
+    DevBuf<uint32_t> d_rowptr, d_col;
+    DevBuf<double> d_wt, d_aloss, d_vloss, d_selfLat, d_selfLoss;
+    DevBuf<unsigned long long> d_dist, d_best, d_memo;
+    DevBuf<uint32_t> d_stamp, d_fstamp, d_qa, d_qb, d_far, d_cnt, d_bslot, d_par, d_pathbuf,
+        d_counters;
+    int slots = 0;
+    DevBuf<double2> d_lr;
+    DevBuf<uint16_t> d_hops;
+    DevBuf<double> d_rowmin;
+    DevBuf<double> d_elatAA, d_elossAA, d_vlossA;
+    DevBuf<uint32_t> d_sources, d_targets;
+    DevBuf<unsigned long long> d_stats;
+    // host-batch staging
+    DevBuf<int32_t> b_src, b_dst;
+    DevBuf<uint32_t> b_pay, b_sin, b_sout;
+    DevBuf<uint64_t> b_now, b_time;
+    DevBuf<uint8_t> b_dl;
+
+    // host mirror of the table (for the per-call getters)
+    std::vector<double> hlat, hrel, hrowmin;
+    std::vector<uint16_t> hhops;
+    double eagerMin = -1.0;
+
+    // lazy emulation
+    std::unique_ptr<std::atomic<uint8_t>[]> matRow;    // per vertex (SSSP branch)
+    std::unique_ptr<std::atomic<uint64_t>[]> matPair;  // per (vertex pair) bit (complete branch)
+    size_t matPairWords = 0;
+    std::mutex minMu;
+    double lazyMin = 0.0;  // top->minimumPathLatency
+
+    // stats
+    bool rowsPending = false;  // a launch whose stats have not been read back yet
+    bool routePending = false;
+    ShdStats stats{};
+};
+
+namespace {
+
+void fatal_or_continue(Topology* top, const char* what) {
+    CRITICAL("%s", what);
+    if (top->abortOnError) abort();
+}
+
+// ---------------------------------------------------------------------------------------------
+// validation (shd-topology.c:125-432)
+// ---------------------------------------------------------------------------------------------
+bool check_graph(Topology* top) {
+    HostGraph& g = top->g;
+    if (g.V == 0) {
+        CRITICAL("topology has no vertices");
+        return false;
+    }
+    // strong connectivity (igraph_is_connected(STRONG) + igraph_clusters, :134-151)
+    std::vector<std::vector<int32_t>> dummy;
+    std::vector<int64_t> optr((size_t)g.V + 1, 0), iptr((size_t)g.V + 1, 0);
+    for (int64_t e = 0; e < g.E; e++) {
+        optr[(size_t)g.eu[(size_t)e] + 1]++;
+        iptr[(size_t)g.ev[(size_t)e] + 1]++;
+    }
+    for (int32_t v = 0; v < g.V; v++) {
+        optr[(size_t)v + 1] += optr[(size_t)v];
+        iptr[(size_t)v + 1] += iptr[(size_t)v];
+    }
+    std::vector<int32_t> oadj((size_t)g.E), iadj((size_t)g.E);
+    {
+        std::vector<int64_t> po(optr.begin(), optr.end() - 1), pi(iptr.begin(), iptr.end() - 1);
+        for (int64_t e = 0; e < g.E; e++) {
+            oadj[(size_t)po[(size_t)g.eu[(size_t)e]]++] = g.ev[(size_t)e];
+            iadj[(size_t)pi[(size_t)g.ev[(size_t)e]]++] = g.eu[(size_t)e];
+        }
+    }
+    auto reach_all = [&](bool forward, bool both) {
+        std::vector<uint8_t> seen((size_t)g.V, 0);
+        std::vector<int32_t> st{0};
+        seen[0] = 1;
+        int64_t cnt = 1;
+        while (!st.empty()) {
+            int32_t x = st.back();
+            st.pop_back();
+            auto visit = [&](const std::vector<int64_t>& ptr, const std::vector<int32_t>& adj) {
+                for (int64_t i = ptr[(size_t)x]; i < ptr[(size_t)x + 1]; i++) {
+                    int32_t y = adj[(size_t)i];
+                    if (!seen[(size_t)y]) { seen[(size_t)y] = 1; cnt++; st.push_back(y); }
+                }
+            };
+            if (forward || both) visit(optr, oadj);
+            if (!forward || both) visit(iptr, iadj);
+        }
+        return cnt == g.V;
+    };
+    bool connected = g.directed ? (reach_all(true, false) && reach_all(false, false))
+                                : reach_all(true, true);
+    if (!connected) {
+        CRITICAL("topology must be but is not strongly connected");
+        return false;
+    }
+    top->isDirected = g.directed;
+    // complete <=> clique number == V (:156-165): every distinct pair adjacent (direction,
+    // loops and multi-edges ignored)
+    {
+        std::vector<uint64_t> keys;
+        keys.reserve((size_t)g.E);
+        for (int64_t e = 0; e < g.E; e++) {
+            uint64_t a = (uint64_t)g.eu[(size_t)e], b = (uint64_t)g.ev[(size_t)e];
+            if (a == b) continue;
+            if (a > b) std::swap(a, b);
+            keys.push_back(a * (uint64_t)g.V + b);
+        }
+        std::sort(keys.begin(), keys.end());
+        size_t uniq = (size_t)(std::unique(keys.begin(), keys.end()) - keys.begin());
+        top->hasMultiEdges = (uniq != keys.size()) && !g.directed;
+        top->isComplete = (uint64_t)uniq == (uint64_t)g.V * (uint64_t)(g.V - 1) / 2;
+    }
+    if (top->hasMultiEdges)
+        WARNING("topology has parallel edges: igraph_get_eid picks one of them "
+                "(implementation-defined); the lowest edge id is used here");
+    // edge latency > 0 (:312-317; the reference calls error() here)
+    for (int64_t e = 0; e < g.E; e++) {
+        if (g.elat[(size_t)e] <= 0) {
+            CRITICAL("invalid latency %f on edge %lld", g.elat[(size_t)e], (long long)e);
+            return false;
+        }
+    }
+    MESSAGE("topology graph is %s, %s, strongly connected, %d vertices, %lld edges",
+            top->isComplete ? "complete" : "incomplete",
+            top->isDirected ? "directed" : "undirected", g.V, (long long)g.E);
+    top->aidx.build(g);
+    top->matRow.reset(new std::atomic<uint8_t>[(size_t)g.V]);
+    for (int32_t v = 0; v < g.V; v++) top->matRow[(size_t)v].store(0);
+    return true;
+}
+
+Topology* finish_new(Topology* top) {
+    if (!check_graph(top)) {
+        delete top;
+        return nullptr;
+    }
+    if (const char* d = getenv("SHDTOPO_DEVICE")) top->device = atoi(d);
+    return top;
+}
+
+// ---------------------------------------------------------------------------------------------
+// device setup
+// ---------------------------------------------------------------------------------------------
+int dev_init(Topology* top) {
+    if (top->devInit) return 0;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) {
+        CRITICAL("no HIP device available: the routing engine runs on the GPU only "
+                 "(no CPU fallback)");
+        return -1;
+    }
+    HIPCHK(hipSetDevice(top->device % n));
+    HIPCHK(hipStreamCreateWithFlags(&top->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&top->ev0));
+    HIPCHK(hipEventCreate(&top->ev1));
+    HIPCHK(hipEventCreate(&top->ev2));
+    HIPCHK(hipEventCreate(&top->ev3));
+    HIPCHK(top->d_stats.ensure(ST_COUNT));
+    top->devInit = true;
+    return 0;
+}
+
+// CSR without self loops, vertices relabelled by descending degree so that the hot (hub)
+// distance words cluster in a few cache lines (power-law graphs: most adjacency entries point
+// at hubs).  Self loops go to selfLat/selfLoss (first = lowest edge id, as orc_get_eid).
+int upload_csr(Topology* top) {
+    if (top->csrUploaded) return 0;
+    HostGraph& g = top->g;
+    const int32_t V = g.V;
+    std::vector<uint32_t> deg((size_t)V, 0);
+    for (int64_t e = 0; e < g.E; e++) {
+        int32_t a = g.eu[(size_t)e], b = g.ev[(size_t)e];
+        if (a == b) continue;
+        deg[(size_t)a]++;
+        deg[(size_t)b]++;
+    }
+    top->perm.resize((size_t)V);
+    std::iota(top->perm.begin(), top->perm.end(), 0);
+    std::stable_sort(top->perm.begin(), top->perm.end(),
+                     [&](int32_t x, int32_t y) { return deg[(size_t)x] > deg[(size_t)y]; });
+    top->inv.resize((size_t)V);
+    for (int32_t i = 0; i < V; i++) top->inv[(size_t)top->perm[(size_t)i]] = i;
+    std::vector<uint32_t> rowptr((size_t)V + 1, 0);
+    for (int32_t i = 0; i < V; i++) rowptr[(size_t)i + 1] = rowptr[(size_t)i] + deg[(size_t)top->perm[(size_t)i]];
+    const size_t nadj = rowptr[(size_t)V];
+    std::vector<uint32_t> col(nadj);
+    std::vector<double> wt(nadj), aloss(nadj);
+    std::vector<uint32_t> fillp(rowptr.begin(), rowptr.end() - 1);
+    std::vector<double> selfLat((size_t)V, NAN), selfLoss((size_t)V, 0.0), vloss((size_t)V);
+    for (int64_t e = 0; e < g.E; e++) {
+        int32_t a = g.eu[(size_t)e], b = g.ev[(size_t)e];
+        int32_t na = top->inv[(size_t)a], nb = top->inv[(size_t)b];
+        if (a == b) {
+            if (std::isnan(selfLat[(size_t)na])) {
+                selfLat[(size_t)na] = g.elat[(size_t)e];
+                selfLoss[(size_t)na] = g.eloss[(size_t)e];
+            }
+            continue;
+        }
+        size_t pa = fillp[(size_t)na]++, pb = fillp[(size_t)nb]++;
+        col[pa] = (uint32_t)nb; wt[pa] = g.elat[(size_t)e]; aloss[pa] = g.eloss[(size_t)e];
+        col[pb] = (uint32_t)na; wt[pb] = g.elat[(size_t)e]; aloss[pb] = g.eloss[(size_t)e];
+    }
+    for (int32_t i = 0; i < V; i++) vloss[(size_t)i] = g.vloss[(size_t)top->perm[(size_t)i]];
+    HIPCHK(top->d_rowptr.ensure((size_t)V + 1));
+    HIPCHK(top->d_col.ensure(nadj));
+    HIPCHK(top->d_wt.ensure(nadj));
+    HIPCHK(top->d_aloss.ensure(nadj));
+    HIPCHK(top->d_vloss.ensure((size_t)V));
+    HIPCHK(top->d_selfLat.ensure((size_t)V));
+    HIPCHK(top->d_selfLoss.ensure((size_t)V));
+    HIPCHK(hipMemcpy(top->d_rowptr.p, rowptr.data(), sizeof(uint32_t) * ((size_t)V + 1), hipMemcpyHostToDevice));
+    if (nadj) {
+        HIPCHK(hipMemcpy(top->d_col.p, col.data(), sizeof(uint32_t) * nadj, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_wt.p, wt.data(), sizeof(double) * nadj, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_aloss.p, aloss.data(), sizeof(double) * nadj, hipMemcpyHostToDevice));
+    }
+    HIPCHK(hipMemcpy(top->d_vloss.p, vloss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(top->d_selfLat.p, selfLat.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(top->d_selfLoss.p, selfLoss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
+    top->csrUploaded = true;
+    return 0;
+}
+
+DevCSR dev_csr(Topology* top) {
+    DevCSR c;
+    c.V = top->g.V;
+    c.nadj = (int64_t)top->d_col.n;
+    c.rowptr = top->d_rowptr.p;
+    c.col = top->d_col.p;
+    c.wt = top->d_wt.p;
+    c.aloss = top->d_aloss.p;
+    c.vloss = top->d_vloss.p;
+    c.selfLat = top->d_selfLat.p;
+    c.selfLoss = top->d_selfLoss.p;
+    return c;
+}
+
+int ensure_workspace(Topology* top, int nsrc) {
+    const int64_t V = top->g.V;
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, top->device));
+    int want = top->slotsOpt > 0 ? top->slotsOpt : prop.multiProcessorCount * sssp_max_blocks_per_cu();
+    size_t per_slot = (size_t)V * 56 + (size_t)kMaxHops * kSsspBlock * 4 + 16;
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    int memcap = (int)std::max<size_t>(1, (freeb / 2) / per_slot);
+    want = std::min(want, memcap);
+    want = std::max(1, std::min(want, std::max(1, nsrc)));
+    if (top->slots >= want) return 0;
+    const size_t n = (size_t)want * (size_t)V;
+    HIPCHK(top->d_dist.ensure(n));
+    HIPCHK(top->d_best.ensure(n));
+    HIPCHK(top->d_memo.ensure(n));
+    HIPCHK(top->d_stamp.ensure(n));
+    HIPCHK(top->d_fstamp.ensure(n));
+    HIPCHK(top->d_qa.ensure(n));
+    HIPCHK(top->d_qb.ensure(n));
+    HIPCHK(top->d_far.ensure(n));
+    HIPCHK(top->d_cnt.ensure(n));
+    HIPCHK(top->d_bslot.ensure(n));
+    HIPCHK(top->d_par.ensure(n));
+    HIPCHK(top->d_pathbuf.ensure((size_t)want * kMaxHops * kSsspBlock));
+    HIPCHK(top->d_counters.ensure((size_t)want * 4));
+    HIPCHK(hipMemsetAsync(top->d_stamp.p, 0, sizeof(uint32_t) * n, top->stream));
+    HIPCHK(hipMemsetAsync(top->d_fstamp.p, 0, sizeof(uint32_t) * n, top->stream));
+    HIPCHK(hipMemsetAsync(top->d_memo.p, 0, sizeof(unsigned long long) * n, top->stream));
+    HIPCHK(hipMemsetAsync(top->d_counters.p, 0, sizeof(uint32_t) * (size_t)want * 4, top->stream));
+    HIPCHK(hipStreamSynchronize(top->stream));
+    top->slots = want;
+    return 0;
+}
+
+SlotWs slot_ws(Topology* top) {
+    SlotWs w;
+    w.slots = top->slots;
+    w.V = top->g.V;
+    w.dist = top->d_dist.p; w.stamp = top->d_stamp.p; w.fstamp = top->d_fstamp.p;
+    w.qa = top->d_qa.p; w.qb = top->d_qb.p; w.far = top->d_far.p;
+    w.best = top->d_best.p; w.cnt = top->d_cnt.p; w.bslot = top->d_bslot.p;
+    w.memo = top->d_memo.p; w.par = top->d_par.p; w.pathbuf = top->d_pathbuf.p;
+    w.counters = top->d_counters.p;
+    return w;
+}
+
+// columns = distinct attached vertices in ascending vertex order
+void compute_geometry(Topology* top) {
+    std::vector<int32_t> vs;
+    {
+        std::shared_lock<std::shared_mutex> lk(top->ipMu);
+        vs.reserve(top->virtualIP.size());
+        for (auto& kv : top->virtualIP)
+            if (kv.second >= 0) vs.push_back(kv.second);
+    }
+    std::sort(vs.begin(), vs.end());
+    vs.erase(std::unique(vs.begin(), vs.end()), vs.end());
+    top->attached = vs;
+    top->A = (int64_t)vs.size();
+    top->colOf.assign((size_t)top->g.V, -1);
+    for (size_t i = 0; i < vs.size(); i++) top->colOf[(size_t)vs[i]] = (int32_t)i;
+    // complete branch materialisation bits are per (attached pair)
+    top->matPairWords = (size_t)((top->A * top->A + 63) / 64);
+    top->matPair.reset(new std::atomic<uint64_t>[top->matPairWords ? top->matPairWords : 1]);
+    for (size_t i = 0; i < top->matPairWords; i++) top->matPair[i].store(0);
+}
+
+double default_delta(Topology* top) {
+    if (top->delta > 0) return top->delta;
+    const HostGraph& g = top->g;
+    double s = 0;
+    int64_t n = 0;
+    for (int64_t e = 0; e < g.E; e++)
+        if (g.eu[(size_t)e] != g.ev[(size_t)e]) { s += g.elat[(size_t)e]; n++; }
+    double mean = n ? s / (double)n : 1.0;
+    return std::max(1e-9, 0.25 * mean);
+}
+
+// Enqueue rows [row0,row1) into out buffers (device pointers) on `st`.
+int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uint16_t* out_hops,
+                 double* out_rowmin, hipStream_t st) {
+    const int64_t A = top->A;
+    const int64_t rows = row1 - row0;
+    if (rows <= 0 || A <= 0) return 0;
+    HIPCHK(hipMemsetAsync(top->d_stats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
+    HIPCHK(launch_fill_u64(top->d_stats.p + ST_GLOBAL_MIN, 0x7FF0000000000000ull, 1, st));
+    if (top->isComplete) {
+        // dense A x A direct-edge matrices (lowest edge id wins, as orc_get_eid)
+        std::vector<double> elat((size_t)(A * A), -1.0), eloss((size_t)(A * A), 0.0), vl((size_t)A);
+        const HostGraph& g = top->g;
+        for (int64_t e = 0; e < g.E; e++) {
+            int32_t ca = top->colOf[(size_t)g.eu[(size_t)e]], cb = top->colOf[(size_t)g.ev[(size_t)e]];
+            if (ca < 0 || cb < 0) continue;
+            size_t k1 = (size_t)ca * (size_t)A + (size_t)cb;
+            if (elat[k1] < 0) { elat[k1] = g.elat[(size_t)e]; eloss[k1] = g.eloss[(size_t)e]; }
+            if (!g.directed) {
+                size_t k2 = (size_t)cb * (size_t)A + (size_t)ca;
+                if (elat[k2] < 0) { elat[k2] = g.elat[(size_t)e]; eloss[k2] = g.eloss[(size_t)e]; }
+            }
+        }
+        for (int64_t i = 0; i < A; i++) vl[(size_t)i] = g.vloss[(size_t)top->attached[(size_t)i]];
+        HIPCHK(top->d_elatAA.ensure((size_t)(A * A)));
+        HIPCHK(top->d_elossAA.ensure((size_t)(A * A)));
+        HIPCHK(top->d_vlossA.ensure((size_t)A));
+        HIPCHK(hipMemcpyAsync(top->d_elatAA.p, elat.data(), sizeof(double) * (size_t)(A * A), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(top->d_elossAA.p, eloss.data(), sizeof(double) * (size_t)(A * A), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(top->d_vlossA.p, vl.data(), sizeof(double) * (size_t)A, hipMemcpyHostToDevice, st));
+        HIPCHK(hipEventRecord(top->ev0, st));
+        HIPCHK(launch_pair_table_complete((int)A, row0, rows, top->d_elatAA.p, top->d_elossAA.p,
+                                          top->d_vlossA.p, out_lr, out_hops, out_rowmin,
+                                          top->d_stats.p, st));
+        HIPCHK(hipEventRecord(top->ev1, st));
+        // the host vectors must outlive the async copies
+        HIPCHK(hipStreamSynchronize(st));
+    } else {
+        if (top->isDirected) {
+            CRITICAL("directed non-complete topologies are not supported by the GPU SSSP yet");
+            return -3;
+        }
+        int r = upload_csr(top);
+        if (r) return r;
+        r = ensure_workspace(top, (int)rows);
+        if (r) return r;
+        std::vector<uint32_t> src((size_t)rows), tgt((size_t)A);
+        for (int64_t i = 0; i < rows; i++) src[(size_t)i] = (uint32_t)top->inv[(size_t)top->attached[(size_t)(row0 + i)]];
+        for (int64_t i = 0; i < A; i++) tgt[(size_t)i] = (uint32_t)top->inv[(size_t)top->attached[(size_t)i]];
+        HIPCHK(top->d_sources.ensure((size_t)rows));
+        HIPCHK(top->d_targets.ensure((size_t)A));
+        HIPCHK(hipMemcpyAsync(top->d_sources.p, src.data(), sizeof(uint32_t) * (size_t)rows, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(top->d_targets.p, tgt.data(), sizeof(uint32_t) * (size_t)A, hipMemcpyHostToDevice, st));
+        HIPCHK(hipEventRecord(top->ev0, st));
+        HIPCHK(launch_sssp_rows(dev_csr(top), slot_ws(top), top->d_sources.p, (int)rows,
+                                top->d_targets.p, (int)A, default_delta(top), out_lr, out_hops,
+                                out_rowmin, top->d_stats.p, st));
+        HIPCHK(hipEventRecord(top->ev1, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    top->rowsPending = true;
+    top->stats.sources = rows;
+    top->stats.targets = A;
+    return 0;
+}
+
+int collect_row_stats(Topology* top) {
+    if (!top->rowsPending) return 0;
+    HIPCHK(hipEventSynchronize(top->ev1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, top->ev0, top->ev1));
+    unsigned long long h[ST_COUNT];
+    HIPCHK(hipMemcpy(h, top->d_stats.p, sizeof h, hipMemcpyDeviceToHost));
+    top->stats.sssp_kernel_ms = ms;
+    top->stats.build_ms = ms;
+    top->stats.ambiguous_pairs = (int64_t)h[ST_AMBIGUOUS];
+    top->stats.relaxations = (int64_t)h[ST_RELAX];
+    top->stats.long_paths = (int64_t)h[ST_LONGPATH];
+    top->stats.errors = (int64_t)h[ST_ERRORS];
+    double gm;
+    memcpy(&gm, &h[ST_GLOBAL_MIN], sizeof gm);
+    top->eagerMin = std::isinf(gm) ? -1.0 : gm;
+    if (h[ST_OVERFLOW]) CRITICAL("SSSP queue overflow / iteration guard (code %llu)", h[ST_OVERFLOW]);
+    if (top->stats.ambiguous_pairs)
+        WARNING("%lld pairs cross a parent tie (equal d[u]): igraph's heap pop order decides them "
+                "in the reference; the lowest adjacency slot is used here",
+                (long long)top->stats.ambiguous_pairs);
+    top->rowsPending = false;
+    return (h[ST_OVERFLOW] ? -4 : 0);
+}
+
+void push_min_to_engine(double m) {
+    if (worker_updateMinTimeJump && m > 0) worker_updateMinTimeJump(m);
+}
+
+// whole-table build on this GPU
+int ensure_table(Topology* top) {
+    if (top->tableValid.load(std::memory_order_acquire)) return 0;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    if (top->tableValid.load()) return 0;
+    int r = dev_init(top);
+    if (r) return r;
+    compute_geometry(top);
+    const int64_t A = top->A;
+    if (A == 0) {
+        top->tableValid.store(true);
+        return 0;
+    }
+    HIPCHK(top->d_lr.ensure((size_t)(A * A)));
+    HIPCHK(top->d_hops.ensure((size_t)(A * A)));
+    HIPCHK(top->d_rowmin.ensure((size_t)A));
+    r = enqueue_rows(top, 0, A, top->d_lr.p, top->d_hops.p, top->d_rowmin.p, top->stream);
+    if (r) return r;
+    r = collect_row_stats(top);
+    if (r) return r;
+    if (top->stats.errors) {
+        CRITICAL("%lld attached pairs have no path/edge (e.g. a vertex without self loop)",
+                 (long long)top->stats.errors);
+    }
+    top->hostValid.store(false);
+    top->tableValid.store(true, std::memory_order_release);
+    if (!top->lazy) push_min_to_engine(top->eagerMin);
+    return 0;
+}
+
+int ensure_host(Topology* top) {
+    int r = ensure_table(top);
+    if (r) return r;
+    if (top->hostValid.load(std::memory_order_acquire)) return 0;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    if (top->hostValid.load()) return 0;
+    const size_t n = (size_t)(top->A * top->A);
+    std::vector<double2> lr(n);
+    top->hhops.resize(n);
+    top->hrowmin.resize((size_t)top->A);
+    if (n) {
+        HIPCHK(hipMemcpy(lr.data(), top->d_lr.p, sizeof(double2) * n, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(top->hhops.data(), top->d_hops.p, sizeof(uint16_t) * n, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(top->hrowmin.data(), top->d_rowmin.p, sizeof(double) * (size_t)top->A, hipMemcpyDeviceToHost));
+    }
+    top->hlat.resize(n);
+    top->hrel.resize(n);
+    for (size_t i = 0; i < n; i++) {
+        top->hlat[i] = lr[i].x;
+        top->hrel[i] = lr[i].y;
+    }
+    top->hostValid.store(true, std::memory_order_release);
+    return 0;
+}
+
+int32_t vertex_of_ip(Topology* top, uint32_t ip) {
+    std::shared_lock<std::shared_mutex> lk(top->ipMu);
+    auto it = top->virtualIP.find(ip);
+    return it == top->virtualIP.end() ? -1 : it->second;
+}
+
+void lazy_store_min(Topology* top, double lat) {
+    // shd-topology.c:500-511: if (min == 0 || lat < min) { min = lat; push }
+    std::lock_guard<std::mutex> lk(top->minMu);
+    if (top->lazyMin == 0 || lat < top->lazyMin) {
+        top->lazyMin = lat;
+        push_min_to_engine(lat);
+    }
+}
+
+// _topology_getPathEntry (shd-topology.c:876-938) over the prebuilt table
+bool get_path_entry(Topology* top, uint32_t srcIP, uint32_t dstIP, double* lat, double* rel) {
+    int32_t s = vertex_of_ip(top, srcIP);
+    if (s < 0) {
+        CRITICAL("invalid vertex %d, source address is not connected to topology", s);
+        return false;
+    }
+    int32_t d = vertex_of_ip(top, dstIP);
+    if (d < 0) {
+        CRITICAL("invalid vertex %d, destination address is not connected to topology", d);
+        return false;
+    }
+    int r = ensure_host(top);
+    if (r) {
+        fatal_or_continue(top, "unable to build the routing table");
+        return false;
+    }
+    const int64_t A = top->A;
+    int64_t cs = top->colOf[(size_t)s], cd = top->colOf[(size_t)d];
+    size_t k;
+    if (top->isComplete) {
+        k = (size_t)(cs * A + cd);
+        if (top->lazy) {
+            // per-pair cache: first touch of (s,d) (or (d,s) if undirected) stores the pair
+            size_t b1 = k, b2 = (size_t)(cd * A + cs);
+            bool have = (top->matPair[b1 >> 6].load(std::memory_order_relaxed) >> (b1 & 63)) & 1;
+            if (!have && !top->isDirected)
+                have = (top->matPair[b2 >> 6].load(std::memory_order_relaxed) >> (b2 & 63)) & 1;
+            if (!have) {
+                uint64_t old = top->matPair[b1 >> 6].fetch_or(1ull << (b1 & 63));
+                if (!((old >> (b1 & 63)) & 1) && top->hlat[k] > 0) lazy_store_min(top, top->hlat[k]);
+            }
+        }
+    } else if (!top->lazy) {
+        k = (size_t)(cs * A + cd);
+    } else {
+        // first-rooted-wins: row s if materialised, else row d (undirected)
+        if (top->matRow[(size_t)s].load(std::memory_order_acquire)) {
+            k = (size_t)(cs * A + cd);
+        } else if (!top->isDirected && top->matRow[(size_t)d].load(std::memory_order_acquire)) {
+            k = (size_t)(cd * A + cs);
+        } else {
+            uint8_t was = top->matRow[(size_t)s].exchange(1);
+            if (!was && top->hrowmin[(size_t)cs] > 0 && !std::isinf(top->hrowmin[(size_t)cs]))
+                lazy_store_min(top, top->hrowmin[(size_t)cs]);
+            k = (size_t)(cs * A + cd);
+        }
+    }
+    double L = top->hlat[k], R = top->hrel[k];
+    if (L < 0) {
+        // the reference error()s: "unable to find path between node ..." (shd-topology.c:924)
+        fatal_or_continue(top, "unable to find path between attached vertices");
+        return false;
+    }
+    if (lat) *lat = L;
+    if (rel) *rel = R;
+    return true;
+}
+
+// _topology_findAttachmentVertex (shd-topology.c:1068-1152) over the candidate index.
+// draw(): one random_nextDouble on the host's stream.
+template <class Draw>
+int32_t find_attachment_vertex(Topology* top, const char* ipHint, const char* geocodeHint,
+                               const char* typeHint, Draw&& draw) {
+    const AttachIndex& ix = top->aidx;
+    const uint32_t requested = ipHint ? string_to_ip(ipHint) : 0xFFFFFFFFu;
+    auto lower = [](const char* s) {
+        std::string o(s);
+        for (auto& c : o) if (c >= 'A' && c <= 'Z') c = (char)(c - 'A' + 'a');
+        return o;
+    };
+    const std::vector<int32_t>* cands = nullptr;
+    std::vector<int32_t> exact;
+    bool foundExact = false;
+    if (ipHint && requested != 0xFFFFFFFFu && requested != 0u) {
+        auto it = ix.byIP.find(requested);
+        if (it != ix.byIP.end() && !it->second.empty()) {
+            foundExact = true;
+            cands = &it->second;  // all matches, vertex order (queues cleared at first match)
+        }
+    }
+    static const std::vector<int32_t> kEmpty;
+    bool useLPM = false;
+    if (!foundExact) {
+        auto count_ips = [&](const std::vector<int32_t>& l) {
+            for (int32_t v : l) if (ix.usable[(size_t)v]) return true;
+            return false;
+        };
+        const std::vector<int32_t>* tc = &kEmpty;
+        const std::vector<int32_t>* ty = &kEmpty;
+        const std::vector<int32_t>* co = &kEmpty;
+        if (typeHint) {
+            auto it = ix.byType.find(lower(typeHint));
+            if (it != ix.byType.end()) ty = &it->second;
+        }
+        if (geocodeHint) {
+            auto it = ix.byCode.find(lower(geocodeHint));
+            if (it != ix.byCode.end()) co = &it->second;
+        }
+        if (typeHint && geocodeHint) {
+            auto it = ix.byTypeCode.find(lower(typeHint) + '\x01' + lower(geocodeHint));
+            if (it != ix.byTypeCode.end()) tc = &it->second;
+        }
+        if (!tc->empty()) cands = tc;
+        else if (!ty->empty()) cands = ty;
+        else if (!co->empty()) cands = co;
+        else cands = &ix.all;
+        useLPM = ipHint && count_ips(*cands);
+    }
+    if (!cands || cands->empty()) {
+        CRITICAL("no attachment candidates (no vertex id contains \"poi\")");
+        return -1;
+    }
+    if (useLPM && !foundExact) {
+        uint32_t bestMatch = 0;
+        int32_t best = -1;
+        for (int32_t v : *cands) {
+            uint32_t m = ix.ip[(size_t)v] & requested;
+            if (m > bestMatch) { bestMatch = m; best = v; }
+        }
+        return best;
+    }
+    double r = draw();
+    int indexRange = (int)cands->size() - 1;
+    int chosen = (int)round((double)(indexRange * r));
+    return (*cands)[(size_t)chosen];
+}
+
+void do_attach(Topology* top, uint32_t ip, int32_t v, uint64_t* bwDownOut, uint64_t* bwUpOut) {
+    {
+        std::unique_lock<std::shared_mutex> lk(top->ipMu);
+        top->virtualIP[ip] = v;
+    }
+    if (v >= 0) {
+        if (bwUpOut) *bwUpOut = (uint64_t)top->g.vbwup[(size_t)v];
+        if (bwDownOut) *bwDownOut = (uint64_t)top->g.vbwdown[(size_t)v];
+        // an attach onto a vertex outside the current columns invalidates the table
+        if (top->tableValid.load() && ((size_t)v >= top->colOf.size() || top->colOf[(size_t)v] < 0)) {
+            std::lock_guard<std::mutex> lk(top->buildMu);
+            top->tableValid.store(false);
+            top->hostValid.store(false);
+        }
+    }
+}
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" {
+
+int shdtopo_version(void) { return 10000; }
+
+Topology* topology_new(const char* graphPath) {
+    if (!graphPath) return nullptr;
+    Topology* top = new Topology();
+    std::string err;
+    MESSAGE("reading graphml topology graph at '%s'...", graphPath);
+    if (!graphml_load_file(graphPath, top->g, err)) {
+        CRITICAL("reading graphml topology '%s' failed: %s", graphPath, err.c_str());
+        delete top;
+        return nullptr;
+    }
+    return finish_new(top);
+}
+
+Topology* shdtopo_new_from_buffer(const char* graphml, size_t len) {
+    if (!graphml) return nullptr;
+    Topology* top = new Topology();
+    std::string err;
+    if (!graphml_parse(graphml, len, top->g, err)) {
+        CRITICAL("parsing graphml buffer failed: %s", err.c_str());
+        delete top;
+        return nullptr;
+    }
+    return finish_new(top);
+}
+
+Topology* shdtopo_new_synthetic(const ShdSynthParams* p) {
+    if (!p) return nullptr;
+    Topology* top = new Topology();
+    SynthParams sp{p->seed, p->n_routers, p->n_poi, p->n_edges, p->integer_latency,
+                   p->alpha > 0 ? p->alpha : 1.0 / 1.1};
+    std::string err;
+    if (!synth_graph(sp, top->g, err)) {
+        CRITICAL("synthetic topology: %s", err.c_str());
+        delete top;
+        return nullptr;
+    }
+    return finish_new(top);
+}
+
+void topology_free(Topology* top) {
+    if (!top) return;
+    if (top->devInit) {
+        (void)hipStreamSynchronize(top->stream);
+        (void)hipEventDestroy(top->ev0);
+        (void)hipEventDestroy(top->ev1);
+        (void)hipEventDestroy(top->ev2);
+        (void)hipEventDestroy(top->ev3);
+        (void)hipStreamDestroy(top->stream);
+    }
+    delete top;
+}
+
+int shdtopo_set_option(Topology* top, const char* key, double value) {
+    if (!top || !key) return -1;
+    std::string k(key);
+    if (k == "abort_on_error") top->abortOnError = value != 0;
+    else if (k == "lazy") top->lazy = value != 0;
+    else if (k == "delta") top->delta = value;
+    else if (k == "slots") top->slotsOpt = (int)value;
+    else if (k == "device") top->device = (int)value;
+    else return -1;
+    return 0;
+}
+
+void topology_attach(Topology* top, Address* address, Random* randomSourcePool, char* ipHint,
+                     char* geocodeHint, char* typeHint, uint64_t* bwDownOut, uint64_t* bwUpOut) {
+    if (!top || !address) return;
+    if (!address_toNetworkIP || !random_nextDouble) {
+        fatal_or_continue(top, "Shadow symbols address_toNetworkIP/random_nextDouble not found "
+                               "(link into shadow or preload libshdtopo_shim.so)");
+        return;
+    }
+    uint32_t ip = address_toNetworkIP(address);
+    int32_t v = find_attachment_vertex(top, ipHint, geocodeHint, typeHint,
+                                       [&]() { return random_nextDouble(randomSourcePool); });
+    do_attach(top, ip, v, bwDownOut, bwUpOut);
+}
+
+int32_t shdtopo_attach_ip(Topology* top, uint32_t ip, uint32_t* rngState, const char* ipHint,
+                          const char* geocodeHint, const char* typeHint, uint64_t* bwDownOut,
+                          uint64_t* bwUpOut) {
+    if (!top || !rngState) return -1;
+    int32_t v = find_attachment_vertex(top, ipHint, geocodeHint, typeHint,
+                                       [&]() { return rand_r_double(rngState); });
+    do_attach(top, ip, v, bwDownOut, bwUpOut);
+    return v;
+}
+
+void topology_detach(Topology* top, Address* address) {
+    if (!top || !address || !address_toNetworkIP) return;
+    uint32_t ip = address_toNetworkIP(address);
+    std::unique_lock<std::shared_mutex> lk(top->ipMu);
+    top->virtualIP.erase(ip);
+}
+
+double shdtopo_get_latency_ip(Topology* top, uint32_t srcIP, uint32_t dstIP) {
+    double l = 0;
+    if (top && get_path_entry(top, srcIP, dstIP, &l, nullptr)) return l;
+    return -1.0;
+}
+
+double shdtopo_get_reliability_ip(Topology* top, uint32_t srcIP, uint32_t dstIP) {
+    double r = 0;
+    if (top && get_path_entry(top, srcIP, dstIP, nullptr, &r)) return r;
+    return -1.0;
+}
+
+double topology_getLatency(Topology* top, Address* srcAddress, Address* dstAddress) {
+    if (!top || !srcAddress || !dstAddress || !address_toNetworkIP) return -1.0;
+    return shdtopo_get_latency_ip(top, address_toNetworkIP(srcAddress), address_toNetworkIP(dstAddress));
+}
+
+double topology_getReliability(Topology* top, Address* srcAddress, Address* dstAddress) {
+    if (!top || !srcAddress || !dstAddress || !address_toNetworkIP) return -1.0;
+    return shdtopo_get_reliability_ip(top, address_toNetworkIP(srcAddress), address_toNetworkIP(dstAddress));
+}
+
+int topology_isRoutable(Topology* top, Address* srcAddress, Address* dstAddress) {
+    return topology_getLatency(top, srcAddress, dstAddress) > -1;
+}
+
+double topology_getMinimumLatency(Topology* top) {
+    if (!top) return -1.0;
+    if (ensure_table(top)) return -1.0;
+    return top->eagerMin;
+}
+
+double shdtopo_get_lazy_minimum_latency(Topology* top) {
+    if (!top) return -1.0;
+    std::lock_guard<std::mutex> lk(top->minMu);
+    return top->lazyMin;
+}
+
+int64_t shdtopo_num_vertices(Topology* top) { return top ? top->g.V : -1; }
+int64_t shdtopo_num_edges(Topology* top) { return top ? top->g.E : -1; }
+int shdtopo_is_complete(Topology* top) { return top ? (int)top->isComplete : -1; }
+int shdtopo_is_directed(Topology* top) { return top ? (int)top->isDirected : -1; }
+
+int64_t shdtopo_num_attached(Topology* top) {
+    if (!top) return -1;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    if (!top->tableValid.load()) compute_geometry(top);
+    return top->A;
+}
+
+int64_t shdtopo_attached_vertices(Topology* top, int32_t* out, int64_t cap) {
+    if (!top) return -1;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    if (!top->tableValid.load()) compute_geometry(top);
+    int64_t n = std::min<int64_t>(cap, top->A);
+    for (int64_t i = 0; i < n; i++) out[i] = top->attached[(size_t)i];
+    return top->A;
+}
+
+int32_t shdtopo_vertex_of_ip(Topology* top, uint32_t ip) { return top ? vertex_of_ip(top, ip) : -1; }
+
+int32_t shdtopo_column_of_ip(Topology* top, uint32_t ip) {
+    if (!top) return -1;
+    int32_t v = vertex_of_ip(top, ip);
+    if (v < 0) return -1;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    if (!top->tableValid.load() && (top->colOf.size() != (size_t)top->g.V || top->colOf[(size_t)v] < 0))
+        compute_geometry(top);
+    return top->colOf[(size_t)v];
+}
+
+int shdtopo_build(Topology* top) {
+    if (!top) return -1;
+    return ensure_table(top);
+}
+
+int shdtopo_build_rows(Topology* top, int64_t row0, int64_t row1, void* d_lr, void* d_hops,
+                       void* d_rowmin, void* stream) {
+    if (!top || !d_lr || !d_hops) return -1;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    int r = dev_init(top);
+    if (r) return r;
+    compute_geometry(top);
+    if (row0 < 0 || row1 > top->A || row0 > row1) return -2;
+    hipStream_t st = stream ? (hipStream_t)stream : top->stream;
+    r = enqueue_rows(top, row0, row1, (double2*)d_lr, (uint16_t*)d_hops, (double*)d_rowmin, st);
+    if (r) return r;
+    return collect_row_stats(top);
+}
+
+int shdtopo_bind_table(Topology* top, const void* d_lr, const void* d_hops, double globalMin,
+                       void* stream) {
+    if (!top || !d_lr || !d_hops) return -1;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    int r = dev_init(top);
+    if (r) return r;
+    compute_geometry(top);
+    const size_t n = (size_t)(top->A * top->A);
+    hipStream_t st = stream ? (hipStream_t)stream : top->stream;
+    HIPCHK(top->d_lr.ensure(n));
+    HIPCHK(top->d_hops.ensure(n));
+    HIPCHK(top->d_rowmin.ensure((size_t)top->A));
+    HIPCHK(hipMemcpyAsync(top->d_lr.p, d_lr, sizeof(double2) * n, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(top->d_hops.p, d_hops, sizeof(uint16_t) * n, hipMemcpyDeviceToDevice, st));
+    if (top->A) HIPCHK(launch_row_min(top->A, top->A, top->d_lr.p, top->d_rowmin.p, st));
+    HIPCHK(hipStreamSynchronize(st));
+    top->eagerMin = globalMin;
+    top->hostValid.store(false);
+    top->tableValid.store(true);
+    return 0;
+}
+
+int shdtopo_table_to_host(Topology* top, double* lat, double* rel, uint16_t* hops) {
+    if (!top) return -1;
+    int r = ensure_host(top);
+    if (r) return r;
+    const size_t n = (size_t)(top->A * top->A);
+    if (lat) memcpy(lat, top->hlat.data(), sizeof(double) * n);
+    if (rel) memcpy(rel, top->hrel.data(), sizeof(double) * n);
+    if (hops) memcpy(hops, top->hhops.data(), sizeof(uint16_t) * n);
+    return 0;
+}
+
+int shdtopo_route_batch_device(Topology* top, const int32_t* d_srcCol, const int32_t* d_dstCol,
+                               const uint32_t* d_payload, const uint32_t* d_stateIn,
+                               const uint64_t* d_now, int64_t n, uint64_t jumpNs, int clamp,
+                               uint64_t* d_time, uint32_t* d_stateOut, uint8_t* d_delivered,
+                               void* stream) {
+    if (!top) return -1;
+    int r = ensure_table(top);
+    if (r) return r;
+    hipStream_t st = stream ? (hipStream_t)stream : top->stream;
+    HIPCHK(hipEventRecord(top->ev2, st));
+    HIPCHK(launch_packet_route(n, d_srcCol, d_dstCol, d_payload, d_stateIn, d_now, top->d_lr.p,
+                               top->A, jumpNs, clamp, d_time, d_stateOut, d_delivered, st));
+    HIPCHK(hipEventRecord(top->ev3, st));
+    top->routePending = true;
+    return 0;
+}
+
+int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketOut* out, size_t n,
+                              uint64_t jumpNs, int clampInterHost) {
+    if (!top || (!in && n) || (!out && n)) return -1;
+    int r = ensure_table(top);
+    if (r) return r;
+    if (n == 0) return 0;
+    std::vector<int32_t> sc(n), dc(n);
+    std::vector<uint32_t> pay(n), sin(n), sout(n);
+    std::vector<uint64_t> now(n), tim(n);
+    std::vector<uint8_t> dl(n);
+    {
+        std::shared_lock<std::shared_mutex> lk(top->ipMu);
+        for (size_t i = 0; i < n; i++) {
+            auto a = top->virtualIP.find(in[i].srcIP);
+            auto b = top->virtualIP.find(in[i].dstIP);
+            if (a == top->virtualIP.end() || b == top->virtualIP.end() || a->second < 0 || b->second < 0) {
+                CRITICAL("packet %zu: address is not connected to the topology", i);
+                return -2;
+            }
+            sc[i] = top->colOf[(size_t)a->second];
+            dc[i] = top->colOf[(size_t)b->second];
+            pay[i] = in[i].payloadLength;
+            sin[i] = in[i].rngState;
+            now[i] = in[i].now;
+        }
+    }
+    hipStream_t st = top->stream;
+    HIPCHK(top->b_src.ensure(n)); HIPCHK(top->b_dst.ensure(n)); HIPCHK(top->b_pay.ensure(n));
+    HIPCHK(top->b_sin.ensure(n)); HIPCHK(top->b_sout.ensure(n)); HIPCHK(top->b_now.ensure(n));
+    HIPCHK(top->b_time.ensure(n)); HIPCHK(top->b_dl.ensure(n));
+    HIPCHK(hipMemcpyAsync(top->b_src.p, sc.data(), 4 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(top->b_dst.p, dc.data(), 4 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(top->b_pay.p, pay.data(), 4 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(top->b_sin.p, sin.data(), 4 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(top->b_now.p, now.data(), 8 * n, hipMemcpyHostToDevice, st));
+    r = shdtopo_route_batch_device(top, top->b_src.p, top->b_dst.p, top->b_pay.p, top->b_sin.p,
+                                   top->b_now.p, (int64_t)n, jumpNs, clampInterHost, top->b_time.p,
+                                   top->b_sout.p, top->b_dl.p, st);
+    if (r) return r;
+    HIPCHK(hipMemcpyAsync(tim.data(), top->b_time.p, 8 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(sout.data(), top->b_sout.p, 4 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(dl.data(), top->b_dl.p, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (size_t i = 0; i < n; i++) {
+        out[i].time = tim[i];
+        out[i].rngState = sout[i];
+        out[i].delivered = dl[i];
+        out[i]._pad[0] = out[i]._pad[1] = out[i]._pad[2] = 0;
+    }
+    return 0;
+}
+
+int shdtopo_get_stats(Topology* top, ShdStats* out) {
+    if (!top || !out) return -1;
+    int r = collect_row_stats(top);
+    if (r) return r;
+    if (top->routePending) {
+        HIPCHK(hipEventSynchronize(top->ev3));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, top->ev2, top->ev3));
+        top->stats.route_kernel_ms = ms;
+        top->routePending = false;
+    }
+    *out = top->stats;
+    return 0;
+}
+
+int shdtopo_write_graphml(Topology* top, const char* path) {
+    if (!top || !path) return -1;
+    return graphml_write_file(top->g, path) ? 0 : -1;
+}
+
+int shdtopo_synth_packets(Topology* top, uint64_t seed, int64_t n_hosts, int64_t n_packets,
+                          uint64_t t0, uint64_t jump, int32_t* srcCol, int32_t* dstCol,
+                          uint32_t* payload, uint32_t* stateIn, uint64_t* now, uint32_t* srcIP,
+                          uint32_t* dstIP) {
+    if (!top || n_hosts < 2) return -1;
+    // seed chain: master Random(seed) -> slave seed = rand_r(master) ->
+    // per-host nodeSeed = rand_r(slave) (shd-master.c:65,134; shd-create-node.c:216)
+    uint32_t master = (uint32_t)seed;
+    uint32_t slave = (uint32_t)glibc_rand_r(&master);
+    std::vector<uint32_t> hostState((size_t)n_hosts), hostIP((size_t)n_hosts);
+    std::vector<int32_t> hostVertex((size_t)n_hosts);
+    std::vector<int> role((size_t)n_hosts);
+    static const char* kRole[] = {"client", "relay", "server"};
+    std::vector<int64_t> relays, servers;
+    for (int64_t h = 0; h < n_hosts; h++) {
+        int64_t m = h % 100;
+        role[(size_t)h] = m < 94 ? 0 : (m < 99 ? 1 : 2);
+        if (role[(size_t)h] == 1) relays.push_back(h);
+        if (role[(size_t)h] == 2) servers.push_back(h);
+        hostState[(size_t)h] = (uint32_t)glibc_rand_r(&slave);
+        hostIP[(size_t)h] = htonl(0x0B000001u + (uint32_t)h);
+        hostVertex[(size_t)h] = shdtopo_attach_ip(top, hostIP[(size_t)h], &hostState[(size_t)h],
+                                                  nullptr, nullptr, kRole[role[(size_t)h]],
+                                                  nullptr, nullptr);
+        if (hostVertex[(size_t)h] < 0) return -2;
+    }
+    if (relays.empty()) relays.push_back(0);
+    if (servers.empty()) servers = relays;
+    {
+        std::lock_guard<std::mutex> lk(top->buildMu);
+        if (!top->tableValid.load()) compute_geometry(top);
+    }
+    SplitMix rng(seed ^ 0x5eed5eed5eedull);
+    for (int64_t k = 0; k < n_packets; k++) {
+        int64_t s = (int64_t)rng.below((uint64_t)n_hosts);
+        int64_t d;
+        do {
+            int rl = role[(size_t)s];
+            if (rl == 0 || rl == 2) d = relays[(size_t)rng.below(relays.size())];
+            else d = (rng.below(2) == 0) ? relays[(size_t)rng.below(relays.size())]
+                                         : servers[(size_t)rng.below(servers.size())];
+        } while (d == s && n_hosts > 1 && relays.size() + servers.size() > 1);
+        srcCol[k] = top->colOf[(size_t)hostVertex[(size_t)s]];
+        dstCol[k] = top->colOf[(size_t)hostVertex[(size_t)d]];
+        payload[k] = rng.uniform() < 0.8 ? 1448u : 0u;
+        stateIn[k] = hostState[(size_t)s];
+        (void)glibc_rand_r(&hostState[(size_t)s]);  // the route's draw advances the host stream
+        now[k] = t0 + (jump ? rng.below(jump) : 0);
+        if (srcIP) srcIP[k] = hostIP[(size_t)s];
+        if (dstIP) dstIP[k] = hostIP[(size_t)d];
+    }
+    return 0;
+}
+
+}  // extern "C"

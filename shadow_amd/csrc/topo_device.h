@@ -1,0 +1,87 @@
+// topo_device.h -- device data layout and kernel launchers (implemented in topo_kernels.hip).
+//
+// HBM layout (all arrays in the degree-relabelled vertex order, see DESIGN.md "Data layout"):
+//   CSR of the undirected topology without self loops:
+//     rowptr u32[V+1], col u32[2E'], wt f64[2E'] (edge latency), aloss f64[2E'] (edge loss)
+//   per vertex: vloss f64[V], selfLat f64[V] (NaN = no self loop), selfLoss f64[V]
+//   per SSSP slot (one workgroup = one source at a time): 56 B x V of workspace
+//   routing table: {f64 lat, f64 rel}[A][A] (16-B records, one gather per packet) + u16 hops
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace shdtopo {
+
+constexpr int kSsspBlock = 1024;  // threads per SSSP workgroup (16 waves)
+constexpr int kMaxHops = 48;      // per-thread path buffer depth (longer paths: O(h^2) walk)
+
+// indices into the device stats block (unsigned long long[16])
+enum StatIdx {
+    ST_GLOBAL_MIN = 0,  // f64 bits of the min latency over every computed pair
+    ST_AMBIGUOUS = 1,   // pairs whose parent chain crosses a d-tied parent
+    ST_RELAX = 2,       // edge relaxations attempted
+    ST_LONGPATH = 3,    // pairs longer than kMaxHops
+    ST_ERRORS = 4,      // pairs with a missing edge / unreachable target
+    ST_DEQUEUE = 5,     // next source to take (persistent workgroups)
+    ST_OVERFLOW = 6,    // queue overflow / iteration guard tripped
+    ST_COUNT = 16
+};
+
+struct DevCSR {
+    int32_t V = 0;
+    int64_t nadj = 0;
+    const uint32_t* rowptr = nullptr;
+    const uint32_t* col = nullptr;
+    const double* wt = nullptr;
+    const double* aloss = nullptr;
+    const double* vloss = nullptr;
+    const double* selfLat = nullptr;
+    const double* selfLoss = nullptr;
+};
+
+// per-slot workspace, slot-major: array + slot * V
+struct SlotWs {
+    int slots = 0;
+    int64_t V = 0;
+    unsigned long long* dist = nullptr;  // f64 bits, +inf = unreached
+    uint32_t* stamp = nullptr;           // near-queue / chain-queue dedupe (iteration id)
+    uint32_t* fstamp = nullptr;          // far-pile dedupe (far epoch)
+    uint32_t* qa = nullptr;
+    uint32_t* qb = nullptr;
+    uint32_t* far = nullptr;
+    unsigned long long* best = nullptr;  // parent pass: min d[u] over candidates
+    uint32_t* cnt = nullptr;             // parent pass: candidates at the min
+    uint32_t* bslot = nullptr;           // parent pass: lowest adjacency slot at the min
+    unsigned long long* memo = nullptr;  // (source epoch << 32) | ambiguous << 31 | slot
+    uint32_t* par = nullptr;             // parent vertex
+    uint32_t* pathbuf = nullptr;         // [slot][kMaxHops][kSsspBlock]
+    uint32_t* counters = nullptr;        // [slot][4]: iteration id, far epoch, source epoch
+};
+
+hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
+                            int nsrc, const uint32_t* d_targets, int A, double delta,
+                            double2* out_lr, uint16_t* out_hops, double* out_rowmin,
+                            unsigned long long* d_stats, hipStream_t stream);
+
+hipError_t launch_pair_table_complete(int A, int64_t row0, int64_t rows, const double* elatAA,
+                                      const double* elossAA, const double* vlossA, double2* out_lr,
+                                      uint16_t* out_hops, double* out_rowmin,
+                                      unsigned long long* d_stats, hipStream_t stream);
+
+hipError_t launch_packet_route(int64_t n, const int32_t* src, const int32_t* dst,
+                               const uint32_t* payload, const uint32_t* state_in,
+                               const uint64_t* now, const double2* table, int64_t A,
+                               uint64_t jump, int clamp, uint64_t* t_out, uint32_t* state_out,
+                               uint8_t* delivered, hipStream_t stream);
+
+hipError_t launch_row_min(int64_t rows, int64_t A, const double2* lr, double* out_rowmin,
+                          hipStream_t stream);
+
+hipError_t launch_fill_u64(unsigned long long* p, unsigned long long v, int64_t n,
+                           hipStream_t stream);
+
+int sssp_max_blocks_per_cu();
+
+}  // namespace shdtopo

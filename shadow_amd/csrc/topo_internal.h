@@ -1,0 +1,87 @@
+// topo_internal.h -- host-side data structures shared by the libshdtopo translation units.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "topo_device.h"
+
+namespace shdtopo {
+
+// The parsed topology: what igraph_read_graph_graphml + the C attribute table hold for the
+// reference (shd-topology.c:95-123).  Vertex index = order of first appearance of the node id,
+// edge id = order of <edge> elements (igraph 0.7.1 GraphML reader).
+struct HostGraph {
+    int32_t V = 0;
+    int64_t E = 0;
+    bool directed = false;
+    std::vector<int32_t> eu, ev;           // endpoints in document order
+    std::vector<double> elat, ejitter, eloss;
+    std::vector<std::string> vid, vtype, vip, vgeo;
+    std::vector<double> vbwup, vbwdown, vloss;
+};
+
+bool graphml_parse(const char* buf, size_t len, HostGraph& g, std::string& err);
+bool graphml_load_file(const char* path, HostGraph& g, std::string& err);
+bool graphml_write_file(const HostGraph& g, const char* path);
+
+struct SynthParams {
+    uint64_t seed;
+    int64_t n_routers, n_poi, n_edges;
+    int integer_latency;
+    double alpha;
+};
+bool synth_graph(const SynthParams& p, HostGraph& g, std::string& err);
+
+// splitmix64: the generators' deterministic RNG
+struct SplitMix {
+    uint64_t s;
+    explicit SplitMix(uint64_t seed) : s(seed) {}
+    uint64_t next() {
+        uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    double uniform() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }  // [0,1)
+    uint64_t below(uint64_t n) { return next() % n; }
+};
+
+// glibc rand_r (the generator behind src/utility/shd-random.c:30-37)
+inline int32_t glibc_rand_r(uint32_t* seed) {
+    uint32_t next = *seed;
+    int32_t result;
+    next = next * 1103515245u + 12345u;
+    result = (int32_t)((next / 65536u) % 2048u);
+    next = next * 1103515245u + 12345u;
+    result <<= 10;
+    result ^= (int32_t)((next / 65536u) % 1024u);
+    next = next * 1103515245u + 12345u;
+    result <<= 10;
+    result ^= (int32_t)((next / 65536u) % 1024u);
+    *seed = next;
+    return result;
+}
+inline double rand_r_double(uint32_t* seed) { return (double)glibc_rand_r(seed) / 2147483647.0; }
+
+uint32_t string_to_ip(const char* s);  // inet_pton(AF_INET) as shd-address.c:137-144
+
+// Index of the attachment candidates (the "poi" vertices) so that attaching H hosts costs
+// O(H + V) instead of the reference's O(H * V) string scan (shd-topology.c:1087); candidate
+// lists keep vertex order, so the chosen vertex and RNG use are identical.
+struct AttachIndex {
+    bool built = false;
+    std::vector<int32_t> all;                                   // poi vertices, index order
+    std::vector<uint32_t> ip;                                   // per vertex (poi only)
+    std::vector<uint8_t> usable;                                // per vertex
+    std::unordered_map<std::string, std::vector<int32_t>> byType, byCode, byTypeCode;
+    std::unordered_map<uint32_t, std::vector<int32_t>> byIP;
+    void build(const HostGraph& g);
+};
+
+}  // namespace shdtopo

@@ -1,0 +1,664 @@
+// topo_kernels.hip -- CDNA4 (gfx950) kernels of the routing engine.
+//
+//   sssp_rows_kernel            replaces igraph_get_shortest_paths_dijkstra
+//                               (src/topology/shd-topology.c:753-787) + the per-target helper
+//                               (shd-topology.c:561-671, 808-823): one persistent workgroup per
+//                               SSSP slot runs a near-far (delta-stepping) label-correcting SSSP
+//                               for one source at a time, then derives igraph's parents with the
+//                               argmin (d[u]) rule and walks them to produce
+//                               latency (== dist, bit-exact), reliability (reference product
+//                               order) and hop count for every attached target.
+//   pair_table_complete_kernel  replaces _topology_lookupPath (shd-topology.c:835-873).
+//   packet_route_kernel         replaces worker_schedulePacket (src/engine/shd-worker.c:332-370)
+//                               for a whole scheduler window.
+//
+// f64 arithmetic: every latency add is a single IEEE add (no contraction: built with
+// -ffp-contract=off, and there is no multiply to fuse with); reliability multiplies happen in the
+// reference order.  Distances are the unique monotone-rounding fixpoint, so any correct
+// label-correcting order yields the same bits as igraph's heap order.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "topo_device.h"
+
+namespace shdtopo {
+
+namespace {
+
+constexpr unsigned long long kInfBits = 0x7FF0000000000000ull;
+
+__device__ __forceinline__ unsigned long long ld_l2_u64(const unsigned long long* p) {
+    // L1-bypassing (sc1) load: values written by atomics of other waves must not be read from a
+    // stale vector-L1 line (MI355X_MICROARCH.md "inter-workgroup visibility").
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_l2_u32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double bits2d(unsigned long long b) { return __longlong_as_double((long long)b); }
+__device__ __forceinline__ unsigned long long d2bits(double d) { return (unsigned long long)__double_as_longlong(d); }
+
+struct Lds {
+    uint32_t off[kSsspBlock + 1];
+    uint32_t rs[kSsspBlock];
+    uint32_t vx[kSsspBlock];
+    double val[kSsspBlock];
+    uint32_t wave[kSsspBlock / 64];
+    uint32_t qtail;
+    uint32_t ftail;
+    uint32_t src_idx;
+    uint32_t pad0;
+    unsigned long long dmin;
+    unsigned long long relax;
+};
+
+// Wave-aggregated queue append: one LDS atomic per wave instead of one per lane.
+__device__ __forceinline__ void wave_push(bool pred, uint32_t val, uint32_t* q, uint32_t* lds_tail,
+                                          uint32_t cap, unsigned long long* stats) {
+    unsigned long long m = __ballot(pred);
+    if (m == 0ull) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(lds_tail, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (pred) {
+        uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (pos < cap) q[pos] = val;
+        else atomicOr(&stats[ST_OVERFLOW], 1ull);
+    }
+}
+
+// Block-wide exclusive scan of one u32 per thread; *total receives the sum.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, Lds& L, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int NW = kSsspBlock / 64;
+    uint32_t v = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    if (lane == 63) L.wave[wid] = v;
+    __syncthreads();
+    if (wid == 0) {
+        uint32_t w = lane < NW ? L.wave[lane] : 0u;
+#pragma unroll
+        for (int o = 1; o < NW; o <<= 1) {
+            uint32_t y = __shfl_up(w, o, 64);
+            if (lane >= o) w += y;
+        }
+        if (lane < NW) L.wave[lane] = w;
+    }
+    __syncthreads();
+    uint32_t base = wid ? L.wave[wid - 1] : 0u;
+    *total = L.wave[NW - 1];
+    __syncthreads();
+    return base + v - x;
+}
+
+// Load-balanced expansion of the adjacency lists of queue Q[0..nq): the queue is taken in chunks
+// of kSsspBlock vertices; a block scan of their degrees flattens the chunk's edges and every
+// lane takes edges (tid, tid+B, ...) and finds its vertex by binary search in LDS.  Hubs with
+// 10^5 edges are spread over the whole workgroup.  VF decides per vertex whether to expand and
+// the f64 value carried with it; EF handles one edge (vertex, value, adjacency slot, valid).
+template <class VF, class EF>
+__device__ __forceinline__ void expand_queue(const uint32_t* Q, uint32_t nq, const DevCSR& g,
+                                             Lds& L, VF&& vf, EF&& ef) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t base = 0; base < nq; base += kSsspBlock) {
+        const uint32_t cnt = min((uint32_t)kSsspBlock, nq - base);
+        uint32_t deg = 0;
+        if (tid < cnt) {
+            uint32_t v = Q[base + tid];
+            double val;
+            if (vf(v, val)) {
+                uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
+                deg = r1 - r0;
+                L.rs[tid] = r0;
+            } else {
+                L.rs[tid] = 0;
+            }
+            L.vx[tid] = v;
+            L.val[tid] = val;
+        }
+        uint32_t total;
+        uint32_t off = block_excl_scan(deg, L, &total);
+        if (tid < cnt) L.off[tid] = off;
+        if (tid == 0) L.off[cnt] = total;
+        __syncthreads();
+        const uint32_t lane = tid & 63;
+        for (uint32_t eb = tid - lane; eb < total; eb += kSsspBlock) {
+            const uint32_t e = eb + lane;
+            const bool valid = e < total;
+            int lo = 0;
+            if (valid) {
+                int hi = (int)cnt - 1;
+                while (lo < hi) {
+                    int mid = (lo + hi + 1) >> 1;
+                    if (L.off[mid] <= e) lo = mid; else hi = mid - 1;
+                }
+            }
+            const uint32_t j = valid ? L.rs[lo] + (e - L.off[lo]) : 0u;
+            ef(L.vx[lo], L.val[lo], j, valid);
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(kSsspBlock)
+sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int nsrc,
+                 const uint32_t* __restrict__ targets, int A, double delta,
+                 double2* __restrict__ out_lr, uint16_t* __restrict__ out_hops,
+                 double* __restrict__ out_rowmin, unsigned long long* __restrict__ stats) {
+    __shared__ Lds L;
+    const int slot = blockIdx.x;
+    const uint32_t tid = threadIdx.x;
+    const int64_t V = ws.V;
+    unsigned long long* dist = ws.dist + (size_t)slot * V;
+    uint32_t* stamp = ws.stamp + (size_t)slot * V;
+    uint32_t* fstamp = ws.fstamp + (size_t)slot * V;
+    uint32_t* qa = ws.qa + (size_t)slot * V;
+    uint32_t* qb = ws.qb + (size_t)slot * V;
+    uint32_t* farq = ws.far + (size_t)slot * V;
+    unsigned long long* best = ws.best + (size_t)slot * V;
+    uint32_t* cntc = ws.cnt + (size_t)slot * V;
+    uint32_t* bslot = ws.bslot + (size_t)slot * V;
+    unsigned long long* memo = ws.memo + (size_t)slot * V;
+    uint32_t* par = ws.par + (size_t)slot * V;
+    uint32_t* pbuf = ws.pathbuf + (size_t)slot * kMaxHops * kSsspBlock;
+    uint32_t* ctr = ws.counters + (size_t)slot * 4;
+    const uint32_t cap = (uint32_t)V;
+
+    // slot-persistent epoch counters (never reset, so stamp/fstamp/memo need no clearing)
+    uint32_t iter = ctr[0], fep = ctr[1], mep = ctr[2];
+    unsigned long long relax_local = 0;
+
+    for (;;) {
+        if (tid == 0) L.src_idx = (uint32_t)atomicAdd(&stats[ST_DEQUEUE], 1ull);
+        __syncthreads();
+        const uint32_t s_idx = L.src_idx;
+        __syncthreads();
+        if (s_idx >= (uint32_t)nsrc) break;
+        const uint32_t src = sources[s_idx];
+
+        // ---------------- SSSP (near-far) ----------------
+        for (int64_t v = tid; v < V; v += kSsspBlock) dist[v] = kInfBits;
+        __syncthreads();
+        iter++;
+        fep++;
+        if (tid == 0) {
+            dist[src] = 0ull;
+            qa[0] = src;
+            stamp[src] = iter;
+            L.ftail = 0;
+        }
+        __syncthreads();
+        uint32_t* cur = qa;
+        uint32_t* nxt = qb;
+        uint32_t nq = 1, nf = 0;
+        double thr = delta;
+        uint32_t guard = 0;
+        for (;;) {
+            while (nq > 0) {
+                iter++;
+                if (tid == 0) L.qtail = 0;
+                __syncthreads();
+                const uint32_t it = iter, fe = fep;
+                const double th = thr;
+                expand_queue(
+                    cur, nq, g, L,
+                    [&](uint32_t v, double& val) {
+                        val = bits2d(ld_l2_u64(&dist[v]));
+                        return true;
+                    },
+                    [&](uint32_t u, double du, uint32_t j, bool valid) {
+                        bool pushN = false, pushF = false;
+                        uint32_t n = 0;
+                        if (valid) {
+                            n = g.col[j];
+                            const double alt = __dadd_rn(du, g.wt[j]);
+                            const unsigned long long ab = d2bits(alt);
+                            relax_local++;
+                            if (ab < dist[n]) {  // plain (possibly stale = larger) pre-check
+                                unsigned long long old = atomicMin(&dist[n], ab);
+                                if (ab < old) {
+                                    if (alt < th) pushN = atomicExch(&stamp[n], it) != it;
+                                    else pushF = atomicExch(&fstamp[n], fe) != fe;
+                                }
+                            }
+                        }
+                        wave_push(pushN, n, nxt, &L.qtail, cap, stats);
+                        wave_push(pushF, n, farq, &L.ftail, cap, stats);
+                    });
+                // expand_queue ends with a barrier
+                nq = min(L.qtail, cap);
+                nf = min(L.ftail, cap);
+                uint32_t* t = cur; cur = nxt; nxt = t;
+                if (++guard > 50000000u) { if (tid == 0) atomicOr(&stats[ST_OVERFLOW], 2ull); nq = 0; nf = 0; }
+                __syncthreads();
+            }
+            if (nf == 0) break;
+            // split the far pile: next threshold from the smallest live far distance
+            if (tid == 0) L.dmin = kInfBits;
+            __syncthreads();
+            {
+                unsigned long long m = kInfBits;
+                for (uint32_t i = tid; i < nf; i += kSsspBlock) {
+                    unsigned long long d = ld_l2_u64(&dist[farq[i]]);
+                    if (bits2d(d) >= thr && d < m) m = d;
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    unsigned long long y = __shfl_xor(m, o, 64);
+                    m = y < m ? y : m;
+                }
+                if ((tid & 63) == 0 && m != kInfBits) atomicMin(&L.dmin, m);
+            }
+            __syncthreads();
+            const unsigned long long dminb = L.dmin;
+            if (dminb == kInfBits) break;
+            const double oldthr = thr;
+            const double newthr = __dadd_rn(bits2d(dminb), delta);
+            const uint32_t fnew = fep + 1;
+            iter++;
+            if (tid == 0) L.qtail = 0;
+            __syncthreads();
+            uint32_t kept = 0;
+            for (uint32_t base = 0; base < nf; base += kSsspBlock) {
+                const uint32_t i = base + tid;
+                uint32_t v = 0;
+                int cls = 0;  // 0 drop, 1 near, 2 keep
+                if (i < nf) {
+                    v = farq[i];
+                    const double d = bits2d(ld_l2_u64(&dist[v]));
+                    cls = d < oldthr ? 0 : (d < newthr ? 1 : 2);
+                }
+                __syncthreads();  // every lane has read its chunk entry before compaction writes
+                uint32_t tot;
+                const uint32_t o = block_excl_scan(cls == 2 ? 1u : 0u, L, &tot);
+                if (cls == 2) {
+                    farq[kept + o] = v;
+                    fstamp[v] = fnew;
+                }
+                wave_push(cls == 1, v, cur, &L.qtail, cap, stats);
+                if (cls == 1) stamp[v] = iter;
+                kept += tot;
+                __syncthreads();
+            }
+            nq = min(L.qtail, cap);
+            nf = kept;
+            fep = fnew;
+            thr = newthr;
+            if (tid == 0) L.ftail = kept;
+            __syncthreads();
+        }
+
+        // ---------------- parents for the target chains (argmin d[u]) ----------
+        mep++;
+        const unsigned long long mtag = (unsigned long long)mep << 32;
+        iter++;
+        if (tid == 0) L.qtail = 0;
+        __syncthreads();
+        for (uint32_t kb = 0; kb < (uint32_t)A; kb += kSsspBlock) {
+            const uint32_t k = kb + tid;
+            bool p = false;
+            uint32_t t = 0;
+            if (k < (uint32_t)A) {
+                t = targets[k];
+                p = (t != src) && (atomicExch(&stamp[t], iter) != iter);
+                if (p) { best[t] = kInfBits; cntc[t] = 0; bslot[t] = 0xFFFFFFFFu; }
+            }
+            wave_push(p, t, cur, &L.qtail, cap, stats);
+        }
+        __syncthreads();
+        uint32_t nF = min(L.qtail, cap);
+        __syncthreads();
+        while (nF > 0) {
+            // pass A: smallest d[u] among candidates fl(d[u] + w) == d[v]
+            expand_queue(
+                cur, nF, g, L,
+                [&](uint32_t v, double& val) {
+                    val = bits2d(ld_l2_u64(&dist[v]));
+                    return true;
+                },
+                [&](uint32_t v, double dv, uint32_t j, bool valid) {
+                    if (!valid) return;
+                    const uint32_t u = g.col[j];
+                    const unsigned long long du = ld_l2_u64(&dist[u]);
+                    if (__dadd_rn(bits2d(du), g.wt[j]) == dv) atomicMin(&best[v], du);
+                });
+            // pass B: count the candidates at the minimum, keep the lowest slot
+            expand_queue(
+                cur, nF, g, L,
+                [&](uint32_t v, double& val) {
+                    val = bits2d(ld_l2_u64(&dist[v]));
+                    return true;
+                },
+                [&](uint32_t v, double dv, uint32_t j, bool valid) {
+                    if (!valid) return;
+                    const uint32_t u = g.col[j];
+                    const unsigned long long du = ld_l2_u64(&dist[u]);
+                    if (__dadd_rn(bits2d(du), g.wt[j]) == dv && du == ld_l2_u64(&best[v])) {
+                        atomicAdd(&cntc[v], 1u);
+                        atomicMin(&bslot[v], j);
+                    }
+                });
+            for (uint32_t i = tid; i < nF; i += kSsspBlock) {
+                const uint32_t v = cur[i];
+                const uint32_t j = ld_l2_u32(&bslot[v]);
+                const uint32_t c = ld_l2_u32(&cntc[v]);
+                if (j == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
+                    atomicAdd(&stats[ST_ERRORS], 1ull);
+                    memo[v] = mtag | 0x7FFFFFFFull;
+                    par[v] = src;
+                } else {
+                    memo[v] = mtag | (c > 1 ? 0x80000000ull : 0ull) | (unsigned long long)j;
+                    par[v] = g.col[j];
+                }
+            }
+            __syncthreads();
+            iter++;
+            if (tid == 0) L.qtail = 0;
+            __syncthreads();
+            for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
+                const uint32_t i = ib + tid;
+                bool p = false;
+                uint32_t u = 0;
+                if (i < nF) {
+                    u = par[cur[i]];
+                    p = (u != src) && ((memo[u] & 0xFFFFFFFF00000000ull) != mtag) &&
+                        (atomicExch(&stamp[u], iter) != iter);
+                    if (p) { best[u] = kInfBits; cntc[u] = 0; bslot[u] = 0xFFFFFFFFu; }
+                }
+                wave_push(p, u, nxt, &L.qtail, cap, stats);
+            }
+            __syncthreads();
+            nF = min(L.qtail, cap);
+            uint32_t* t = cur; cur = nxt; nxt = t;
+            __syncthreads();
+        }
+
+        // ---------------- per-target latency / reliability / hops (shd-topology.c:561-671) ----
+        double rmin = INFINITY;
+        const size_t rowbase = (size_t)s_idx * (size_t)A;
+        for (uint32_t k = tid; k < (uint32_t)A; k += kSsspBlock) {
+            const uint32_t t = targets[k];
+            double lat, rel;
+            uint32_t h = 0;
+            if (t == src) {
+                // path [src]: the self loop (n == 1 branch), no destination loss
+                const double sl = g.selfLat[src];
+                if (isnan(sl)) {
+                    atomicAdd(&stats[ST_ERRORS], 1ull);
+                    lat = -1.0;
+                    rel = -1.0;
+                } else {
+                    lat = 0.0 + sl;
+                    rel = 1.0;
+                    rel *= (1.0 - g.vloss[src]);
+                    rel *= (1.0 - g.selfLoss[src]);
+                    h = 1;
+                }
+            } else {
+                lat = bits2d(ld_l2_u64(&dist[t]));
+                bool amb = false, bad = false;
+                uint32_t v = t;
+                while (v != src) {
+                    const unsigned long long m = memo[v];
+                    if ((m & 0xFFFFFFFF00000000ull) != mtag || (m & 0x7FFFFFFFull) == 0x7FFFFFFFull) {
+                        bad = true;
+                        break;
+                    }
+                    amb |= (m >> 31) & 1ull;
+                    if (h < kMaxHops) pbuf[(size_t)h * kSsspBlock + tid] = (uint32_t)(m & 0x7FFFFFFFull);
+                    h++;
+                    v = par[v];
+                    if (h > (uint32_t)V) { bad = true; break; }
+                }
+                rel = 1.0;
+                rel *= (1.0 - g.vloss[src]);
+                rel *= (1.0 - g.vloss[t]);
+                if (bad) {
+                    atomicAdd(&stats[ST_ERRORS], 1ull);
+                    lat = -1.0;
+                    rel = -1.0;
+                } else if (h <= (uint32_t)kMaxHops) {
+                    for (int i = (int)h - 1; i >= 0; --i)
+                        rel *= (1.0 - g.aloss[pbuf[(size_t)i * kSsspBlock + tid]]);
+                } else {
+                    atomicAdd(&stats[ST_LONGPATH], 1ull);
+                    for (int i = (int)h - 1; i >= 0; --i) {  // edge at depth i from t
+                        uint32_t x = t;
+                        for (int s = 0; s < i; ++s) x = par[x];
+                        rel *= (1.0 - g.aloss[(uint32_t)(memo[x] & 0x7FFFFFFFull)]);
+                    }
+                }
+                if (amb) atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
+                if (lat == 0.0) lat = 1.0;
+            }
+            out_lr[rowbase + k] = make_double2(lat, rel);
+            out_hops[rowbase + k] = (uint16_t)(h > 65535u ? 65535u : h);
+            if (lat >= 0.0) rmin = fmin(rmin, lat);
+        }
+        // row minimum (feeds the runahead, shd-topology.c:500-511)
+        {
+            unsigned long long m = d2bits(rmin);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                unsigned long long y = __shfl_xor(m, o, 64);
+                m = y < m ? y : m;
+            }
+            if (tid == 0) L.dmin = kInfBits;
+            __syncthreads();
+            if ((tid & 63) == 0) atomicMin(&L.dmin, m);
+            __syncthreads();
+            if (tid == 0) {
+                if (out_rowmin) out_rowmin[s_idx] = bits2d(L.dmin);
+                atomicMin(&stats[ST_GLOBAL_MIN], L.dmin);
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        ctr[0] = iter;
+        ctr[1] = fep;
+        ctr[2] = mep;
+        L.relax = 0;
+    }
+    __syncthreads();
+    atomicAdd(&L.relax, relax_local);
+    __syncthreads();
+    if (tid == 0) atomicAdd(&stats[ST_RELAX], L.relax);
+}
+
+// ------------------------------------------------------------------------------------------
+// complete graphs: _topology_lookupPath (shd-topology.c:835-873) for every attached pair.
+// 34 B of HBM traffic per pair (8 B lat + 8 B loss read, 16 B record + 2 B hops written).
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+pair_table_complete_kernel(int A, int64_t row0, int64_t rows, const double* __restrict__ elatAA,
+                           const double* __restrict__ elossAA, const double* __restrict__ vlossA,
+                           double2* __restrict__ out_lr, uint16_t* __restrict__ out_hops,
+                           double* __restrict__ out_rowmin, unsigned long long* __restrict__ stats) {
+    const int64_t total = rows * (int64_t)A;
+    unsigned long long m = kInfBits;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = k / A;
+        const int64_t c = k - r * A;
+        const int64_t i = row0 + r;
+        const double el = elatAA[i * A + c];
+        double lat, rel;
+        if (el < 0.0) {  // no edge between the pair: igraph_get_eid fails (shd-topology.c:857)
+            atomicAdd(&stats[ST_ERRORS], 1ull);
+            lat = -1.0;
+            rel = -1.0;
+        } else {
+            rel = 1.0;
+            rel *= (1.0 - vlossA[i]);
+            rel *= (1.0 - vlossA[c]);
+            lat = 0.0;
+            lat += el;
+            rel *= (1.0 - elossAA[i * A + c]);
+            unsigned long long b = d2bits(lat);
+            m = b < m ? b : m;
+        }
+        out_lr[k] = make_double2(lat, rel);
+        out_hops[k] = 1;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        unsigned long long y = __shfl_xor(m, o, 64);
+        m = y < m ? y : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m != kInfBits) atomicMin(&stats[ST_GLOBAL_MIN], m);
+    (void)out_rowmin;
+}
+
+// per-row minimum for the complete table (lazy-runahead bookkeeping)
+__global__ void row_min_kernel(int64_t rows, int64_t A, const double2* __restrict__ lr,
+                               double* __restrict__ out_rowmin) {
+    const int64_t r = blockIdx.x;
+    if (r >= rows) return;
+    unsigned long long m = kInfBits;
+    for (int64_t c = threadIdx.x; c < A; c += blockDim.x) {
+        double l = lr[r * A + c].x;
+        if (l >= 0.0) { unsigned long long b = d2bits(l); m = b < m ? b : m; }
+    }
+    __shared__ unsigned long long sm;
+    if (threadIdx.x == 0) sm = kInfBits;
+    __syncthreads();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        unsigned long long y = __shfl_xor(m, o, 64);
+        m = y < m ? y : m;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMin(&sm, m);
+    __syncthreads();
+    if (threadIdx.x == 0) out_rowmin[r] = bits2d(sm);
+}
+
+// ------------------------------------------------------------------------------------------
+// packet route: worker_schedulePacket (shd-worker.c:332-370) + clamp (shd-worker.c:310-324).
+// 53 B per packet: 24 B of inputs, one 16-B {lat, rel} record gather, 13 B of outputs.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+packet_route_kernel(int64_t n, const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                    const uint32_t* __restrict__ payload, const uint32_t* __restrict__ state_in,
+                    const uint64_t* __restrict__ now, const double2* __restrict__ table, int64_t A,
+                    uint64_t jump, int clamp, uint64_t* __restrict__ t_out,
+                    uint32_t* __restrict__ state_out, uint8_t* __restrict__ delivered) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const double2 rec = table[(int64_t)src[k] * A + dst[k]];
+        uint32_t next = state_in[k];
+        // glibc rand_r: three LCG steps, 11 + 10 + 10 bits
+        next = next * 1103515245u + 12345u;
+        uint32_t r = (next / 65536u) % 2048u;
+        next = next * 1103515245u + 12345u;
+        r = (r << 10) ^ ((next / 65536u) % 1024u);
+        next = next * 1103515245u + 12345u;
+        r = (r << 10) ^ ((next / 65536u) % 1024u);
+        const double chance = (double)(int32_t)r / 2147483647.0;
+        const uint64_t tnow = now[k];
+        uint64_t t = 0;
+        uint8_t dl = 0;
+        if (chance <= rec.y || payload[k] == 0u) {
+            const uint64_t delay = (uint64_t)ceil(rec.x * 1000000.0);
+            t = tnow + delay;
+            if (clamp) {
+                const uint64_t minTime = tnow + jump;
+                if (t < minTime) t = minTime;
+            }
+            dl = 1;
+        }
+        t_out[k] = t;
+        state_out[k] = next;
+        delivered[k] = dl;
+    }
+}
+
+__global__ void fill_u64_kernel(unsigned long long* p, unsigned long long v, int64_t n) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (int64_t)gridDim.x * blockDim.x)
+        p[k] = v;
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------
+static int grid_for(int64_t n, int block) {
+    int64_t g = (n + block - 1) / block;
+    if (g > 256 * 16) g = 256 * 16;  // 16 workgroups per CU, grid-stride beyond
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
+                            int nsrc, const uint32_t* d_targets, int A, double delta,
+                            double2* out_lr, uint16_t* out_hops, double* out_rowmin,
+                            unsigned long long* d_stats, hipStream_t stream) {
+    int grid = ws.slots < nsrc ? ws.slots : nsrc;
+    if (grid < 1) return hipSuccess;
+    hipLaunchKernelGGL(sssp_rows_kernel, dim3(grid), dim3(kSsspBlock), 0, stream, g, ws,
+                       d_sources, nsrc, d_targets, A, delta, out_lr, out_hops, out_rowmin,
+                       d_stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_table_complete(int A, int64_t row0, int64_t rows, const double* elatAA,
+                                      const double* elossAA, const double* vlossA, double2* out_lr,
+                                      uint16_t* out_hops, double* out_rowmin,
+                                      unsigned long long* d_stats, hipStream_t stream) {
+    if (rows <= 0 || A <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pair_table_complete_kernel, dim3(grid_for(rows * A, 256)), dim3(256), 0,
+                       stream, A, row0, rows, elatAA, elossAA, vlossA, out_lr, out_hops,
+                       out_rowmin, d_stats);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !out_rowmin) return e;
+    hipLaunchKernelGGL(row_min_kernel, dim3((unsigned)rows), dim3(256), 0, stream, rows,
+                       (int64_t)A, out_lr, out_rowmin);
+    return hipGetLastError();
+}
+
+hipError_t launch_packet_route(int64_t n, const int32_t* src, const int32_t* dst,
+                               const uint32_t* payload, const uint32_t* state_in,
+                               const uint64_t* now, const double2* table, int64_t A,
+                               uint64_t jump, int clamp, uint64_t* t_out, uint32_t* state_out,
+                               uint8_t* delivered, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(packet_route_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, src,
+                       dst, payload, state_in, now, table, A, jump, clamp, t_out, state_out,
+                       delivered);
+    return hipGetLastError();
+}
+
+hipError_t launch_row_min(int64_t rows, int64_t A, const double2* lr, double* out_rowmin,
+                          hipStream_t stream) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(row_min_kernel, dim3((unsigned)rows), dim3(256), 0, stream, rows, A, lr,
+                       out_rowmin);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_u64(unsigned long long* p, unsigned long long v, int64_t n,
+                           hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(fill_u64_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, p, v, n);
+    return hipGetLastError();
+}
+
+int sssp_max_blocks_per_cu() {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sssp_rows_kernel, kSsspBlock, 0) !=
+        hipSuccess)
+        return 1;
+    return nb < 1 ? 1 : nb;
+}
+
+}  // namespace shdtopo

@@ -1,0 +1,52 @@
+"""Quick GPU probe: C4 synthetic graph, time the SSSP rows kernel on a row range."""
+import argparse
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+import shadow_amd as sa  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rows", type=int, default=256)
+ap.add_argument("--delta", type=float, default=0)
+ap.add_argument("--slots", type=int, default=0)
+ap.add_argument("--routers", type=int, default=990_000)
+ap.add_argument("--poi", type=int, default=10_000)
+ap.add_argument("--edges", type=int, default=10_000_000)
+ap.add_argument("--hosts", type=int, default=100_000)
+ap.add_argument("--reps", type=int, default=2)
+args = ap.parse_args()
+
+t = time.time()
+top = sa.Topology.synthetic(n_routers=args.routers, n_poi=args.poi, n_edges=args.edges)
+print("graph %.1fs V=%d E=%d" % (time.time() - t, top.num_vertices, top.num_edges), flush=True)
+if args.delta:
+    top.set_option("delta", args.delta)
+if args.slots:
+    top.set_option("slots", args.slots)
+t = time.time()
+pk = top.synth_packets(20261015, args.hosts, 1000, 10**9, 10**7)
+A = len(top.attached_vertices())
+print("attach %.1fs A=%d" % (time.time() - t, A), flush=True)
+rows = min(args.rows, A)
+lr = torch.empty((rows, A, 2), dtype=torch.float64, device="cuda")
+hp = torch.empty((rows, A), dtype=torch.int16, device="cuda")
+for rep in range(args.reps):
+    torch.cuda.synchronize()
+    t = time.time()
+    top.build_rows_into(0, rows, lr, hp)
+    torch.cuda.synchronize()
+    dt = time.time() - t
+    st = top.stats()
+    E = top.num_edges
+    print("rep %d rows=%d wall %.3fs kernel %.3fms  GTEPS %.2f  relax/src %.3g  amb %d err %d long %d"
+          % (rep, rows, dt, st["sssp_kernel_ms"], rows * E / (st["sssp_kernel_ms"] / 1e3) / 1e9,
+             st["relaxations"] / rows, st["ambiguous_pairs"], st["errors"], st["long_paths"]),
+          flush=True)
+x = lr[..., 0].cpu().numpy()
+print("lat min %.4f max %.4f mean %.3f" % (x.min(), x.max(), x.mean()))
+h = hp.cpu().numpy()
+print("hops max %d mean %.2f" % (h.max(), h.mean()))
