@@ -150,6 +150,11 @@ typedef struct {
     int64_t relaxations;      /* edge relaxations attempted by the last SSSP launch */
     int64_t long_paths;       /* pairs with more hops than the in-register path buffer */
     int64_t errors;           /* pairs with a missing edge (no self loop etc.) */
+    double phase_ms[4];       /* SSSP kernel time summed over workgroups: init, near-far SSSP,
+                                 parent derivation, per-target epilogue */
+    int64_t near_iterations;  /* near-phase iterations summed over sources */
+    int64_t far_splits;       /* far-pile splits summed over sources */
+    int64_t slots;            /* concurrent SSSP workgroups of the last launch */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

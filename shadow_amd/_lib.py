@@ -31,7 +31,9 @@ class TopoPacketOut(ctypes.Structure):
 class ShdStats(ctypes.Structure):
     _fields_ = [("build_ms", dbl), ("sssp_kernel_ms", dbl), ("route_kernel_ms", dbl),
                 ("sources", i64), ("targets", i64), ("ambiguous_pairs", i64),
-                ("relaxations", i64), ("long_paths", i64), ("errors", i64)]
+                ("relaxations", i64), ("long_paths", i64), ("errors", i64),
+                ("phase_ms", dbl * 4), ("near_iterations", i64), ("far_splits", i64),
+                ("slots", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):

@@ -101,6 +101,7 @@ struct _Topology {
     double delta = 0.0;  // 0 = auto
     int slotsOpt = 0;
     int device = 0;
+    int64_t hubLimit = -1;  // LDS-cached hub distances (-1 = fill the LDS)
 
     // attach state (shd-topology.c:20-24 virtualIP)
     std::shared_mutex ipMu;
@@ -327,6 +328,29 @@ int upload_csr(Topology* top) {
         col[pa] = (uint32_t)nb; wt[pa] = g.elat[(size_t)e]; aloss[pa] = g.eloss[(size_t)e];
         col[pb] = (uint32_t)na; wt[pb] = g.elat[(size_t)e]; aloss[pb] = g.eloss[(size_t)e];
     }
+    // each row sorted by neighbour: a hub's expansion then walks the distance array in address
+    // order (neighbours sharing a line coalesce, DRAM pages are reused)
+    if (getenv("SHDTOPO_NO_ROWSORT") == nullptr) {
+        std::vector<uint32_t> idx;
+        std::vector<uint32_t> c2;
+        std::vector<double> w2, l2;
+        for (int32_t i = 0; i < V; i++) {
+            size_t b = rowptr[(size_t)i], e = rowptr[(size_t)i + 1];
+            if (e - b < 2) continue;
+            idx.resize(e - b);
+            std::iota(idx.begin(), idx.end(), 0u);
+            std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
+                return col[b + x] < col[b + y] || (col[b + x] == col[b + y] && x < y);
+            });
+            c2.resize(e - b); w2.resize(e - b); l2.resize(e - b);
+            for (size_t k = 0; k < e - b; k++) {
+                c2[k] = col[b + idx[k]]; w2[k] = wt[b + idx[k]]; l2[k] = aloss[b + idx[k]];
+            }
+            std::copy(c2.begin(), c2.end(), col.begin() + (long)b);
+            std::copy(w2.begin(), w2.end(), wt.begin() + (long)b);
+            std::copy(l2.begin(), l2.end(), aloss.begin() + (long)b);
+        }
+    }
     for (int32_t i = 0; i < V; i++) vloss[(size_t)i] = g.vloss[(size_t)top->perm[(size_t)i]];
     HIPCHK(top->d_rowptr.ensure((size_t)V + 1));
     HIPCHK(top->d_col.ensure(nadj));
@@ -495,7 +519,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         HIPCHK(hipMemcpyAsync(top->d_targets.p, tgt.data(), sizeof(uint32_t) * (size_t)A, hipMemcpyHostToDevice, st));
         HIPCHK(hipEventRecord(top->ev0, st));
         HIPCHK(launch_sssp_rows(dev_csr(top), slot_ws(top), top->d_sources.p, (int)rows,
-                                top->d_targets.p, (int)A, default_delta(top), out_lr, out_hops,
+                                top->d_targets.p, (int)A, default_delta(top), top->hubLimit,
+                                out_lr, out_hops,
                                 out_rowmin, top->d_stats.p, st));
         HIPCHK(hipEventRecord(top->ev1, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -519,6 +544,15 @@ int collect_row_stats(Topology* top) {
     top->stats.relaxations = (int64_t)h[ST_RELAX];
     top->stats.long_paths = (int64_t)h[ST_LONGPATH];
     top->stats.errors = (int64_t)h[ST_ERRORS];
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->device) != hipSuccess || khz <= 0)
+            khz = 100000;
+        for (int i = 0; i < 4; i++) top->stats.phase_ms[i] = (double)h[ST_T_INIT + i] / (double)khz;
+    }
+    top->stats.near_iterations = (int64_t)h[ST_NEAR_IT];
+    top->stats.far_splits = (int64_t)h[ST_SPLITS];
+    top->stats.slots = top->isComplete ? 0 : top->slots;
     double gm;
     memcpy(&gm, &h[ST_GLOBAL_MIN], sizeof gm);
     top->eagerMin = std::isinf(gm) ? -1.0 : gm;
@@ -819,6 +853,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "delta") top->delta = value;
     else if (k == "slots") top->slotsOpt = (int)value;
     else if (k == "device") top->device = (int)value;
+    else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
     else return -1;
     return 0;
 }

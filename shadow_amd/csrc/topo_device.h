@@ -26,6 +26,12 @@ enum StatIdx {
     ST_ERRORS = 4,      // pairs with a missing edge / unreachable target
     ST_DEQUEUE = 5,     // next source to take (persistent workgroups)
     ST_OVERFLOW = 6,    // queue overflow / iteration guard tripped
+    ST_T_INIT = 7,      // wall-clock ticks summed over workgroups: distance init
+    ST_T_SSSP = 8,      //   near-far SSSP
+    ST_T_PARENT = 9,    //   parent derivation for the target chains
+    ST_T_TARGET = 10,   //   per-target latency / reliability / hops
+    ST_NEAR_IT = 11,    // near-phase iterations
+    ST_SPLITS = 12,     // far-pile splits
     ST_COUNT = 16
 };
 
@@ -60,10 +66,12 @@ struct SlotWs {
     uint32_t* counters = nullptr;        // [slot][4]: iteration id, far epoch, source epoch
 };
 
+// hub_limit: cap on LDS-cached vertices (-1 = as many as fit, ~18k)
 hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                             int nsrc, const uint32_t* d_targets, int A, double delta,
-                            double2* out_lr, uint16_t* out_hops, double* out_rowmin,
-                            unsigned long long* d_stats, hipStream_t stream);
+                            int64_t hub_limit, double2* out_lr, uint16_t* out_hops,
+                            double* out_rowmin, unsigned long long* d_stats, hipStream_t stream);
+uint32_t sssp_hub_capacity();
 
 hipError_t launch_pair_table_complete(int A, int64_t row0, int64_t rows, const double* elatAA,
                                       const double* elossAA, const double* vlossA, double2* out_lr,

@@ -41,7 +41,7 @@ __device__ __forceinline__ double bits2d(unsigned long long b) { return __longlo
 __device__ __forceinline__ unsigned long long d2bits(double d) { return (unsigned long long)__double_as_longlong(d); }
 
 struct Lds {
-    uint32_t off[kSsspBlock + 1];
+    uint32_t off[kSsspBlock + 4];
     uint32_t rs[kSsspBlock];
     uint32_t vx[kSsspBlock];
     double val[kSsspBlock];
@@ -53,6 +53,9 @@ struct Lds {
     unsigned long long dmin;
     unsigned long long relax;
 };
+constexpr size_t kLdsCtrlBytes = (sizeof(Lds) + 15) / 16 * 16;
+constexpr size_t kSsspMaxLds = 160 * 1024;  // one workgroup per CU owns the whole LDS
+constexpr int kRelaxUnroll = 4;
 
 // Wave-aggregated queue append: one LDS atomic per wave instead of one per lane.
 __device__ __forceinline__ void wave_push(bool pred, uint32_t val, uint32_t* q, uint32_t* lds_tail,
@@ -148,18 +151,113 @@ __device__ __forceinline__ void expand_queue(const uint32_t* Q, uint32_t nq, con
     }
 }
 
+
+// Hot-distance cache: after the degree relabel the first H vertex ids are the hubs, which receive
+// most relaxations of a power-law graph.  Their distance words live in LDS for the whole SSSP of
+// a source (the authoritative copy: LDS atomics, no DRAM traffic); the tail stays in HBM.
+struct DistView {
+    unsigned long long* hd;    // LDS, H words
+    unsigned long long* dist;  // HBM, V words (words < H unused while the source runs)
+    uint32_t H;
+    __device__ __forceinline__ unsigned long long get(uint32_t v) const {
+        return v < H ? hd[v] : ld_l2_u64(&dist[v]);
+    }
+};
+
+// Near-phase relaxation of queue Q: the load-balanced chunking of expand_queue, with U edges in
+// flight per lane: U (col, wt) loads, then the U tail pre-checks, then the LDS / HBM atomics, then
+// the queue pushes.
+template <int U>
+__device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, const DevCSR& g,
+                                            Lds& L, const DistView& D, uint32_t* stamp,
+                                            uint32_t* fstamp, uint32_t* nxt, uint32_t* farq,
+                                            uint32_t it, uint32_t fe, double th, uint32_t cap,
+                                            unsigned long long* stats,
+                                            unsigned long long& relax) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    for (uint32_t base = 0; base < nq; base += kSsspBlock) {
+        const uint32_t cnt = min((uint32_t)kSsspBlock, nq - base);
+        uint32_t deg = 0;
+        if (tid < cnt) {
+            const uint32_t v = Q[base + tid];
+            const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
+            deg = r1 - r0;
+            L.rs[tid] = r0;
+            L.vx[tid] = v;
+            L.val[tid] = bits2d(D.get(v));
+        }
+        uint32_t total;
+        const uint32_t off = block_excl_scan(deg, L, &total);
+        if (tid < cnt) L.off[tid] = off;
+        if (tid == 0) L.off[cnt] = total;
+        __syncthreads();
+        for (uint32_t eb = tid - lane; eb < total; eb += kSsspBlock * U) {
+            uint32_t n[U];
+            unsigned long long ab[U];
+            bool valid[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t e = eb + (uint32_t)u * kSsspBlock + lane;
+                valid[u] = e < total;
+                int lo = 0;
+                if (valid[u]) {
+                    int hi = (int)cnt - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (L.off[mid] <= e) lo = mid; else hi = mid - 1;
+                    }
+                }
+                const uint32_t j = valid[u] ? L.rs[lo] + (e - L.off[lo]) : 0u;
+                n[u] = valid[u] ? g.col[j] : 0u;
+                ab[u] = valid[u] ? d2bits(__dadd_rn(L.val[lo], g.wt[j])) : ~0ull;
+            }
+            unsigned long long cur[U];
+#pragma unroll
+            for (int u = 0; u < U; u++)  // tail pre-check (plain load: stale = larger = safe)
+                cur[u] = (valid[u] && n[u] >= D.H) ? D.dist[n[u]] : 0ull;
+            bool imp[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                imp[u] = false;
+                if (valid[u] && n[u] < D.H) imp[u] = ab[u] < atomicMin(&D.hd[n[u]], ab[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (ab[u] < cur[u]) imp[u] = ab[u] < atomicMin(&D.dist[n[u]], ab[u]);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                bool pN = false, pF = false;
+                if (imp[u]) {
+                    if (bits2d(ab[u]) < th) pN = atomicExch(&stamp[n[u]], it) != it;
+                    else pF = atomicExch(&fstamp[n[u]], fe) != fe;
+                }
+                wave_push(pN, n[u], nxt, &L.qtail, cap, stats);
+                wave_push(pF, n[u], farq, &L.ftail, cap, stats);
+                relax += valid[u] ? 1ull : 0ull;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 __global__ void __launch_bounds__(kSsspBlock)
 sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int nsrc,
-                 const uint32_t* __restrict__ targets, int A, double delta,
+                 const uint32_t* __restrict__ targets, int A, double delta, uint32_t hubs,
                  double2* __restrict__ out_lr, uint16_t* __restrict__ out_hops,
                  double* __restrict__ out_rowmin, unsigned long long* __restrict__ stats) {
-    __shared__ Lds L;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Lds& L = *reinterpret_cast<Lds*>(smem);
     const int slot = blockIdx.x;
     const uint32_t tid = threadIdx.x;
     const int64_t V = ws.V;
-    unsigned long long* dist = ws.dist + (size_t)slot * V;
+    DistView D;
+    D.hd = reinterpret_cast<unsigned long long*>(smem + kLdsCtrlBytes);
+    D.dist = ws.dist + (size_t)slot * V;
+    D.H = hubs;
+    unsigned long long* dist = D.dist;
     uint32_t* stamp = ws.stamp + (size_t)slot * V;
     uint32_t* fstamp = ws.fstamp + (size_t)slot * V;
     uint32_t* qa = ws.qa + (size_t)slot * V;
@@ -177,6 +275,8 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     // slot-persistent epoch counters (never reset, so stamp/fstamp/memo need no clearing)
     uint32_t iter = ctr[0], fep = ctr[1], mep = ctr[2];
     unsigned long long relax_local = 0;
+    unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, n_near = 0, n_split = 0;
+    unsigned long long tk = wall_clock64();
 
     for (;;) {
         if (tid == 0) L.src_idx = (uint32_t)atomicAdd(&stats[ST_DEQUEUE], 1ull);
@@ -185,14 +285,17 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         __syncthreads();
         if (s_idx >= (uint32_t)nsrc) break;
         const uint32_t src = sources[s_idx];
+        tk = wall_clock64();
 
         // ---------------- SSSP (near-far) ----------------
-        for (int64_t v = tid; v < V; v += kSsspBlock) dist[v] = kInfBits;
+        for (uint32_t v = tid; v < D.H; v += kSsspBlock) D.hd[v] = kInfBits;
+        for (int64_t v = (int64_t)D.H + tid; v < V; v += kSsspBlock) dist[v] = kInfBits;
         __syncthreads();
+        { unsigned long long t = wall_clock64(); t_init += t - tk; tk = t; }
         iter++;
         fep++;
         if (tid == 0) {
-            dist[src] = 0ull;
+            if (src < D.H) D.hd[src] = 0ull; else dist[src] = 0ull;
             qa[0] = src;
             stamp[src] = iter;
             L.ftail = 0;
@@ -208,38 +311,14 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 iter++;
                 if (tid == 0) L.qtail = 0;
                 __syncthreads();
-                const uint32_t it = iter, fe = fep;
-                const double th = thr;
-                expand_queue(
-                    cur, nq, g, L,
-                    [&](uint32_t v, double& val) {
-                        val = bits2d(ld_l2_u64(&dist[v]));
-                        return true;
-                    },
-                    [&](uint32_t u, double du, uint32_t j, bool valid) {
-                        bool pushN = false, pushF = false;
-                        uint32_t n = 0;
-                        if (valid) {
-                            n = g.col[j];
-                            const double alt = __dadd_rn(du, g.wt[j]);
-                            const unsigned long long ab = d2bits(alt);
-                            relax_local++;
-                            if (ab < dist[n]) {  // plain (possibly stale = larger) pre-check
-                                unsigned long long old = atomicMin(&dist[n], ab);
-                                if (ab < old) {
-                                    if (alt < th) pushN = atomicExch(&stamp[n], it) != it;
-                                    else pushF = atomicExch(&fstamp[n], fe) != fe;
-                                }
-                            }
-                        }
-                        wave_push(pushN, n, nxt, &L.qtail, cap, stats);
-                        wave_push(pushF, n, farq, &L.ftail, cap, stats);
-                    });
-                // expand_queue ends with a barrier
+                relax_queue<kRelaxUnroll>(cur, nq, g, L, D, stamp, fstamp, nxt, farq, iter, fep,
+                                          thr, cap, stats, relax_local);
+                // relax_queue ends with a barrier
                 nq = min(L.qtail, cap);
                 nf = min(L.ftail, cap);
                 uint32_t* t = cur; cur = nxt; nxt = t;
-                if (++guard > 50000000u) { if (tid == 0) atomicOr(&stats[ST_OVERFLOW], 2ull); nq = 0; nf = 0; }
+                n_near++;
+                if (++guard > 4000000u) { if (tid == 0) atomicOr(&stats[ST_OVERFLOW], 2ull); nq = 0; nf = 0; }
                 __syncthreads();
             }
             if (nf == 0) break;
@@ -249,7 +328,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             {
                 unsigned long long m = kInfBits;
                 for (uint32_t i = tid; i < nf; i += kSsspBlock) {
-                    unsigned long long d = ld_l2_u64(&dist[farq[i]]);
+                    const unsigned long long d = D.get(farq[i]);
                     if (bits2d(d) >= thr && d < m) m = d;
                 }
 #pragma unroll
@@ -262,6 +341,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             __syncthreads();
             const unsigned long long dminb = L.dmin;
             if (dminb == kInfBits) break;
+            n_split++;
             const double oldthr = thr;
             const double newthr = __dadd_rn(bits2d(dminb), delta);
             const uint32_t fnew = fep + 1;
@@ -275,7 +355,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 int cls = 0;  // 0 drop, 1 near, 2 keep
                 if (i < nf) {
                     v = farq[i];
-                    const double d = bits2d(ld_l2_u64(&dist[v]));
+                    const double d = bits2d(D.get(v));
                     cls = d < oldthr ? 0 : (d < newthr ? 1 : 2);
                 }
                 __syncthreads();  // every lane has read its chunk entry before compaction writes
@@ -298,7 +378,11 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             __syncthreads();
         }
 
+        { unsigned long long t = wall_clock64(); t_sssp += t - tk; tk = t; }
         // ---------------- parents for the target chains (argmin d[u]) ----------
+        // One adjacency pass per chain level finds min d[u] over the candidates
+        // fl(d[u] + w) == d[v] and counts them; only vertices with more than one candidate get a
+        // second pass that counts the candidates AT the minimum and keeps the lowest slot.
         mep++;
         const unsigned long long mtag = (unsigned long long)mep << 32;
         iter++;
@@ -319,35 +403,59 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         uint32_t nF = min(L.qtail, cap);
         __syncthreads();
         while (nF > 0) {
-            // pass A: smallest d[u] among candidates fl(d[u] + w) == d[v]
             expand_queue(
                 cur, nF, g, L,
                 [&](uint32_t v, double& val) {
-                    val = bits2d(ld_l2_u64(&dist[v]));
+                    val = bits2d(D.get(v));
                     return true;
                 },
                 [&](uint32_t v, double dv, uint32_t j, bool valid) {
                     if (!valid) return;
                     const uint32_t u = g.col[j];
-                    const unsigned long long du = ld_l2_u64(&dist[u]);
-                    if (__dadd_rn(bits2d(du), g.wt[j]) == dv) atomicMin(&best[v], du);
-                });
-            // pass B: count the candidates at the minimum, keep the lowest slot
-            expand_queue(
-                cur, nF, g, L,
-                [&](uint32_t v, double& val) {
-                    val = bits2d(ld_l2_u64(&dist[v]));
-                    return true;
-                },
-                [&](uint32_t v, double dv, uint32_t j, bool valid) {
-                    if (!valid) return;
-                    const uint32_t u = g.col[j];
-                    const unsigned long long du = ld_l2_u64(&dist[u]);
-                    if (__dadd_rn(bits2d(du), g.wt[j]) == dv && du == ld_l2_u64(&best[v])) {
+                    const unsigned long long du = D.get(u);
+                    if (__dadd_rn(bits2d(du), g.wt[j]) == dv) {
+                        atomicMin(&best[v], du);
                         atomicAdd(&cntc[v], 1u);
                         atomicMin(&bslot[v], j);
                     }
                 });
+            // vertices with several candidates: recount at the minimum
+            if (tid == 0) L.qtail = 0;
+            __syncthreads();
+            for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
+                const uint32_t i = ib + tid;
+                bool multi = false;
+                uint32_t v = 0;
+                if (i < nF) {
+                    v = cur[i];
+                    multi = ld_l2_u32(&cntc[v]) > 1u;
+                    if (multi) {
+                        atomicExch(&cntc[v], 0u);
+                        atomicExch(&bslot[v], 0xFFFFFFFFu);
+                    }
+                }
+                wave_push(multi, v, nxt, &L.qtail, cap, stats);
+            }
+            __syncthreads();
+            const uint32_t nM = min(L.qtail, cap);
+            __syncthreads();
+            if (nM > 0) {
+                expand_queue(
+                    nxt, nM, g, L,
+                    [&](uint32_t v, double& val) {
+                        val = bits2d(D.get(v));
+                        return true;
+                    },
+                    [&](uint32_t v, double dv, uint32_t j, bool valid) {
+                        if (!valid) return;
+                        const uint32_t u = g.col[j];
+                        const unsigned long long du = D.get(u);
+                        if (__dadd_rn(bits2d(du), g.wt[j]) == dv && du == ld_l2_u64(&best[v])) {
+                            atomicAdd(&cntc[v], 1u);
+                            atomicMin(&bslot[v], j);
+                        }
+                    });
+            }
             for (uint32_t i = tid; i < nF; i += kSsspBlock) {
                 const uint32_t v = cur[i];
                 const uint32_t j = ld_l2_u32(&bslot[v]);
@@ -383,6 +491,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             __syncthreads();
         }
 
+        { unsigned long long t = wall_clock64(); t_par += t - tk; tk = t; }
         // ---------------- per-target latency / reliability / hops (shd-topology.c:561-671) ----
         double rmin = INFINITY;
         const size_t rowbase = (size_t)s_idx * (size_t)A;
@@ -405,7 +514,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                     h = 1;
                 }
             } else {
-                lat = bits2d(ld_l2_u64(&dist[t]));
+                lat = bits2d(D.get(t));
                 bool amb = false, bad = false;
                 uint32_t v = t;
                 while (v != src) {
@@ -463,6 +572,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             }
         }
         __syncthreads();
+        { unsigned long long t = wall_clock64(); t_tgt += t - tk; tk = t; }
     }
     if (tid == 0) {
         ctr[0] = iter;
@@ -473,7 +583,15 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     __syncthreads();
     atomicAdd(&L.relax, relax_local);
     __syncthreads();
-    if (tid == 0) atomicAdd(&stats[ST_RELAX], L.relax);
+    if (tid == 0) {
+        atomicAdd(&stats[ST_RELAX], L.relax);
+        atomicAdd(&stats[ST_T_INIT], t_init);
+        atomicAdd(&stats[ST_T_SSSP], t_sssp);
+        atomicAdd(&stats[ST_T_PARENT], t_par);
+        atomicAdd(&stats[ST_T_TARGET], t_tgt);
+        atomicAdd(&stats[ST_NEAR_IT], n_near);
+        atomicAdd(&stats[ST_SPLITS], n_split);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -599,14 +717,28 @@ static int grid_for(int64_t n, int block) {
     return (int)g;
 }
 
+uint32_t sssp_hub_capacity() { return (uint32_t)((kSsspMaxLds - kLdsCtrlBytes) / 8); }
+
 hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                             int nsrc, const uint32_t* d_targets, int A, double delta,
-                            double2* out_lr, uint16_t* out_hops, double* out_rowmin,
-                            unsigned long long* d_stats, hipStream_t stream) {
+                            int64_t hub_limit, double2* out_lr, uint16_t* out_hops,
+                            double* out_rowmin, unsigned long long* d_stats, hipStream_t stream) {
     int grid = ws.slots < nsrc ? ws.slots : nsrc;
     if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL(sssp_rows_kernel, dim3(grid), dim3(kSsspBlock), 0, stream, g, ws,
-                       d_sources, nsrc, d_targets, A, delta, out_lr, out_hops, out_rowmin,
+    uint32_t hubs = sssp_hub_capacity();
+    if (hub_limit >= 0 && (uint32_t)hub_limit < hubs) hubs = (uint32_t)hub_limit;
+    if ((int64_t)hubs > g.V) hubs = (uint32_t)g.V;
+    const size_t lds = kLdsCtrlBytes + (size_t)hubs * 8;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)sssp_rows_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)kSsspMaxLds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(sssp_rows_kernel, dim3(grid), dim3(kSsspBlock), lds, stream, g, ws,
+                       d_sources, nsrc, d_targets, A, delta, hubs, out_lr, out_hops, out_rowmin,
                        d_stats);
     return hipGetLastError();
 }
@@ -655,7 +787,8 @@ hipError_t launch_fill_u64(unsigned long long* p, unsigned long long v, int64_t 
 
 int sssp_max_blocks_per_cu() {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sssp_rows_kernel, kSsspBlock, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sssp_rows_kernel, kSsspBlock,
+                                                     kSsspMaxLds) !=
         hipSuccess)
         return 1;
     return nb < 1 ? 1 : nb;

@@ -233,7 +233,9 @@ class Topology:
         r = self._lib.shdtopo_get_stats(self._h, ctypes.byref(s))
         if r != 0:
             raise RuntimeError("shdtopo_get_stats failed: %d" % r)
-        return {k: getattr(s, k) for k, _ in L.ShdStats._fields_}
+        out = {k: getattr(s, k) for k, _ in L.ShdStats._fields_}
+        out["phase_ms"] = list(out["phase_ms"])
+        return out
 
     def write_graphml(self, path):
         if self._lib.shdtopo_write_graphml(self._h, path.encode()) != 0:

@@ -33,10 +33,13 @@ def test_complete_table_bundled(name):
     assert top.getMinimumLatency() == olat.min()
 
 
+@pytest.mark.parametrize("hubs", [-1, 0, 700])
 @pytest.mark.parametrize("integer", [False, True])
-def test_sssp_synthetic_table(integer):
-    """SSSP branch: sssp_rows_kernel vs igraph-0.7 Dijkstra + helper restatement."""
+def test_sssp_synthetic_table(integer, hubs):
+    """SSSP branch: sssp_rows_kernel vs igraph-0.7 Dijkstra + helper restatement.  `hubs` caps
+    the LDS-resident distance words: all (-1: the whole small graph fits), none, or mixed."""
     top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
+    top.set_option("lds_hubs", hubs)
     otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()

@@ -6,7 +6,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import shadow_amd as sa  # noqa: E402
 
 ap = argparse.ArgumentParser()
@@ -46,6 +46,11 @@ for rep in range(args.reps):
           % (rep, rows, dt, st["sssp_kernel_ms"], rows * E / (st["sssp_kernel_ms"] / 1e3) / 1e9,
              st["relaxations"] / rows, st["ambiguous_pairs"], st["errors"], st["long_paths"]),
           flush=True)
+    ph = st["phase_ms"]
+    print("   per-source ms: init %.2f sssp %.2f parents %.2f targets %.2f | near-it/src %.0f "
+          "splits/src %.0f slots %d" % tuple([x / rows for x in ph] +
+                                            [st["near_iterations"] / rows,
+                                             st["far_splits"] / rows, st["slots"]]), flush=True)
 x = lr[..., 0].cpu().numpy()
 print("lat min %.4f max %.4f mean %.3f" % (x.min(), x.max(), x.mean()))
 h = hp.cpu().numpy()
