@@ -158,6 +158,11 @@ typedef struct {
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 
+/* Copy the parsed graph into host arrays (document order; any pointer may be NULL):
+ * eu, ev int32[E]; elat, eloss f64[E]; vloss f64[V].  Used by tools and oracle cross-checks. */
+int shdtopo_export_graph(Topology* top, int32_t* eu, int32_t* ev, double* elat, double* eloss,
+                         double* vloss);
+
 /* Write the loaded graph back out as GraphML (same key schema as the bundled resource files). */
 int shdtopo_write_graphml(Topology* top, const char* path);
 

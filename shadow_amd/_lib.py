@@ -75,6 +75,7 @@ SIGNATURES = {
     "shdtopo_get_lazy_minimum_latency": (dbl, [P]),
     "shdtopo_get_stats": (ctypes.c_int, [P, P]),
     "shdtopo_write_graphml": (ctypes.c_int, [P, cstr]),
+    "shdtopo_export_graph": (ctypes.c_int, [P, P, P, P, P, P]),
     "shdtopo_new_synthetic": (P, [P]),
     "shdtopo_synth_packets": (ctypes.c_int, [P, u64, i64, i64, u64, u64, P, P, P, P, P, P, P]),
 }

@@ -301,10 +301,29 @@ int upload_csr(Topology* top) {
         deg[(size_t)a]++;
         deg[(size_t)b]++;
     }
+    // 1) hubs: the H highest-degree vertices take ids 0..H-1 (their distances live in LDS)
     top->perm.resize((size_t)V);
     std::iota(top->perm.begin(), top->perm.end(), 0);
     std::stable_sort(top->perm.begin(), top->perm.end(),
                      [&](int32_t x, int32_t y) { return deg[(size_t)x] > deg[(size_t)y]; });
+    // 2) tail: grouped by "primary hub" (its highest-degree hub neighbour), so that expanding a
+    //    hub relaxes a dense run of tail distance words (8 per 64-B line) instead of one random
+    //    line per neighbour -- the SSSP is bound by random DRAM requests (profiles/).
+    const int64_t H = std::min<int64_t>(V, (int64_t)sssp_hub_capacity());
+    if (getenv("SHDTOPO_NO_TAILGROUP") == nullptr && H < V) {
+        std::vector<int32_t> hubrank((size_t)V, INT32_MAX);
+        for (int64_t i = 0; i < H; i++) hubrank[(size_t)top->perm[(size_t)i]] = (int32_t)i;
+        std::vector<int32_t> primary((size_t)V, INT32_MAX);
+        for (int64_t e = 0; e < g.E; e++) {
+            int32_t a = g.eu[(size_t)e], b = g.ev[(size_t)e];
+            if (a == b) continue;
+            primary[(size_t)a] = std::min(primary[(size_t)a], hubrank[(size_t)b]);
+            primary[(size_t)b] = std::min(primary[(size_t)b], hubrank[(size_t)a]);
+        }
+        std::stable_sort(top->perm.begin() + H, top->perm.end(), [&](int32_t x, int32_t y) {
+            return primary[(size_t)x] < primary[(size_t)y];
+        });
+    }
     top->inv.resize((size_t)V);
     for (int32_t i = 0; i < V; i++) top->inv[(size_t)top->perm[(size_t)i]] = i;
     std::vector<uint32_t> rowptr((size_t)V + 1, 0);
@@ -1093,6 +1112,19 @@ int shdtopo_get_stats(Topology* top, ShdStats* out) {
         top->routePending = false;
     }
     *out = top->stats;
+    return 0;
+}
+
+int shdtopo_export_graph(Topology* top, int32_t* eu, int32_t* ev, double* elat, double* eloss,
+                         double* vloss) {
+    if (!top) return -1;
+    const HostGraph& g = top->g;
+    const size_t E = (size_t)g.E, V = (size_t)g.V;
+    if (eu) memcpy(eu, g.eu.data(), 4 * E);
+    if (ev) memcpy(ev, g.ev.data(), 4 * E);
+    if (elat) memcpy(elat, g.elat.data(), 8 * E);
+    if (eloss) memcpy(eloss, g.eloss.data(), 8 * E);
+    if (vloss) memcpy(vloss, g.vloss.data(), 8 * V);
     return 0;
 }
 

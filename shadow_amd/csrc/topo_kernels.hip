@@ -54,8 +54,12 @@ struct Lds {
     unsigned long long relax;
 };
 constexpr size_t kLdsCtrlBytes = (sizeof(Lds) + 15) / 16 * 16;
+constexpr uint32_t kHubBitWords = 640;  // queue-dedupe bitmaps for up to 20480 LDS hubs
+constexpr size_t kLdsBitsBytes = 2 * kHubBitWords * 4;
 constexpr size_t kSsspMaxLds = 160 * 1024;  // one workgroup per CU owns the whole LDS
 constexpr int kRelaxUnroll = 4;
+static_assert((kSsspMaxLds - kLdsCtrlBytes - kLdsBitsBytes) / 8 <= kHubBitWords * 32,
+              "hub bitmaps must cover every LDS-resident hub");
 
 // Wave-aggregated queue append: one LDS atomic per wave instead of one per lane.
 __device__ __forceinline__ void wave_push(bool pred, uint32_t val, uint32_t* q, uint32_t* lds_tail,
@@ -158,6 +162,8 @@ __device__ __forceinline__ void expand_queue(const uint32_t* Q, uint32_t nq, con
 struct DistView {
     unsigned long long* hd;    // LDS, H words
     unsigned long long* dist;  // HBM, V words (words < H unused while the source runs)
+    uint32_t* nbits;           // LDS: hub already in the next near queue (this iteration)
+    uint32_t* fbits;           // LDS: hub already in the far pile (this far epoch)
     uint32_t H;
     __device__ __forceinline__ unsigned long long get(uint32_t v) const {
         return v < H ? hd[v] : ld_l2_u64(&dist[v]);
@@ -229,8 +235,18 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
             for (int u = 0; u < U; u++) {
                 bool pN = false, pF = false;
                 if (imp[u]) {
-                    if (bits2d(ab[u]) < th) pN = atomicExch(&stamp[n[u]], it) != it;
-                    else pF = atomicExch(&fstamp[n[u]], fe) != fe;
+                    const bool near = bits2d(ab[u]) < th;
+                    if (n[u] < D.H) {  // hub: dedupe in LDS, no memory-side atomic
+                        const uint32_t bit = 1u << (n[u] & 31);
+                        uint32_t* w = (near ? D.nbits : D.fbits) + (n[u] >> 5);
+                        const bool first = (atomicOr(w, bit) & bit) == 0u;
+                        pN = near && first;
+                        pF = !near && first;
+                    } else if (near) {
+                        pN = atomicExch(&stamp[n[u]], it) != it;
+                    } else {
+                        pF = atomicExch(&fstamp[n[u]], fe) != fe;
+                    }
                 }
                 wave_push(pN, n[u], nxt, &L.qtail, cap, stats);
                 wave_push(pF, n[u], farq, &L.ftail, cap, stats);
@@ -254,7 +270,9 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     const uint32_t tid = threadIdx.x;
     const int64_t V = ws.V;
     DistView D;
-    D.hd = reinterpret_cast<unsigned long long*>(smem + kLdsCtrlBytes);
+    D.nbits = reinterpret_cast<uint32_t*>(smem + kLdsCtrlBytes);
+    D.fbits = D.nbits + kHubBitWords;
+    D.hd = reinterpret_cast<unsigned long long*>(smem + kLdsCtrlBytes + kLdsBitsBytes);
     D.dist = ws.dist + (size_t)slot * V;
     D.H = hubs;
     unsigned long long* dist = D.dist;
@@ -289,6 +307,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
 
         // ---------------- SSSP (near-far) ----------------
         for (uint32_t v = tid; v < D.H; v += kSsspBlock) D.hd[v] = kInfBits;
+        for (uint32_t w = tid; w < kHubBitWords; w += kSsspBlock) D.fbits[w] = 0u;
         for (int64_t v = (int64_t)D.H + tid; v < V; v += kSsspBlock) dist[v] = kInfBits;
         __syncthreads();
         { unsigned long long t = wall_clock64(); t_init += t - tk; tk = t; }
@@ -310,6 +329,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             while (nq > 0) {
                 iter++;
                 if (tid == 0) L.qtail = 0;
+                for (uint32_t w = tid; w < kHubBitWords; w += kSsspBlock) D.nbits[w] = 0u;
                 __syncthreads();
                 relax_queue<kRelaxUnroll>(cur, nq, g, L, D, stamp, fstamp, nxt, farq, iter, fep,
                                           thr, cap, stats, relax_local);
@@ -347,6 +367,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             const uint32_t fnew = fep + 1;
             iter++;
             if (tid == 0) L.qtail = 0;
+            for (uint32_t w = tid; w < kHubBitWords; w += kSsspBlock) D.fbits[w] = 0u;
             __syncthreads();
             uint32_t kept = 0;
             for (uint32_t base = 0; base < nf; base += kSsspBlock) {
@@ -363,10 +384,10 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 const uint32_t o = block_excl_scan(cls == 2 ? 1u : 0u, L, &tot);
                 if (cls == 2) {
                     farq[kept + o] = v;
-                    fstamp[v] = fnew;
+                    if (v < D.H) atomicOr(&D.fbits[v >> 5], 1u << (v & 31));
+                    else fstamp[v] = fnew;
                 }
                 wave_push(cls == 1, v, cur, &L.qtail, cap, stats);
-                if (cls == 1) stamp[v] = iter;
                 kept += tot;
                 __syncthreads();
             }
@@ -717,7 +738,9 @@ static int grid_for(int64_t n, int block) {
     return (int)g;
 }
 
-uint32_t sssp_hub_capacity() { return (uint32_t)((kSsspMaxLds - kLdsCtrlBytes) / 8); }
+uint32_t sssp_hub_capacity() {
+    return (uint32_t)((kSsspMaxLds - kLdsCtrlBytes - kLdsBitsBytes) / 8);
+}
 
 hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                             int nsrc, const uint32_t* d_targets, int A, double delta,
@@ -728,7 +751,7 @@ hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d
     uint32_t hubs = sssp_hub_capacity();
     if (hub_limit >= 0 && (uint32_t)hub_limit < hubs) hubs = (uint32_t)hub_limit;
     if ((int64_t)hubs > g.V) hubs = (uint32_t)g.V;
-    const size_t lds = kLdsCtrlBytes + (size_t)hubs * 8;
+    const size_t lds = kLdsCtrlBytes + kLdsBitsBytes + (size_t)hubs * 8;
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void*)sssp_rows_kernel,

@@ -237,6 +237,18 @@ class Topology:
         out["phase_ms"] = list(out["phase_ms"])
         return out
 
+    def export_graph(self):
+        """(V, eu, ev, elat, eloss, vloss) host arrays of the parsed graph (document order)."""
+        V, E = self.num_vertices, self.num_edges
+        eu = np.empty(E, np.int32)
+        ev = np.empty(E, np.int32)
+        el = np.empty(E, np.float64)
+        lo = np.empty(E, np.float64)
+        vl = np.empty(V, np.float64)
+        if self._lib.shdtopo_export_graph(self._h, _p(eu), _p(ev), _p(el), _p(lo), _p(vl)) != 0:
+            raise RuntimeError("export_graph failed")
+        return V, eu, ev, el, lo, vl
+
     def write_graphml(self, path):
         if self._lib.shdtopo_write_graphml(self._h, path.encode()) != 0:
             raise RuntimeError("write_graphml failed")
