@@ -123,8 +123,8 @@ struct _Topology {
     bool csrUploaded = false;
     std::vector<int32_t> perm;  // new -> old
     std::vector<int32_t> inv;   // old -> new
-    DevBuf<uint32_t> d_rowptr, d_col;
-    DevBuf<double> d_wt, d_aloss, d_vloss, d_selfLat, d_selfLoss;
+    DevBuf<uint32_t> d_rowptr, d_adj;
+    DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
     DevBuf<unsigned long long> d_dist, d_best, d_memo;
     DevBuf<uint32_t> d_stamp, d_fstamp, d_qa, d_qb, d_far, d_cnt, d_bslot, d_par, d_pathbuf,
         d_counters;
@@ -372,16 +372,22 @@ int upload_csr(Topology* top) {
     }
     for (int32_t i = 0; i < V; i++) vloss[(size_t)i] = g.vloss[(size_t)top->perm[(size_t)i]];
     HIPCHK(top->d_rowptr.ensure((size_t)V + 1));
-    HIPCHK(top->d_col.ensure(nadj));
-    HIPCHK(top->d_wt.ensure(nadj));
+    HIPCHK(top->d_adj.ensure(3 * nadj));
     HIPCHK(top->d_aloss.ensure(nadj));
     HIPCHK(top->d_vloss.ensure((size_t)V));
     HIPCHK(top->d_selfLat.ensure((size_t)V));
     HIPCHK(top->d_selfLoss.ensure((size_t)V));
     HIPCHK(hipMemcpy(top->d_rowptr.p, rowptr.data(), sizeof(uint32_t) * ((size_t)V + 1), hipMemcpyHostToDevice));
     if (nadj) {
-        HIPCHK(hipMemcpy(top->d_col.p, col.data(), sizeof(uint32_t) * nadj, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_wt.p, wt.data(), sizeof(double) * nadj, hipMemcpyHostToDevice));
+        std::vector<uint32_t> adj(3 * nadj);
+        for (size_t k = 0; k < nadj; k++) {
+            uint64_t wb;
+            memcpy(&wb, &wt[k], 8);
+            adj[3 * k] = col[k];
+            adj[3 * k + 1] = (uint32_t)wb;
+            adj[3 * k + 2] = (uint32_t)(wb >> 32);
+        }
+        HIPCHK(hipMemcpy(top->d_adj.p, adj.data(), sizeof(uint32_t) * 3 * nadj, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_aloss.p, aloss.data(), sizeof(double) * nadj, hipMemcpyHostToDevice));
     }
     HIPCHK(hipMemcpy(top->d_vloss.p, vloss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
@@ -394,10 +400,9 @@ int upload_csr(Topology* top) {
 DevCSR dev_csr(Topology* top) {
     DevCSR c;
     c.V = top->g.V;
-    c.nadj = (int64_t)top->d_col.n;
+    c.nadj = (int64_t)(top->d_adj.n / 3);
     c.rowptr = top->d_rowptr.p;
-    c.col = top->d_col.p;
-    c.wt = top->d_wt.p;
+    c.adj = top->d_adj.p;
     c.aloss = top->d_aloss.p;
     c.vloss = top->d_vloss.p;
     c.selfLat = top->d_selfLat.p;

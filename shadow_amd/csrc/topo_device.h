@@ -2,7 +2,7 @@
 //
 // HBM layout (all arrays in the degree-relabelled vertex order, see DESIGN.md "Data layout"):
 //   CSR of the undirected topology without self loops:
-//     rowptr u32[V+1], col u32[2E'], wt f64[2E'] (edge latency), aloss f64[2E'] (edge loss)
+//     rowptr u32[V+1], adj {u32 col, f64 latency}[2E'] (12-B AoS), aloss f64[2E'] (edge loss)
 //   per vertex: vloss f64[V], selfLat f64[V] (NaN = no self loop), selfLoss f64[V]
 //   per SSSP slot (one workgroup = one source at a time): 56 B x V of workspace
 //   routing table: {f64 lat, f64 rel}[A][A] (16-B records, one gather per packet) + u16 hops
@@ -39,8 +39,7 @@ struct DevCSR {
     int32_t V = 0;
     int64_t nadj = 0;
     const uint32_t* rowptr = nullptr;
-    const uint32_t* col = nullptr;
-    const double* wt = nullptr;
+    const uint32_t* adj = nullptr;  // 12-B records {u32 col, f64 wt (two words)}: one line per short row
     const double* aloss = nullptr;
     const double* vloss = nullptr;
     const double* selfLat = nullptr;

@@ -40,6 +40,16 @@ __device__ __forceinline__ uint32_t ld_l2_u32(const uint32_t* p) {
 __device__ __forceinline__ double bits2d(unsigned long long b) { return __longlong_as_double((long long)b); }
 __device__ __forceinline__ unsigned long long d2bits(double d) { return (unsigned long long)__double_as_longlong(d); }
 
+struct __attribute__((packed, aligned(4))) W3 {
+    uint32_t a, b, c;
+};
+__device__ __forceinline__ uint32_t adj_col(const DevCSR& g, uint32_t j) { return g.adj[3ull * j]; }
+__device__ __forceinline__ void adj_load(const DevCSR& g, uint32_t j, uint32_t& col, double& wt) {
+    const W3 r = *reinterpret_cast<const W3*>(g.adj + 3ull * j);
+    col = r.a;
+    wt = __hiloint2double((int)r.c, (int)r.b);
+}
+
 struct Lds {
     uint32_t off[kSsspBlock + 4];
     uint32_t rs[kSsspBlock];
@@ -215,8 +225,11 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
                     }
                 }
                 const uint32_t j = valid[u] ? L.rs[lo] + (e - L.off[lo]) : 0u;
-                n[u] = valid[u] ? g.col[j] : 0u;
-                ab[u] = valid[u] ? d2bits(__dadd_rn(L.val[lo], g.wt[j])) : ~0ull;
+                uint32_t c = 0u;
+                double w = 0.0;
+                if (valid[u]) adj_load(g, j, c, w);
+                n[u] = c;
+                ab[u] = valid[u] ? d2bits(__dadd_rn(L.val[lo], w)) : ~0ull;
             }
             unsigned long long cur[U];
 #pragma unroll
@@ -432,9 +445,11 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 },
                 [&](uint32_t v, double dv, uint32_t j, bool valid) {
                     if (!valid) return;
-                    const uint32_t u = g.col[j];
+                    uint32_t u;
+                    double w;
+                    adj_load(g, j, u, w);
                     const unsigned long long du = D.get(u);
-                    if (__dadd_rn(bits2d(du), g.wt[j]) == dv) {
+                    if (__dadd_rn(bits2d(du), w) == dv) {
                         atomicMin(&best[v], du);
                         atomicAdd(&cntc[v], 1u);
                         atomicMin(&bslot[v], j);
@@ -469,9 +484,11 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                     },
                     [&](uint32_t v, double dv, uint32_t j, bool valid) {
                         if (!valid) return;
-                        const uint32_t u = g.col[j];
+                        uint32_t u;
+                        double w;
+                        adj_load(g, j, u, w);
                         const unsigned long long du = D.get(u);
-                        if (__dadd_rn(bits2d(du), g.wt[j]) == dv && du == ld_l2_u64(&best[v])) {
+                        if (__dadd_rn(bits2d(du), w) == dv && du == ld_l2_u64(&best[v])) {
                             atomicAdd(&cntc[v], 1u);
                             atomicMin(&bslot[v], j);
                         }
@@ -487,7 +504,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                     par[v] = src;
                 } else {
                     memo[v] = mtag | (c > 1 ? 0x80000000ull : 0ull) | (unsigned long long)j;
-                    par[v] = g.col[j];
+                    par[v] = adj_col(g, j);
                 }
             }
             __syncthreads();

