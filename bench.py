@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""bench.py -- routing-table build GTEPS + packet-routes/s on 1..8 MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs 4 + 5; synthetic, generated in memory):
+  * C4: power-law Internet topology, 990,000 routers + 10,000 poi, exactly 10,000,000 undirected
+    edges (Chung-Lu, deduplicated, spanning path, poi uplinks + self loops), seed 20261015;
+  * C5: 100,000 Tor-like hosts attached by type hint (94/5/1 % client/relay/server) through
+    Shadow's seed chain; one scheduler window of 10,000,000 packets.
+A step = one build of the whole attached-vertex routing table (all A ~ 10^4 sources x A targets:
+near-far SSSP + parent/epilogue kernel per source, rows sharded over the ranks, RCCL all-gather of
+the rows, all-reduce(MIN) of the runahead minimum, table installed in the library).
+value = A * E / t_step / 1e9 (Graph500 SSSP convention, undirected E) = GTEPS, whole job.
+Packet routes are timed separately over resident windows and reported as packet_routes_per_s.
+
+Launch: python bench.py [--gpus 1 --steps K --warmup W]   or, for N > 1,
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import shadow_amd as sa  # noqa: E402
+from shadow_amd import sharding  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SEED = 20261015
+
+
+def log(rank, *a):
+    if rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(top, attached, n_sample, nthreads):
+    """The reference path's CPU restatement (oracle: igraph-0.7 binary-heap Dijkstra + helper),
+    timed on this host on a bounded sample of sources; extrapolated linearly by source count."""
+    import oracle
+    V, eu, ev, elat, eloss, vloss = top.export_graph()
+    t0 = time.time()
+    g = oracle.OGraph(V, eu, ev, elat, eloss, vloss)
+    t_setup = time.time() - t0
+    srcs = attached[:n_sample]
+    t0 = time.time()
+    g.source_rows(srcs, attached, nthreads=nthreads)
+    t = time.time() - t0
+    E = len(eu)
+    return dict(value=len(srcs) * E / t / 1e9, unit="GTEPS", cores=nthreads, kind="port",
+                sample="%d of %d sources x %d targets (Dijkstra + per-target helper), %.1f s, "
+                       "extrapolated linearly to the full table: %.0f s" %
+                       (len(srcs), len(attached), len(attached), t, t / len(srcs) * len(attached)),
+                seconds_per_source=t / len(srcs), oracle_setup_s=t_setup)
+
+
+def cpu_route_baseline(lat, rel, payload, state, now, jump):
+    import oracle
+    t0 = time.time()
+    oracle.route_packets(lat, rel, payload, state, now, jump, 1)
+    return len(lat) / (time.time() - t0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--routers", type=int, default=990_000)
+    ap.add_argument("--poi", type=int, default=10_000)
+    ap.add_argument("--edges", type=int, default=10_000_000)
+    ap.add_argument("--hosts", type=int, default=100_000)
+    ap.add_argument("--packets", type=int, default=10_000_000)
+    ap.add_argument("--route-steps", type=int, default=20)
+    ap.add_argument("--cpu-sample", type=int, default=8, help="sources timed on the CPU")
+    ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--delta", type=float, default=0.0)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_sssp_pmc.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    # ---- workload (identical on every rank; generation is outside the timed region) ----
+    t0 = time.time()
+    top = sa.Topology.synthetic(seed=SEED, n_routers=args.routers, n_poi=args.poi,
+                                n_edges=args.edges)
+    top.set_option("device", local)
+    if args.delta:
+        top.set_option("delta", args.delta)
+    window0 = 10_000_000  # Shadow's default 10 ms window until the runahead is known
+    pk = top.synth_packets(SEED, args.hosts, args.packets, 10**9, window0)
+    attached = top.attached_vertices()
+    A, V, E = len(attached), top.num_vertices, top.num_edges
+    log(rank, "workload ready in %.1fs: V=%d E=%d A=%d packets=%d" %
+        (time.time() - t0, V, E, A, args.packets))
+
+    table = sharding.ShardedTable(A, rank, world, dev)
+    builder = sharding.hip_builder(top)
+    kernel_ms = []
+
+    def step():
+        table.build(builder)
+        kernel_ms.append(top.stats()["sssp_kernel_ms"])
+        table.exchange()
+        lr, hops = table.table()
+        top.bind_table(lr, hops, float(table.gmin.item()),
+                       stream=torch.cuda.current_stream().cuda_stream)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    kernel_ms.clear()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    t_step = float(elapsed.item()) / args.steps
+    st = top.stats()
+    gmin = float(table.gmin.item())
+    jump = int(gmin) * 1_000_000 if gmin >= 1.0 else window0   # shd-master.c:113-124
+    gteps = A * E / t_step / 1e9
+
+    # ---- packet routes: this rank's slice of the window, inputs resident in HBM ----
+    p0, p1 = sharding.packet_range(args.packets, rank, world)
+    cu = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    d_src = cu(pk["src_col"][p0:p1])
+    d_dst = cu(pk["dst_col"][p0:p1])
+    d_pay = cu(pk["payload"][p0:p1].view(np.int32))
+    d_sin = cu(pk["state_in"][p0:p1].view(np.int32))
+    d_now = cu(pk["now"][p0:p1].view(np.int64))
+    n = p1 - p0
+    t_out = torch.empty(n, dtype=torch.int64, device=dev)
+    s_out = torch.empty(n, dtype=torch.int32, device=dev)
+    d_out = torch.empty(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    route_ms = []
+    for i in range(2 + args.route_steps):
+        if i == 2:
+            barrier()
+            tr0 = time.perf_counter()
+        top.route_batch_device(d_src, d_dst, d_pay, d_sin, d_now, jump, 1, t_out, s_out, d_out,
+                               stream=stream)
+        if i >= 2:
+            route_ms.append(top.stats()["route_kernel_ms"])
+    barrier()
+    rel_t = torch.tensor([time.perf_counter() - tr0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(rel_t, op=dist.ReduceOp.MAX)
+    t_window = float(rel_t.item()) / args.route_steps
+    routes_per_s = args.packets / t_window
+
+    if rank == 0:
+        # roofline of the dominant kernel (sssp_rows_kernel), algorithmic bytes per source =
+        # 2E (4 B col + 8 B weight) + V (4 B rowptr + 8 B dist read + 8 B dist write)
+        rows = table.r1 - table.r0
+        b_src = 24 * E + 20 * V
+        k_s = float(np.mean(kernel_ms)) / 1e3
+        achieved = rows * b_src / k_s / 1e9
+        traffic = None
+        pmc_note = None
+        if os.path.exists(args.pmc_json):
+            try:
+                pm = json.load(open(args.pmc_json))
+                if pm.get("config_key") == "C4-%d-%d-%d-rows%d" % (V, E, A, rows):
+                    traffic = pm["hbm_bytes_per_launch"]
+                    pmc_note = pm.get("source")
+            except Exception:
+                traffic = None
+        roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS,
+                        unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic,
+                        kernel="sssp_rows_kernel", kernel_ms=round(k_s * 1e3, 3),
+                        units_per_launch=rows, bytes_per_unit=b_src, pmc=pmc_note)
+        r_ms = float(np.mean(route_ms))
+        route_roof = dict(bound="hbm", kernel="packet_route_kernel", kernel_ms=round(r_ms, 4),
+                          achieved=round(n * 53 / (r_ms / 1e3) / 1e9, 1), peak=HBM_PEAK_GBS,
+                          unit="GB/s", bytes_per_unit=53, units_per_launch=n)
+        route_roof["frac"] = round(route_roof["achieved"] / HBM_PEAK_GBS, 4)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            log(rank, "cpu baseline: %d sources on %d thread(s)..." % (args.cpu_sample,
+                                                                        args.cpu_threads))
+            cpu = cpu_baseline(top, attached, args.cpu_sample, args.cpu_threads)
+            nr = min(args.packets, 2_000_000)
+            a_, lat_t, rel_t_, _ = top.table()
+            cpu["packet_routes_per_s"] = cpu_route_baseline(
+                lat_t[pk["src_col"][:nr], pk["dst_col"][:nr]],
+                rel_t_[pk["src_col"][:nr], pk["dst_col"][:nr]], pk["payload"][:nr],
+                pk["state_in"][:nr], pk["now"][:nr], jump)
+            cpu["host_nproc"] = os.cpu_count()
+        out = {
+            "metric": "routing-table build GTEPS + packet-routes/sec at 1/2/4/8 MI355X "
+                      "(%HBM roofline)",
+            "value": round(gteps, 3),
+            "unit": "GTEPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_step * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": "C4 synthetic power-law topology (1M vertices / 10M undirected edges, "
+                            "seed 20261015): full attached-vertex table, all %d sources x %d "
+                            "targets; C5: %d hosts, %d packets per window" %
+                            (A, A, args.hosts, args.packets),
+                "vertices": V, "edges": E, "sources": A, "targets": A,
+                "packets_per_window": args.packets, "hosts": args.hosts,
+                "parallelism": "sources sharded /%d, RCCL all-gather + all-reduce(min)" % world,
+            },
+            "packet_routes_per_s": round(routes_per_s, 1),
+            "ms_per_window": round(t_window * 1e3, 4),
+            "roofline": roofline,
+            "route_roofline": route_roof,
+            "cpu_baseline": cpu,
+            "runahead_min_latency_ms": gmin,
+            "ambiguous_pairs": st["ambiguous_pairs"],
+            "slots": st["slots"],
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

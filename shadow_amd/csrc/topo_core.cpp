@@ -486,7 +486,7 @@ double default_delta(Topology* top) {
     for (int64_t e = 0; e < g.E; e++)
         if (g.eu[(size_t)e] != g.ev[(size_t)e]) { s += g.elat[(size_t)e]; n++; }
     double mean = n ? s / (double)n : 1.0;
-    return std::max(1e-9, 0.25 * mean);
+    return std::max(1e-9, 0.08 * mean);  // ~4 ms on the C4 topology (tuned, profiles/)
 }
 
 // Enqueue rows [row0,row1) into out buffers (device pointers) on `st`.
