@@ -155,6 +155,8 @@ typedef struct {
     int64_t near_iterations;  /* near-phase iterations summed over sources */
     int64_t far_splits;       /* far-pile splits summed over sources */
     int64_t slots;            /* concurrent SSSP workgroups of the last launch */
+    int64_t events[8];        /* expanded vertices, tail relaxations, tail improvements, far
+                                 entries scanned, far entries kept, parent-pass vertices */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -576,6 +576,7 @@ int collect_row_stats(Topology* top) {
     }
     top->stats.near_iterations = (int64_t)h[ST_NEAR_IT];
     top->stats.far_splits = (int64_t)h[ST_SPLITS];
+    for (int i = 0; i < 8; i++) top->stats.events[i] = i < 6 ? (int64_t)h[ST_EV0 + i] : 0;
     top->stats.slots = top->isComplete ? 0 : top->slots;
     double gm;
     memcpy(&gm, &h[ST_GLOBAL_MIN], sizeof gm);

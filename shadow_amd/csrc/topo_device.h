@@ -32,7 +32,10 @@ enum StatIdx {
     ST_T_TARGET = 10,   //   per-target latency / reliability / hops
     ST_NEAR_IT = 11,    // near-phase iterations
     ST_SPLITS = 12,     // far-pile splits
-    ST_COUNT = 16
+    ST_EV0 = 13,        // event counters (ShdStats.events): expanded vertices, tail relaxations,
+                        // tail improvements, far entries scanned, far entries kept, parent-pass
+                        // vertices
+    ST_COUNT = 24
 };
 
 struct DevCSR {

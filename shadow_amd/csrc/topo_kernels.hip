@@ -61,6 +61,7 @@ struct Lds {
     uint32_t src_idx;
     uint32_t pad0;
     unsigned long long dmin;
+    unsigned long long fmin;  // lower bound of the far pile's live distances
     unsigned long long relax;
 };
 constexpr size_t kLdsCtrlBytes = (sizeof(Lds) + 15) / 16 * 16;
@@ -173,7 +174,7 @@ struct DistView {
     unsigned long long* hd;    // LDS, H words
     unsigned long long* dist;  // HBM, V words (words < H unused while the source runs)
     uint32_t* nbits;           // LDS: hub already in the next near queue (this iteration)
-    uint32_t* fbits;           // LDS: hub already in the far pile (this far epoch)
+    uint32_t* fbits;           // LDS: hub currently in the far pile
     uint32_t H;
     __device__ __forceinline__ unsigned long long get(uint32_t v) const {
         return v < H ? hd[v] : ld_l2_u64(&dist[v]);
@@ -189,7 +190,8 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
                                             uint32_t* fstamp, uint32_t* nxt, uint32_t* farq,
                                             uint32_t it, uint32_t fe, double th, uint32_t cap,
                                             unsigned long long* stats,
-                                            unsigned long long& relax) {
+                                            unsigned long long& relax,
+                                            unsigned long long* ev) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     for (uint32_t base = 0; base < nq; base += kSsspBlock) {
@@ -244,6 +246,18 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
 #pragma unroll
             for (int u = 0; u < U; u++)
                 if (ab[u] < cur[u]) imp[u] = ab[u] < atomicMin(&D.dist[n[u]], ab[u]);
+            // every far-side improvement lowers the far pile's running minimum (LDS), so the
+            // split needs no extra pass over the pile
+            unsigned long long fm = kInfBits;
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (imp[u] && !(bits2d(ab[u]) < th) && ab[u] < fm) fm = ab[u];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long y = __shfl_xor(fm, o, 64);
+                fm = y < fm ? y : fm;
+            }
+            if (lane == 0 && fm != kInfBits) atomicMin(&L.fmin, fm);
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 bool pN = false, pF = false;
@@ -264,6 +278,8 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
                 wave_push(pN, n[u], nxt, &L.qtail, cap, stats);
                 wave_push(pF, n[u], farq, &L.ftail, cap, stats);
                 relax += valid[u] ? 1ull : 0ull;
+                ev[1] += (valid[u] && n[u] >= D.H) ? 1ull : 0ull;
+                ev[2] += (imp[u] && n[u] >= D.H) ? 1ull : 0ull;
             }
         }
         __syncthreads();
@@ -306,6 +322,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     // slot-persistent epoch counters (never reset, so stamp/fstamp/memo need no clearing)
     uint32_t iter = ctr[0], fep = ctr[1], mep = ctr[2];
     unsigned long long relax_local = 0;
+    unsigned long long ev[6] = {0, 0, 0, 0, 0, 0};
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, n_near = 0, n_split = 0;
     unsigned long long tk = wall_clock64();
 
@@ -331,6 +348,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             qa[0] = src;
             stamp[src] = iter;
             L.ftail = 0;
+            L.fmin = kInfBits;
         }
         __syncthreads();
         uint32_t* cur = qa;
@@ -344,8 +362,9 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 if (tid == 0) L.qtail = 0;
                 for (uint32_t w = tid; w < kHubBitWords; w += kSsspBlock) D.nbits[w] = 0u;
                 __syncthreads();
+                ev[0] += (tid == 0) ? nq : 0u;
                 relax_queue<kRelaxUnroll>(cur, nq, g, L, D, stamp, fstamp, nxt, farq, iter, fep,
-                                          thr, cap, stats, relax_local);
+                                          thr, cap, stats, relax_local, ev);
                 // relax_queue ends with a barrier
                 nq = min(L.qtail, cap);
                 nf = min(L.ftail, cap);
@@ -355,58 +374,58 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 __syncthreads();
             }
             if (nf == 0) break;
-            // split the far pile: next threshold from the smallest live far distance
-            if (tid == 0) L.dmin = kInfBits;
-            __syncthreads();
-            {
-                unsigned long long m = kInfBits;
-                for (uint32_t i = tid; i < nf; i += kSsspBlock) {
-                    const unsigned long long d = D.get(farq[i]);
-                    if (bits2d(d) >= thr && d < m) m = d;
-                }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    unsigned long long y = __shfl_xor(m, o, 64);
-                    m = y < m ? y : m;
-                }
-                if ((tid & 63) == 0 && m != kInfBits) atomicMin(&L.dmin, m);
-            }
-            __syncthreads();
-            const unsigned long long dminb = L.dmin;
-            if (dminb == kInfBits) break;
+            // Split the far pile.  L.fmin is <= every live entry's distance (it saw every far-side
+            // improvement and every kept entry), so [thr, max(fmin, thr) + delta) holds at least
+            // the smallest live entry.  One pass classifies on the true distances: drop (< thr:
+            // already expanded when it went below thr), near, or keep.  "In the far pile" is a
+            // per-source flag (fstamp == fep / LDS bit for hubs) cleared on removal, so kept
+            // entries need no rewrite.
             n_split++;
+            ev[3] += (tid == 0) ? nf : 0u;
+            const unsigned long long fminb = L.fmin;
             const double oldthr = thr;
-            const double newthr = __dadd_rn(bits2d(dminb), delta);
-            const uint32_t fnew = fep + 1;
+            const double newthr = __dadd_rn(fmax(bits2d(fminb), thr), delta);
             iter++;
-            if (tid == 0) L.qtail = 0;
-            for (uint32_t w = tid; w < kHubBitWords; w += kSsspBlock) D.fbits[w] = 0u;
+            __syncthreads();
+            if (tid == 0) {
+                L.qtail = 0;
+                L.fmin = kInfBits;
+            }
             __syncthreads();
             uint32_t kept = 0;
             for (uint32_t base = 0; base < nf; base += kSsspBlock) {
                 const uint32_t i = base + tid;
                 uint32_t v = 0;
                 int cls = 0;  // 0 drop, 1 near, 2 keep
+                unsigned long long db = kInfBits;
                 if (i < nf) {
                     v = farq[i];
-                    const double d = bits2d(D.get(v));
+                    db = D.get(v);
+                    const double d = bits2d(db);
                     cls = d < oldthr ? 0 : (d < newthr ? 1 : 2);
+                    if (cls != 2) {  // leaves the far pile
+                        if (v < D.H) atomicAnd(&D.fbits[v >> 5], ~(1u << (v & 31)));
+                        else fstamp[v] = 0u;
+                    }
                 }
                 __syncthreads();  // every lane has read its chunk entry before compaction writes
                 uint32_t tot;
                 const uint32_t o = block_excl_scan(cls == 2 ? 1u : 0u, L, &tot);
-                if (cls == 2) {
-                    farq[kept + o] = v;
-                    if (v < D.H) atomicOr(&D.fbits[v >> 5], 1u << (v & 31));
-                    else fstamp[v] = fnew;
+                if (cls == 2) farq[kept + o] = v;
+                unsigned long long km = cls == 2 ? db : kInfBits;
+#pragma unroll
+                for (int s = 32; s > 0; s >>= 1) {
+                    const unsigned long long y = __shfl_xor(km, s, 64);
+                    km = y < km ? y : km;
                 }
+                if ((tid & 63) == 0 && km != kInfBits) atomicMin(&L.fmin, km);
                 wave_push(cls == 1, v, cur, &L.qtail, cap, stats);
                 kept += tot;
                 __syncthreads();
             }
             nq = min(L.qtail, cap);
             nf = kept;
-            fep = fnew;
+            ev[4] += (tid == 0) ? kept : 0u;
             thr = newthr;
             if (tid == 0) L.ftail = kept;
             __syncthreads();
@@ -437,6 +456,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         uint32_t nF = min(L.qtail, cap);
         __syncthreads();
         while (nF > 0) {
+            ev[5] += (tid == 0) ? nF : 0u;
             expand_queue(
                 cur, nF, g, L,
                 [&](uint32_t v, double& val) {
@@ -629,6 +649,13 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         atomicAdd(&stats[ST_T_TARGET], t_tgt);
         atomicAdd(&stats[ST_NEAR_IT], n_near);
         atomicAdd(&stats[ST_SPLITS], n_split);
+    }
+    // per-lane event counts -> one atomic per wave
+    for (int k = 0; k < 6; k++) {
+        unsigned long long x = ev[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        if ((tid & 63) == 0 && x) atomicAdd(&stats[ST_EV0 + k], x);
     }
 }
 

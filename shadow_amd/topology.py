@@ -235,6 +235,8 @@ class Topology:
             raise RuntimeError("shdtopo_get_stats failed: %d" % r)
         out = {k: getattr(s, k) for k, _ in L.ShdStats._fields_}
         out["phase_ms"] = list(out["phase_ms"])
+        out["events"] = dict(zip(("expanded", "tail_relax", "tail_improve", "far_scanned",
+                                  "far_kept", "parent_vertices"), list(out["events"])[:6]))
         return out
 
     def export_graph(self):

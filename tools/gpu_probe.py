@@ -51,6 +51,8 @@ for rep in range(args.reps):
           "splits/src %.0f slots %d" % tuple([x / rows for x in ph] +
                                             [st["near_iterations"] / rows,
                                              st["far_splits"] / rows, st["slots"]]), flush=True)
+    print("   per-source events:", {k: "%.3g" % (v / rows) for k, v in st["events"].items()},
+          flush=True)
 x = lr[..., 0].cpu().numpy()
 print("lat min %.4f max %.4f mean %.3f" % (x.min(), x.max(), x.mean()))
 h = hp.cpu().numpy()
