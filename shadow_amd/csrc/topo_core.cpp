@@ -102,6 +102,7 @@ struct _Topology {
     int slotsOpt = 0;
     int device = 0;
     int64_t hubLimit = -1;  // LDS-cached hub distances (-1 = fill the LDS)
+    int64_t parHubs = 2048; // hubs whose parent is hinted during the SSSP (0 = always scan)
 
     // attach state (shd-topology.c:20-24 virtualIP)
     std::shared_mutex ipMu;
@@ -121,6 +122,7 @@ struct _Topology {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     bool csrUploaded = false;
+    bool rowsSorted = false;
     std::vector<int32_t> perm;  // new -> old
     std::vector<int32_t> inv;   // old -> new
     DevBuf<uint32_t> d_rowptr, d_adj;
@@ -349,7 +351,8 @@ int upload_csr(Topology* top) {
     }
     // each row sorted by neighbour: a hub's expansion then walks the distance array in address
     // order (neighbours sharing a line coalesce, DRAM pages are reused)
-    if (getenv("SHDTOPO_NO_ROWSORT") == nullptr) {
+    top->rowsSorted = getenv("SHDTOPO_NO_ROWSORT") == nullptr;
+    if (top->rowsSorted) {
         std::vector<uint32_t> idx;
         std::vector<uint32_t> c2;
         std::vector<double> w2, l2;
@@ -407,6 +410,7 @@ DevCSR dev_csr(Topology* top) {
     c.vloss = top->d_vloss.p;
     c.selfLat = top->d_selfLat.p;
     c.selfLoss = top->d_selfLoss.p;
+    c.rows_sorted = top->rowsSorted ? 1 : 0;
     return c;
 }
 
@@ -486,7 +490,7 @@ double default_delta(Topology* top) {
     for (int64_t e = 0; e < g.E; e++)
         if (g.eu[(size_t)e] != g.ev[(size_t)e]) { s += g.elat[(size_t)e]; n++; }
     double mean = n ? s / (double)n : 1.0;
-    return std::max(1e-9, 0.08 * mean);  // ~4 ms on the C4 topology (tuned, profiles/)
+    return std::max(1e-9, 0.06 * mean);  // ~3 ms on the C4 topology (tuned, profiles/)
 }
 
 // Enqueue rows [row0,row1) into out buffers (device pointers) on `st`.
@@ -544,6 +548,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         HIPCHK(hipEventRecord(top->ev0, st));
         HIPCHK(launch_sssp_rows(dev_csr(top), slot_ws(top), top->d_sources.p, (int)rows,
                                 top->d_targets.p, (int)A, default_delta(top), top->hubLimit,
+                                (uint32_t)top->parHubs,
                                 out_lr, out_hops,
                                 out_rowmin, top->d_stats.p, st));
         HIPCHK(hipEventRecord(top->ev1, st));
@@ -576,7 +581,7 @@ int collect_row_stats(Topology* top) {
     }
     top->stats.near_iterations = (int64_t)h[ST_NEAR_IT];
     top->stats.far_splits = (int64_t)h[ST_SPLITS];
-    for (int i = 0; i < 8; i++) top->stats.events[i] = i < 6 ? (int64_t)h[ST_EV0 + i] : 0;
+    for (int i = 0; i < 8; i++) top->stats.events[i] = (int64_t)h[ST_EV0 + i];
     top->stats.slots = top->isComplete ? 0 : top->slots;
     double gm;
     memcpy(&gm, &h[ST_GLOBAL_MIN], sizeof gm);
@@ -879,6 +884,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "slots") top->slotsOpt = (int)value;
     else if (k == "device") top->device = (int)value;
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
+    else if (k == "par_hubs") top->parHubs = (int64_t)value;
     else return -1;
     return 0;
 }

@@ -47,6 +47,7 @@ struct DevCSR {
     const double* vloss = nullptr;
     const double* selfLat = nullptr;
     const double* selfLoss = nullptr;
+    int rows_sorted = 0;  // adjacency rows ascending by neighbour (enables binary row search)
 };
 
 // per-slot workspace, slot-major: array + slot * V
@@ -71,8 +72,9 @@ struct SlotWs {
 // hub_limit: cap on LDS-cached vertices (-1 = as many as fit, ~18k)
 hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                             int nsrc, const uint32_t* d_targets, int A, double delta,
-                            int64_t hub_limit, double2* out_lr, uint16_t* out_hops,
-                            double* out_rowmin, unsigned long long* d_stats, hipStream_t stream);
+                            int64_t hub_limit, uint32_t par_hubs, double2* out_lr,
+                            uint16_t* out_hops, double* out_rowmin, unsigned long long* d_stats,
+                            hipStream_t stream);
 uint32_t sssp_hub_capacity();
 
 hipError_t launch_pair_table_complete(int A, int64_t row0, int64_t rows, const double* elatAA,

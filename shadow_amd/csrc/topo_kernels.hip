@@ -66,7 +66,8 @@ struct Lds {
 };
 constexpr size_t kLdsCtrlBytes = (sizeof(Lds) + 15) / 16 * 16;
 constexpr uint32_t kHubBitWords = 640;  // queue-dedupe bitmaps for up to 20480 LDS hubs
-constexpr size_t kLdsBitsBytes = 2 * kHubBitWords * 4;
+constexpr uint32_t kParHubs = 2048;      // hubs whose parent is tracked during the SSSP
+constexpr size_t kLdsBitsBytes = 2 * kHubBitWords * 4 + kParHubs / 8 + kParHubs * 4;
 constexpr size_t kSsspMaxLds = 160 * 1024;  // one workgroup per CU owns the whole LDS
 constexpr int kRelaxUnroll = 4;
 static_assert((kSsspMaxLds - kLdsCtrlBytes - kLdsBitsBytes) / 8 <= kHubBitWords * 32,
@@ -175,7 +176,10 @@ struct DistView {
     unsigned long long* dist;  // HBM, V words (words < H unused while the source runs)
     uint32_t* nbits;           // LDS: hub already in the next near queue (this iteration)
     uint32_t* fbits;           // LDS: hub currently in the far pile
+    uint32_t* hpar;            // LDS: vertex whose relaxation last lowered hub v (v < kParHubs)
+    uint32_t* tbits;           // LDS: a relaxation tied hub v's current distance (v < kParHubs)
     uint32_t H;
+    uint32_t P;                // hubs with parent hints (<= kParHubs)
     __device__ __forceinline__ unsigned long long get(uint32_t v) const {
         return v < H ? hd[v] : ld_l2_u64(&dist[v]);
     }
@@ -188,7 +192,8 @@ template <int U>
 __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, const DevCSR& g,
                                             Lds& L, const DistView& D, uint32_t* stamp,
                                             uint32_t* fstamp, uint32_t* nxt, uint32_t* farq,
-                                            uint32_t it, uint32_t fe, double th, uint32_t cap,
+                                            uint32_t it, uint32_t fe, double th, double lb,
+                                            uint32_t cap,
                                             unsigned long long* stats,
                                             unsigned long long& relax,
                                             unsigned long long* ev) {
@@ -211,7 +216,7 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
         if (tid == 0) L.off[cnt] = total;
         __syncthreads();
         for (uint32_t eb = tid - lane; eb < total; eb += kSsspBlock * U) {
-            uint32_t n[U];
+            uint32_t n[U], from[U];
             unsigned long long ab[U];
             bool valid[U];
 #pragma unroll
@@ -231,6 +236,7 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
                 double w = 0.0;
                 if (valid[u]) adj_load(g, j, c, w);
                 n[u] = c;
+                from[u] = L.vx[lo];
                 ab[u] = valid[u] ? d2bits(__dadd_rn(L.val[lo], w)) : ~0ull;
             }
             unsigned long long cur[U];
@@ -241,7 +247,14 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 imp[u] = false;
-                if (valid[u] && n[u] < D.H) imp[u] = ab[u] < atomicMin(&D.hd[n[u]], ab[u]);
+                if (valid[u] && n[u] < D.H) {
+                    const unsigned long long old = atomicMin(&D.hd[n[u]], ab[u]);
+                    imp[u] = ab[u] < old;
+                    if (n[u] < D.P) {  // parent hint for the heaviest rows (see epilogue)
+                        if (imp[u]) D.hpar[n[u]] = from[u];
+                        else if (ab[u] == old) atomicOr(&D.tbits[n[u] >> 5], 1u << (n[u] & 31));
+                    }
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; u++)
@@ -280,6 +293,7 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
                 relax += valid[u] ? 1ull : 0ull;
                 ev[1] += (valid[u] && n[u] >= D.H) ? 1ull : 0ull;
                 ev[2] += (imp[u] && n[u] >= D.H) ? 1ull : 0ull;
+                ev[6] += (valid[u] && n[u] >= D.H && bits2d(cur[u]) < lb) ? 1ull : 0ull;
             }
         }
         __syncthreads();
@@ -291,6 +305,7 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
 __global__ void __launch_bounds__(kSsspBlock)
 sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int nsrc,
                  const uint32_t* __restrict__ targets, int A, double delta, uint32_t hubs,
+                 uint32_t parhubs,
                  double2* __restrict__ out_lr, uint16_t* __restrict__ out_hops,
                  double* __restrict__ out_rowmin, unsigned long long* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -301,9 +316,12 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     DistView D;
     D.nbits = reinterpret_cast<uint32_t*>(smem + kLdsCtrlBytes);
     D.fbits = D.nbits + kHubBitWords;
+    D.tbits = D.fbits + kHubBitWords;
+    D.hpar = D.tbits + kParHubs / 32;
     D.hd = reinterpret_cast<unsigned long long*>(smem + kLdsCtrlBytes + kLdsBitsBytes);
     D.dist = ws.dist + (size_t)slot * V;
     D.H = hubs;
+    D.P = parhubs < kParHubs ? parhubs : kParHubs;
     unsigned long long* dist = D.dist;
     uint32_t* stamp = ws.stamp + (size_t)slot * V;
     uint32_t* fstamp = ws.fstamp + (size_t)slot * V;
@@ -322,7 +340,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     // slot-persistent epoch counters (never reset, so stamp/fstamp/memo need no clearing)
     uint32_t iter = ctr[0], fep = ctr[1], mep = ctr[2];
     unsigned long long relax_local = 0;
-    unsigned long long ev[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, n_near = 0, n_split = 0;
     unsigned long long tk = wall_clock64();
 
@@ -338,6 +356,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         // ---------------- SSSP (near-far) ----------------
         for (uint32_t v = tid; v < D.H; v += kSsspBlock) D.hd[v] = kInfBits;
         for (uint32_t w = tid; w < kHubBitWords; w += kSsspBlock) D.fbits[w] = 0u;
+        for (uint32_t w = tid; w < kParHubs / 32; w += kSsspBlock) D.tbits[w] = 0u;
         for (int64_t v = (int64_t)D.H + tid; v < V; v += kSsspBlock) dist[v] = kInfBits;
         __syncthreads();
         { unsigned long long t = wall_clock64(); t_init += t - tk; tk = t; }
@@ -355,6 +374,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         uint32_t* nxt = qb;
         uint32_t nq = 1, nf = 0;
         double thr = delta;
+        double lb = 0.0;  // every vertex with d < lb is final (the last completed bucket)
         uint32_t guard = 0;
         for (;;) {
             while (nq > 0) {
@@ -364,7 +384,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 __syncthreads();
                 ev[0] += (tid == 0) ? nq : 0u;
                 relax_queue<kRelaxUnroll>(cur, nq, g, L, D, stamp, fstamp, nxt, farq, iter, fep,
-                                          thr, cap, stats, relax_local, ev);
+                                          thr, lb, cap, stats, relax_local, ev);
                 // relax_queue ends with a barrier
                 nq = min(L.qtail, cap);
                 nf = min(L.ftail, cap);
@@ -426,6 +446,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             nq = min(L.qtail, cap);
             nf = kept;
             ev[4] += (tid == 0) ? kept : 0u;
+            lb = oldthr;
             thr = newthr;
             if (tid == 0) L.ftail = kept;
             __syncthreads();
@@ -457,8 +478,50 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         __syncthreads();
         while (nF > 0) {
             ev[5] += (tid == 0) ? nF : 0u;
+            // Heavy hubs first: the SSSP recorded which vertex last lowered each of the first
+            // kParHubs hubs and whether any relaxation tied its value.  Every candidate u of v
+            // relaxes v with fl(d[u]+w) == d[v] when u is expanded at its final distance, so
+            // "no tie seen" + "the recorded u is a candidate" means u is the only candidate:
+            // the igraph parent, found without scanning the hub's (up to 10^5-entry) row.
+            // Anything else falls back to the exact scan below.
+            if (tid == 0) L.qtail = 0;
+            __syncthreads();
+            for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
+                const uint32_t i = ib + tid;
+                bool scan = false;
+                uint32_t v = 0;
+                if (i < nF) {
+                    v = cur[i];
+                    scan = true;
+                    if (g.rows_sorted && v < D.P && v < D.H &&
+                        !((D.tbits[v >> 5] >> (v & 31)) & 1u)) {
+                        const uint32_t u = D.hpar[v];
+                        if (u < (uint32_t)V) {
+                            uint32_t lo = g.rowptr[u], hi = g.rowptr[u + 1];
+                            while (lo < hi) {  // rows are sorted by neighbour
+                                const uint32_t mid = (lo + hi) >> 1;
+                                if (adj_col(g, mid) < v) lo = mid + 1; else hi = mid;
+                            }
+                            if (lo < g.rowptr[u + 1] && adj_col(g, lo) == v) {
+                                uint32_t c;
+                                double w;
+                                adj_load(g, lo, c, w);
+                                if (__dadd_rn(bits2d(D.get(u)), w) == bits2d(D.get(v))) {
+                                    memo[v] = mtag | (unsigned long long)lo;  // slot in u's row
+                                    par[v] = u;
+                                    scan = false;
+                                }
+                            }
+                        }
+                    }
+                }
+                wave_push(scan, v, farq, &L.qtail, cap, stats);
+            }
+            __syncthreads();
+            const uint32_t nS = min(L.qtail, cap);
+            __syncthreads();
             expand_queue(
-                cur, nF, g, L,
+                farq, nS, g, L,
                 [&](uint32_t v, double& val) {
                     val = bits2d(D.get(v));
                     return true;
@@ -478,12 +541,12 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             // vertices with several candidates: recount at the minimum
             if (tid == 0) L.qtail = 0;
             __syncthreads();
-            for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
+            for (uint32_t ib = 0; ib < nS; ib += kSsspBlock) {
                 const uint32_t i = ib + tid;
                 bool multi = false;
                 uint32_t v = 0;
-                if (i < nF) {
-                    v = cur[i];
+                if (i < nS) {
+                    v = farq[i];
                     multi = ld_l2_u32(&cntc[v]) > 1u;
                     if (multi) {
                         atomicExch(&cntc[v], 0u);
@@ -514,8 +577,8 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                         }
                     });
             }
-            for (uint32_t i = tid; i < nF; i += kSsspBlock) {
-                const uint32_t v = cur[i];
+            for (uint32_t i = tid; i < nS; i += kSsspBlock) {
+                const uint32_t v = farq[i];
                 const uint32_t j = ld_l2_u32(&bslot[v]);
                 const uint32_t c = ld_l2_u32(&cntc[v]);
                 if (j == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
@@ -651,7 +714,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         atomicAdd(&stats[ST_SPLITS], n_split);
     }
     // per-lane event counts -> one atomic per wave
-    for (int k = 0; k < 6; k++) {
+    for (int k = 0; k < 8; k++) {
         unsigned long long x = ev[k];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
@@ -788,8 +851,9 @@ uint32_t sssp_hub_capacity() {
 
 hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                             int nsrc, const uint32_t* d_targets, int A, double delta,
-                            int64_t hub_limit, double2* out_lr, uint16_t* out_hops,
-                            double* out_rowmin, unsigned long long* d_stats, hipStream_t stream) {
+                            int64_t hub_limit, uint32_t par_hubs, double2* out_lr,
+                            uint16_t* out_hops, double* out_rowmin, unsigned long long* d_stats,
+                            hipStream_t stream) {
     int grid = ws.slots < nsrc ? ws.slots : nsrc;
     if (grid < 1) return hipSuccess;
     uint32_t hubs = sssp_hub_capacity();
@@ -805,8 +869,8 @@ hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d
         attr_set = true;
     }
     hipLaunchKernelGGL(sssp_rows_kernel, dim3(grid), dim3(kSsspBlock), lds, stream, g, ws,
-                       d_sources, nsrc, d_targets, A, delta, hubs, out_lr, out_hops, out_rowmin,
-                       d_stats);
+                       d_sources, nsrc, d_targets, A, delta, hubs, par_hubs, out_lr, out_hops,
+                       out_rowmin, d_stats);
     return hipGetLastError();
 }
 

@@ -236,7 +236,8 @@ class Topology:
         out = {k: getattr(s, k) for k, _ in L.ShdStats._fields_}
         out["phase_ms"] = list(out["phase_ms"])
         out["events"] = dict(zip(("expanded", "tail_relax", "tail_improve", "far_scanned",
-                                  "far_kept", "parent_vertices"), list(out["events"])[:6]))
+                                  "far_kept", "parent_vertices", "tail_settled_relax", "ev7"),
+                                 list(out["events"])))
         return out
 
     def export_graph(self):

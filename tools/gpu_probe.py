@@ -13,6 +13,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=256)
 ap.add_argument("--delta", type=float, default=0)
 ap.add_argument("--slots", type=int, default=0)
+ap.add_argument("--opt", action="append", default=[], help="key=value library option")
 ap.add_argument("--routers", type=int, default=990_000)
 ap.add_argument("--poi", type=int, default=10_000)
 ap.add_argument("--edges", type=int, default=10_000_000)
@@ -27,6 +28,9 @@ if args.delta:
     top.set_option("delta", args.delta)
 if args.slots:
     top.set_option("slots", args.slots)
+for kv in args.opt:
+    k, v = kv.split("=")
+    top.set_option(k, float(v))
 t = time.time()
 pk = top.synth_packets(20261015, args.hosts, 1000, 10**9, 10**7)
 A = len(top.attached_vertices())
