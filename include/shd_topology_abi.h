@@ -95,7 +95,9 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
 
 /* options: "abort_on_error" (1), "lazy" (1 = K3 first-rooted-wins emulation, 0 = eager
  * forward rows), "delta" (near-far bucket width, ms), "slots" (concurrent SSSP workgroups),
- * "device" (HIP device ordinal).  Returns 0 or -1 for an unknown key. */
+ * "device" (HIP device ordinal), "lds_hubs" (cap on LDS-resident hub distances, -1 = fill),
+ * "par_hubs" (hubs with SSSP parent hints), "far_cap" (far-pile entries per slot, 0 = 2V;
+ * small values force the scanning-split fallback).  Returns 0 or -1 for an unknown key. */
 int shdtopo_set_option(Topology* top, const char* key, double value);
 
 /* attach by raw IP and a rand_r state (same algorithm and RNG use as topology_attach) */
@@ -156,7 +158,11 @@ typedef struct {
     int64_t far_splits;       /* far-pile splits summed over sources */
     int64_t slots;            /* concurrent SSSP workgroups of the last launch */
     int64_t events[8];        /* expanded vertices, tail relaxations, tail improvements, far
-                                 entries scanned, far entries kept, parent-pass vertices */
+                                 entries scanned, far entries kept, parent-pass vertices,
+                                 relaxations onto settled tail vertices, far-entry distance
+                                 reads */
+    int64_t far_scan_sources; /* sources whose far pile overflowed (scanning splits instead) */
+    double split_ms;          /* far-pile split time summed over workgroups (part of phase 1) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libshdtopo.so")
+# SHDTOPO_LIB: an alternative build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("SHDTOPO_LIB") or os.path.join(HERE, "libshdtopo.so")
 SHIM_PATH = os.path.join(HERE, "libshdtopo_shim.so")
 
 P = ctypes.c_void_p
@@ -33,7 +34,7 @@ class ShdStats(ctypes.Structure):
                 ("sources", i64), ("targets", i64), ("ambiguous_pairs", i64),
                 ("relaxations", i64), ("long_paths", i64), ("errors", i64),
                 ("phase_ms", dbl * 4), ("near_iterations", i64), ("far_splits", i64),
-                ("slots", i64), ("events", i64 * 8)]
+                ("slots", i64), ("events", i64 * 8), ("far_scan_sources", i64), ("split_ms", dbl)]
 
 
 class ShdSynthParams(ctypes.Structure):

@@ -103,6 +103,12 @@ struct _Topology {
     int device = 0;
     int64_t hubLimit = -1;  // LDS-cached hub distances (-1 = fill the LDS)
     int64_t parHubs = 2048; // hubs whose parent is hinted during the SSSP (0 = always scan)
+    double farWindow = 8.0; // pile-1 key window, in multiples of delta
+    bool events = false;    // per-edge event counters (diagnostic kernel build)
+    int64_t nearCap = 0;    // near-queue entries per slot (0 = 2V; small values force the
+                            // bucket-rescan fallback, for tests)
+    int64_t farCap = 0;     // far-pile entries per slot (0 = 2V; small values force the
+                            // scanning-split fallback, for tests)
 
     // attach state (shd-topology.c:20-24 virtualIP)
     std::shared_mutex ipMu;
@@ -127,8 +133,8 @@ struct _Topology {
     std::vector<int32_t> inv;   // old -> new
     DevBuf<uint32_t> d_rowptr, d_adj;
     DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
-    DevBuf<unsigned long long> d_dist, d_best, d_memo;
-    DevBuf<uint32_t> d_stamp, d_fstamp, d_qa, d_qb, d_far, d_cnt, d_bslot, d_par, d_pathbuf,
+    DevBuf<unsigned long long> d_dist, d_best, d_memo, d_far, d_farkey, d_qa, d_qb;
+    DevBuf<uint32_t> d_stamp, d_cnt, d_bslot, d_par, d_pathbuf,
         d_counters;
     int slots = 0;
     DevBuf<double2> d_lr;
@@ -419,7 +425,7 @@ int ensure_workspace(Topology* top, int nsrc) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, top->device));
     int want = top->slotsOpt > 0 ? top->slotsOpt : prop.multiProcessorCount * sssp_max_blocks_per_cu();
-    size_t per_slot = (size_t)V * 56 + (size_t)kMaxHops * kSsspBlock * 4 + 16;
+    size_t per_slot = (size_t)V * (48 + 16 * kFarPerVertex + 16 * kNearPerVertex) + (size_t)kMaxHops * kSsspBlock * 4 + 16;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     int memcap = (int)std::max<size_t>(1, (freeb / 2) / per_slot);
@@ -431,18 +437,18 @@ int ensure_workspace(Topology* top, int nsrc) {
     HIPCHK(top->d_best.ensure(n));
     HIPCHK(top->d_memo.ensure(n));
     HIPCHK(top->d_stamp.ensure(n));
-    HIPCHK(top->d_fstamp.ensure(n));
-    HIPCHK(top->d_qa.ensure(n));
-    HIPCHK(top->d_qb.ensure(n));
-    HIPCHK(top->d_far.ensure(n));
+    HIPCHK(top->d_qa.ensure(n * kNearPerVertex));
+    HIPCHK(top->d_qb.ensure(n * kNearPerVertex));
+    HIPCHK(top->d_far.ensure(n * 2 * kFarPerVertex));
+    HIPCHK(top->d_farkey.ensure(n));
     HIPCHK(top->d_cnt.ensure(n));
     HIPCHK(top->d_bslot.ensure(n));
     HIPCHK(top->d_par.ensure(n));
     HIPCHK(top->d_pathbuf.ensure((size_t)want * kMaxHops * kSsspBlock));
     HIPCHK(top->d_counters.ensure((size_t)want * 4));
     HIPCHK(hipMemsetAsync(top->d_stamp.p, 0, sizeof(uint32_t) * n, top->stream));
-    HIPCHK(hipMemsetAsync(top->d_fstamp.p, 0, sizeof(uint32_t) * n, top->stream));
     HIPCHK(hipMemsetAsync(top->d_memo.p, 0, sizeof(unsigned long long) * n, top->stream));
+    HIPCHK(hipMemsetAsync(top->d_farkey.p, 0xFF, sizeof(unsigned long long) * n, top->stream));
     HIPCHK(hipMemsetAsync(top->d_counters.p, 0, sizeof(uint32_t) * (size_t)want * 4, top->stream));
     HIPCHK(hipStreamSynchronize(top->stream));
     top->slots = want;
@@ -453,8 +459,8 @@ SlotWs slot_ws(Topology* top) {
     SlotWs w;
     w.slots = top->slots;
     w.V = top->g.V;
-    w.dist = top->d_dist.p; w.stamp = top->d_stamp.p; w.fstamp = top->d_fstamp.p;
-    w.qa = top->d_qa.p; w.qb = top->d_qb.p; w.far = top->d_far.p;
+    w.dist = top->d_dist.p; w.stamp = top->d_stamp.p;
+    w.qa = top->d_qa.p; w.qb = top->d_qb.p; w.far = top->d_far.p; w.farkey = top->d_farkey.p;
     w.best = top->d_best.p; w.cnt = top->d_cnt.p; w.bslot = top->d_bslot.p;
     w.memo = top->d_memo.p; w.par = top->d_par.p; w.pathbuf = top->d_pathbuf.p;
     w.counters = top->d_counters.p;
@@ -548,7 +554,9 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         HIPCHK(hipEventRecord(top->ev0, st));
         HIPCHK(launch_sssp_rows(dev_csr(top), slot_ws(top), top->d_sources.p, (int)rows,
                                 top->d_targets.p, (int)A, default_delta(top), top->hubLimit,
-                                (uint32_t)top->parHubs,
+                                (uint32_t)top->parHubs, (uint32_t)top->farCap,
+                                (uint32_t)top->nearCap,
+                                top->farWindow, top->events,
                                 out_lr, out_hops,
                                 out_rowmin, top->d_stats.p, st));
         HIPCHK(hipEventRecord(top->ev1, st));
@@ -586,6 +594,17 @@ int collect_row_stats(Topology* top) {
     double gm;
     memcpy(&gm, &h[ST_GLOBAL_MIN], sizeof gm);
     top->eagerMin = std::isinf(gm) ? -1.0 : gm;
+    if (h[ST_OVERSITE]) WARNING("queue overflow sites 0x%llx", h[ST_OVERSITE]);
+    if (h[ST_FARSCAN])
+        MESSAGE("%llu sources overflowed the far pile and finished with scanning splits",
+                h[ST_FARSCAN]);
+    top->stats.far_scan_sources = (int64_t)h[ST_FARSCAN];
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->device) != hipSuccess || khz <= 0)
+            khz = 100000;
+        top->stats.split_ms = (double)h[ST_T_SPLIT] / (double)khz;
+    }
     if (h[ST_OVERFLOW]) CRITICAL("SSSP queue overflow / iteration guard (code %llu)", h[ST_OVERFLOW]);
     if (top->stats.ambiguous_pairs)
         WARNING("%lld pairs cross a parent tie (equal d[u]): igraph's heap pop order decides them "
@@ -885,6 +904,10 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "device") top->device = (int)value;
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
     else if (k == "par_hubs") top->parHubs = (int64_t)value;
+    else if (k == "far_cap") top->farCap = (int64_t)value;
+    else if (k == "near_cap") top->nearCap = (int64_t)value;
+    else if (k == "far_window") top->farWindow = value;
+    else if (k == "events") top->events = value != 0;
     else return -1;
     return 0;
 }

@@ -16,6 +16,10 @@ namespace shdtopo {
 
 constexpr int kSsspBlock = 1024;  // threads per SSSP workgroup (16 waves)
 constexpr int kMaxHops = 48;      // per-thread path buffer depth (longer paths: O(h^2) walk)
+constexpr int kFarPerVertex = 3;  // far-pile capacity per slot, in entries per vertex (pile 1:
+                                  // V, pile 2: 2V; pile 2 keeps superseded entries until a
+                                  // refill), each pile double buffered
+constexpr int kNearPerVertex = 2; // near-queue capacity per slot, in entries per vertex
 
 // indices into the device stats block (unsigned long long[16])
 enum StatIdx {
@@ -35,6 +39,9 @@ enum StatIdx {
     ST_EV0 = 13,        // event counters (ShdStats.events): expanded vertices, tail relaxations,
                         // tail improvements, far entries scanned, far entries kept, parent-pass
                         // vertices
+    ST_FARSCAN = 21,
+    ST_T_SPLIT = 22,
+    ST_OVERSITE = 23,   // OR of the push sites that overflowed (diagnostic)    // wall-clock ticks summed over workgroups: far-pile splits (in T_SSSP)    // sources whose far pile overflowed (finished with scanning splits)
     ST_COUNT = 24
 };
 
@@ -56,10 +63,12 @@ struct SlotWs {
     int64_t V = 0;
     unsigned long long* dist = nullptr;  // f64 bits, +inf = unreached
     uint32_t* stamp = nullptr;           // near-queue / chain-queue dedupe (iteration id)
-    uint32_t* fstamp = nullptr;          // far-pile dedupe (far epoch)
-    uint32_t* qa = nullptr;
-    uint32_t* qb = nullptr;
-    uint32_t* far = nullptr;
+    unsigned long long* qa = nullptr;  // near queues: (hi32 of the pushed distance << 32) |
+    unsigned long long* qb = nullptr;  // vertex, kNearPerVertex * V entries (no dedupe)
+    unsigned long long* farkey = nullptr;  // per vertex: (~source epoch << 32) | hi32 of the
+                                           // smallest far key pushed (atomicMin dedupe)
+    unsigned long long* far = nullptr;   // far pile: (hi32 of the f64 key << 32) | vertex, 2V
+                                         // entries (tail entries are not deduplicated)
     unsigned long long* best = nullptr;  // parent pass: min d[u] over candidates
     uint32_t* cnt = nullptr;             // parent pass: candidates at the min
     uint32_t* bslot = nullptr;           // parent pass: lowest adjacency slot at the min
@@ -72,7 +81,9 @@ struct SlotWs {
 // hub_limit: cap on LDS-cached vertices (-1 = as many as fit, ~18k)
 hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                             int nsrc, const uint32_t* d_targets, int A, double delta,
-                            int64_t hub_limit, uint32_t par_hubs, double2* out_lr,
+                            int64_t hub_limit, uint32_t par_hubs, uint32_t far_cap,
+                            uint32_t near_cap, double far_window, bool events,
+                            double2* out_lr,
                             uint16_t* out_hops, double* out_rowmin, unsigned long long* d_stats,
                             hipStream_t stream);
 uint32_t sssp_hub_capacity();

@@ -59,9 +59,12 @@ struct Lds {
     uint32_t qtail;
     uint32_t ftail;
     uint32_t src_idx;
-    uint32_t pad0;
+    uint32_t fover;  // far pile overflowed for this source: splits scan the distances instead
+    uint32_t nover;  // a near queue overflowed since the last split: rescan the whole bucket
+    uint32_t f2tail;  // entries in the second-level far pile
     unsigned long long dmin;
-    unsigned long long fmin;  // lower bound of the far pile's live distances
+    unsigned long long fmin;  // lower bound of the live distances in far pile 1
+    unsigned long long fmin2; // lower bound of the live keys in far pile 2
     unsigned long long relax;
 };
 constexpr size_t kLdsCtrlBytes = (sizeof(Lds) + 15) / 16 * 16;
@@ -88,6 +91,34 @@ __device__ __forceinline__ void wave_push(bool pred, uint32_t val, uint32_t* q, 
         if (pos < cap) q[pos] = val;
         else atomicOr(&stats[ST_OVERFLOW], 1ull);
     }
+}
+
+__device__ __forceinline__ void wave_push64(bool pred, unsigned long long val,
+                                            unsigned long long* q, uint32_t* lds_tail,
+                                            uint32_t cap, uint32_t* lds_over,
+                                            uint32_t code = 1u) {
+    unsigned long long m = __ballot(pred);
+    if (m == 0ull) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(lds_tail, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (pred) {
+        uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (pos < cap) q[pos] = val;
+        else atomicOr(lds_over, code);
+    }
+}
+
+// Far-pile entry: the high word of the f64 key's bit pattern over the vertex id.  For d >= 0
+// the bit pattern orders like the value, so hi32 truncation gives a lower bound of the key
+// (key_lb(e) <= the distance the vertex had when the entry was pushed).
+__device__ __forceinline__ unsigned long long far_entry(unsigned long long dbits, uint32_t v) {
+    return (dbits & 0xFFFFFFFF00000000ull) | (unsigned long long)v;
+}
+__device__ __forceinline__ double far_key_lb(unsigned long long e) {
+    return bits2d(e & 0xFFFFFFFF00000000ull);
 }
 
 // Block-wide exclusive scan of one u32 per thread; *total receives the sum.
@@ -188,12 +219,15 @@ struct DistView {
 // Near-phase relaxation of queue Q: the load-balanced chunking of expand_queue, with U edges in
 // flight per lane: U (col, wt) loads, then the U tail pre-checks, then the LDS / HBM atomics, then
 // the queue pushes.
-template <int U>
-__device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, const DevCSR& g,
-                                            Lds& L, const DistView& D, uint32_t* stamp,
-                                            uint32_t* fstamp, uint32_t* nxt, uint32_t* farq,
-                                            uint32_t it, uint32_t fe, double th, double lb,
-                                            uint32_t cap,
+template <int U, bool EV>
+__device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_t nq,
+                                            const DevCSR& g, Lds& L, const DistView& D,
+                                            uint32_t* stamp, bool dedupe,
+                                            unsigned long long* nxt, unsigned long long* farq,
+                                            unsigned long long* farq2,
+                                            unsigned long long* farkey, unsigned long long fe,
+                                            uint32_t it, double th, double bound, double lb,
+                                            uint32_t ncap, uint32_t fcap, uint32_t fcap2,
                                             unsigned long long* stats,
                                             unsigned long long& relax,
                                             unsigned long long* ev) {
@@ -203,17 +237,25 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
         const uint32_t cnt = min((uint32_t)kSsspBlock, nq - base);
         uint32_t deg = 0;
         if (tid < cnt) {
-            const uint32_t v = Q[base + tid];
+            // a tail entry pushed by a non-deduplicating relaxation carries the high word of its
+            // distance; a later (smaller) push of the same vertex supersedes it, so an entry
+            // whose word is above the current distance's is stale and expands nothing (entries
+            // of deduplicated pushes carry 0)
+            const unsigned long long e = Q[base + tid];
+            const uint32_t v = (uint32_t)e;
             const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
-            deg = r1 - r0;
+            const unsigned long long dv = D.get(v);
+            const bool stale = v >= D.H && (dv >> 32) < (e >> 32);
+            deg = stale ? 0u : r1 - r0;
             L.rs[tid] = r0;
             L.vx[tid] = v;
-            L.val[tid] = bits2d(D.get(v));
+            L.val[tid] = bits2d(dv);
         }
         uint32_t total;
         const uint32_t off = block_excl_scan(deg, L, &total);
         if (tid < cnt) L.off[tid] = off;
         if (tid == 0) L.off[cnt] = total;
+        relax += total;  // uniform: every adjacency entry of the chunk is relaxed once
         __syncthreads();
         for (uint32_t eb = tid - lane; eb < total; eb += kSsspBlock * U) {
             uint32_t n[U], from[U];
@@ -259,18 +301,27 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
 #pragma unroll
             for (int u = 0; u < U; u++)
                 if (ab[u] < cur[u]) imp[u] = ab[u] < atomicMin(&D.dist[n[u]], ab[u]);
-            // every far-side improvement lowers the far pile's running minimum (LDS), so the
-            // split needs no extra pass over the pile
-            unsigned long long fm = kInfBits;
+            // every far-side improvement lowers its pile's running minimum (LDS), so a split
+            // needs no extra pass.  Pile 1 takes hubs and keys whose lower bound is < bound.
+            bool p1[U];
+            unsigned long long fm = kInfBits, fm2 = kInfBits;
 #pragma unroll
-            for (int u = 0; u < U; u++)
-                if (imp[u] && !(bits2d(ab[u]) < th) && ab[u] < fm) fm = ab[u];
+            for (int u = 0; u < U; u++) {
+                p1[u] = n[u] < D.H || far_key_lb(ab[u]) < bound;
+                if (imp[u] && !(bits2d(ab[u]) < th)) {
+                    if (p1[u]) fm = ab[u] < fm ? ab[u] : fm;
+                    else fm2 = ab[u] < fm2 ? ab[u] : fm2;
+                }
+            }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
                 const unsigned long long y = __shfl_xor(fm, o, 64);
                 fm = y < fm ? y : fm;
+                const unsigned long long y2 = __shfl_xor(fm2, o, 64);
+                fm2 = y2 < fm2 ? y2 : fm2;
             }
             if (lane == 0 && fm != kInfBits) atomicMin(&L.fmin, fm);
+            if (lane == 0 && fm2 != kInfBits) atomicMin(&L.fmin2, fm2 & 0xFFFFFFFF00000000ull);
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 bool pN = false, pF = false;
@@ -283,17 +334,34 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
                         pN = near && first;
                         pF = !near && first;
                     } else if (near) {
-                        pN = atomicExch(&stamp[n[u]], it) != it;
+                        // no dedupe: every strict improvement pushes (its value rides along
+                        // and stale entries are skipped at expansion), which keeps a returning
+                        // atomic off the relaxation's dependency chain.  After an overflow the
+                        // source deduplicates per iteration (<= V entries: always fits).
+                        pN = !dedupe || atomicExch(&stamp[n[u]], it) != it;
                     } else {
-                        pF = atomicExch(&fstamp[n[u]], fe) != fe;
+                        // tail: the entry carries its key, so a split never reads the distance
+                        // of an entry that stays far.  A vertex is pushed again only when its
+                        // key's high word drops below every key already pushed for it this
+                        // source (epoch-tagged atomicMin); the older entry is dropped when the
+                        // threshold passes its key.
+                        const unsigned long long fk = fe | (ab[u] >> 32);
+                        pF = fk < atomicMin(&farkey[n[u]], fk);
                     }
                 }
-                wave_push(pN, n[u], nxt, &L.qtail, cap, stats);
-                wave_push(pF, n[u], farq, &L.ftail, cap, stats);
-                relax += valid[u] ? 1ull : 0ull;
-                ev[1] += (valid[u] && n[u] >= D.H) ? 1ull : 0ull;
-                ev[2] += (imp[u] && n[u] >= D.H) ? 1ull : 0ull;
-                ev[6] += (valid[u] && n[u] >= D.H && bits2d(cur[u]) < lb) ? 1ull : 0ull;
+                // deduplicated pushes carry key 0 (never stale): a later improvement of the
+                // vertex in the same iteration is not pushed again
+                wave_push64(pN, far_entry((n[u] < D.H || dedupe) ? 0ull : ab[u], n[u]), nxt,
+                            &L.qtail, ncap, &L.nover, 1u);
+                wave_push64(pF && p1[u], far_entry(ab[u], n[u]), farq, &L.ftail, fcap, &L.fover,
+                            2u);
+                wave_push64(pF && !p1[u], far_entry(ab[u], n[u]), farq2, &L.f2tail, fcap2,
+                            &L.fover, 4u);
+                if constexpr (EV) {
+                    ev[1] += (valid[u] && n[u] >= D.H) ? 1ull : 0ull;
+                    ev[2] += (imp[u] && n[u] >= D.H) ? 1ull : 0ull;
+                    ev[6] += (valid[u] && n[u] >= D.H && bits2d(cur[u]) < lb) ? 1ull : 0ull;
+                }
             }
         }
         __syncthreads();
@@ -302,10 +370,11 @@ __device__ __forceinline__ void relax_queue(const uint32_t* Q, uint32_t nq, cons
 
 }  // namespace
 
+template <bool EV>
 __global__ void __launch_bounds__(kSsspBlock)
 sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int nsrc,
                  const uint32_t* __restrict__ targets, int A, double delta, uint32_t hubs,
-                 uint32_t parhubs,
+                 uint32_t parhubs, uint32_t far_cap, uint32_t near_cap, double far_window,
                  double2* __restrict__ out_lr, uint16_t* __restrict__ out_hops,
                  double* __restrict__ out_rowmin, unsigned long long* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -324,10 +393,11 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     D.P = parhubs < kParHubs ? parhubs : kParHubs;
     unsigned long long* dist = D.dist;
     uint32_t* stamp = ws.stamp + (size_t)slot * V;
-    uint32_t* fstamp = ws.fstamp + (size_t)slot * V;
-    uint32_t* qa = ws.qa + (size_t)slot * V;
-    uint32_t* qb = ws.qb + (size_t)slot * V;
-    uint32_t* farq = ws.far + (size_t)slot * V;
+    unsigned long long* qa = ws.qa + (size_t)slot * kNearPerVertex * V;
+    unsigned long long* qb = ws.qb + (size_t)slot * kNearPerVertex * V;
+    unsigned long long* farq = ws.far + (size_t)slot * 2 * kFarPerVertex * V;
+    uint32_t* fscr = reinterpret_cast<uint32_t*>(farq);  // parent-pass scratch queue (u32)
+    unsigned long long* farkey = ws.farkey + (size_t)slot * V;
     unsigned long long* best = ws.best + (size_t)slot * V;
     uint32_t* cntc = ws.cnt + (size_t)slot * V;
     uint32_t* bslot = ws.bslot + (size_t)slot * V;
@@ -336,11 +406,26 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     uint32_t* pbuf = ws.pathbuf + (size_t)slot * kMaxHops * kSsspBlock;
     uint32_t* ctr = ws.counters + (size_t)slot * 4;
     const uint32_t cap = (uint32_t)V;
+    // near queues hold kNearPerVertex * V entries; deduplicated pushes (splits, and relaxations
+    // after an overflow) never exceed V.  near_cap only limits non-deduplicated relaxation
+    // pushes (tests force the overflow fallback with it).
+    const uint32_t ncap = (uint32_t)(kNearPerVertex * V);
+    const uint32_t ncap_free = (near_cap > 0 && near_cap < ncap) ? near_cap : ncap;
+    // far pile 1 (fcap entries, V by default) and pile 2 (fcap2, the rest), each double
+    // buffered: a split / refill streams the kept entries into the other buffer
+    const uint32_t fall = (far_cap > 0 && far_cap < (uint32_t)(kFarPerVertex * V))
+                              ? far_cap : (uint32_t)(kFarPerVertex * V);
+    const uint32_t fcap = max(1u, fall / (uint32_t)kFarPerVertex);
+    const uint32_t fcap2 = max(1u, fall - fcap);
+    const double fwin = far_window * delta;
 
-    // slot-persistent epoch counters (never reset, so stamp/fstamp/memo need no clearing)
+    // slot-persistent epoch counters (never reset, so stamp/memo need no clearing)
     uint32_t iter = ctr[0], fep = ctr[1], mep = ctr[2];
     unsigned long long relax_local = 0;
-    unsigned long long ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long nfarscan = 0;
+    unsigned long long ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per-lane (EV builds only)
+    unsigned long long ev0 = 0, ev3 = 0, ev4 = 0, ev5 = 0;  // uniform across the workgroup
+    unsigned long long t_split = 0;
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, n_near = 0, n_split = 0;
     unsigned long long tk = wall_clock64();
 
@@ -362,98 +447,250 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         { unsigned long long t = wall_clock64(); t_init += t - tk; tk = t; }
         iter++;
         fep++;
+        const unsigned long long fe = (unsigned long long)(~fep) << 32;
         if (tid == 0) {
+            L.fover = 0u;
             if (src < D.H) D.hd[src] = 0ull; else dist[src] = 0ull;
-            qa[0] = src;
+            L.nover = 0u;
+            qa[0] = far_entry(0ull, src);
             stamp[src] = iter;
             L.ftail = 0;
+            L.f2tail = 0;
             L.fmin = kInfBits;
+            L.fmin2 = kInfBits;
         }
         __syncthreads();
-        uint32_t* cur = qa;
-        uint32_t* nxt = qb;
-        uint32_t nq = 1, nf = 0;
+        unsigned long long* cur = qa;
+        unsigned long long* nxt = qb;
+        unsigned long long* f1 = farq;
+        unsigned long long* f1alt = farq + fcap;
+        unsigned long long* f2 = farq + 2 * (size_t)fcap;
+        unsigned long long* f2alt = f2 + fcap2;
+        uint32_t nq = 1, n1 = 0, n2 = 0;
         double thr = delta;
+        double bound = __dadd_rn(thr, fwin);  // pile 1 holds keys below bound, pile 2 the rest
         double lb = 0.0;  // every vertex with d < lb is final (the last completed bucket)
         uint32_t guard = 0;
+        constexpr int FU = 4;  // pile entries per lane per chunk (reads in flight)
+        unsigned long long tsplit0 = 0;
         for (;;) {
+            if (tsplit0) {
+                t_split += wall_clock64() - tsplit0;
+                tsplit0 = 0;
+            }
             while (nq > 0) {
                 iter++;
                 if (tid == 0) L.qtail = 0;
                 for (uint32_t w = tid; w < kHubBitWords; w += kSsspBlock) D.nbits[w] = 0u;
                 __syncthreads();
-                ev[0] += (tid == 0) ? nq : 0u;
-                relax_queue<kRelaxUnroll>(cur, nq, g, L, D, stamp, fstamp, nxt, farq, iter, fep,
-                                          thr, lb, cap, stats, relax_local, ev);
+                ev0 += nq;
+                const bool dedupe = L.fover != 0u;
+                relax_queue<kRelaxUnroll, EV>(cur, nq, g, L, D, stamp, dedupe, nxt, f1, f2,
+                                              farkey, fe, iter, thr, bound, lb,
+                                              dedupe ? ncap : ncap_free, fcap, fcap2, stats,
+                                              relax_local, ev);
                 // relax_queue ends with a barrier
-                nq = min(L.qtail, cap);
-                nf = min(L.ftail, cap);
-                uint32_t* t = cur; cur = nxt; nxt = t;
+                nq = min(L.qtail, ncap);
+                n1 = min(L.ftail, fcap);
+                n2 = min(L.f2tail, fcap2);
+                unsigned long long* t = cur; cur = nxt; nxt = t;
                 n_near++;
-                if (++guard > 4000000u) { if (tid == 0) atomicOr(&stats[ST_OVERFLOW], 2ull); nq = 0; nf = 0; }
+                if (++guard > 4000000u) {
+                    if (tid == 0) atomicOr(&stats[ST_OVERFLOW], 2ull);
+                    nq = 0;
+                    n1 = n2 = 0;
+                }
                 __syncthreads();
             }
-            if (nf == 0) break;
-            // Split the far pile.  L.fmin is <= every live entry's distance (it saw every far-side
-            // improvement and every kept entry), so [thr, max(fmin, thr) + delta) holds at least
-            // the smallest live entry.  One pass classifies on the true distances: drop (< thr:
-            // already expanded when it went below thr), near, or keep.  "In the far pile" is a
-            // per-source flag (fstamp == fep / LDS bit for hubs) cleared on removal, so kept
-            // entries need no rewrite.
+            const bool nov = L.nover != 0u;
+            const bool scanmode = L.fover != 0u || nov;
+            const unsigned long long fmin1b = L.fmin, fmin2b = L.fmin2;
+            const unsigned long long fminall = fmin1b < fmin2b ? fmin1b : fmin2b;
+            if (!nov && (scanmode ? fminall == kInfBits : (n1 == 0 && n2 == 0))) break;
             n_split++;
-            ev[3] += (tid == 0) ? nf : 0u;
-            const unsigned long long fminb = L.fmin;
+            tsplit0 = wall_clock64();
             const double oldthr = thr;
-            const double newthr = __dadd_rn(fmax(bits2d(fminb), thr), delta);
+            double newthr;
+            if (scanmode) {
+                // A pile overflowed (entries were lost): classify every vertex by its distance
+                // instead, for the rest of this source.  Every unexpanded vertex has d >= thr,
+                // so d in [thr, newthr) is exactly the next near set -- unless a near queue
+                // overflowed since the last split: then vertices of the current bucket
+                // [lb, thr) may have been lost too, and the whole bucket is expanded again
+                // (re-expansion is harmless for a label-correcting SSSP).  Sequential,
+                // coalesced reads.
+                newthr = fminall == kInfBits ? thr : __dadd_rn(fmax(bits2d(fminall), thr), delta);
+                const double lo = nov ? lb : oldthr;
+                iter++;
+                __syncthreads();
+                if (tid == 0) {
+                    L.qtail = 0;
+                    L.fmin = kInfBits;
+                    L.fmin2 = kInfBits;
+                    L.nover = 0u;
+                    L.fover |= 64u;
+                }
+                __syncthreads();
+                for (uint32_t base = 0; base < (uint32_t)V; base += kSsspBlock * FU) {
+                    unsigned long long km = kInfBits;
+#pragma unroll
+                    for (int u = 0; u < FU; u++) {
+                        const uint32_t v = base + (uint32_t)u * kSsspBlock + tid;
+                        bool pN = false;
+                        unsigned long long b = kInfBits;
+                        if (v < (uint32_t)V) {
+                            b = D.get(v);
+                            const double d = bits2d(b);
+                            pN = !(d < lo) && d < newthr;
+                            if (!(d < newthr) && b < km) km = b;
+                        }
+                        wave_push64(pN, far_entry(0ull, v), cur, &L.qtail, ncap, &L.nover, 32u);
+                    }
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) {
+                        const unsigned long long y = __shfl_xor(km, o, 64);
+                        km = y < km ? y : km;
+                    }
+                    if ((tid & 63) == 0 && km != kInfBits) atomicMin(&L.fmin, km);
+                }
+                __syncthreads();
+                nq = min(L.qtail, ncap);
+                if (!nov) lb = oldthr;
+                thr = newthr;
+                __syncthreads();
+                continue;
+            }
+            // ---- two-level far pile ----
+            // Invariants: an entry's key lower bound (hi32 truncation of the f64 bits) never
+            // exceeds its vertex's distance at push time; every live (unexpanded) vertex v has
+            // d_v >= thr and an entry with key_lb <= d_v, in pile 1 whenever key_lb < bound
+            // (pushes and refills route by key_lb; hubs always go to pile 1).  L.fmin / fmin2
+            // are lower bounds of their pile's keys.
+            // (a) Refill: once pile 1 is exhausted or the threshold reached bound, move the
+            //     entries of pile 2 with key_lb < the new bound into pile 1.  Pile 2 entries are
+            //     tail keys: no distance reads.
+            if (n1 == 0 || !(thr < bound)) {
+                const double nb = __dadd_rn(fmax(bits2d(fminall), thr), fwin);
+                __syncthreads();
+                if (tid == 0) {
+                    L.fmin2 = kInfBits;
+                    L.f2tail = 0;  // kept entries stream into the other pile-2 buffer
+                }
+                __syncthreads();
+                for (uint32_t base = 0; base < n2; base += kSsspBlock * FU) {
+                    unsigned long long k1 = kInfBits, k2 = kInfBits;
+#pragma unroll
+                    for (int u = 0; u < FU; u++) {
+                        const uint32_t i = base + (uint32_t)u * kSsspBlock + tid;
+                        const unsigned long long e = i < n2 ? f2[i] : 0ull;
+                        const unsigned long long kb = e & 0xFFFFFFFF00000000ull;
+                        const bool mv = i < n2 && bits2d(kb) < nb;
+                        const bool kp = i < n2 && !mv;
+                        if (kp) k2 = kb < k2 ? kb : k2;
+                        if (mv) k1 = kb < k1 ? kb : k1;
+                        wave_push64(mv, e, f1, &L.ftail, fcap, &L.fover, 8u);
+                        wave_push64(kp, e, f2alt, &L.f2tail, fcap2, &L.fover, 8u);
+                    }
+#pragma unroll
+                    for (int sh = 32; sh > 0; sh >>= 1) {
+                        const unsigned long long y1 = __shfl_xor(k1, sh, 64);
+                        k1 = y1 < k1 ? y1 : k1;
+                        const unsigned long long y2 = __shfl_xor(k2, sh, 64);
+                        k2 = y2 < k2 ? y2 : k2;
+                    }
+                    if ((tid & 63) == 0 && k1 != kInfBits) atomicMin(&L.fmin, k1);
+                    if ((tid & 63) == 0 && k2 != kInfBits) atomicMin(&L.fmin2, k2);
+                }
+                __syncthreads();
+                ev3 += n2;
+                bound = nb;
+                n2 = min(L.f2tail, fcap2);
+                n1 = min(L.ftail, fcap);
+                { unsigned long long* t = f2; f2 = f2alt; f2alt = t; }
+                if (L.fover) continue;  // a pile overflowed while refilling: scanning splits
+            }
+            // (b) Split pile 1 on [thr, newthr), newthr <= bound.  An entry whose key lower
+            //     bound is already >= newthr stays without touching its distance; the others
+            //     read the true distance and are dropped (< thr: expanded when it went below
+            //     the threshold, or a stale duplicate), moved to the near queue (deduplicated
+            //     by stamp), or kept with a refreshed key.  One streaming pass with no
+            //     barriers: kept entries go to the other pile-1 buffer.
+            ev3 += n1;
+            newthr = fmin(__dadd_rn(fmax(bits2d(L.fmin), thr), delta), bound);
             iter++;
             __syncthreads();
             if (tid == 0) {
                 L.qtail = 0;
                 L.fmin = kInfBits;
+                L.ftail = 0;
             }
             __syncthreads();
-            uint32_t kept = 0;
-            for (uint32_t base = 0; base < nf; base += kSsspBlock) {
-                const uint32_t i = base + tid;
-                uint32_t v = 0;
-                int cls = 0;  // 0 drop, 1 near, 2 keep
-                unsigned long long db = kInfBits;
-                if (i < nf) {
-                    v = farq[i];
-                    db = D.get(v);
-                    const double d = bits2d(db);
-                    cls = d < oldthr ? 0 : (d < newthr ? 1 : 2);
-                    if (cls != 2) {  // leaves the far pile
-                        if (v < D.H) atomicAnd(&D.fbits[v >> 5], ~(1u << (v & 31)));
-                        else fstamp[v] = 0u;
+            for (uint32_t base = 0; base < n1; base += kSsspBlock * FU) {
+                unsigned long long e[FU], db[FU];
+                int cls[FU];  // -1 none, 0 drop, 1 near, 2 keep, 3 undecided
+#pragma unroll
+                for (int u = 0; u < FU; u++) {
+                    const uint32_t i = base + (uint32_t)u * kSsspBlock + tid;
+                    e[u] = i < n1 ? f1[i] : 0ull;
+                    cls[u] = i < n1 ? 3 : -1;
+                }
+#pragma unroll
+                for (int u = 0; u < FU; u++) {
+                    db[u] = kInfBits;
+                    if (cls[u] == 3) {
+                        const uint32_t v = (uint32_t)e[u];
+                        if (v >= D.H && !(far_key_lb(e[u]) < newthr)) {
+                            cls[u] = 2;
+                            db[u] = e[u] & 0xFFFFFFFF00000000ull;
+                        } else {
+                            db[u] = D.get(v);
+                            if constexpr (EV) ev[7] += v >= D.H ? 1u : 0u;
+                        }
                     }
                 }
-                __syncthreads();  // every lane has read its chunk entry before compaction writes
-                uint32_t tot;
-                const uint32_t o = block_excl_scan(cls == 2 ? 1u : 0u, L, &tot);
-                if (cls == 2) farq[kept + o] = v;
-                unsigned long long km = cls == 2 ? db : kInfBits;
+                unsigned long long km = kInfBits;
 #pragma unroll
-                for (int s = 32; s > 0; s >>= 1) {
-                    const unsigned long long y = __shfl_xor(km, s, 64);
+                for (int u = 0; u < FU; u++) {
+                    const uint32_t v = (uint32_t)e[u];
+                    if (cls[u] == 3) {
+                        const double d = bits2d(db[u]);
+                        cls[u] = d < oldthr ? 0 : (d < newthr ? 1 : 2);
+                        if (v < D.H) {
+                            if (cls[u] != 2) atomicAnd(&D.fbits[v >> 5], ~(1u << (v & 31)));
+                        } else if (cls[u] == 2) {
+                            e[u] = far_entry(db[u], v);  // refreshed key
+                        }
+                    }
+                    if (cls[u] == 2) km = db[u] < km ? db[u] : km;
+                    wave_push64(cls[u] == 2, e[u], f1alt, &L.ftail, fcap, &L.fover, 2u);
+                    const bool pN = cls[u] == 1 &&
+                                    (v < D.H || atomicExch(&stamp[v], iter) != iter);
+                    wave_push64(pN, far_entry(0ull, v), cur, &L.qtail, ncap, &L.nover, 16u);
+                }
+#pragma unroll
+                for (int sh = 32; sh > 0; sh >>= 1) {
+                    const unsigned long long y = __shfl_xor(km, sh, 64);
                     km = y < km ? y : km;
                 }
                 if ((tid & 63) == 0 && km != kInfBits) atomicMin(&L.fmin, km);
-                wave_push(cls == 1, v, cur, &L.qtail, cap, stats);
-                kept += tot;
-                __syncthreads();
             }
-            nq = min(L.qtail, cap);
-            nf = kept;
-            ev[4] += (tid == 0) ? kept : 0u;
+            __syncthreads();
+            const uint32_t kept = min(L.ftail, fcap);
+            { unsigned long long* t = f1; f1 = f1alt; f1alt = t; }
+            nq = min(L.qtail, ncap);
+            n1 = kept;
+            ev4 += kept;
             lb = oldthr;
             thr = newthr;
-            if (tid == 0) L.ftail = kept;
             __syncthreads();
         }
 
+        nfarscan += L.fover ? 1u : 0u;
+        if (tid == 0 && (L.fover | L.nover)) atomicOr(&stats[ST_OVERSITE], (unsigned long long)(L.fover | L.nover));
         { unsigned long long t = wall_clock64(); t_sssp += t - tk; tk = t; }
         // ---------------- parents for the target chains (argmin d[u]) ----------
+        uint32_t* pcur = reinterpret_cast<uint32_t*>(qa);  // u32 views of the near queues
+        uint32_t* pnxt = reinterpret_cast<uint32_t*>(qb);
         // One adjacency pass per chain level finds min d[u] over the candidates
         // fl(d[u] + w) == d[v] and counts them; only vertices with more than one candidate get a
         // second pass that counts the candidates AT the minimum and keeps the lowest slot.
@@ -471,13 +708,13 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 p = (t != src) && (atomicExch(&stamp[t], iter) != iter);
                 if (p) { best[t] = kInfBits; cntc[t] = 0; bslot[t] = 0xFFFFFFFFu; }
             }
-            wave_push(p, t, cur, &L.qtail, cap, stats);
+            wave_push(p, t, pcur, &L.qtail, cap, stats);
         }
         __syncthreads();
         uint32_t nF = min(L.qtail, cap);
         __syncthreads();
         while (nF > 0) {
-            ev[5] += (tid == 0) ? nF : 0u;
+            ev5 += nF;
             // Heavy hubs first: the SSSP recorded which vertex last lowered each of the first
             // kParHubs hubs and whether any relaxation tied its value.  Every candidate u of v
             // relaxes v with fl(d[u]+w) == d[v] when u is expanded at its final distance, so
@@ -491,7 +728,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 bool scan = false;
                 uint32_t v = 0;
                 if (i < nF) {
-                    v = cur[i];
+                    v = pcur[i];
                     scan = true;
                     if (g.rows_sorted && v < D.P && v < D.H &&
                         !((D.tbits[v >> 5] >> (v & 31)) & 1u)) {
@@ -515,13 +752,13 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                         }
                     }
                 }
-                wave_push(scan, v, farq, &L.qtail, cap, stats);
+                wave_push(scan, v, fscr, &L.qtail, cap, stats);
             }
             __syncthreads();
             const uint32_t nS = min(L.qtail, cap);
             __syncthreads();
             expand_queue(
-                farq, nS, g, L,
+                fscr, nS, g, L,
                 [&](uint32_t v, double& val) {
                     val = bits2d(D.get(v));
                     return true;
@@ -546,21 +783,21 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 bool multi = false;
                 uint32_t v = 0;
                 if (i < nS) {
-                    v = farq[i];
+                    v = fscr[i];
                     multi = ld_l2_u32(&cntc[v]) > 1u;
                     if (multi) {
                         atomicExch(&cntc[v], 0u);
                         atomicExch(&bslot[v], 0xFFFFFFFFu);
                     }
                 }
-                wave_push(multi, v, nxt, &L.qtail, cap, stats);
+                wave_push(multi, v, pnxt, &L.qtail, cap, stats);
             }
             __syncthreads();
             const uint32_t nM = min(L.qtail, cap);
             __syncthreads();
             if (nM > 0) {
                 expand_queue(
-                    nxt, nM, g, L,
+                    pnxt, nM, g, L,
                     [&](uint32_t v, double& val) {
                         val = bits2d(D.get(v));
                         return true;
@@ -578,7 +815,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                     });
             }
             for (uint32_t i = tid; i < nS; i += kSsspBlock) {
-                const uint32_t v = farq[i];
+                const uint32_t v = fscr[i];
                 const uint32_t j = ld_l2_u32(&bslot[v]);
                 const uint32_t c = ld_l2_u32(&cntc[v]);
                 if (j == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
@@ -599,16 +836,16 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 bool p = false;
                 uint32_t u = 0;
                 if (i < nF) {
-                    u = par[cur[i]];
+                    u = par[pcur[i]];
                     p = (u != src) && ((memo[u] & 0xFFFFFFFF00000000ull) != mtag) &&
                         (atomicExch(&stamp[u], iter) != iter);
                     if (p) { best[u] = kInfBits; cntc[u] = 0; bslot[u] = 0xFFFFFFFFu; }
                 }
-                wave_push(p, u, nxt, &L.qtail, cap, stats);
+                wave_push(p, u, pnxt, &L.qtail, cap, stats);
             }
             __syncthreads();
             nF = min(L.qtail, cap);
-            uint32_t* t = cur; cur = nxt; nxt = t;
+            uint32_t* t = pcur; pcur = pnxt; pnxt = t;
             __syncthreads();
         }
 
@@ -696,29 +933,30 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         { unsigned long long t = wall_clock64(); t_tgt += t - tk; tk = t; }
     }
     if (tid == 0) {
+        if (nfarscan) atomicAdd(&stats[ST_FARSCAN], nfarscan);
         ctr[0] = iter;
         ctr[1] = fep;
         ctr[2] = mep;
-        L.relax = 0;
-    }
-    __syncthreads();
-    atomicAdd(&L.relax, relax_local);
-    __syncthreads();
-    if (tid == 0) {
-        atomicAdd(&stats[ST_RELAX], L.relax);
+        atomicAdd(&stats[ST_RELAX], relax_local);
         atomicAdd(&stats[ST_T_INIT], t_init);
         atomicAdd(&stats[ST_T_SSSP], t_sssp);
         atomicAdd(&stats[ST_T_PARENT], t_par);
         atomicAdd(&stats[ST_T_TARGET], t_tgt);
+        atomicAdd(&stats[ST_T_SPLIT], t_split);
         atomicAdd(&stats[ST_NEAR_IT], n_near);
         atomicAdd(&stats[ST_SPLITS], n_split);
+        atomicAdd(&stats[ST_EV0 + 0], ev0);
+        atomicAdd(&stats[ST_EV0 + 3], ev3);
+        atomicAdd(&stats[ST_EV0 + 4], ev4);
+        atomicAdd(&stats[ST_EV0 + 5], ev5);
     }
-    // per-lane event counts -> one atomic per wave
-    for (int k = 0; k < 8; k++) {
-        unsigned long long x = ev[k];
+    if constexpr (EV) {  // per-lane event counts -> one atomic per wave
+        for (int k = 0; k < 8; k++) {
+            unsigned long long x = ev[k];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        if ((tid & 63) == 0 && x) atomicAdd(&stats[ST_EV0 + k], x);
+            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+            if ((tid & 63) == 0 && x) atomicAdd(&stats[ST_EV0 + k], x);
+        }
     }
 }
 
@@ -851,7 +1089,9 @@ uint32_t sssp_hub_capacity() {
 
 hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                             int nsrc, const uint32_t* d_targets, int A, double delta,
-                            int64_t hub_limit, uint32_t par_hubs, double2* out_lr,
+                            int64_t hub_limit, uint32_t par_hubs, uint32_t far_cap,
+                            uint32_t near_cap, double far_window, bool events,
+                            double2* out_lr,
                             uint16_t* out_hops, double* out_rowmin, unsigned long long* d_stats,
                             hipStream_t stream) {
     int grid = ws.slots < nsrc ? ws.slots : nsrc;
@@ -862,14 +1102,19 @@ hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d
     const size_t lds = kLdsCtrlBytes + kLdsBitsBytes + (size_t)hubs * 8;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)sssp_rows_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)kSsspMaxLds);
-        if (e != hipSuccess) return e;
+        for (const void* k : {(const void*)sssp_rows_kernel<false>,
+                              (const void*)sssp_rows_kernel<true>}) {
+            hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)kSsspMaxLds);
+            if (e != hipSuccess) return e;
+        }
         attr_set = true;
     }
-    hipLaunchKernelGGL(sssp_rows_kernel, dim3(grid), dim3(kSsspBlock), lds, stream, g, ws,
-                       d_sources, nsrc, d_targets, A, delta, hubs, par_hubs, out_lr, out_hops,
+    hipLaunchKernelGGL(events ? sssp_rows_kernel<true> : sssp_rows_kernel<false>, dim3(grid),
+                       dim3(kSsspBlock), lds, stream, g, ws,
+                       d_sources, nsrc, d_targets, A, delta, hubs, par_hubs, far_cap, near_cap,
+                       far_window > 0 ? far_window : 8.0, out_lr,
+                       out_hops,
                        out_rowmin, d_stats);
     return hipGetLastError();
 }
@@ -918,7 +1163,7 @@ hipError_t launch_fill_u64(unsigned long long* p, unsigned long long v, int64_t 
 
 int sssp_max_blocks_per_cu() {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sssp_rows_kernel, kSsspBlock,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sssp_rows_kernel<false>, kSsspBlock,
                                                      kSsspMaxLds) !=
         hipSuccess)
         return 1;

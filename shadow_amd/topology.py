@@ -236,7 +236,7 @@ class Topology:
         out = {k: getattr(s, k) for k, _ in L.ShdStats._fields_}
         out["phase_ms"] = list(out["phase_ms"])
         out["events"] = dict(zip(("expanded", "tail_relax", "tail_improve", "far_scanned",
-                                  "far_kept", "parent_vertices", "tail_settled_relax", "ev7"),
+                                  "far_kept", "parent_vertices", "tail_settled_relax", "far_reads"),
                                  list(out["events"])))
         return out
 

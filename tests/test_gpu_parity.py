@@ -73,6 +73,25 @@ def test_sssp_synthetic_table(integer, hubs):
     assert top.getMinimumLatency() == olat.min()
 
 
+@pytest.mark.parametrize("which", ["far", "near"])
+@pytest.mark.parametrize("hubs", [-1, 0])
+def test_sssp_queue_overflow_fallback(hubs, which):
+    """A far pile / near queue too small for the source: entries are lost, the source switches
+    to splits that scan every distance (re-expanding the current bucket after a near-queue
+    loss) with deduplicated pushes, and the table is still bit-exact."""
+    top, g = synthetic_pair(seed=13, n_routers=2500, n_poi=120, n_edges=25000)
+    top.set_option("lds_hubs", hubs)
+    top.set_option(which + "_cap", 48)
+    otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    oa, olat, orel, ohops = g.table(verts)
+    assert st["far_scan_sources"] > 0 and st["errors"] == 0
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+
+
 def test_sssp_rows_shard_equals_full():
     """build_rows on a row range == the same rows of the full table (sharding correctness)."""
     import torch
