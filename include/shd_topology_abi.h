@@ -94,10 +94,12 @@ int shdtopo_version(void);
 Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
 
 /* options: "abort_on_error" (1), "lazy" (1 = K3 first-rooted-wins emulation, 0 = eager
- * forward rows), "delta" (near-far bucket width, ms), "slots" (concurrent SSSP workgroups),
- * "device" (HIP device ordinal), "lds_hubs" (cap on LDS-resident hub distances, -1 = fill),
- * "par_hubs" (hubs with SSSP parent hints), "far_cap" (far-pile entries per slot, 0 = 2V;
- * small values force the scanning-split fallback).  Returns 0 or -1 for an unknown key. */
+ * forward rows), "delta" (delta-stepping bucket width, ms), "slots" (concurrent SSSP
+ * workgroups), "device" (HIP device ordinal), "lds_hubs" (cap on LDS-resident hub distances,
+ * -1 = fill), "par_hubs" (hubs with SSSP parent hints), "wg_per_cu" (SSSP workgroups sharing a
+ * CU's LDS), "far_cap" / "near_cap" (entries per window bucket and overflow pile / per near
+ * queue, 0 = sized from V; small values force the scanning fallback), "events" (1 = diagnostic
+ * kernel with event counters).  Returns 0 or -1 for an unknown key. */
 int shdtopo_set_option(Topology* top, const char* key, double value);
 
 /* attach by raw IP and a rand_r state (same algorithm and RNG use as topology_attach) */
@@ -155,14 +157,14 @@ typedef struct {
     double phase_ms[4];       /* SSSP kernel time summed over workgroups: init, near-far SSSP,
                                  parent derivation, per-target epilogue */
     int64_t near_iterations;  /* near-phase iterations summed over sources */
-    int64_t far_splits;       /* far-pile splits summed over sources */
+    int64_t far_splits;       /* buckets taken from the bucket window, summed over sources */
     int64_t slots;            /* concurrent SSSP workgroups of the last launch */
-    int64_t events[8];        /* expanded vertices, tail relaxations, tail improvements, far
-                                 entries scanned, far entries kept, parent-pass vertices,
-                                 relaxations onto settled tail vertices, far-entry distance
-                                 reads */
-    int64_t far_scan_sources; /* sources whose far pile overflowed (scanning splits instead) */
-    double split_ms;          /* far-pile split time summed over workgroups (part of phase 1) */
+    int64_t events[8];        /* queue entries expanded, tail relaxations, tail improvements,
+                                 window entries taken, overflow entries refilled, parent-pass
+                                 vertices, relaxations onto settled tail vertices, stale
+                                 entries skipped (events 1, 2, 6, 7 need option "events") */
+    int64_t far_scan_sources; /* sources that overflowed a queue (scanning buckets instead) */
+    double split_ms;          /* bucket changes + refills, summed over workgroups (in phase 1) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

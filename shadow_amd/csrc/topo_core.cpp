@@ -103,12 +103,13 @@ struct _Topology {
     int device = 0;
     int64_t hubLimit = -1;  // LDS-cached hub distances (-1 = fill the LDS)
     int64_t parHubs = 2048; // hubs whose parent is hinted during the SSSP (0 = always scan)
-    double farWindow = 8.0; // pile-1 key window, in multiples of delta
+    int wgPerCu = 1;        // SSSP workgroups per CU (each owns 1/wgPerCu of the LDS)
     bool events = false;    // per-edge event counters (diagnostic kernel build)
     int64_t nearCap = 0;    // near-queue entries per slot (0 = 2V; small values force the
                             // bucket-rescan fallback, for tests)
-    int64_t farCap = 0;     // far-pile entries per slot (0 = 2V; small values force the
-                            // scanning-split fallback, for tests)
+    int64_t farCap = 0;     // cap on the entries of one window bucket and of the overflow pile
+                            // (0 = sized from V; small values force the scanning fallback,
+                            // for tests)
 
     // attach state (shd-topology.c:20-24 virtualIP)
     std::shared_mutex ipMu;
@@ -133,7 +134,7 @@ struct _Topology {
     std::vector<int32_t> inv;   // old -> new
     DevBuf<uint32_t> d_rowptr, d_adj;
     DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
-    DevBuf<unsigned long long> d_dist, d_best, d_memo, d_far, d_farkey, d_qa, d_qb;
+    DevBuf<unsigned long long> d_dist, d_best, d_memo, d_ring, d_over, d_qa, d_qb;
     DevBuf<uint32_t> d_stamp, d_cnt, d_bslot, d_par, d_pathbuf,
         d_counters;
     int slots = 0;
@@ -298,6 +299,8 @@ int dev_init(Topology* top) {
 // CSR without self loops, vertices relabelled by descending degree so that the hot (hub)
 // distance words cluster in a few cache lines (power-law graphs: most adjacency entries point
 // at hubs).  Self loops go to selfLat/selfLoss (first = lowest edge id, as orc_get_eid).
+SsspLdsPlan lds_plan(Topology* top);
+
 int upload_csr(Topology* top) {
     if (top->csrUploaded) return 0;
     HostGraph& g = top->g;
@@ -317,7 +320,7 @@ int upload_csr(Topology* top) {
     // 2) tail: grouped by "primary hub" (its highest-degree hub neighbour), so that expanding a
     //    hub relaxes a dense run of tail distance words (8 per 64-B line) instead of one random
     //    line per neighbour -- the SSSP is bound by random DRAM requests (profiles/).
-    const int64_t H = std::min<int64_t>(V, (int64_t)sssp_hub_capacity());
+    const int64_t H = (int64_t)lds_plan(top).H;
     if (getenv("SHDTOPO_NO_TAILGROUP") == nullptr && H < V) {
         std::vector<int32_t> hubrank((size_t)V, INT32_MAX);
         for (int64_t i = 0; i < H; i++) hubrank[(size_t)top->perm[(size_t)i]] = (int32_t)i;
@@ -406,6 +409,12 @@ int upload_csr(Topology* top) {
     return 0;
 }
 
+SsspLdsPlan lds_plan(Topology* top) {
+    return sssp_lds_plan(top->wgPerCu, top->hubLimit,
+                         (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 30)),
+                         top->g.V);
+}
+
 DevCSR dev_csr(Topology* top) {
     DevCSR c;
     c.V = top->g.V;
@@ -424,8 +433,11 @@ int ensure_workspace(Topology* top, int nsrc) {
     const int64_t V = top->g.V;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, top->device));
-    int want = top->slotsOpt > 0 ? top->slotsOpt : prop.multiProcessorCount * sssp_max_blocks_per_cu();
-    size_t per_slot = (size_t)V * (48 + 16 * kFarPerVertex + 16 * kNearPerVertex) + (size_t)kMaxHops * kSsspBlock * 4 + 16;
+    int want = top->slotsOpt > 0 ? top->slotsOpt
+                                 : prop.multiProcessorCount * sssp_max_blocks_per_cu(top->wgPerCu);
+    // dist/best/memo 24 B, stamp/cnt/bslot/par 16 B, near queues, window, overflow piles
+    size_t per_slot = (size_t)V * (40 + 16 * kNearPerVertex + 8 * kRingPerVertex + 16 * kOverPerVertex) +
+                      (size_t)kMaxHops * kSsspBlock * 4 + 16;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     int memcap = (int)std::max<size_t>(1, (freeb / 2) / per_slot);
@@ -439,8 +451,8 @@ int ensure_workspace(Topology* top, int nsrc) {
     HIPCHK(top->d_stamp.ensure(n));
     HIPCHK(top->d_qa.ensure(n * kNearPerVertex));
     HIPCHK(top->d_qb.ensure(n * kNearPerVertex));
-    HIPCHK(top->d_far.ensure(n * 2 * kFarPerVertex));
-    HIPCHK(top->d_farkey.ensure(n));
+    HIPCHK(top->d_ring.ensure(n * kRingPerVertex));
+    HIPCHK(top->d_over.ensure(n * 2 * kOverPerVertex));
     HIPCHK(top->d_cnt.ensure(n));
     HIPCHK(top->d_bslot.ensure(n));
     HIPCHK(top->d_par.ensure(n));
@@ -448,7 +460,6 @@ int ensure_workspace(Topology* top, int nsrc) {
     HIPCHK(top->d_counters.ensure((size_t)want * 4));
     HIPCHK(hipMemsetAsync(top->d_stamp.p, 0, sizeof(uint32_t) * n, top->stream));
     HIPCHK(hipMemsetAsync(top->d_memo.p, 0, sizeof(unsigned long long) * n, top->stream));
-    HIPCHK(hipMemsetAsync(top->d_farkey.p, 0xFF, sizeof(unsigned long long) * n, top->stream));
     HIPCHK(hipMemsetAsync(top->d_counters.p, 0, sizeof(uint32_t) * (size_t)want * 4, top->stream));
     HIPCHK(hipStreamSynchronize(top->stream));
     top->slots = want;
@@ -460,7 +471,7 @@ SlotWs slot_ws(Topology* top) {
     w.slots = top->slots;
     w.V = top->g.V;
     w.dist = top->d_dist.p; w.stamp = top->d_stamp.p;
-    w.qa = top->d_qa.p; w.qb = top->d_qb.p; w.far = top->d_far.p; w.farkey = top->d_farkey.p;
+    w.qa = top->d_qa.p; w.qb = top->d_qb.p; w.ring = top->d_ring.p; w.over = top->d_over.p;
     w.best = top->d_best.p; w.cnt = top->d_cnt.p; w.bslot = top->d_bslot.p;
     w.memo = top->d_memo.p; w.par = top->d_par.p; w.pathbuf = top->d_pathbuf.p;
     w.counters = top->d_counters.p;
@@ -553,10 +564,9 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         HIPCHK(hipMemcpyAsync(top->d_targets.p, tgt.data(), sizeof(uint32_t) * (size_t)A, hipMemcpyHostToDevice, st));
         HIPCHK(hipEventRecord(top->ev0, st));
         HIPCHK(launch_sssp_rows(dev_csr(top), slot_ws(top), top->d_sources.p, (int)rows,
-                                top->d_targets.p, (int)A, default_delta(top), top->hubLimit,
-                                (uint32_t)top->parHubs, (uint32_t)top->farCap,
-                                (uint32_t)top->nearCap,
-                                top->farWindow, top->events,
+                                top->d_targets.p, (int)A, default_delta(top), lds_plan(top),
+                                (uint32_t)top->farCap,
+                                (uint32_t)top->nearCap, top->events,
                                 out_lr, out_hops,
                                 out_rowmin, top->d_stats.p, st));
         HIPCHK(hipEventRecord(top->ev1, st));
@@ -904,9 +914,9 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "device") top->device = (int)value;
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
     else if (k == "par_hubs") top->parHubs = (int64_t)value;
+    else if (k == "wg_per_cu") top->wgPerCu = std::max(1, std::min(8, (int)value));
     else if (k == "far_cap") top->farCap = (int64_t)value;
     else if (k == "near_cap") top->nearCap = (int64_t)value;
-    else if (k == "far_window") top->farWindow = value;
     else if (k == "events") top->events = value != 0;
     else return -1;
     return 0;

@@ -4,7 +4,7 @@
 //   CSR of the undirected topology without self loops:
 //     rowptr u32[V+1], adj {u32 col, f64 latency}[2E'] (12-B AoS), aloss f64[2E'] (edge loss)
 //   per vertex: vloss f64[V], selfLat f64[V] (NaN = no self loop), selfLoss f64[V]
-//   per SSSP slot (one workgroup = one source at a time): 56 B x V of workspace
+//   per SSSP slot (one workgroup = one source at a time): 232 B x V of workspace
 //   routing table: {f64 lat, f64 rel}[A][A] (16-B records, one gather per packet) + u16 hops
 #pragma once
 
@@ -14,11 +14,18 @@
 
 namespace shdtopo {
 
-constexpr int kSsspBlock = 1024;  // threads per SSSP workgroup (16 waves)
+#ifndef SHD_SSSP_BLOCK
+#define SHD_SSSP_BLOCK 1024
+#endif
+constexpr int kSsspBlock = SHD_SSSP_BLOCK;  // threads per SSSP workgroup
 constexpr int kMaxHops = 48;      // per-thread path buffer depth (longer paths: O(h^2) walk)
-constexpr int kFarPerVertex = 3;  // far-pile capacity per slot, in entries per vertex (pile 1:
-                                  // V, pile 2: 2V; pile 2 keeps superseded entries until a
-                                  // refill), each pile double buffered
+#ifndef SHD_RING_PER_VERTEX
+#define SHD_RING_PER_VERTEX 16
+#endif
+constexpr int kRingPerVertex = SHD_RING_PER_VERTEX;  // bucket-window entries per slot, in entries
+                                                     // per vertex (split evenly over the buckets)
+constexpr int kOverPerVertex = 2;  // overflow-pile capacity per slot, in entries per vertex
+                                   // (double buffered: a refill streams the kept entries over)
 constexpr int kNearPerVertex = 2; // near-queue capacity per slot, in entries per vertex
 
 // indices into the device stats block (unsigned long long[16])
@@ -35,13 +42,14 @@ enum StatIdx {
     ST_T_PARENT = 9,    //   parent derivation for the target chains
     ST_T_TARGET = 10,   //   per-target latency / reliability / hops
     ST_NEAR_IT = 11,    // near-phase iterations
-    ST_SPLITS = 12,     // far-pile splits
-    ST_EV0 = 13,        // event counters (ShdStats.events): expanded vertices, tail relaxations,
-                        // tail improvements, far entries scanned, far entries kept, parent-pass
-                        // vertices
-    ST_FARSCAN = 21,
-    ST_T_SPLIT = 22,
-    ST_OVERSITE = 23,   // OR of the push sites that overflowed (diagnostic)    // wall-clock ticks summed over workgroups: far-pile splits (in T_SSSP)    // sources whose far pile overflowed (finished with scanning splits)
+    ST_SPLITS = 12,     // buckets taken from the bucket window
+    ST_EV0 = 13,        // event counters (ShdStats.events): queue entries expanded, tail
+                        // relaxations, tail improvements, window entries taken, overflow entries
+                        // refilled, parent-pass vertices, relaxations onto settled tail vertices,
+                        // stale entries skipped
+    ST_FARSCAN = 21,    // sources that overflowed a queue (finished with scanning buckets)
+    ST_T_SPLIT = 22,    // wall-clock ticks summed over workgroups: bucket changes + refills
+    ST_OVERSITE = 23,   // OR of the push sites that overflowed (diagnostic)
     ST_COUNT = 24
 };
 
@@ -65,28 +73,35 @@ struct SlotWs {
     uint32_t* stamp = nullptr;           // near-queue / chain-queue dedupe (iteration id)
     unsigned long long* qa = nullptr;  // near queues: (hi32 of the pushed distance << 32) |
     unsigned long long* qb = nullptr;  // vertex, kNearPerVertex * V entries (no dedupe)
-    unsigned long long* farkey = nullptr;  // per vertex: (~source epoch << 32) | hi32 of the
-                                           // smallest far key pushed (atomicMin dedupe)
-    unsigned long long* far = nullptr;   // far pile: (hi32 of the f64 key << 32) | vertex, 2V
-                                         // entries (tail entries are not deduplicated)
+    unsigned long long* ring = nullptr;  // bucket window: kRingPerVertex * V entries, same format
+    unsigned long long* over = nullptr;  // overflow pile (buckets past the window), 2 buffers of
+                                         // kOverPerVertex * V entries
     unsigned long long* best = nullptr;  // parent pass: min d[u] over candidates
     uint32_t* cnt = nullptr;             // parent pass: candidates at the min
     uint32_t* bslot = nullptr;           // parent pass: lowest adjacency slot at the min
     unsigned long long* memo = nullptr;  // (source epoch << 32) | ambiguous << 31 | slot
     uint32_t* par = nullptr;             // parent vertex
     uint32_t* pathbuf = nullptr;         // [slot][kMaxHops][kSsspBlock]
-    uint32_t* counters = nullptr;        // [slot][4]: iteration id, far epoch, source epoch
+    uint32_t* counters = nullptr;        // [slot][4]: iteration id, (unused), source epoch
 };
 
-// hub_limit: cap on LDS-cached vertices (-1 = as many as fit, ~18k)
+// LDS plan of one SSSP workgroup: H hub distance words (+ their queue bitmaps) and P parent
+// hints, sized to the workgroup's share of the CU's 160 KiB (wg_per_cu workgroups per CU).
+struct SsspLdsPlan {
+    uint32_t H = 0;     // LDS-resident hub distances (vertex ids 0..H-1 after the relabel)
+    uint32_t P = 0;     // hubs with parent hints (P <= H)
+    size_t bytes = 0;   // dynamic LDS per workgroup
+};
+// hub_limit: cap on H (-1 = as many as fit); V: vertices of the graph (H <= V)
+SsspLdsPlan sssp_lds_plan(int wg_per_cu, int64_t hub_limit, uint32_t par_hubs, int64_t V);
+
 hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                             int nsrc, const uint32_t* d_targets, int A, double delta,
-                            int64_t hub_limit, uint32_t par_hubs, uint32_t far_cap,
-                            uint32_t near_cap, double far_window, bool events,
+                            const SsspLdsPlan& plan, uint32_t far_cap,
+                            uint32_t near_cap, bool events,
                             double2* out_lr,
                             uint16_t* out_hops, double* out_rowmin, unsigned long long* d_stats,
                             hipStream_t stream);
-uint32_t sssp_hub_capacity();
 
 hipError_t launch_pair_table_complete(int A, int64_t row0, int64_t rows, const double* elatAA,
                                       const double* elossAA, const double* vlossA, double2* out_lr,
@@ -105,6 +120,7 @@ hipError_t launch_row_min(int64_t rows, int64_t A, const double2* lr, double* ou
 hipError_t launch_fill_u64(unsigned long long* p, unsigned long long v, int64_t n,
                            hipStream_t stream);
 
-int sssp_max_blocks_per_cu();
+// SSSP workgroups one CU holds with the LDS plan of wg_per_cu (registers and LDS permitting)
+int sssp_max_blocks_per_cu(int wg_per_cu);
 
 }  // namespace shdtopo

@@ -50,31 +50,60 @@ __device__ __forceinline__ void adj_load(const DevCSR& g, uint32_t j, uint32_t& 
     wt = __hiloint2double((int)r.c, (int)r.b);
 }
 
+#ifndef SHD_RING_SLOTS
+#define SHD_RING_SLOTS 48
+#endif
+constexpr int kRingSlots = SHD_RING_SLOTS;  // buckets in the window (<= 64: one ballot scans them)
+static_assert(kRingSlots >= 2 && kRingSlots <= 64, "window slots must fit one wave ballot");
+
 struct Lds {
     uint32_t off[kSsspBlock + 4];
     uint32_t rs[kSsspBlock];
     uint32_t vx[kSsspBlock];
     double val[kSsspBlock];
     uint32_t wave[kSsspBlock / 64];
+    uint32_t rtail[kRingSlots];  // entries pushed into each bucket of the window
     uint32_t qtail;
-    uint32_t ftail;
+    uint32_t otail;    // entries in the overflow pile
     uint32_t src_idx;
-    uint32_t fover;  // far pile overflowed for this source: splits scan the distances instead
-    uint32_t nover;  // a near queue overflowed since the last split: rescan the whole bucket
-    uint32_t f2tail;  // entries in the second-level far pile
+    uint32_t fover;    // a window slot / the overflow pile overflowed: scanning buckets from now on
+    uint32_t nover;    // a near queue overflowed since the last bucket change: re-expand the bucket
+    uint32_t pad;
     unsigned long long dmin;
-    unsigned long long fmin;  // lower bound of the live distances in far pile 1
-    unsigned long long fmin2; // lower bound of the live keys in far pile 2
-    unsigned long long relax;
+    unsigned long long fmin;  // scanning mode: lower bound of the unexpanded distances above cb
+    unsigned long long omin;  // lower bound of the keys in the overflow pile
 };
 constexpr size_t kLdsCtrlBytes = (sizeof(Lds) + 15) / 16 * 16;
-constexpr uint32_t kHubBitWords = 640;  // queue-dedupe bitmaps for up to 20480 LDS hubs
-constexpr uint32_t kParHubs = 2048;      // hubs whose parent is tracked during the SSSP
-constexpr size_t kLdsBitsBytes = 2 * kHubBitWords * 4 + kParHubs / 8 + kParHubs * 4;
-constexpr size_t kSsspMaxLds = 160 * 1024;  // one workgroup per CU owns the whole LDS
-constexpr int kRelaxUnroll = 4;
-static_assert((kSsspMaxLds - kLdsCtrlBytes - kLdsBitsBytes) / 8 <= kHubBitWords * 32,
-              "hub bitmaps must cover every LDS-resident hub");
+constexpr uint32_t kParHubs = 2048;         // hubs whose parent is tracked during the SSSP
+constexpr size_t kSsspMaxLds = 160 * 1024;  // LDS of one CU, shared by its SSSP workgroups
+#ifndef SHD_RELAX_UNROLL
+#define SHD_RELAX_UNROLL 4
+#endif
+constexpr int kRelaxUnroll = SHD_RELAX_UNROLL;
+// Tail relaxations: a plain pre-check load, then a no-return atomicMin when the candidate is
+// smaller; the push is decided on the pre-check (a lost race pushes a stale entry, skipped or
+// re-expanded harmlessly), so no returning atomic sits on the relaxation's dependency chain.
+#ifndef SHD_TAIL_NORET
+#define SHD_TAIL_NORET 1
+#endif
+
+// Dynamic LDS after the control block: the near-queue dedupe bitmap nbits[hw], parent-tie bits
+// tbits[pw], parent hints hpar[P] (u32), then the hub distance words hd[H] (u64).
+struct LdsLayout {
+    uint32_t hw, pw;
+    size_t nbits, tbits, hpar, hd, bytes;
+};
+__host__ __device__ inline LdsLayout lds_layout(uint32_t H, uint32_t P) {
+    LdsLayout l;
+    l.hw = (H + 31) / 32;
+    l.pw = (P + 31) / 32;
+    l.nbits = kLdsCtrlBytes;
+    l.tbits = l.nbits + 4 * (size_t)l.hw;
+    l.hpar = l.tbits + 4 * (size_t)l.pw;
+    l.hd = (l.hpar + 4 * (size_t)P + 7) & ~(size_t)7;
+    l.bytes = l.hd + 8 * (size_t)H;
+    return l;
+}
 
 // Wave-aggregated queue append: one LDS atomic per wave instead of one per lane.
 __device__ __forceinline__ void wave_push(bool pred, uint32_t val, uint32_t* q, uint32_t* lds_tail,
@@ -206,7 +235,6 @@ struct DistView {
     unsigned long long* hd;    // LDS, H words
     unsigned long long* dist;  // HBM, V words (words < H unused while the source runs)
     uint32_t* nbits;           // LDS: hub already in the next near queue (this iteration)
-    uint32_t* fbits;           // LDS: hub currently in the far pile
     uint32_t* hpar;            // LDS: vertex whose relaxation last lowered hub v (v < kParHubs)
     uint32_t* tbits;           // LDS: a relaxation tied hub v's current distance (v < kParHubs)
     uint32_t H;
@@ -216,37 +244,87 @@ struct DistView {
     }
 };
 
+// Bucket of a distance: floor(d / delta) by one IEEE multiply, monotone non-decreasing in d (so a
+// bucket is an interval of distances); +inf and huge values land in the last bucket.
+__device__ __forceinline__ uint32_t bucket_of(double d, double inv_delta) {
+    const double b = d * inv_delta;
+    return b < 4.0e9 ? (uint32_t)b : 4000000000u;
+}
+
+// The buckets of one source.  The window holds the kRingSlots buckets [wbase, wbase + kRingSlots)
+// in fixed slots; later buckets go to the overflow pile, which a refill re-sorts into the window
+// once the window is used up.  cb = the bucket being settled.
+struct Buckets {
+    double inv_delta;
+    uint32_t cb, wbase;
+    unsigned long long* ring;  // kRingSlots slots of slot_cap entries
+    uint32_t slot_cap;
+    unsigned long long* over;  // overflow pile (current buffer)
+    uint32_t ocap;
+};
+
+// Window push: lanes may target different slots; one LDS atomic per (wave, slot).
+__device__ __forceinline__ void ring_push(bool pred, uint32_t slot, unsigned long long val,
+                                          const Buckets& B, Lds& L) {
+    unsigned long long m = __ballot(pred);
+    const int lane = threadIdx.x & 63;
+    while (m) {
+        const int leader = __ffsll((long long)m) - 1;
+        const uint32_t s = __shfl(slot, leader, 64);
+        const bool mine = pred && slot == s;
+        const unsigned long long mm = __ballot(mine);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&L.rtail[s], (uint32_t)__popcll(mm));
+        base = __shfl(base, leader, 64);
+        if (mine) {
+            const uint32_t pos = base + (uint32_t)__popcll(mm & ((1ull << lane) - 1ull));
+            if (pos < B.slot_cap) B.ring[(size_t)s * B.slot_cap + pos] = val;
+            else atomicOr(&L.fover, 2u);
+        }
+        m &= ~mm;
+    }
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(x, o, 64);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
 // Near-phase relaxation of queue Q: the load-balanced chunking of expand_queue, with U edges in
-// flight per lane: U (col, wt) loads, then the U tail pre-checks, then the LDS / HBM atomics, then
-// the queue pushes.
+// flight per lane: U (col, wt) loads, then the U tail pre-checks, then the LDS atomics / no-return
+// HBM atomics, then the pushes.  An improvement to bucket b goes to the near queue (b <= cb), the
+// window slot of b, or the overflow pile.  scan: scanning mode after an overflow (near pushes
+// deduplicated by stamp, far improvements only lower L.fmin).
 template <int U, bool EV>
 __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_t nq,
                                             const DevCSR& g, Lds& L, const DistView& D,
-                                            uint32_t* stamp, bool dedupe,
-                                            unsigned long long* nxt, unsigned long long* farq,
-                                            unsigned long long* farq2,
-                                            unsigned long long* farkey, unsigned long long fe,
-                                            uint32_t it, double th, double bound, double lb,
-                                            uint32_t ncap, uint32_t fcap, uint32_t fcap2,
-                                            unsigned long long* stats,
+                                            uint32_t* stamp, bool scan,
+                                            unsigned long long* nxt, const Buckets& B,
+                                            uint32_t it, uint32_t ncap,
                                             unsigned long long& relax,
                                             unsigned long long* ev) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
+    const uint32_t wend = B.wbase + (uint32_t)kRingSlots;
     for (uint32_t base = 0; base < nq; base += kSsspBlock) {
         const uint32_t cnt = min((uint32_t)kSsspBlock, nq - base);
         uint32_t deg = 0;
         if (tid < cnt) {
-            // a tail entry pushed by a non-deduplicating relaxation carries the high word of its
-            // distance; a later (smaller) push of the same vertex supersedes it, so an entry
-            // whose word is above the current distance's is stale and expands nothing (entries
-            // of deduplicated pushes carry 0)
+            // an entry of a non-deduplicating push carries the high word of its distance; a
+            // later (smaller) push of the same vertex supersedes it, so an entry whose word is
+            // above the current distance's is stale and expands nothing (entries of deduplicated
+            // pushes carry 0)
             const unsigned long long e = Q[base + tid];
             const uint32_t v = (uint32_t)e;
             const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
             const unsigned long long dv = D.get(v);
-            const bool stale = v >= D.H && (dv >> 32) < (e >> 32);
+            const bool stale = (dv >> 32) < (e >> 32);
             deg = stale ? 0u : r1 - r0;
+            if constexpr (EV) ev[7] += stale ? 1ull : 0ull;
             L.rs[tid] = r0;
             L.vx[tid] = v;
             L.val[tid] = bits2d(dv);
@@ -300,70 +378,62 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
             }
 #pragma unroll
             for (int u = 0; u < U; u++)
-                if (ab[u] < cur[u]) imp[u] = ab[u] < atomicMin(&D.dist[n[u]], ab[u]);
-            // every far-side improvement lowers its pile's running minimum (LDS), so a split
-            // needs no extra pass.  Pile 1 takes hubs and keys whose lower bound is < bound.
-            bool p1[U];
-            unsigned long long fm = kInfBits, fm2 = kInfBits;
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                p1[u] = n[u] < D.H || far_key_lb(ab[u]) < bound;
-                if (imp[u] && !(bits2d(ab[u]) < th)) {
-                    if (p1[u]) fm = ab[u] < fm ? ab[u] : fm;
-                    else fm2 = ab[u] < fm2 ? ab[u] : fm2;
+                if (ab[u] < cur[u]) {
+#if SHD_TAIL_NORET
+                    (void)atomicMin(&D.dist[n[u]], ab[u]);
+                    imp[u] = true;
+#else
+                    imp[u] = ab[u] < atomicMin(&D.dist[n[u]], ab[u]);
+#endif
                 }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const unsigned long long y = __shfl_xor(fm, o, 64);
-                fm = y < fm ? y : fm;
-                const unsigned long long y2 = __shfl_xor(fm2, o, 64);
-                fm2 = y2 < fm2 ? y2 : fm2;
-            }
-            if (lane == 0 && fm != kInfBits) atomicMin(&L.fmin, fm);
-            if (lane == 0 && fm2 != kInfBits) atomicMin(&L.fmin2, fm2 & 0xFFFFFFFF00000000ull);
+            unsigned long long om = kInfBits, fm = kInfBits;
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                bool pN = false, pF = false;
+                bool pN = false, pR = false, pO = false;
+                const uint32_t b = imp[u] ? bucket_of(bits2d(ab[u]), B.inv_delta) : 0u;
                 if (imp[u]) {
-                    const bool near = bits2d(ab[u]) < th;
-                    if (n[u] < D.H) {  // hub: dedupe in LDS, no memory-side atomic
-                        const uint32_t bit = 1u << (n[u] & 31);
-                        uint32_t* w = (near ? D.nbits : D.fbits) + (n[u] >> 5);
-                        const bool first = (atomicOr(w, bit) & bit) == 0u;
-                        pN = near && first;
-                        pF = !near && first;
-                    } else if (near) {
-                        // no dedupe: every strict improvement pushes (its value rides along
-                        // and stale entries are skipped at expansion), which keeps a returning
-                        // atomic off the relaxation's dependency chain.  After an overflow the
-                        // source deduplicates per iteration (<= V entries: always fits).
-                        pN = !dedupe || atomicExch(&stamp[n[u]], it) != it;
+                    if (b <= B.cb) {
+                        if (n[u] < D.H) {  // hub: dedupe in LDS, no memory-side atomic
+                            const uint32_t bit = 1u << (n[u] & 31);
+                            pN = (atomicOr(D.nbits + (n[u] >> 5), bit) & bit) == 0u;
+                        } else {
+                            // no dedupe: every strict improvement pushes (its value rides
+                            // along and stale entries are skipped at expansion).  In scanning
+                            // mode the source deduplicates per iteration (<= V entries).
+                            pN = !scan || atomicExch(&stamp[n[u]], it) != it;
+                        }
+                    } else if (scan) {
+                        fm = ab[u] < fm ? ab[u] : fm;
+                    } else if (b < wend) {
+                        pR = true;
                     } else {
-                        // tail: the entry carries its key, so a split never reads the distance
-                        // of an entry that stays far.  A vertex is pushed again only when its
-                        // key's high word drops below every key already pushed for it this
-                        // source (epoch-tagged atomicMin); the older entry is dropped when the
-                        // threshold passes its key.
-                        const unsigned long long fk = fe | (ab[u] >> 32);
-                        pF = fk < atomicMin(&farkey[n[u]], fk);
+                        pO = true;
+                        const unsigned long long k = ab[u] & 0xFFFFFFFF00000000ull;
+                        om = k < om ? k : om;
                     }
                 }
-                // deduplicated pushes carry key 0 (never stale): a later improvement of the
-                // vertex in the same iteration is not pushed again
-                wave_push64(pN, far_entry((n[u] < D.H || dedupe) ? 0ull : ab[u], n[u]), nxt,
+                // hub near pushes and scanning-mode pushes are deduplicated: key 0 (never stale)
+                wave_push64(pN, far_entry((n[u] < D.H || scan) ? 0ull : ab[u], n[u]), nxt,
                             &L.qtail, ncap, &L.nover, 1u);
-                wave_push64(pF && p1[u], far_entry(ab[u], n[u]), farq, &L.ftail, fcap, &L.fover,
-                            2u);
-                wave_push64(pF && !p1[u], far_entry(ab[u], n[u]), farq2, &L.f2tail, fcap2,
-                            &L.fover, 4u);
+                ring_push(pR, b - B.wbase, far_entry(ab[u], n[u]), B, L);
+                wave_push64(pO, far_entry(ab[u], n[u]), B.over, &L.otail, B.ocap, &L.fover, 4u);
                 if constexpr (EV) {
                     ev[1] += (valid[u] && n[u] >= D.H) ? 1ull : 0ull;
                     ev[2] += (imp[u] && n[u] >= D.H) ? 1ull : 0ull;
-                    ev[6] += (valid[u] && n[u] >= D.H && bits2d(cur[u]) < lb) ? 1ull : 0ull;
+                    ev[6] += (valid[u] && n[u] >= D.H &&
+                              bucket_of(bits2d(cur[u]), B.inv_delta) < B.cb) ? 1ull : 0ull;
                 }
             }
+            if (__ballot(om != kInfBits || fm != kInfBits)) {
+                om = wave_min_u64(om);
+                fm = wave_min_u64(fm);
+                if (lane == 0 && om != kInfBits) atomicMin(&L.omin, om);
+                if (lane == 0 && fm != kInfBits) atomicMin(&L.fmin, fm);
+            }
         }
+        // the no-return atomics and queue stores of this wave complete before any wave reads
+        // the distances or queues after the barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
 }
@@ -371,10 +441,10 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
 }  // namespace
 
 template <bool EV>
-__global__ void __launch_bounds__(kSsspBlock)
+__global__ void __launch_bounds__(kSsspBlock, 4)
 sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int nsrc,
                  const uint32_t* __restrict__ targets, int A, double delta, uint32_t hubs,
-                 uint32_t parhubs, uint32_t far_cap, uint32_t near_cap, double far_window,
+                 uint32_t parhubs, uint32_t far_cap, uint32_t near_cap,
                  double2* __restrict__ out_lr, uint16_t* __restrict__ out_hops,
                  double* __restrict__ out_rowmin, unsigned long long* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -383,21 +453,24 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     const uint32_t tid = threadIdx.x;
     const int64_t V = ws.V;
     DistView D;
-    D.nbits = reinterpret_cast<uint32_t*>(smem + kLdsCtrlBytes);
-    D.fbits = D.nbits + kHubBitWords;
-    D.tbits = D.fbits + kHubBitWords;
-    D.hpar = D.tbits + kParHubs / 32;
-    D.hd = reinterpret_cast<unsigned long long*>(smem + kLdsCtrlBytes + kLdsBitsBytes);
+    const LdsLayout lay = lds_layout(hubs, parhubs);
+    const uint32_t hw = lay.hw;
+    D.nbits = reinterpret_cast<uint32_t*>(smem + lay.nbits);
+    D.tbits = reinterpret_cast<uint32_t*>(smem + lay.tbits);
+    D.hpar = reinterpret_cast<uint32_t*>(smem + lay.hpar);
+    D.hd = reinterpret_cast<unsigned long long*>(smem + lay.hd);
     D.dist = ws.dist + (size_t)slot * V;
     D.H = hubs;
-    D.P = parhubs < kParHubs ? parhubs : kParHubs;
+    D.P = parhubs;
     unsigned long long* dist = D.dist;
     uint32_t* stamp = ws.stamp + (size_t)slot * V;
     unsigned long long* qa = ws.qa + (size_t)slot * kNearPerVertex * V;
     unsigned long long* qb = ws.qb + (size_t)slot * kNearPerVertex * V;
-    unsigned long long* farq = ws.far + (size_t)slot * 2 * kFarPerVertex * V;
-    uint32_t* fscr = reinterpret_cast<uint32_t*>(farq);  // parent-pass scratch queue (u32)
-    unsigned long long* farkey = ws.farkey + (size_t)slot * V;
+    const size_t ring_all = (size_t)kRingPerVertex * (size_t)V;
+    const size_t over_all = (size_t)kOverPerVertex * (size_t)V;
+    unsigned long long* over0 = ws.over + (size_t)slot * 2 * over_all;
+    unsigned long long* over1 = over0 + over_all;
+    uint32_t* fscr = reinterpret_cast<uint32_t*>(over0);  // parent-pass scratch queue (u32)
     unsigned long long* best = ws.best + (size_t)slot * V;
     uint32_t* cntc = ws.cnt + (size_t)slot * V;
     uint32_t* bslot = ws.bslot + (size_t)slot * V;
@@ -406,21 +479,23 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     uint32_t* pbuf = ws.pathbuf + (size_t)slot * kMaxHops * kSsspBlock;
     uint32_t* ctr = ws.counters + (size_t)slot * 4;
     const uint32_t cap = (uint32_t)V;
-    // near queues hold kNearPerVertex * V entries; deduplicated pushes (splits, and relaxations
-    // after an overflow) never exceed V.  near_cap only limits non-deduplicated relaxation
-    // pushes (tests force the overflow fallback with it).
+    // near queues hold kNearPerVertex * V entries; deduplicated pushes (scanning mode) never
+    // exceed V.  near_cap / far_cap only shrink the non-deduplicated queues (tests force the
+    // overflow fallback with them).
     const uint32_t ncap = (uint32_t)(kNearPerVertex * V);
     const uint32_t ncap_free = (near_cap > 0 && near_cap < ncap) ? near_cap : ncap;
-    // far pile 1 (fcap entries, V by default) and pile 2 (fcap2, the rest), each double
-    // buffered: a split / refill streams the kept entries into the other buffer
-    const uint32_t fall = (far_cap > 0 && far_cap < (uint32_t)(kFarPerVertex * V))
-                              ? far_cap : (uint32_t)(kFarPerVertex * V);
-    const uint32_t fcap = max(1u, fall / (uint32_t)kFarPerVertex);
-    const uint32_t fcap2 = max(1u, fall - fcap);
-    const double fwin = far_window * delta;
+    Buckets B;
+    B.inv_delta = 1.0 / delta;
+    B.ring = ws.ring + (size_t)slot * ring_all;
+    B.slot_cap = (uint32_t)(ring_all / kRingSlots);
+    B.ocap = (uint32_t)over_all;
+    if (far_cap > 0) {
+        B.slot_cap = min(B.slot_cap, far_cap);
+        B.ocap = min(B.ocap, far_cap);
+    }
 
     // slot-persistent epoch counters (never reset, so stamp/memo need no clearing)
-    uint32_t iter = ctr[0], fep = ctr[1], mep = ctr[2];
+    uint32_t iter = ctr[0], mep = ctr[2];
     unsigned long long relax_local = 0;
     unsigned long long nfarscan = 0;
     unsigned long long ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per-lane (EV builds only)
@@ -438,40 +513,34 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         const uint32_t src = sources[s_idx];
         tk = wall_clock64();
 
-        // ---------------- SSSP (near-far) ----------------
+        // ---------------- SSSP (delta-stepping: near queue + bucket window + overflow) -------
         for (uint32_t v = tid; v < D.H; v += kSsspBlock) D.hd[v] = kInfBits;
-        for (uint32_t w = tid; w < kHubBitWords; w += kSsspBlock) D.fbits[w] = 0u;
-        for (uint32_t w = tid; w < kParHubs / 32; w += kSsspBlock) D.tbits[w] = 0u;
+        for (uint32_t w = tid; w < lay.pw; w += kSsspBlock) D.tbits[w] = 0u;
+        for (uint32_t k = tid; k < (uint32_t)kRingSlots; k += kSsspBlock) L.rtail[k] = 0u;
         for (int64_t v = (int64_t)D.H + tid; v < V; v += kSsspBlock) dist[v] = kInfBits;
         __syncthreads();
         { unsigned long long t = wall_clock64(); t_init += t - tk; tk = t; }
         iter++;
-        fep++;
-        const unsigned long long fe = (unsigned long long)(~fep) << 32;
         if (tid == 0) {
             L.fover = 0u;
-            if (src < D.H) D.hd[src] = 0ull; else dist[src] = 0ull;
             L.nover = 0u;
+            if (src < D.H) D.hd[src] = 0ull; else dist[src] = 0ull;
             qa[0] = far_entry(0ull, src);
             stamp[src] = iter;
-            L.ftail = 0;
-            L.f2tail = 0;
+            L.otail = 0;
+            L.omin = kInfBits;
             L.fmin = kInfBits;
-            L.fmin2 = kInfBits;
         }
         __syncthreads();
-        unsigned long long* cur = qa;
-        unsigned long long* nxt = qb;
-        unsigned long long* f1 = farq;
-        unsigned long long* f1alt = farq + fcap;
-        unsigned long long* f2 = farq + 2 * (size_t)fcap;
-        unsigned long long* f2alt = f2 + fcap2;
-        uint32_t nq = 1, n1 = 0, n2 = 0;
-        double thr = delta;
-        double bound = __dadd_rn(thr, fwin);  // pile 1 holds keys below bound, pile 2 the rest
-        double lb = 0.0;  // every vertex with d < lb is final (the last completed bucket)
+        B.cb = 0;
+        B.wbase = 0;
+        B.over = over0;
+        unsigned long long* over_alt = over1;
+        const unsigned long long* inq = qa;  // near-phase input: a near queue or a window slot
+        unsigned long long* qnxt = qb;       // near-phase output (never aliases inq)
+        uint32_t nq = 1;
         uint32_t guard = 0;
-        constexpr int FU = 4;  // pile entries per lane per chunk (reads in flight)
+        constexpr int FU = 4;  // entries per lane per chunk in the streaming passes
         unsigned long long tsplit0 = 0;
         for (;;) {
             if (tsplit0) {
@@ -481,52 +550,44 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
             while (nq > 0) {
                 iter++;
                 if (tid == 0) L.qtail = 0;
-                for (uint32_t w = tid; w < kHubBitWords; w += kSsspBlock) D.nbits[w] = 0u;
+                for (uint32_t w = tid; w < hw; w += kSsspBlock) D.nbits[w] = 0u;
                 __syncthreads();
                 ev0 += nq;
-                const bool dedupe = L.fover != 0u;
-                relax_queue<kRelaxUnroll, EV>(cur, nq, g, L, D, stamp, dedupe, nxt, f1, f2,
-                                              farkey, fe, iter, thr, bound, lb,
-                                              dedupe ? ncap : ncap_free, fcap, fcap2, stats,
-                                              relax_local, ev);
+                const bool scan = L.fover != 0u;
+                relax_queue<kRelaxUnroll, EV>(inq, nq, g, L, D, stamp, scan, qnxt, B, iter,
+                                              scan ? ncap : ncap_free, relax_local, ev);
                 // relax_queue ends with a barrier
                 nq = min(L.qtail, ncap);
-                n1 = min(L.ftail, fcap);
-                n2 = min(L.f2tail, fcap2);
-                unsigned long long* t = cur; cur = nxt; nxt = t;
+                inq = qnxt;
+                qnxt = (qnxt == qa) ? qb : qa;
                 n_near++;
                 if (++guard > 4000000u) {
                     if (tid == 0) atomicOr(&stats[ST_OVERFLOW], 2ull);
                     nq = 0;
-                    n1 = n2 = 0;
                 }
                 __syncthreads();
             }
-            const bool nov = L.nover != 0u;
-            const bool scanmode = L.fover != 0u || nov;
-            const unsigned long long fmin1b = L.fmin, fmin2b = L.fmin2;
-            const unsigned long long fminall = fmin1b < fmin2b ? fmin1b : fmin2b;
-            if (!nov && (scanmode ? fminall == kInfBits : (n1 == 0 && n2 == 0))) break;
-            n_split++;
+            if (guard > 4000000u) break;
             tsplit0 = wall_clock64();
-            const double oldthr = thr;
-            double newthr;
-            if (scanmode) {
-                // A pile overflowed (entries were lost): classify every vertex by its distance
-                // instead, for the rest of this source.  Every unexpanded vertex has d >= thr,
-                // so d in [thr, newthr) is exactly the next near set -- unless a near queue
-                // overflowed since the last split: then vertices of the current bucket
-                // [lb, thr) may have been lost too, and the whole bucket is expanded again
-                // (re-expansion is harmless for a label-correcting SSSP).  Sequential,
-                // coalesced reads.
-                newthr = fminall == kInfBits ? thr : __dadd_rn(fmax(bits2d(fminall), thr), delta);
-                const double lo = nov ? lb : oldthr;
+            const bool nov = L.nover != 0u;
+            if (L.fover != 0u || nov) {
+                // Scanning mode: a queue overflowed (entries were lost), so for the rest of this
+                // source the next bucket is found by classifying every vertex by its distance.
+                // Every unexpanded vertex is in a bucket > cb -- unless a near queue overflowed
+                // since the last bucket change: then the whole bucket cb is expanded again
+                // (re-expansion is harmless for a label-correcting SSSP).  L.fmin is exact after
+                // the first scanning pass (bit 64 of fover), a lower bound before.
+                const bool exact = (L.fover & 64u) != 0u;
+                const unsigned long long fmb = L.fmin;
+                if (!nov && exact && fmb == kInfBits) break;
+                uint32_t nb = B.cb + 1;
+                if (exact && fmb != kInfBits) nb = max(nb, bucket_of(bits2d(fmb), B.inv_delta));
+                const uint32_t lob = nov ? B.cb : B.cb + 1;
                 iter++;
                 __syncthreads();
                 if (tid == 0) {
                     L.qtail = 0;
                     L.fmin = kInfBits;
-                    L.fmin2 = kInfBits;
                     L.nover = 0u;
                     L.fover |= 64u;
                 }
@@ -537,152 +598,93 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                     for (int u = 0; u < FU; u++) {
                         const uint32_t v = base + (uint32_t)u * kSsspBlock + tid;
                         bool pN = false;
-                        unsigned long long b = kInfBits;
                         if (v < (uint32_t)V) {
-                            b = D.get(v);
-                            const double d = bits2d(b);
-                            pN = !(d < lo) && d < newthr;
-                            if (!(d < newthr) && b < km) km = b;
+                            const unsigned long long b = D.get(v);
+                            const uint32_t k = bucket_of(bits2d(b), B.inv_delta);
+                            pN = b != kInfBits && k >= lob && k <= nb;
+                            if (b != kInfBits && k > nb && b < km) km = b;
                         }
-                        wave_push64(pN, far_entry(0ull, v), cur, &L.qtail, ncap, &L.nover, 32u);
+                        wave_push64(pN, far_entry(0ull, v), qnxt, &L.qtail, ncap, &L.nover, 32u);
                     }
-#pragma unroll
-                    for (int o = 32; o > 0; o >>= 1) {
-                        const unsigned long long y = __shfl_xor(km, o, 64);
-                        km = y < km ? y : km;
-                    }
+                    km = wave_min_u64(km);
                     if ((tid & 63) == 0 && km != kInfBits) atomicMin(&L.fmin, km);
                 }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 nq = min(L.qtail, ncap);
-                if (!nov) lb = oldthr;
-                thr = newthr;
+                inq = qnxt;
+                qnxt = (qnxt == qa) ? qb : qa;
+                B.cb = nb;
+                n_split++;
                 __syncthreads();
                 continue;
             }
-            // ---- two-level far pile ----
-            // Invariants: an entry's key lower bound (hi32 truncation of the f64 bits) never
-            // exceeds its vertex's distance at push time; every live (unexpanded) vertex v has
-            // d_v >= thr and an entry with key_lb <= d_v, in pile 1 whenever key_lb < bound
-            // (pushes and refills route by key_lb; hubs always go to pile 1).  L.fmin / fmin2
-            // are lower bounds of their pile's keys.
-            // (a) Refill: once pile 1 is exhausted or the threshold reached bound, move the
-            //     entries of pile 2 with key_lb < the new bound into pile 1.  Pile 2 entries are
-            //     tail keys: no distance reads.
-            if (n1 == 0 || !(thr < bound)) {
-                const double nb = __dadd_rn(fmax(bits2d(fminall), thr), fwin);
+            // next non-empty bucket of the window after cb (every wave scans the slot tails)
+            int s = -1;
+            {
+                const int lane = (int)(tid & 63);
+                const int lo_slot = (int)B.cb - (int)B.wbase + 1;  // 0 right after a refill
+                const bool ne = lane < kRingSlots && lane >= lo_slot && L.rtail[lane] > 0u;
+                const unsigned long long m = __ballot(ne);
+                s = m ? __ffsll((long long)m) - 1 : -1;
+            }
+            if (s >= 0) {
+                const uint32_t n = min(L.rtail[s], B.slot_cap);
+                __syncthreads();
+                // the slot receives no pushes before the next refill (only buckets > cb do)
+                if (tid == 0) L.rtail[s] = 0u;
+                ev3 += n;
+                B.cb = B.wbase + (uint32_t)s;
+                inq = B.ring + (size_t)s * B.slot_cap;
+                nq = n;
+                n_split++;
+                continue;
+            }
+            // window used up: refill it from the overflow pile (or the source is done).  The
+            // window restarts at the overflow's smallest key; an entry goes to the bucket of
+            // its key's lower bound (never later than its true bucket: an early expansion is
+            // harmless), or back to the pile.  No distance reads.
+            const uint32_t no = min(L.otail, B.ocap);
+            if (no == 0) break;
+            {
+                const uint32_t kb = bucket_of(bits2d(L.omin), B.inv_delta);
+                const uint32_t wb = max(B.cb + 1, kb);
+                const uint32_t we = wb + (uint32_t)kRingSlots;
                 __syncthreads();
                 if (tid == 0) {
-                    L.fmin2 = kInfBits;
-                    L.f2tail = 0;  // kept entries stream into the other pile-2 buffer
+                    L.otail = 0;
+                    L.omin = kInfBits;
                 }
                 __syncthreads();
-                for (uint32_t base = 0; base < n2; base += kSsspBlock * FU) {
-                    unsigned long long k1 = kInfBits, k2 = kInfBits;
+                Buckets R = B;
+                R.wbase = wb;
+                for (uint32_t base = 0; base < no; base += kSsspBlock * FU) {
+                    unsigned long long k2 = kInfBits;
 #pragma unroll
                     for (int u = 0; u < FU; u++) {
                         const uint32_t i = base + (uint32_t)u * kSsspBlock + tid;
-                        const unsigned long long e = i < n2 ? f2[i] : 0ull;
-                        const unsigned long long kb = e & 0xFFFFFFFF00000000ull;
-                        const bool mv = i < n2 && bits2d(kb) < nb;
-                        const bool kp = i < n2 && !mv;
-                        if (kp) k2 = kb < k2 ? kb : k2;
-                        if (mv) k1 = kb < k1 ? kb : k1;
-                        wave_push64(mv, e, f1, &L.ftail, fcap, &L.fover, 8u);
-                        wave_push64(kp, e, f2alt, &L.f2tail, fcap2, &L.fover, 8u);
+                        const unsigned long long e = i < no ? B.over[i] : 0ull;
+                        const uint32_t b = max(bucket_of(far_key_lb(e), B.inv_delta), wb);
+                        const bool mv = i < no && b < we;
+                        const bool kp = i < no && !mv;
+                        if (kp) {
+                            const unsigned long long kk = e & 0xFFFFFFFF00000000ull;
+                            k2 = kk < k2 ? kk : k2;
+                        }
+                        ring_push(mv, b - wb, e, R, L);
+                        wave_push64(kp, e, over_alt, &L.otail, B.ocap, &L.fover, 8u);
                     }
-#pragma unroll
-                    for (int sh = 32; sh > 0; sh >>= 1) {
-                        const unsigned long long y1 = __shfl_xor(k1, sh, 64);
-                        k1 = y1 < k1 ? y1 : k1;
-                        const unsigned long long y2 = __shfl_xor(k2, sh, 64);
-                        k2 = y2 < k2 ? y2 : k2;
-                    }
-                    if ((tid & 63) == 0 && k1 != kInfBits) atomicMin(&L.fmin, k1);
-                    if ((tid & 63) == 0 && k2 != kInfBits) atomicMin(&L.fmin2, k2);
+                    k2 = wave_min_u64(k2);
+                    if ((tid & 63) == 0 && k2 != kInfBits) atomicMin(&L.omin, k2);
                 }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
-                ev3 += n2;
-                bound = nb;
-                n2 = min(L.f2tail, fcap2);
-                n1 = min(L.ftail, fcap);
-                { unsigned long long* t = f2; f2 = f2alt; f2alt = t; }
-                if (L.fover) continue;  // a pile overflowed while refilling: scanning splits
+                ev4 += no;
+                { unsigned long long* t = B.over; B.over = over_alt; over_alt = t; }
+                B.wbase = wb;
+                B.cb = wb - 1;
+                nq = 0;
             }
-            // (b) Split pile 1 on [thr, newthr), newthr <= bound.  An entry whose key lower
-            //     bound is already >= newthr stays without touching its distance; the others
-            //     read the true distance and are dropped (< thr: expanded when it went below
-            //     the threshold, or a stale duplicate), moved to the near queue (deduplicated
-            //     by stamp), or kept with a refreshed key.  One streaming pass with no
-            //     barriers: kept entries go to the other pile-1 buffer.
-            ev3 += n1;
-            newthr = fmin(__dadd_rn(fmax(bits2d(L.fmin), thr), delta), bound);
-            iter++;
-            __syncthreads();
-            if (tid == 0) {
-                L.qtail = 0;
-                L.fmin = kInfBits;
-                L.ftail = 0;
-            }
-            __syncthreads();
-            for (uint32_t base = 0; base < n1; base += kSsspBlock * FU) {
-                unsigned long long e[FU], db[FU];
-                int cls[FU];  // -1 none, 0 drop, 1 near, 2 keep, 3 undecided
-#pragma unroll
-                for (int u = 0; u < FU; u++) {
-                    const uint32_t i = base + (uint32_t)u * kSsspBlock + tid;
-                    e[u] = i < n1 ? f1[i] : 0ull;
-                    cls[u] = i < n1 ? 3 : -1;
-                }
-#pragma unroll
-                for (int u = 0; u < FU; u++) {
-                    db[u] = kInfBits;
-                    if (cls[u] == 3) {
-                        const uint32_t v = (uint32_t)e[u];
-                        if (v >= D.H && !(far_key_lb(e[u]) < newthr)) {
-                            cls[u] = 2;
-                            db[u] = e[u] & 0xFFFFFFFF00000000ull;
-                        } else {
-                            db[u] = D.get(v);
-                            if constexpr (EV) ev[7] += v >= D.H ? 1u : 0u;
-                        }
-                    }
-                }
-                unsigned long long km = kInfBits;
-#pragma unroll
-                for (int u = 0; u < FU; u++) {
-                    const uint32_t v = (uint32_t)e[u];
-                    if (cls[u] == 3) {
-                        const double d = bits2d(db[u]);
-                        cls[u] = d < oldthr ? 0 : (d < newthr ? 1 : 2);
-                        if (v < D.H) {
-                            if (cls[u] != 2) atomicAnd(&D.fbits[v >> 5], ~(1u << (v & 31)));
-                        } else if (cls[u] == 2) {
-                            e[u] = far_entry(db[u], v);  // refreshed key
-                        }
-                    }
-                    if (cls[u] == 2) km = db[u] < km ? db[u] : km;
-                    wave_push64(cls[u] == 2, e[u], f1alt, &L.ftail, fcap, &L.fover, 2u);
-                    const bool pN = cls[u] == 1 &&
-                                    (v < D.H || atomicExch(&stamp[v], iter) != iter);
-                    wave_push64(pN, far_entry(0ull, v), cur, &L.qtail, ncap, &L.nover, 16u);
-                }
-#pragma unroll
-                for (int sh = 32; sh > 0; sh >>= 1) {
-                    const unsigned long long y = __shfl_xor(km, sh, 64);
-                    km = y < km ? y : km;
-                }
-                if ((tid & 63) == 0 && km != kInfBits) atomicMin(&L.fmin, km);
-            }
-            __syncthreads();
-            const uint32_t kept = min(L.ftail, fcap);
-            { unsigned long long* t = f1; f1 = f1alt; f1alt = t; }
-            nq = min(L.qtail, ncap);
-            n1 = kept;
-            ev4 += kept;
-            lb = oldthr;
-            thr = newthr;
-            __syncthreads();
         }
 
         nfarscan += L.fover ? 1u : 0u;
@@ -935,7 +937,6 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     if (tid == 0) {
         if (nfarscan) atomicAdd(&stats[ST_FARSCAN], nfarscan);
         ctr[0] = iter;
-        ctr[1] = fep;
         ctr[2] = mep;
         atomicAdd(&stats[ST_RELAX], relax_local);
         atomicAdd(&stats[ST_T_INIT], t_init);
@@ -1083,23 +1084,38 @@ static int grid_for(int64_t n, int block) {
     return (int)g;
 }
 
-uint32_t sssp_hub_capacity() {
-    return (uint32_t)((kSsspMaxLds - kLdsCtrlBytes - kLdsBitsBytes) / 8);
+SsspLdsPlan sssp_lds_plan(int wg_per_cu, int64_t hub_limit, uint32_t par_hubs, int64_t V) {
+    const size_t budget = kSsspMaxLds / (size_t)(wg_per_cu > 1 ? wg_per_cu : 1);
+    uint32_t P = par_hubs < kParHubs ? par_hubs : kParHubs;
+    // largest H whose layout fits the budget (8 B of distance + 1 bit per hub)
+    int64_t H = 0;
+    const size_t fixed = lds_layout(0, P).bytes + 8;
+    if (budget > fixed) H = (int64_t)((budget - fixed) * 32 / (32 * 8 + 1));
+    while (H > 0 && lds_layout((uint32_t)H, P).bytes > budget) H--;
+    if (hub_limit >= 0 && hub_limit < H) H = hub_limit;
+    if (H > V) H = V;
+    if (P > (uint32_t)H) P = (uint32_t)H;
+    SsspLdsPlan p;
+    p.H = (uint32_t)H;
+    p.P = P;
+    p.bytes = lds_layout(p.H, p.P).bytes;
+    return p;
 }
 
 hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                             int nsrc, const uint32_t* d_targets, int A, double delta,
-                            int64_t hub_limit, uint32_t par_hubs, uint32_t far_cap,
-                            uint32_t near_cap, double far_window, bool events,
+                            const SsspLdsPlan& plan, uint32_t far_cap,
+                            uint32_t near_cap, bool events,
                             double2* out_lr,
                             uint16_t* out_hops, double* out_rowmin, unsigned long long* d_stats,
                             hipStream_t stream) {
     int grid = ws.slots < nsrc ? ws.slots : nsrc;
     if (grid < 1) return hipSuccess;
-    uint32_t hubs = sssp_hub_capacity();
-    if (hub_limit >= 0 && (uint32_t)hub_limit < hubs) hubs = (uint32_t)hub_limit;
-    if ((int64_t)hubs > g.V) hubs = (uint32_t)g.V;
-    const size_t lds = kLdsCtrlBytes + kLdsBitsBytes + (size_t)hubs * 8;
+    if ((int64_t)plan.H > g.V || plan.P > plan.H || plan.bytes > kSsspMaxLds ||
+        lds_layout(plan.H, plan.P).bytes != plan.bytes)
+        return hipErrorInvalidValue;
+    const uint32_t hubs = plan.H, par_hubs = plan.P;
+    const size_t lds = plan.bytes;
     static bool attr_set = false;
     if (!attr_set) {
         for (const void* k : {(const void*)sssp_rows_kernel<false>,
@@ -1113,7 +1129,7 @@ hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d
     hipLaunchKernelGGL(events ? sssp_rows_kernel<true> : sssp_rows_kernel<false>, dim3(grid),
                        dim3(kSsspBlock), lds, stream, g, ws,
                        d_sources, nsrc, d_targets, A, delta, hubs, par_hubs, far_cap, near_cap,
-                       far_window > 0 ? far_window : 8.0, out_lr,
+                       out_lr,
                        out_hops,
                        out_rowmin, d_stats);
     return hipGetLastError();
@@ -1161,11 +1177,14 @@ hipError_t launch_fill_u64(unsigned long long* p, unsigned long long v, int64_t 
     return hipGetLastError();
 }
 
-int sssp_max_blocks_per_cu() {
+int sssp_max_blocks_per_cu(int wg_per_cu) {
+    const SsspLdsPlan p = sssp_lds_plan(wg_per_cu, -1, kParHubs, INT64_MAX);
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sssp_rows_kernel<false>, kSsspBlock,
-                                                     kSsspMaxLds) !=
-        hipSuccess)
+    if (hipFuncSetAttribute((const void*)sssp_rows_kernel<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSsspMaxLds) !=
+            hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sssp_rows_kernel<false>, kSsspBlock,
+                                                     p.bytes) != hipSuccess)
         return 1;
     return nb < 1 ? 1 : nb;
 }

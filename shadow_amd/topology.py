@@ -235,8 +235,9 @@ class Topology:
             raise RuntimeError("shdtopo_get_stats failed: %d" % r)
         out = {k: getattr(s, k) for k, _ in L.ShdStats._fields_}
         out["phase_ms"] = list(out["phase_ms"])
-        out["events"] = dict(zip(("expanded", "tail_relax", "tail_improve", "far_scanned",
-                                  "far_kept", "parent_vertices", "tail_settled_relax", "far_reads"),
+        out["events"] = dict(zip(("expanded", "tail_relax", "tail_improve", "window_taken",
+                                  "overflow_refilled", "parent_vertices", "tail_settled_relax",
+                                  "stale_skipped"),
                                  list(out["events"])))
         return out
 

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build an A/B variant of libshdtopo.so with extra compile-time defines (kernel experiments).
+#   tools/build_variant.sh NAME -DSHD_SSSP_BLOCK=512 ...   ->  abtest/NAME/libshdtopo.so
+# Load it with SHDTOPO_LIB=abtest/NAME/libshdtopo.so (shadow_amd/_lib.py).
+set -euo pipefail
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+NAME=$1
+shift
+OUT=$ROOT/abtest/$NAME
+mkdir -p "$OUT/obj"
+FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-result $*"
+cd "$ROOT/shadow_amd/csrc"
+/opt/rocm/bin/hipcc $FLAGS -x hip -c topo_core.cpp -o "$OUT/obj/core.o" &
+/opt/rocm/bin/hipcc $FLAGS -x hip -c topo_graph.cpp -o "$OUT/obj/graph.o" &
+/opt/rocm/bin/hipcc $FLAGS -c topo_kernels.hip -o "$OUT/obj/kernels.o" &
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libshdtopo.so" "$OUT"/obj/*.o -lpthread
+echo "$OUT/libshdtopo.so"
