@@ -436,7 +436,7 @@ int ensure_workspace(Topology* top, int nsrc) {
     int want = top->slotsOpt > 0 ? top->slotsOpt
                                  : prop.multiProcessorCount * sssp_max_blocks_per_cu(top->wgPerCu);
     // dist/best/memo 24 B, stamp/cnt/bslot/par 16 B, near queues, window, overflow piles
-    size_t per_slot = (size_t)V * (40 + 16 * kNearPerVertex + 8 * kRingPerVertex + 16 * kOverPerVertex) +
+    size_t per_slot = (size_t)V * (40 + 16 * kNearPerVertex + 8 * kRingPerVertex + 32 * kOverPerVertex) +
                       (size_t)kMaxHops * kSsspBlock * 4 + 16;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
@@ -452,7 +452,7 @@ int ensure_workspace(Topology* top, int nsrc) {
     HIPCHK(top->d_qa.ensure(n * kNearPerVertex));
     HIPCHK(top->d_qb.ensure(n * kNearPerVertex));
     HIPCHK(top->d_ring.ensure(n * kRingPerVertex));
-    HIPCHK(top->d_over.ensure(n * 2 * kOverPerVertex));
+    HIPCHK(top->d_over.ensure(n * 4 * kOverPerVertex));
     HIPCHK(top->d_cnt.ensure(n));
     HIPCHK(top->d_bslot.ensure(n));
     HIPCHK(top->d_par.ensure(n));

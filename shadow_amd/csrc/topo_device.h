@@ -24,7 +24,7 @@ constexpr int kMaxHops = 48;      // per-thread path buffer depth (longer paths:
 #endif
 constexpr int kRingPerVertex = SHD_RING_PER_VERTEX;  // bucket-window entries per slot, in entries
                                                      // per vertex (split evenly over the buckets)
-constexpr int kOverPerVertex = 2;  // overflow-pile capacity per slot, in entries per vertex
+constexpr int kOverPerVertex = 1;  // overflow-pile capacity per slot, in 16-B entries per vertex
                                    // (double buffered: a refill streams the kept entries over)
 constexpr int kNearPerVertex = 2; // near-queue capacity per slot, in entries per vertex
 
@@ -75,7 +75,7 @@ struct SlotWs {
     unsigned long long* qb = nullptr;  // vertex, kNearPerVertex * V entries (no dedupe)
     unsigned long long* ring = nullptr;  // bucket window: kRingPerVertex * V entries, same format
     unsigned long long* over = nullptr;  // overflow pile (buckets past the window), 2 buffers of
-                                         // kOverPerVertex * V entries
+                                         // kOverPerVertex * V {u64 key, u64 vertex} entries
     unsigned long long* best = nullptr;  // parent pass: min d[u] over candidates
     uint32_t* cnt = nullptr;             // parent pass: candidates at the min
     uint32_t* bslot = nullptr;           // parent pass: lowest adjacency slot at the min

@@ -259,9 +259,26 @@ struct Buckets {
     uint32_t cb, wbase;
     unsigned long long* ring;  // kRingSlots slots of slot_cap entries
     uint32_t slot_cap;
-    unsigned long long* over;  // overflow pile (current buffer)
+    ulonglong2* over;          // overflow pile (current buffer): {exact key bits, vertex}
     uint32_t ocap;
 };
+
+__device__ __forceinline__ void wave_push_over(bool pred, unsigned long long key, uint32_t v,
+                                               ulonglong2* q, uint32_t* lds_tail, uint32_t cap,
+                                               uint32_t* lds_over, uint32_t code) {
+    unsigned long long m = __ballot(pred);
+    if (m == 0ull) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(lds_tail, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (pred) {
+        const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (pos < cap) q[pos] = make_ulonglong2(key, (unsigned long long)v);
+        else atomicOr(lds_over, code);
+    }
+}
 
 // Window push: lanes may target different slots; one LDS atomic per (wave, slot).
 __device__ __forceinline__ void ring_push(bool pred, uint32_t slot, unsigned long long val,
@@ -297,12 +314,19 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x)
 // Near-phase relaxation of queue Q: the load-balanced chunking of expand_queue, with U edges in
 // flight per lane: U (col, wt) loads, then the U tail pre-checks, then the LDS atomics / no-return
 // HBM atomics, then the pushes.  An improvement to bucket b goes to the near queue (b <= cb), the
-// window slot of b, or the overflow pile.  scan: scanning mode after an overflow (near pushes
-// deduplicated by stamp, far improvements only lower L.fmin).
+// window slot of b, or the overflow pile.
+//   Far entries: pushed only when the improvement moves the vertex to an EARLIER bucket than the
+//   value it had (hubs: the LDS atomic's return; tails: the pre-check, whose staleness can only
+//   overstate the old bucket).  Invariant: every unexpanded vertex with bucket(d) > cb has an
+//   entry in exactly bucket(d), so a same-bucket improvement needs none.  A window-slot entry is
+//   stale once its vertex has moved to a bucket < cb (win); a near entry once its vertex's
+//   distance dropped below the entry's key (the high word rides in the entry).
+//   scan: scanning mode after an overflow (near pushes deduplicated by stamp, far improvements
+//   only lower L.fmin).
 template <int U, bool EV>
 __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_t nq,
                                             const DevCSR& g, Lds& L, const DistView& D,
-                                            uint32_t* stamp, bool scan,
+                                            uint32_t* stamp, bool scan, bool win,
                                             unsigned long long* nxt, const Buckets& B,
                                             uint32_t it, uint32_t ncap,
                                             unsigned long long& relax,
@@ -322,7 +346,8 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
             const uint32_t v = (uint32_t)e;
             const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
             const unsigned long long dv = D.get(v);
-            const bool stale = (dv >> 32) < (e >> 32);
+            const bool stale = win ? bucket_of(bits2d(dv), B.inv_delta) < B.cb
+                                   : (dv >> 32) < (e >> 32);
             deg = stale ? 0u : r1 - r0;
             if constexpr (EV) ev[7] += stale ? 1ull : 0ull;
             L.rs[tid] = r0;
@@ -369,6 +394,7 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
                 imp[u] = false;
                 if (valid[u] && n[u] < D.H) {
                     const unsigned long long old = atomicMin(&D.hd[n[u]], ab[u]);
+                    cur[u] = old;  // hubs: the exact previous value (bucket dedupe below)
                     imp[u] = ab[u] < old;
                     if (n[u] < D.P) {  // parent hint for the heaviest rows (see epilogue)
                         if (imp[u]) D.hpar[n[u]] = from[u];
@@ -404,19 +430,20 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
                         }
                     } else if (scan) {
                         fm = ab[u] < fm ? ab[u] : fm;
-                    } else if (b < wend) {
-                        pR = true;
-                    } else {
-                        pO = true;
-                        const unsigned long long k = ab[u] & 0xFFFFFFFF00000000ull;
-                        om = k < om ? k : om;
+                    } else if (b < bucket_of(bits2d(cur[u]), B.inv_delta)) {
+                        if (b < wend) {
+                            pR = true;
+                        } else {
+                            pO = true;
+                            om = ab[u] < om ? ab[u] : om;
+                        }
                     }
                 }
                 // hub near pushes and scanning-mode pushes are deduplicated: key 0 (never stale)
                 wave_push64(pN, far_entry((n[u] < D.H || scan) ? 0ull : ab[u], n[u]), nxt,
                             &L.qtail, ncap, &L.nover, 1u);
                 ring_push(pR, b - B.wbase, far_entry(ab[u], n[u]), B, L);
-                wave_push64(pO, far_entry(ab[u], n[u]), B.over, &L.otail, B.ocap, &L.fover, 4u);
+                wave_push_over(pO, ab[u], n[u], B.over, &L.otail, B.ocap, &L.fover, 4u);
                 if constexpr (EV) {
                     ev[1] += (valid[u] && n[u] >= D.H) ? 1ull : 0ull;
                     ev[2] += (imp[u] && n[u] >= D.H) ? 1ull : 0ull;
@@ -468,8 +495,8 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
     unsigned long long* qb = ws.qb + (size_t)slot * kNearPerVertex * V;
     const size_t ring_all = (size_t)kRingPerVertex * (size_t)V;
     const size_t over_all = (size_t)kOverPerVertex * (size_t)V;
-    unsigned long long* over0 = ws.over + (size_t)slot * 2 * over_all;
-    unsigned long long* over1 = over0 + over_all;
+    ulonglong2* over0 = reinterpret_cast<ulonglong2*>(ws.over) + (size_t)slot * 2 * over_all;
+    ulonglong2* over1 = over0 + over_all;
     uint32_t* fscr = reinterpret_cast<uint32_t*>(over0);  // parent-pass scratch queue (u32)
     unsigned long long* best = ws.best + (size_t)slot * V;
     uint32_t* cntc = ws.cnt + (size_t)slot * V;
@@ -535,7 +562,8 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
         B.cb = 0;
         B.wbase = 0;
         B.over = over0;
-        unsigned long long* over_alt = over1;
+        ulonglong2* over_alt = over1;
+        bool win = false;  // inq is a window slot (bucket-based stale test)
         const unsigned long long* inq = qa;  // near-phase input: a near queue or a window slot
         unsigned long long* qnxt = qb;       // near-phase output (never aliases inq)
         uint32_t nq = 1;
@@ -554,10 +582,11 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 __syncthreads();
                 ev0 += nq;
                 const bool scan = L.fover != 0u;
-                relax_queue<kRelaxUnroll, EV>(inq, nq, g, L, D, stamp, scan, qnxt, B, iter,
+                relax_queue<kRelaxUnroll, EV>(inq, nq, g, L, D, stamp, scan, win, qnxt, B, iter,
                                               scan ? ncap : ncap_free, relax_local, ev);
                 // relax_queue ends with a barrier
                 nq = min(L.qtail, ncap);
+                win = false;
                 inq = qnxt;
                 qnxt = (qnxt == qa) ? qb : qa;
                 n_near++;
@@ -636,14 +665,14 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 ev3 += n;
                 B.cb = B.wbase + (uint32_t)s;
                 inq = B.ring + (size_t)s * B.slot_cap;
+                win = true;
                 nq = n;
                 n_split++;
                 continue;
             }
             // window used up: refill it from the overflow pile (or the source is done).  The
-            // window restarts at the overflow's smallest key; an entry goes to the bucket of
-            // its key's lower bound (never later than its true bucket: an early expansion is
-            // harmless), or back to the pile.  No distance reads.
+            // window restarts at the overflow's smallest key; an entry goes to the window slot
+            // of its exact key's bucket, or back to the pile.  No distance reads.
             const uint32_t no = min(L.otail, B.ocap);
             if (no == 0) break;
             {
@@ -663,16 +692,14 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
 #pragma unroll
                     for (int u = 0; u < FU; u++) {
                         const uint32_t i = base + (uint32_t)u * kSsspBlock + tid;
-                        const unsigned long long e = i < no ? B.over[i] : 0ull;
-                        const uint32_t b = max(bucket_of(far_key_lb(e), B.inv_delta), wb);
+                        const ulonglong2 e = i < no ? B.over[i] : make_ulonglong2(0ull, 0ull);
+                        const uint32_t b = max(bucket_of(bits2d(e.x), B.inv_delta), wb);
                         const bool mv = i < no && b < we;
                         const bool kp = i < no && !mv;
-                        if (kp) {
-                            const unsigned long long kk = e & 0xFFFFFFFF00000000ull;
-                            k2 = kk < k2 ? kk : k2;
-                        }
-                        ring_push(mv, b - wb, e, R, L);
-                        wave_push64(kp, e, over_alt, &L.otail, B.ocap, &L.fover, 8u);
+                        if (kp) k2 = e.x < k2 ? e.x : k2;
+                        ring_push(mv, b - wb, far_entry(e.x, (uint32_t)e.y), R, L);
+                        wave_push_over(kp, e.x, (uint32_t)e.y, over_alt, &L.otail, B.ocap,
+                                       &L.fover, 8u);
                     }
                     k2 = wave_min_u64(k2);
                     if ((tid & 63) == 0 && k2 != kInfBits) atomicMin(&L.omin, k2);
@@ -680,7 +707,7 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 ev4 += no;
-                { unsigned long long* t = B.over; B.over = over_alt; over_alt = t; }
+                { ulonglong2* t = B.over; B.over = over_alt; over_alt = t; }
                 B.wbase = wb;
                 B.cb = wb - 1;
                 nq = 0;
