@@ -4,7 +4,7 @@
 //   CSR of the undirected topology without self loops:
 //     rowptr u32[V+1], adj {u32 col, f64 latency}[2E'] (12-B AoS), aloss f64[2E'] (edge loss)
 //   per vertex: vloss f64[V], selfLat f64[V] (NaN = no self loop), selfLoss f64[V]
-//   per SSSP slot (one workgroup = one source at a time): 232 B x V of workspace
+//   per SSSP slot (one workgroup = one source at a time): 264 B x V of workspace
 //   routing table: {f64 lat, f64 rel}[A][A] (16-B records, one gather per packet) + u16 hops
 #pragma once
 
@@ -24,7 +24,7 @@ constexpr int kMaxHops = 48;      // per-thread path buffer depth (longer paths:
 #endif
 constexpr int kRingPerVertex = SHD_RING_PER_VERTEX;  // bucket-window entries per slot, in entries
                                                      // per vertex (split evenly over the buckets)
-constexpr int kOverPerVertex = 1;  // overflow-pile capacity per slot, in 16-B entries per vertex
+constexpr int kOverPerVertex = 2;  // overflow-pile capacity per slot, in 16-B entries per vertex
                                    // (double buffered: a refill streams the kept entries over)
 constexpr int kNearPerVertex = 2; // near-queue capacity per slot, in entries per vertex
 

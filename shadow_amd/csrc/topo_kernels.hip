@@ -86,6 +86,9 @@ constexpr int kRelaxUnroll = SHD_RELAX_UNROLL;
 #ifndef SHD_TAIL_NORET
 #define SHD_TAIL_NORET 1
 #endif
+#ifndef SHD_STALE_FIRST
+#define SHD_STALE_FIRST 1
+#endif
 
 // Dynamic LDS after the control block: the near-queue dedupe bitmap nbits[hw], parent-tie bits
 // tbits[pw], parent hints hpar[P] (u32), then the hub distance words hd[H] (u64).
@@ -344,10 +347,23 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
             // pushes carry 0)
             const unsigned long long e = Q[base + tid];
             const uint32_t v = (uint32_t)e;
+#if SHD_STALE_FIRST
+            // the distance decides staleness before the row bounds are fetched: a stale entry
+            // costs one read instead of two
+            const unsigned long long dv = D.get(v);
+            const bool stale = win ? bucket_of(bits2d(dv), B.inv_delta) < B.cb
+                                   : (dv >> 32) < (e >> 32);
+            uint32_t r0 = 0, r1 = 0;
+            if (!stale) {
+                r0 = g.rowptr[v];
+                r1 = g.rowptr[v + 1];
+            }
+#else
             const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
             const unsigned long long dv = D.get(v);
             const bool stale = win ? bucket_of(bits2d(dv), B.inv_delta) < B.cb
                                    : (dv >> 32) < (e >> 32);
+#endif
             deg = stale ? 0u : r1 - r0;
             if constexpr (EV) ev[7] += stale ? 1ull : 0ull;
             L.rs[tid] = r0;
