@@ -16,7 +16,10 @@ os.makedirs(outdir, exist_ok=True)
 
 
 def short(name):
-    return name.split("(")[0].replace("shdtopo::", "")
+    n = name.split("(")[0].replace("shdtopo::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    return n.split("<")[0] if n.startswith("sssp_rows_kernel") else n
 
 
 lines = ["# rocprofv3 summary %s (bench.py, C4/C5, 1 x MI355X)" % tag, ""]
