@@ -377,11 +377,16 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
         relax += total;  // uniform: every adjacency entry of the chunk is relaxed once
         __syncthreads();
         for (uint32_t eb = tid - lane; eb < total; eb += kSsspBlock * U) {
+            // Loads are issued unconditionally (an idle lane reads entry 0 / word 0 and discards
+            // it): a load inside a divergent branch is waited for inside that branch, which
+            // would serialise the U round trips.
             uint32_t n[U], from[U];
             unsigned long long ab[U];
             bool valid[U];
+            W3 rec[U];
+            int los[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
+            for (int u = 0; u < U; u++) {  // U searches, U record loads in flight
                 const uint32_t e = eb + (uint32_t)u * kSsspBlock + lane;
                 valid[u] = e < total;
                 int lo = 0;
@@ -392,25 +397,34 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
                         if (L.off[mid] <= e) lo = mid; else hi = mid - 1;
                     }
                 }
+                los[u] = lo;
                 const uint32_t j = valid[u] ? L.rs[lo] + (e - L.off[lo]) : 0u;
-                uint32_t c = 0u;
-                double w = 0.0;
-                if (valid[u]) adj_load(g, j, c, w);
-                n[u] = c;
-                from[u] = L.vx[lo];
-                ab[u] = valid[u] ? d2bits(__dadd_rn(L.val[lo], w)) : ~0ull;
+                rec[u] = *reinterpret_cast<const W3*>(g.adj + 3ull * j);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const double w = __hiloint2double((int)rec[u].c, (int)rec[u].b);
+                const double a = __dadd_rn(L.val[los[u]], w);
+                n[u] = valid[u] ? rec[u].a : 0u;
+                from[u] = L.vx[los[u]];
+                ab[u] = valid[u] ? d2bits(a) : ~0ull;
             }
             unsigned long long cur[U];
 #pragma unroll
-            for (int u = 0; u < U; u++)  // tail pre-check (plain load: stale = larger = safe)
-                cur[u] = (valid[u] && n[u] >= D.H) ? D.dist[n[u]] : 0ull;
+            for (int u = 0; u < U; u++) {  // tail pre-check (plain load: stale = larger = safe)
+                const bool t = valid[u] && n[u] >= D.H;
+                const unsigned long long x = D.dist[t ? n[u] : 0u];
+                cur[u] = t ? x : 0ull;
+            }
             bool imp[U];
+            unsigned long long hold[U];  // hubs: the exact previous value (bucket dedupe below)
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 imp[u] = false;
+                hold[u] = kInfBits;
                 if (valid[u] && n[u] < D.H) {
                     const unsigned long long old = atomicMin(&D.hd[n[u]], ab[u]);
-                    cur[u] = old;  // hubs: the exact previous value (bucket dedupe below)
+                    hold[u] = old;
                     imp[u] = ab[u] < old;
                     if (n[u] < D.P) {  // parent hint for the heaviest rows (see epilogue)
                         if (imp[u]) D.hpar[n[u]] = from[u];
@@ -446,7 +460,8 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
                         }
                     } else if (scan) {
                         fm = ab[u] < fm ? ab[u] : fm;
-                    } else if (b < bucket_of(bits2d(cur[u]), B.inv_delta)) {
+                    } else if (b < bucket_of(bits2d(n[u] < D.H ? hold[u] : cur[u]),
+                                             B.inv_delta)) {
                         if (b < wend) {
                             pR = true;
                         } else {
