@@ -86,6 +86,9 @@ constexpr int kRelaxUnroll = SHD_RELAX_UNROLL;
 #ifndef SHD_TAIL_NORET
 #define SHD_TAIL_NORET 1
 #endif
+#ifndef SHD_NT_DIST
+#define SHD_NT_DIST 0
+#endif
 #ifndef SHD_STALE_FIRST
 #define SHD_STALE_FIRST 1
 #endif
@@ -413,7 +416,11 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
 #pragma unroll
             for (int u = 0; u < U; u++) {  // tail pre-check (plain load: stale = larger = safe)
                 const bool t = valid[u] && n[u] >= D.H;
+#if SHD_NT_DIST
+                const unsigned long long x = __builtin_nontemporal_load(&D.dist[t ? n[u] : 0u]);
+#else
                 const unsigned long long x = D.dist[t ? n[u] : 0u];
+#endif
                 cur[u] = t ? x : 0ull;
             }
             bool imp[U];
