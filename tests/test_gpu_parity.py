@@ -205,3 +205,39 @@ def test_minimum_latency_simple_config1():
     assert data_top.getReliability(hosts[0], hosts[1]) == 1.0
     assert data_top.getLatency(hosts[0], hosts[0]) == 20.0
     assert data_top.getMinimumLatency() == 20.0
+
+
+def test_sssp_full_size_c4_sampled_rows():
+    """BASELINE config 4 at full size (1M vertices / 10M edges, the bench workload): three rows
+    (first, middle, last source) bit-exact against the oracle's Dijkstra + helper, and
+    size-independent properties of the whole 9,999 x 9,999 table: every latency finite and
+    > 0, reliability in (0, 1], the diagonal is the self loop (1 hop), no overflow fallback,
+    and the kernel's row minima equal the table's."""
+    import torch
+    top = sa.Topology.synthetic(seed=20261015)
+    assert top.num_vertices == 1_000_000 and top.num_edges == 10_000_000
+    top.synth_packets(20261015, 100_000, 1000, 10**9, 10**7)  # attaches the C5 hosts
+    att = top.attached_vertices()
+    A = len(att)
+    lr = torch.empty((A, A, 2), dtype=torch.float64, device="cuda")
+    hp = torch.empty((A, A), dtype=torch.int16, device="cuda")
+    rm = torch.empty((A,), dtype=torch.float64, device="cuda")
+    top.build_rows_into(0, A, lr, hp, rm)
+    torch.cuda.synchronize()
+    st = top.stats()
+    assert st["errors"] == 0 and st["ambiguous_pairs"] == 0 and st["far_scan_sources"] == 0
+    lat = lr[..., 0]
+    rel = lr[..., 1]
+    assert bool(torch.isfinite(lat).all()) and bool((lat > 0).all())
+    assert bool((rel > 0).all()) and bool((rel <= 1).all())
+    diag = torch.arange(A, device="cuda")
+    assert bool((hp[diag, diag] == 1).all()) and bool((hp >= 1).all())
+    assert torch.equal(rm, lat.min(dim=1).values)
+    rows = [0, A // 2, A - 1]
+    V, eu, ev, elat, eloss, vloss = top.export_graph()
+    g = oracle.OGraph(V, eu, ev, elat, eloss, vloss)
+    olat, orel, ohops = g.source_rows(att[rows], att, nthreads=3)
+    glr = lr[rows].cpu().numpy()
+    assert np.array_equal(glr[..., 0].view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(glr[..., 1].view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hp[rows].cpu().numpy().view(np.uint16), ohops.astype(np.uint16))
