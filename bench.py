@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--delta", type=float, default=0.0)
+    ap.add_argument("--integer", action="store_true",
+                    help="C4-int variant (integer latencies U{1..100}: heavy parent ties)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_sssp_pmc.json"))
     args = ap.parse_args()
 
@@ -97,7 +99,7 @@ def main():
     # ---- workload (identical on every rank; generation is outside the timed region) ----
     t0 = time.time()
     top = sa.Topology.synthetic(seed=SEED, n_routers=args.routers, n_poi=args.poi,
-                                n_edges=args.edges)
+                                n_edges=args.edges, integer_latency=args.integer)
     top.set_option("device", local)
     if args.delta:
         top.set_option("delta", args.delta)
@@ -183,7 +185,8 @@ def main():
         if os.path.exists(args.pmc_json):
             try:
                 pm = json.load(open(args.pmc_json))
-                if pm.get("config_key") == "C4-%d-%d-%d-rows%d" % (V, E, A, rows):
+                if not args.integer and pm.get("config_key") == "C4-%d-%d-%d-rows%d" % (
+                        V, E, A, rows):
                     traffic = pm["hbm_bytes_per_launch"]
                     pmc_note = pm.get("source")
             except Exception:
@@ -224,10 +227,10 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": "C4 synthetic power-law topology (1M vertices / 10M undirected edges, "
-                            "seed 20261015): full attached-vertex table, all %d sources x %d "
-                            "targets; C5: %d hosts, %d packets per window" %
-                            (A, A, args.hosts, args.packets),
+                "workload": "C4%s synthetic power-law topology (1M vertices / 10M undirected "
+                            "edges, seed 20261015): full attached-vertex table, all %d sources x "
+                            "%d targets; C5: %d hosts, %d packets per window" %
+                            ("-int" if args.integer else "", A, A, args.hosts, args.packets),
                 "vertices": V, "edges": E, "sources": A, "targets": A,
                 "packets_per_window": args.packets, "hosts": args.hosts,
                 "parallelism": "sources sharded /%d, RCCL all-gather + all-reduce(min)" % world,

@@ -83,7 +83,11 @@ typedef struct {
 } TopoPacketOut;
 
 /* worker_schedulePacket (shd-worker.c:332-370) for n packets of one scheduler window, host
- * buffers (includes the PCIe copies).  jumpNs/clampInterHost: shd-worker.c:310-324.
+ * buffers (includes the PCIe copies).  jumpNs/clampInterHost: shd-worker.c:310-324.  In lazy
+ * mode every packet is answered as the reference's getReliability/getLatency calls would have
+ * been in array (= emission) order: first-rooted-wins orientation and running-minimum pushes.
+ * The caller captures in[i].rngState before the sender's draw and advances the sender's
+ * Random by that one draw itself (tests/c/engine_window.c shows the engine-side adapter).
  * Returns 0, or a negative error (unattached address: -2). */
 int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketOut* out, size_t n,
                               uint64_t jumpNs, int clampInterHost);

@@ -120,6 +120,7 @@ struct _Topology {
     std::mutex buildMu;
     std::atomic<bool> tableValid{false};
     std::atomic<bool> hostValid{false};
+    std::atomic<bool> rowminValid{false};  // hrowmin mirrors d_rowmin (lazy batch orientation)
     std::vector<int32_t> attached;  // columns: distinct attached vertices, ascending
     std::vector<int32_t> colOf;     // vertex -> column
     int64_t A = 0;
@@ -653,6 +654,7 @@ int ensure_table(Topology* top) {
                  (long long)top->stats.errors);
     }
     top->hostValid.store(false);
+    top->rowminValid.store(false);
     top->tableValid.store(true, std::memory_order_release);
     if (!top->lazy) push_min_to_engine(top->eagerMin);
     return 0;
@@ -680,6 +682,22 @@ int ensure_host(Topology* top) {
         top->hrel[i] = lr[i].y;
     }
     top->hostValid.store(true, std::memory_order_release);
+    top->rowminValid.store(true, std::memory_order_release);
+    return 0;
+}
+
+// Row minima on the host without the full table mirror (lazy min pushes of batched routes).
+int ensure_rowmin_host(Topology* top) {
+    int r = ensure_table(top);
+    if (r) return r;
+    if (top->rowminValid.load(std::memory_order_acquire)) return 0;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    if (top->rowminValid.load()) return 0;
+    top->hrowmin.resize((size_t)top->A);
+    if (top->A)
+        HIPCHK(hipMemcpy(top->hrowmin.data(), top->d_rowmin.p, sizeof(double) * (size_t)top->A,
+                         hipMemcpyDeviceToHost));
+    top->rowminValid.store(true, std::memory_order_release);
     return 0;
 }
 
@@ -695,6 +713,34 @@ void lazy_store_min(Topology* top, double lat) {
     if (top->lazyMin == 0 || lat < top->lazyMin) {
         top->lazyMin = lat;
         push_min_to_engine(lat);
+    }
+}
+
+// First-rooted-wins orientation of the SSSP branch (shd-topology.c:894-915):
+// (s,d) is answered from row s if s's paths are materialised, else from row d if d's are and
+// the graph is undirected, else s's row is materialised now (its minimum enters the running
+// minimum, shd-topology.c:500-511).  Returns true when the answer comes from row d.
+bool lazy_orient_row(Topology* top, int32_t s, int32_t d, int64_t cs, int64_t cd) {
+    (void)cd;
+    if (top->matRow[(size_t)s].load(std::memory_order_acquire)) return false;
+    if (!top->isDirected && top->matRow[(size_t)d].load(std::memory_order_acquire)) return true;
+    uint8_t was = top->matRow[(size_t)s].exchange(1);
+    if (!was && top->hrowmin[(size_t)cs] > 0 && !std::isinf(top->hrowmin[(size_t)cs]))
+        lazy_store_min(top, top->hrowmin[(size_t)cs]);
+    return false;
+}
+
+// Per-pair first touch of the complete branch (shd-topology.c:894-915 + :835-873): the pair's
+// values are symmetric bit for bit, only the running minimum depends on the order.
+void lazy_touch_pair(Topology* top, int64_t cs, int64_t cd) {
+    const int64_t A = top->A;
+    const size_t b1 = (size_t)(cs * A + cd), b2 = (size_t)(cd * A + cs);
+    bool have = (top->matPair[b1 >> 6].load(std::memory_order_relaxed) >> (b1 & 63)) & 1;
+    if (!have && !top->isDirected)
+        have = (top->matPair[b2 >> 6].load(std::memory_order_relaxed) >> (b2 & 63)) & 1;
+    if (!have) {
+        uint64_t old = top->matPair[b1 >> 6].fetch_or(1ull << (b1 & 63));
+        if (!((old >> (b1 & 63)) & 1) && top->hlat[b1] > 0) lazy_store_min(top, top->hlat[b1]);
     }
 }
 
@@ -720,31 +766,11 @@ bool get_path_entry(Topology* top, uint32_t srcIP, uint32_t dstIP, double* lat, 
     size_t k;
     if (top->isComplete) {
         k = (size_t)(cs * A + cd);
-        if (top->lazy) {
-            // per-pair cache: first touch of (s,d) (or (d,s) if undirected) stores the pair
-            size_t b1 = k, b2 = (size_t)(cd * A + cs);
-            bool have = (top->matPair[b1 >> 6].load(std::memory_order_relaxed) >> (b1 & 63)) & 1;
-            if (!have && !top->isDirected)
-                have = (top->matPair[b2 >> 6].load(std::memory_order_relaxed) >> (b2 & 63)) & 1;
-            if (!have) {
-                uint64_t old = top->matPair[b1 >> 6].fetch_or(1ull << (b1 & 63));
-                if (!((old >> (b1 & 63)) & 1) && top->hlat[k] > 0) lazy_store_min(top, top->hlat[k]);
-            }
-        }
+        if (top->lazy) lazy_touch_pair(top, cs, cd);
     } else if (!top->lazy) {
         k = (size_t)(cs * A + cd);
     } else {
-        // first-rooted-wins: row s if materialised, else row d (undirected)
-        if (top->matRow[(size_t)s].load(std::memory_order_acquire)) {
-            k = (size_t)(cs * A + cd);
-        } else if (!top->isDirected && top->matRow[(size_t)d].load(std::memory_order_acquire)) {
-            k = (size_t)(cd * A + cs);
-        } else {
-            uint8_t was = top->matRow[(size_t)s].exchange(1);
-            if (!was && top->hrowmin[(size_t)cs] > 0 && !std::isinf(top->hrowmin[(size_t)cs]))
-                lazy_store_min(top, top->hrowmin[(size_t)cs]);
-            k = (size_t)(cs * A + cd);
-        }
+        k = lazy_orient_row(top, s, d, cs, cd) ? (size_t)(cd * A + cs) : (size_t)(cs * A + cd);
     }
     double L = top->hlat[k], R = top->hrel[k];
     if (L < 0) {
@@ -839,6 +865,7 @@ void do_attach(Topology* top, uint32_t ip, int32_t v, uint64_t* bwDownOut, uint6
             std::lock_guard<std::mutex> lk(top->buildMu);
             top->tableValid.store(false);
             top->hostValid.store(false);
+    top->rowminValid.store(false);
         }
     }
 }
@@ -1061,6 +1088,7 @@ int shdtopo_bind_table(Topology* top, const void* d_lr, const void* d_hops, doub
     HIPCHK(hipStreamSynchronize(st));
     top->eagerMin = globalMin;
     top->hostValid.store(false);
+    top->rowminValid.store(false);
     top->tableValid.store(true);
     return 0;
 }
@@ -1103,6 +1131,13 @@ int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketO
     std::vector<uint32_t> pay(n), sin(n), sout(n);
     std::vector<uint64_t> now(n), tim(n);
     std::vector<uint8_t> dl(n);
+    // Lazy mode answers every packet as the reference's getReliability/getLatency pair would in
+    // emission order (first-rooted-wins orientation, running-minimum pushes): the orientation
+    // is resolved here, sequentially, and the kernel reads the chosen row.
+    if (top->lazy) {
+        r = top->isComplete ? ensure_host(top) : ensure_rowmin_host(top);
+        if (r) return r;
+    }
     {
         std::shared_lock<std::shared_mutex> lk(top->ipMu);
         for (size_t i = 0; i < n; i++) {
@@ -1114,6 +1149,13 @@ int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketO
             }
             sc[i] = top->colOf[(size_t)a->second];
             dc[i] = top->colOf[(size_t)b->second];
+            if (top->lazy) {
+                if (top->isComplete) {
+                    lazy_touch_pair(top, sc[i], dc[i]);
+                } else if (lazy_orient_row(top, a->second, b->second, sc[i], dc[i])) {
+                    std::swap(sc[i], dc[i]);
+                }
+            }
             pay[i] = in[i].payloadLength;
             sin[i] = in[i].rngState;
             now[i] = in[i].now;
