@@ -19,7 +19,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <functional>
 #include <numeric>
+#include <queue>
 #include <vector>
 
 #include "../../include/shd_topology_abi.h"
@@ -104,6 +106,10 @@ struct _Topology {
     int64_t hubLimit = -1;  // LDS-cached hub distances (-1 = fill the LDS)
     int64_t parHubs = 2048; // hubs whose parent is hinted during the SSSP (0 = always scan)
     int wgPerCu = 1;        // SSSP workgroups per CU (each owns 1/wgPerCu of the LDS)
+    double ringPerVK = 12.0;  // batch mode: window entries per (vertex, source) per slot, split
+                              // evenly over the 48 buckets (C4 peak: 1.16M in one bucket)
+    int batchK = 8;         // sources per SSSP workgroup (1 = sssp_rows_kernel, else
+                            // sssp_batch_kernel with K in {2, 4, 8, 16})
     bool events = false;    // per-edge event counters (diagnostic kernel build)
     int64_t nearCap = 0;    // near-queue entries per slot (0 = 2V; small values force the
                             // bucket-rescan fallback, for tests)
@@ -133,6 +139,9 @@ struct _Topology {
     bool rowsSorted = false;
     std::vector<int32_t> perm;  // new -> old
     std::vector<int32_t> inv;   // old -> new
+    std::vector<double> pot;    // batch mode: d(h0, v) from the top hub (new ids), the bucket shift
+    int wsK = 0;                // batch width the workspace was laid out for
+    int64_t wsRing = 0, wsOver = 0;
     DevBuf<uint32_t> d_rowptr, d_adj;
     DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
     DevBuf<unsigned long long> d_dist, d_best, d_memo, d_ring, d_over, d_qa, d_qb;
@@ -144,6 +153,9 @@ struct _Topology {
     DevBuf<double> d_rowmin;
     DevBuf<double> d_elatAA, d_elossAA, d_vlossA;
     DevBuf<uint32_t> d_sources, d_targets;
+    DevBuf<double> d_srcsh;
+    DevBuf<uint8_t> d_mask;
+    DevBuf<uint32_t> d_hpar;
     DevBuf<unsigned long long> d_stats;
     // host-batch staging
     DevBuf<int32_t> b_src, b_dst;
@@ -384,6 +396,28 @@ int upload_csr(Topology* top) {
         }
     }
     for (int32_t i = 0; i < V; i++) vloss[(size_t)i] = g.vloss[(size_t)top->perm[(size_t)i]];
+    // batch mode: distances from the top hub (vertex 0 after the relabel).  pi(s) = d(h0, s)
+    // shifts source s's buckets so that the batch's sources reach a vertex in the same bucket
+    // (see topo_sssp_batch.hip); only an estimate: any shift keeps the SSSP exact.
+    {
+        top->pot.assign((size_t)V, INFINITY);
+        using QE = std::pair<double, int32_t>;
+        std::priority_queue<QE, std::vector<QE>, std::greater<QE>> pq;
+        top->pot[0] = 0.0;
+        pq.push({0.0, 0});
+        while (!pq.empty()) {
+            const QE t = pq.top();
+            pq.pop();
+            if (t.first > top->pot[(size_t)t.second]) continue;
+            for (uint32_t k = rowptr[(size_t)t.second]; k < rowptr[(size_t)t.second + 1]; k++) {
+                const double a = t.first + wt[k];
+                if (a < top->pot[col[k]]) {
+                    top->pot[col[k]] = a;
+                    pq.push({a, (int32_t)col[k]});
+                }
+            }
+        }
+    }
     HIPCHK(top->d_rowptr.ensure((size_t)V + 1));
     HIPCHK(top->d_adj.ensure(3 * nadj));
     HIPCHK(top->d_aloss.ensure(nadj));
@@ -430,40 +464,82 @@ DevCSR dev_csr(Topology* top) {
     return c;
 }
 
+int batch_k(Topology* top) {
+    const int k = top->batchK;
+    return (k == 2 || k == 4 || k == 8 || k == 16) ? k : 1;
+}
+int64_t ring_entries(Topology* top, int K) {
+    const int64_t V = top->g.V;
+    if (K <= 1) return (int64_t)kRingPerVertex * V;
+    return std::max<int64_t>(48 * 64, (int64_t)(top->ringPerVK * (double)V * K) / 48 * 48);
+}
+int64_t over_entries(Topology* top, int K) {  // the batch kernel keeps no overflow pile
+    return K <= 1 ? (int64_t)kOverPerVertex * top->g.V : 0;
+}
+
+// Per-slot workspace.  Single-source mode (K = 1): 264 B x V.  Batch mode:
+// dist [V][K], two K-bit masks per vertex, u32 near queues, the (vertex, source) window and pile,
+// plus the per-source parent-pass arrays (reused for each source of the batch).
 int ensure_workspace(Topology* top, int nsrc) {
     const int64_t V = top->g.V;
+    const int K = batch_k(top);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, top->device));
+    const int units = K > 1 ? (nsrc + K - 1) / K : nsrc;
     int want = top->slotsOpt > 0 ? top->slotsOpt
-                                 : prop.multiProcessorCount * sssp_max_blocks_per_cu(top->wgPerCu);
-    // dist/best/memo 24 B, stamp/cnt/bslot/par 16 B, near queues, window, overflow piles
-    size_t per_slot = (size_t)V * (40 + 16 * kNearPerVertex + 8 * kRingPerVertex + 32 * kOverPerVertex) +
+                                 : prop.multiProcessorCount *
+                                       (K > 1 ? 1 : sssp_max_blocks_per_cu(top->wgPerCu));
+    const size_t maskb = K > 1 ? 2 * (((size_t)V * (K <= 8 ? 1 : 2) + 255) / 256 * 256) : 0;
+    const int64_t ringE = ring_entries(top, K);
+    const int64_t overE = over_entries(top, K);
+    const size_t hparN = K > 1 ? (size_t)std::min<int64_t>(top->parHubs, 1 << 20) * K : 0;
+    // dist (K words/vertex), best/memo 16 B, stamp/cnt/bslot/par 16 B, near queues, window
+    // (u64 entries single-source, u32 batched), overflow piles (2 x 16 B)
+    size_t per_slot = (size_t)V * (8 * (size_t)K + 32 + 16 * kNearPerVertex) +
+                      (size_t)ringE * (K > 1 ? 4 : 8) + (size_t)overE * (K > 1 ? 16 : 32) + maskb + 4 * hparN +
                       (size_t)kMaxHops * kSsspBlock * 4 + 16;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
-    int memcap = (int)std::max<size_t>(1, (freeb / 2) / per_slot);
+    // memory already held by this workspace counts as available
+    const size_t held = top->slots > 0 ? top->d_dist.n * 8 + top->d_ring.n * 8 + top->d_over.n * 8 : 0;
+    int memcap = (int)std::max<size_t>(1, ((freeb + held) * 3 / 5) / per_slot);
     want = std::min(want, memcap);
-    want = std::max(1, std::min(want, std::max(1, nsrc)));
-    if (top->slots >= want) return 0;
+    want = std::max(1, std::min(want, std::max(1, units)));
+    if (top->slots >= want && top->wsK == K && top->wsRing == ringE && top->wsOver == overE) return 0;
+    if (top->slots > 0) {
+        // layout change: release before re-allocating
+        top->d_dist.release(); top->d_ring.release(); top->d_over.release();
+        top->d_qa.release(); top->d_qb.release(); top->d_mask.release(); top->d_hpar.release();
+        top->slots = 0;
+    }
     const size_t n = (size_t)want * (size_t)V;
-    HIPCHK(top->d_dist.ensure(n));
+    HIPCHK(top->d_dist.ensure(n * (size_t)K));
     HIPCHK(top->d_best.ensure(n));
     HIPCHK(top->d_memo.ensure(n));
     HIPCHK(top->d_stamp.ensure(n));
     HIPCHK(top->d_qa.ensure(n * kNearPerVertex));
     HIPCHK(top->d_qb.ensure(n * kNearPerVertex));
-    HIPCHK(top->d_ring.ensure(n * kRingPerVertex));
-    HIPCHK(top->d_over.ensure(n * 4 * kOverPerVertex));
+    HIPCHK(top->d_ring.ensure((size_t)want * (size_t)ringE * (K > 1 ? 4 : 8) / 8));
+    HIPCHK(top->d_over.ensure((size_t)want * (size_t)overE * (K > 1 ? 2 : 4)));
     HIPCHK(top->d_cnt.ensure(n));
     HIPCHK(top->d_bslot.ensure(n));
     HIPCHK(top->d_par.ensure(n));
     HIPCHK(top->d_pathbuf.ensure((size_t)want * kMaxHops * kSsspBlock));
     HIPCHK(top->d_counters.ensure((size_t)want * 4));
+    if (K > 1) {
+        HIPCHK(top->d_mask.ensure((size_t)want * maskb));
+        HIPCHK(top->d_hpar.ensure(std::max<size_t>(1, (size_t)want * hparN)));
+        HIPCHK(hipMemsetAsync(top->d_mask.p, 0, (size_t)want * maskb, top->stream));
+    }
     HIPCHK(hipMemsetAsync(top->d_stamp.p, 0, sizeof(uint32_t) * n, top->stream));
     HIPCHK(hipMemsetAsync(top->d_memo.p, 0, sizeof(unsigned long long) * n, top->stream));
     HIPCHK(hipMemsetAsync(top->d_counters.p, 0, sizeof(uint32_t) * (size_t)want * 4, top->stream));
     HIPCHK(hipStreamSynchronize(top->stream));
     top->slots = want;
+    top->wsK = K;
+    top->wsRing = ringE;
+    top->wsOver = overE;
+    top->stats.slots = want;
     return 0;
 }
 
@@ -476,6 +552,11 @@ SlotWs slot_ws(Topology* top) {
     w.best = top->d_best.p; w.cnt = top->d_cnt.p; w.bslot = top->d_bslot.p;
     w.memo = top->d_memo.p; w.par = top->d_par.p; w.pathbuf = top->d_pathbuf.p;
     w.counters = top->d_counters.p;
+    w.K = top->wsK > 1 ? top->wsK : 1;
+    w.ring_entries = top->wsRing;
+    w.over_entries = top->wsOver;
+    w.mask = top->d_mask.p;
+    w.hpar = top->d_hpar.p;
     return w;
 }
 
@@ -563,13 +644,39 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         HIPCHK(top->d_targets.ensure((size_t)A));
         HIPCHK(hipMemcpyAsync(top->d_sources.p, src.data(), sizeof(uint32_t) * (size_t)rows, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(top->d_targets.p, tgt.data(), sizeof(uint32_t) * (size_t)A, hipMemcpyHostToDevice, st));
+        const int K = batch_k(top);
         HIPCHK(hipEventRecord(top->ev0, st));
-        HIPCHK(launch_sssp_rows(dev_csr(top), slot_ws(top), top->d_sources.p, (int)rows,
-                                top->d_targets.p, (int)A, default_delta(top), lds_plan(top),
-                                (uint32_t)top->farCap,
-                                (uint32_t)top->nearCap, top->events,
-                                out_lr, out_hops,
-                                out_rowmin, top->d_stats.p, st));
+        if (K > 1) {
+            // bucket shift per row: sh = C - pi(src) >= 2 delta (topo_sssp_batch.hip)
+            const double delta = default_delta(top);
+            double pmax = 0.0;
+            for (double p : top->pot) if (std::isfinite(p)) pmax = std::max(pmax, p);
+            std::vector<double> sh((size_t)rows);
+            for (int64_t i = 0; i < rows; i++) {
+                const double p = top->pot[(size_t)src[(size_t)i]];
+                sh[(size_t)i] = (pmax - (std::isfinite(p) ? p : pmax)) + 2.0 * delta;
+            }
+            HIPCHK(top->d_srcsh.ensure((size_t)rows));
+            HIPCHK(hipMemcpyAsync(top->d_srcsh.p, sh.data(), sizeof(double) * (size_t)rows,
+                                  hipMemcpyHostToDevice, st));
+            HIPCHK(hipEventRecord(top->ev0, st));
+            const SsspLdsPlan bp = sssp_batch_lds_plan(
+                K, top->hubLimit, (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 20)),
+                top->g.V);
+            HIPCHK(launch_sssp_batch(K, dev_csr(top), slot_ws(top), top->d_sources.p,
+                                     top->d_srcsh.p, (int)rows, top->d_targets.p, (int)A,
+                                     delta, bp, (uint32_t)top->farCap, out_lr, out_hops,
+                                     out_rowmin, top->d_stats.p, st));
+            HIPCHK(hipEventRecord(top->ev1, st));
+            HIPCHK(hipStreamSynchronize(st));  // sh must outlive the async copy
+        } else {
+            HIPCHK(launch_sssp_rows(dev_csr(top), slot_ws(top), top->d_sources.p, (int)rows,
+                                    top->d_targets.p, (int)A, default_delta(top), lds_plan(top),
+                                    (uint32_t)top->farCap,
+                                    (uint32_t)top->nearCap, top->events,
+                                    out_lr, out_hops,
+                                    out_rowmin, top->d_stats.p, st));
+        }
         HIPCHK(hipEventRecord(top->ev1, st));
         HIPCHK(hipStreamSynchronize(st));
     }
@@ -945,6 +1052,8 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "far_cap") top->farCap = (int64_t)value;
     else if (k == "near_cap") top->nearCap = (int64_t)value;
     else if (k == "events") top->events = value != 0;
+    else if (k == "batch") top->batchK = (int)value;
+    else if (k == "ring_per_vk") top->ringPerVK = value;
     else return -1;
     return 0;
 }

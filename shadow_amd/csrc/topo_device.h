@@ -83,6 +83,14 @@ struct SlotWs {
     uint32_t* par = nullptr;             // parent vertex
     uint32_t* pathbuf = nullptr;         // [slot][kMaxHops][kSsspBlock]
     uint32_t* counters = nullptr;        // [slot][4]: iteration id, (unused), source epoch
+    // batched kernel (sssp_batch_kernel, K sources per slot): dist is [V][K] per slot, ring holds
+    // ring_entries u32 (vertex * K + source) entries per slot (no overflow pile: over_entries is
+    // 0); mask = 2 parities of a K-bit mask per vertex; hpar [P][K] parent hints
+    int K = 1;
+    int64_t ring_entries = 0;
+    int64_t over_entries = 0;
+    uint8_t* mask = nullptr;
+    uint32_t* hpar = nullptr;
 };
 
 // LDS plan of one SSSP workgroup: H hub distance words (+ their queue bitmaps) and P parent
@@ -102,6 +110,15 @@ hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d
                             double2* out_lr,
                             uint16_t* out_hops, double* out_rowmin, unsigned long long* d_stats,
                             hipStream_t stream);
+
+// Batched multi-source SSSP (topo_sssp_batch.hip): K in {2, 4, 8, 16} sources per workgroup in
+// lock-step over buckets of d + srcsh[row] (srcsh >= 2 delta).  plan from sssp_batch_lds_plan.
+SsspLdsPlan sssp_batch_lds_plan(int K, int64_t hub_limit, uint32_t par_hubs, int64_t V);
+hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
+                             const double* d_srcsh, int nsrc, const uint32_t* d_targets, int A,
+                             double delta, const SsspLdsPlan& plan, uint32_t far_cap,
+                             double2* out_lr, uint16_t* out_hops, double* out_rowmin,
+                             unsigned long long* d_stats, hipStream_t stream);
 
 hipError_t launch_pair_table_complete(int A, int64_t row0, int64_t rows, const double* elatAA,
                                       const double* elossAA, const double* vlossA, double2* out_lr,

@@ -21,34 +21,13 @@
 #include <cmath>
 #include <cstdint>
 
-#include "topo_device.h"
+#include "topo_dev_common.h"
 
 namespace shdtopo {
 
 namespace {
 
-constexpr unsigned long long kInfBits = 0x7FF0000000000000ull;
-
-__device__ __forceinline__ unsigned long long ld_l2_u64(const unsigned long long* p) {
-    // L1-bypassing (sc1) load: values written by atomics of other waves must not be read from a
-    // stale vector-L1 line (MI355X_MICROARCH.md "inter-workgroup visibility").
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_l2_u32(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double bits2d(unsigned long long b) { return __longlong_as_double((long long)b); }
-__device__ __forceinline__ unsigned long long d2bits(double d) { return (unsigned long long)__double_as_longlong(d); }
-
-struct __attribute__((packed, aligned(4))) W3 {
-    uint32_t a, b, c;
-};
-__device__ __forceinline__ uint32_t adj_col(const DevCSR& g, uint32_t j) { return g.adj[3ull * j]; }
-__device__ __forceinline__ void adj_load(const DevCSR& g, uint32_t j, uint32_t& col, double& wt) {
-    const W3 r = *reinterpret_cast<const W3*>(g.adj + 3ull * j);
-    col = r.a;
-    wt = __hiloint2double((int)r.c, (int)r.b);
-}
+using namespace dev;
 
 #ifndef SHD_RING_SLOTS
 #define SHD_RING_SLOTS 48
@@ -250,13 +229,6 @@ struct DistView {
     }
 };
 
-// Bucket of a distance: floor(d / delta) by one IEEE multiply, monotone non-decreasing in d (so a
-// bucket is an interval of distances); +inf and huge values land in the last bucket.
-__device__ __forceinline__ uint32_t bucket_of(double d, double inv_delta) {
-    const double b = d * inv_delta;
-    return b < 4.0e9 ? (uint32_t)b : 4000000000u;
-}
-
 // The buckets of one source.  The window holds the kRingSlots buckets [wbase, wbase + kRingSlots)
 // in fixed slots; later buckets go to the overflow pile, which a refill re-sorts into the window
 // once the window is used up.  cb = the bucket being settled.
@@ -306,15 +278,6 @@ __device__ __forceinline__ void ring_push(bool pred, uint32_t slot, unsigned lon
         }
         m &= ~mm;
     }
-}
-
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long y = __shfl_xor(x, o, 64);
-        x = y < x ? y : x;
-    }
-    return x;
 }
 
 // Near-phase relaxation of queue Q: the load-balanced chunking of expand_queue, with U edges in

@@ -1,0 +1,1009 @@
+// topo_sssp_batch.hip -- batched multi-source SSSP for gfx950: one persistent workgroup settles
+// K sources at once (K = 8: the K distances of a vertex are one 64-B line).
+//
+// Replaces, like sssp_rows_kernel, igraph_get_shortest_paths_dijkstra + the per-target helper
+// (src/topology/shd-topology.c:561-833): same distances (bit-exact: every latency add is one IEEE
+// add and any label-correcting order reaches the same monotone-rounding fixpoint), same parents
+// (the argmin d[u] rule of SURVEY.md A.3), same per-target epilogue.
+//
+// Why batch.  The single-source kernel is bound by random 64-B DRAM requests: every relaxation of
+// a tail vertex reads (and may atomically lower) one 8-B distance word, i.e. a whole line.  On a
+// power-law Internet topology almost every shortest path runs through the hub core, so
+// d_s(v) ~= d_s(h0) + d(h0, v) for the top hub h0: shifted by pi(s) = d(h0, s), the distances of
+// different sources to the same vertex fall into the same or adjacent delta-buckets (measured on
+// C4: 8 random sources, delta = 3 ms, 1.84 distinct buckets per vertex).  Lock-step buckets over
+// the shifted keys therefore expand a vertex ONCE for all sources that reach it in the current
+// bucket: the adjacency row is read once, and each relaxation reads the target's K distances as
+// one line.  K lanes work on one edge (lane j = source j).
+//
+// Per-source correctness is untouched by the shift: source j's bucket of a distance d is
+// floor((d + sh_j) / delta) with sh_j = C - pi(s_j) >= 0, a monotone function of d, and source j's
+// buckets are settled in increasing order -- lock-step only interleaves independent sources.
+//
+// Near-phase bookkeeping per vertex: a K-bit mask of the sources that must expand it in the next
+// iteration (double buffered by iteration parity; hubs' masks in LDS).  A vertex enters the next
+// near queue when its mask goes from 0 to non-zero, so the queue is deduplicated (<= V entries)
+// and an expansion serves every source of the mask.  Far improvements are (vertex, source)
+// entries in a 48-bucket window, merged into the masks when their bucket becomes current.
+// Improvements past the window are not stored: they only lower the smallest pending bucket, and
+// when the window is used up one streaming pass over the batch's distances (64 MB at K = 8, ~3
+// per batch) classifies every (vertex, source) into the next window -- no overflow pile.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <type_traits>
+
+#include "topo_dev_common.h"
+
+namespace shdtopo {
+
+namespace {
+
+using namespace dev;
+
+#ifndef SHD_BATCH_S
+#define SHD_BATCH_S 8  // sources per lane in the relaxation (lanes per edge = K / S)
+#endif
+#ifndef SHD_BATCH_U
+#define SHD_BATCH_U 1  // edges per lane in flight (U = 2 spills at S = 8)
+#endif
+constexpr int kBChunk = 256;             // queue vertices per expansion chunk
+constexpr int kBRing = 48;               // buckets in the window (<= 64: one ballot scans them)
+constexpr uint32_t kNoBucket = 0xFFFFFFFFu;
+constexpr size_t kBMaxLds = 160 * 1024;  // LDS of one CU (one batch workgroup per CU)
+
+template <int K>
+struct MaskOps {
+    static_assert(K == 2 || K == 4 || K == 8 || K == 16, "batch width");
+    using M = typename std::conditional<(K <= 8), uint8_t, uint16_t>::type;
+    static constexpr int kBits = 8 * (int)sizeof(M);
+    static constexpr int kPer = 32 / kBits;
+    static constexpr uint32_t kFull = (1u << K) - 1u;
+    // returning OR of `bits` into v's mask (LDS or HBM word); returns v's previous mask
+    __device__ static __forceinline__ uint32_t set(M* m, uint32_t v, uint32_t bits) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(m) + v / kPer;
+        const uint32_t s = (v % kPer) * kBits;
+        return (atomicOr(w, bits << s) >> s) & kFull;
+    }
+    // HBM mask read that bypasses L1 (the words are written by atomics of other waves)
+    __device__ static __forceinline__ uint32_t get_l2(const M* m, uint32_t v) {
+        const uint32_t w = ld_l2_u32(reinterpret_cast<const uint32_t*>(m) + v / kPer);
+        return (w >> ((v % kPer) * kBits)) & kFull;
+    }
+};
+
+template <int K>
+struct LdsB {
+    uint32_t off[kBChunk + 4];
+    uint32_t rs[kBChunk];
+    uint32_t vx[kBChunk];
+    uint32_t msk[kBChunk];
+    double val[kBChunk * K];  // the chunk's source distances, [vertex][source]
+    double sh[K];             // per-source bucket shift sh_j = C - pi(s_j)
+    uint32_t wave[kSsspBlock / 64];
+    uint32_t rtail[kBRing];   // entries pushed into each bucket of the window
+    uint32_t qtail;
+    uint32_t beyond;   // an improvement landed past the window since the last refill
+    uint32_t idx;      // batch taken by this workgroup
+    uint32_t fover;    // a window slot overflowed: scanning buckets from now on
+    uint32_t ominb;    // lower bound of the buckets past the window
+    uint32_t fminb;    // scanning mode: smallest bucket of the unexpanded far values
+    unsigned long long dmin;
+    unsigned long long cnt[2];  // per-batch source-relaxations, window entries taken
+};
+
+// Dynamic LDS after the control block: hub masks (two parities), parent-tie bits of the first P
+// hubs (P*K bits), then the hub distances hd[H][K].
+struct BLayout {
+    size_t hmA, hmB, tb, hd, bytes;
+};
+template <int K>
+__host__ __device__ inline BLayout blayout(uint32_t H, uint32_t P) {
+    using M = typename MaskOps<K>::M;
+    BLayout l;
+    const size_t ctrl = (sizeof(LdsB<K>) + 15) / 16 * 16;
+    const size_t mb = ((size_t)H * sizeof(M) + 15) / 16 * 16;
+    l.hmA = ctrl;
+    l.hmB = ctrl + mb;
+    l.tb = ctrl + 2 * mb;
+    const size_t tbw = ((size_t)P * K + 31) / 32;
+    l.hd = (l.tb + 4 * tbw + 15) / 16 * 16;
+    l.bytes = l.hd + 8 * (size_t)H * K;
+    return l;
+}
+
+__device__ __forceinline__ uint32_t bkt(double d, double sh, double inv_delta) {
+    return bucket_of(__dadd_rn(d, sh), inv_delta);
+}
+
+template <int K>
+struct BView {
+    using M = typename MaskOps<K>::M;
+    unsigned long long* hd;    // LDS [H][K]
+    unsigned long long* dist;  // HBM [V][K] (rows < H unused while the batch runs)
+    uint32_t* tb;              // LDS parent-tie bits of (hub < P, source)
+    uint32_t* hpar;            // HBM [P][K]: vertex whose relaxation last lowered hub v for j
+    uint32_t H, P;
+    __device__ __forceinline__ unsigned long long get(uint32_t v, uint32_t j) const {
+        return v < H ? hd[(size_t)v * K + j] : ld_l2_u64(&dist[(size_t)v * K + j]);
+    }
+};
+
+struct BBuckets {
+    double inv_delta;
+    uint32_t cb, wbase;
+    uint32_t* ring;  // kBRing slots of slot_cap (vertex * K + source) entries
+    uint32_t slot_cap;
+};
+
+// Window push: lanes may target different slots; one LDS atomic per (wave, slot).
+template <int K>
+__device__ __forceinline__ void ring_push(bool pred, uint32_t slot, uint32_t val,
+                                          const BBuckets& B, LdsB<K>& L) {
+    unsigned long long m = __ballot(pred);
+    const int lane = threadIdx.x & 63;
+    while (m) {
+        const int leader = __ffsll((long long)m) - 1;
+        const uint32_t s = __shfl(slot, leader, 64);
+        const bool mine = pred && slot == s;
+        const unsigned long long mm = __ballot(mine);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&L.rtail[s], (uint32_t)__popcll(mm));
+        base = __shfl(base, leader, 64);
+        if (mine) {
+            const uint32_t pos = base + (uint32_t)__popcll(mm & ((1ull << lane) - 1ull));
+            if (pos < B.slot_cap) B.ring[(size_t)s * B.slot_cap + pos] = val;
+            else atomicOr(&L.fover, 2u);
+        }
+        m &= ~mm;
+    }
+}
+
+// One near iteration over queue Q (vertices; their source masks in mcur/hcur, cleared here).
+// G = K / S lanes per edge, each lane relaxing the edge for S consecutive sources (its S distance
+// words of the target's line are one vector load), U edges per lane in flight: 1024 * U / G edges
+// per pass keep enough requests in flight (the pass is a chain of dependent round trips).
+// Improvements of bucket cb set the target's mask in mnxt/hnxt (the group's bits OR-ed by its
+// first lane, one returning atomic) and push it to qout when the mask was empty; later buckets go
+// to the window as (vertex, source) entries when they move the vertex to an
+// earlier bucket than it had for that source; in scanning mode they only lower L.fminb.
+template <int K, int S, int U>
+__device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, const DevCSR& g,
+                                            LdsB<K>& L, const BView<K>& D,
+                                            typename MaskOps<K>::M* mcur,
+                                            typename MaskOps<K>::M* hcur,
+                                            typename MaskOps<K>::M* mnxt,
+                                            typename MaskOps<K>::M* hnxt, uint32_t* qout,
+                                            uint32_t qcap, const BBuckets& B, bool scan) {
+    using MO = MaskOps<K>;
+    static_assert(K % S == 0 && (S == 1 || S == 2 || S == 4 || S == 8), "sources per lane");
+    constexpr int G = K / S;                  // lanes per edge
+    constexpr uint32_t NG = kSsspBlock / G;   // edges per workgroup per unrolled step
+    constexpr uint32_t SM = (1u << S) - 1u;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    const uint32_t sub = tid % G;             // this lane's share of the sources: [j0, j0 + S)
+    const uint32_t j0 = sub * S;
+    const uint32_t grp = tid / G;
+    double shj[S];
+#pragma unroll
+    for (int q = 0; q < S; q++) shj[q] = L.sh[j0 + q];
+    const uint32_t wend = B.wbase + (uint32_t)kBRing;
+    for (uint32_t base = 0; base < nq; base += kBChunk) {
+        const uint32_t cnt = min((uint32_t)kBChunk, nq - base);
+        uint32_t deg = 0;
+        unsigned long long act = 0;
+        if (tid < cnt) {
+            const uint32_t v = Q[base + tid];
+            uint32_t m;
+            if (v < D.H) {
+                m = hcur[v];
+                hcur[v] = 0;
+            } else {
+                m = MO::get_l2(mcur, v);
+                mcur[v] = 0;
+            }
+            const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
+            deg = m ? r1 - r0 : 0u;
+            act = (unsigned long long)deg * (unsigned long long)__popc(m);
+            L.rs[tid] = r0;
+            L.vx[tid] = v;
+            L.msk[tid] = m;
+        }
+        uint32_t total;
+        const uint32_t off = block_excl_scan<kSsspBlock>(deg, L.wave, &total);
+        if (tid < cnt) L.off[tid] = off;
+        if (tid == 0) L.off[cnt] = total;
+        act = wave_sum_u64(act);
+        if (lane == 0 && act) atomicAdd(&L.cnt[0], act);
+        // the chunk's source distances: K lanes per vertex read its line once
+        for (uint32_t i = tid; i < cnt * K; i += kSsspBlock) {
+            const uint32_t vi = i / K, jj = i % K;
+            if ((L.msk[vi] >> jj) & 1u) L.val[i] = bits2d(D.get(L.vx[vi], jj));
+        }
+        __syncthreads();
+        for (uint32_t eb = 0; eb < total; eb += NG * U) {
+            uint32_t n[U], from[U], mk[U];
+            int los[U];
+            W3 rec[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {  // U searches, U record loads in flight
+                const uint32_t e = eb + (uint32_t)u * NG + grp;
+                const bool valid = e < total;
+                int lo = 0;
+                if (valid) {
+                    int hi = (int)cnt - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (L.off[mid] <= e) lo = mid; else hi = mid - 1;
+                    }
+                }
+                const uint32_t jr = valid ? L.rs[lo] + (e - L.off[lo]) : 0u;
+                rec[u] = *reinterpret_cast<const W3*>(g.adj + 3ull * jr);
+                mk[u] = valid ? (L.msk[lo] >> j0) & SM : 0u;
+                from[u] = L.vx[lo];
+                los[u] = lo;
+                n[u] = valid ? rec[u].a : 0u;
+            }
+            // tail pre-check: this lane's S words of the target's line (one vector load)
+            unsigned long long cur[U][S];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const bool t = mk[u] && n[u] >= D.H;
+                const unsigned long long* p = D.dist + (t ? (size_t)n[u] * K : (size_t)0) + j0;
+                if constexpr (S >= 2) {
+#pragma unroll
+                    for (int q = 0; q < S; q += 2) {
+                        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + q);
+                        cur[u][q] = t ? x.x : 0ull;
+                        cur[u][q + 1] = t ? x.y : 0ull;
+                    }
+                } else {
+                    const unsigned long long x = *p;
+                    cur[u][0] = t ? x : 0ull;
+                }
+            }
+            uint32_t imp[U], nb[U];
+            uint32_t bk[U][S];
+            unsigned long long ab[U][S];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                imp[u] = 0u;
+                nb[u] = 0u;
+                const double w = rec_wt(rec[u]);
+                const bool hub = n[u] < D.H;
+#pragma unroll
+                for (int q = 0; q < S; q++) {
+                    const bool on = (mk[u] >> q) & 1u;
+                    ab[u][q] = on ? d2bits(__dadd_rn(L.val[los[u] * K + j0 + q], w)) : ~0ull;
+                    unsigned long long prev = cur[u][q];
+                    bool im = false;
+                    if (on && hub) {
+                        const size_t wi = (size_t)n[u] * K + j0 + q;
+                        const unsigned long long old = atomicMin(&D.hd[wi], ab[u][q]);
+                        prev = old;
+                        im = ab[u][q] < old;
+                        if (n[u] < D.P) {  // parent hint (see the parent pass)
+                            if (im) D.hpar[wi] = from[u];
+                            else if (ab[u][q] == old) atomicOr(&D.tb[wi >> 5], 1u << (wi & 31));
+                        }
+                    } else if (on && ab[u][q] < cur[u][q]) {
+                        (void)atomicMin(&D.dist[(size_t)n[u] * K + j0 + q], ab[u][q]);
+                        im = true;
+                    }
+                    bk[u][q] = kNoBucket;
+                    if (im) {
+                        const uint32_t b = bkt(bits2d(ab[u][q]), shj[q], B.inv_delta);
+                        if (b <= B.cb) nb[u] |= 1u << q;
+                        else if (scan || b < bkt(bits2d(prev), shj[q], B.inv_delta)) bk[u][q] = b;
+                    }
+                    imp[u] |= im ? 1u << q : 0u;
+                }
+            }
+            uint32_t om = kNoBucket, fm = kNoBucket;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                // the group's near bits -> one mask OR by its first lane
+                uint32_t gm = nb[u] << j0;
+#pragma unroll
+                for (int o = 1; o < G; o <<= 1) gm |= __shfl_xor(gm, o, 64);
+                bool first = false;
+                if (sub == 0 && gm) {
+                    const uint32_t old = n[u] < D.H ? MO::set(hnxt, n[u], gm) : MO::set(mnxt, n[u], gm);
+                    first = old == 0u;
+                }
+                wave_push_t<uint32_t>(first, n[u], qout, &L.qtail, qcap, &L.fover, 1u);
+#pragma unroll
+                for (int q = 0; q < S; q++) {
+                    const uint32_t b = bk[u][q];
+                    const bool far = b != kNoBucket;
+                    if (scan) {
+                        fm = b < fm ? b : fm;
+                        continue;
+                    }
+                    const bool pR = far && b < wend;
+                    if (far && !pR) om = b < om ? b : om;  // past the window: found by the refill
+                    ring_push<K>(pR, b - B.wbase, n[u] * K + j0 + q, B, L);
+                }
+            }
+            if (__ballot(om != kNoBucket || fm != kNoBucket)) {
+                om = wave_min_u32(om);
+                fm = wave_min_u32(fm);
+                if (lane == 0 && om != kNoBucket) {
+                    atomicMin(&L.ominb, om);
+                    L.beyond = 1u;
+                }
+                if (lane == 0 && fm != kNoBucket) atomicMin(&L.fminb, fm);
+            }
+        }
+        // this wave's atomics and queue stores complete before any wave reads them after the
+        // barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+}
+
+// Plain load-balanced expansion of vertex list Q (parent pass): VF(v, val) decides per vertex,
+// EF(v, val, adjacency slot) handles one edge.
+template <int K, class VF, class EF>
+__device__ __forceinline__ void expand_list(const uint32_t* Q, uint32_t nq, const DevCSR& g,
+                                            LdsB<K>& L, VF&& vf, EF&& ef) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t base = 0; base < nq; base += kBChunk) {
+        const uint32_t cnt = min((uint32_t)kBChunk, nq - base);
+        uint32_t deg = 0;
+        if (tid < cnt) {
+            const uint32_t v = Q[base + tid];
+            double val = 0.0;
+            if (vf(v, val)) {
+                const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
+                deg = r1 - r0;
+                L.rs[tid] = r0;
+            } else {
+                L.rs[tid] = 0;
+            }
+            L.vx[tid] = v;
+            L.val[tid] = val;
+        }
+        uint32_t total;
+        const uint32_t off = block_excl_scan<kSsspBlock>(deg, L.wave, &total);
+        if (tid < cnt) L.off[tid] = off;
+        if (tid == 0) L.off[cnt] = total;
+        __syncthreads();
+        for (uint32_t e = tid; e < total; e += kSsspBlock) {
+            int lo = 0, hi = (int)cnt - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (L.off[mid] <= e) lo = mid; else hi = mid - 1;
+            }
+            ef(L.vx[lo], L.val[lo], L.rs[lo] + (e - L.off[lo]));
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+template <int K>
+__global__ void __launch_bounds__(kSsspBlock, 1)
+sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
+                  const double* __restrict__ srcsh, int nsrc, const uint32_t* __restrict__ targets,
+                  int A, double delta, uint32_t H, uint32_t P, uint32_t far_cap,
+                  double2* __restrict__ out_lr, uint16_t* __restrict__ out_hops,
+                  double* __restrict__ out_rowmin, unsigned long long* __restrict__ stats) {
+    using MO = MaskOps<K>;
+    using M = typename MO::M;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    LdsB<K>& L = *reinterpret_cast<LdsB<K>*>(smem);
+    const BLayout lay = blayout<K>(H, P);
+    M* hmA = reinterpret_cast<M*>(smem + lay.hmA);
+    M* hmB = reinterpret_cast<M*>(smem + lay.hmB);
+    const uint32_t hmw = (uint32_t)((lay.hmB - lay.hmA) / 4);  // u32 words per hub-mask array
+    const uint32_t tbw = (uint32_t)(((size_t)P * K + 31) / 32);
+    const int slot = blockIdx.x;
+    const uint32_t tid = threadIdx.x;
+    const int64_t V = ws.V;
+    BView<K> D;
+    D.tb = reinterpret_cast<uint32_t*>(smem + lay.tb);
+    D.hd = reinterpret_cast<unsigned long long*>(smem + lay.hd);
+    D.dist = ws.dist + (size_t)slot * (size_t)V * K;
+    D.hpar = ws.hpar + (size_t)slot * (size_t)P * K;
+    D.H = H;
+    D.P = P;
+    const size_t mbytes = ((size_t)V * sizeof(M) + 255) / 256 * 256;
+    M* mA = reinterpret_cast<M*>(ws.mask + (size_t)slot * 2 * mbytes);
+    M* mB = reinterpret_cast<M*>(ws.mask + (size_t)slot * 2 * mbytes + mbytes);
+    uint32_t* qa = reinterpret_cast<uint32_t*>(ws.qa + (size_t)slot * kNearPerVertex * V);
+    uint32_t* qb = reinterpret_cast<uint32_t*>(ws.qb + (size_t)slot * kNearPerVertex * V);
+    uint32_t* stamp = ws.stamp + (size_t)slot * V;
+    unsigned long long* best = ws.best + (size_t)slot * V;
+    uint32_t* cntc = ws.cnt + (size_t)slot * V;
+    uint32_t* bslot = ws.bslot + (size_t)slot * V;
+    unsigned long long* memo = ws.memo + (size_t)slot * V;
+    uint32_t* par = ws.par + (size_t)slot * V;
+    uint32_t* pbuf = ws.pathbuf + (size_t)slot * kMaxHops * kSsspBlock;
+    uint32_t* ctr = ws.counters + (size_t)slot * 4;
+    const uint32_t cap = (uint32_t)V;
+    BBuckets B;
+    B.inv_delta = 1.0 / delta;
+    B.ring = reinterpret_cast<uint32_t*>(ws.ring) + (size_t)slot * ws.ring_entries;
+    B.slot_cap = (uint32_t)(ws.ring_entries / kBRing);
+    if (far_cap > 0) B.slot_cap = min(B.slot_cap, far_cap);
+    uint32_t* fscr = B.ring;  // parent-pass scratch list (the window is idle by then)
+
+    uint32_t iter = ctr[0], mep = ctr[2];
+    unsigned long long n_near = 0, n_split = 0, n_scan = 0, n_expand = 0, n_refill = 0, n_par = 0;
+    unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, t_split = 0;
+    if (tid < 2) L.cnt[tid] = 0;
+    unsigned long long tk = wall_clock64();
+
+    for (;;) {
+        if (tid == 0) L.idx = (uint32_t)atomicAdd(&stats[ST_DEQUEUE], 1ull);
+        __syncthreads();
+        const uint32_t bidx = L.idx;
+        __syncthreads();
+        if ((int64_t)bidx * K >= nsrc) break;
+        const int r0 = (int)bidx * K;
+        const int nk = min(K, nsrc - r0);
+        tk = wall_clock64();
+
+        // ---------------- init: hubs in LDS, the tail's K-wide rows in HBM --------------------
+        for (uint32_t i = tid; i < H * K; i += kSsspBlock) D.hd[i] = kInfBits;
+        for (uint32_t i = tid; i < hmw; i += kSsspBlock) {
+            reinterpret_cast<uint32_t*>(hmA)[i] = 0u;
+            reinterpret_cast<uint32_t*>(hmB)[i] = 0u;
+        }
+        for (uint32_t i = tid; i < tbw; i += kSsspBlock) D.tb[i] = 0u;
+        for (uint32_t i = tid; i < (uint32_t)kBRing; i += kSsspBlock) L.rtail[i] = 0u;
+        if (tid < (uint32_t)K) L.sh[tid] = (int)tid < nk ? srcsh[r0 + tid] : 0.0;
+        {
+            ulonglong2* d2 = reinterpret_cast<ulonglong2*>(D.dist);
+            const size_t lo = (size_t)H * K / 2, hi = (size_t)V * K / 2;
+            for (size_t i = lo + tid; i < hi; i += kSsspBlock) d2[i] = make_ulonglong2(kInfBits, kInfBits);
+        }
+        if (tid == 0) {
+            L.beyond = 1u;  // the sources: found by the first refill
+            L.ominb = kNoBucket;
+            L.fminb = kNoBucket;
+            L.fover = 0;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // every source starts at its own (shifted) bucket, past the empty window
+        if ((int)tid < nk) {
+            const uint32_t s = sources[r0 + tid];
+            if (s < H) D.hd[(size_t)s * K + tid] = 0ull;
+            else D.dist[(size_t)s * K + tid] = 0ull;
+            atomicMin(&L.ominb, bkt(0.0, L.sh[tid], B.inv_delta));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        { unsigned long long t = wall_clock64(); t_init += t - tk; tk = t; }
+
+        // ---------------- lock-step delta-stepping over the shifted buckets -------------------
+        B.cb = L.ominb - 1u;  // ominb >= 1: sh_j >= 2 delta (host)
+        B.wbase = 0;
+        M* mcur = mA; M* mnxt = mB;
+        M* hcur = hmA; M* hnxt = hmB;
+        uint32_t* qin = qa; uint32_t* qout = qb;
+        uint32_t nq = 0;
+        uint32_t guard = 0;
+        bool aborted = false;
+        constexpr int FU = 4;
+        for (;;) {
+            while (nq > 0) {
+                if (tid == 0) L.qtail = 0;
+                __syncthreads();
+                n_expand += nq;
+                relax_batch<K, SHD_BATCH_S < K ? SHD_BATCH_S : K, SHD_BATCH_U>(qin, nq, g, L, D, mcur, hcur, mnxt, hnxt, qout, cap, B,
+                                  L.fover != 0u);
+                nq = min(L.qtail, cap);
+                { uint32_t* t = qin; qin = qout; qout = t; }
+                { M* t = mcur; mcur = mnxt; mnxt = t; }
+                { M* t = hcur; hcur = hnxt; hnxt = t; }
+                n_near++;
+                if (++guard > 4000000u) {
+                    aborted = true;
+                    nq = 0;
+                }
+                __syncthreads();
+            }
+            if (aborted) break;
+            const unsigned long long ts0 = wall_clock64();
+            if (L.fover != 0u) {
+                // Scanning mode: a window slot overflowed (entries were lost), so for
+                // the rest of this batch the next bucket is found by classifying every
+                // (vertex, source) distance.  L.fminb is exact after the first scanning pass.
+                const bool exact = (L.fover & 64u) != 0u;
+                const uint32_t fmb = L.fminb;
+                if (exact && fmb == kNoBucket) break;
+                uint32_t nb = B.cb + 1;
+                if (exact) nb = max(nb, fmb);
+                __syncthreads();
+                if (tid == 0) {
+                    L.qtail = 0;
+                    L.fminb = kNoBucket;
+                    L.fover |= 64u;
+                }
+                __syncthreads();
+                for (uint32_t vb = 0; vb < (uint32_t)V; vb += kSsspBlock) {
+                    const uint32_t v = vb + tid;
+                    uint32_t m = 0, km = kNoBucket;
+                    if (v < (uint32_t)V) {
+                        for (int jj = 0; jj < nk; jj++) {
+                            const unsigned long long d = D.get(v, (uint32_t)jj);
+                            if (d == kInfBits) continue;
+                            const uint32_t b = bkt(bits2d(d), L.sh[jj], B.inv_delta);
+                            if (b > B.cb && b <= nb) m |= 1u << jj;
+                            else if (b > nb && b < km) km = b;
+                        }
+                        if (m) {
+                            if (v < H) hcur[v] = (M)m;
+                            else mcur[v] = (M)m;
+                        }
+                    }
+                    wave_push_t<uint32_t>(m != 0u, v, qin, &L.qtail, cap, &L.fover, 32u);
+                    km = wave_min_u32(km);
+                    if ((tid & 63) == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                nq = min(L.qtail, cap);
+                B.cb = nb;
+                n_scan++;
+                t_split += wall_clock64() - ts0;
+                __syncthreads();
+                continue;
+            }
+            // next non-empty bucket of the window after cb (every wave scans the slot tails)
+            int s = -1;
+            {
+                const int lane = (int)(tid & 63);
+                const int lo_slot = (int)B.cb - (int)B.wbase + 1;
+                const bool ne = lane < kBRing && lane >= lo_slot && L.rtail[lane] > 0u;
+                const unsigned long long m = __ballot(ne);
+                s = m ? __ffsll((long long)m) - 1 : -1;
+            }
+            if (s >= 0) {
+                // merge the slot's (vertex, source) entries into the masks: a vertex enters the
+                // near queue once, with every source whose entry is not stale
+                const uint32_t n = min(L.rtail[s], B.slot_cap);
+                if (tid == 0) atomicMax(&stats[ST_EV0 + 2], (unsigned long long)L.rtail[s]);
+                __syncthreads();
+                if (tid == 0) {
+                    L.rtail[s] = 0u;
+                    L.qtail = 0u;
+                }
+                B.cb = B.wbase + (uint32_t)s;
+                __syncthreads();
+                const uint32_t* ent = B.ring + (size_t)s * B.slot_cap;
+                for (uint32_t ib = 0; ib < n; ib += kSsspBlock * FU) {
+                    uint32_t v[FU], jj[FU];
+                    unsigned long long d[FU];
+#pragma unroll
+                    for (int u = 0; u < FU; u++) {
+                        const uint32_t i = ib + (uint32_t)u * kSsspBlock + tid;
+                        const uint32_t x = i < n ? ent[i] : 0u;
+                        v[u] = x / K;
+                        jj[u] = x % K;
+                    }
+#pragma unroll
+                    for (int u = 0; u < FU; u++) d[u] = D.get(v[u], jj[u]);
+#pragma unroll
+                    for (int u = 0; u < FU; u++) {
+                        const uint32_t i = ib + (uint32_t)u * kSsspBlock + tid;
+                        bool first = false;
+                        if (i < n && bkt(bits2d(d[u]), L.sh[jj[u]], B.inv_delta) >= B.cb) {
+                            const uint32_t old = v[u] < H ? MO::set(hcur, v[u], 1u << jj[u])
+                                                          : MO::set(mcur, v[u], 1u << jj[u]);
+                            first = old == 0u;
+                        }
+                        wave_push_t<uint32_t>(first, v[u], qin, &L.qtail, cap, &L.fover, 16u);
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                nq = min(L.qtail, cap);
+                if (tid == 0) L.cnt[1] += n;
+                n_split++;
+                t_split += wall_clock64() - ts0;
+                __syncthreads();
+                continue;
+            }
+            // window used up: refill it by one streaming pass over the batch's distances (or the
+            // batch is done).  No pending (vertex, source) lies in (cb, wb): the window's slots are
+            // empty and every improvement past it lowered ominb.
+            if (L.beyond == 0u) break;
+            {
+                const uint32_t wb = max(B.cb + 1, L.ominb);
+                const uint32_t we = wb + (uint32_t)kBRing;
+                __syncthreads();
+                if (tid == 0) {
+                    L.beyond = 0u;
+                    L.ominb = kNoBucket;
+                }
+                __syncthreads();
+                BBuckets R = B;
+                R.wbase = wb;
+                const size_t npair = (size_t)V * K / 2;  // two (vertex, source) words per lane
+                for (size_t ib = 0; ib < npair; ib += kSsspBlock) {
+                    const size_t i = ib + tid;
+                    unsigned long long d[2] = {kInfBits, kInfBits};
+                    if (i < npair) {
+                        if (2 * i < (size_t)H * K) {
+                            d[0] = D.hd[2 * i];
+                            d[1] = D.hd[2 * i + 1];
+                        } else {
+                            // L1-bypassing 16-B load: the words were lowered by atomics
+                            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+                            const u64x2 x = __builtin_nontemporal_load(
+                                reinterpret_cast<const u64x2*>(D.dist) + i);
+                            d[0] = x.x;
+                            d[1] = x.y;
+                        }
+                    }
+                    uint32_t k2 = kNoBucket;
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint32_t x = (uint32_t)(2 * i + h);
+                        const uint32_t b = d[h] == kInfBits ? kNoBucket
+                                                            : bkt(bits2d(d[h]), L.sh[x % K], B.inv_delta);
+                        const bool mv = b >= wb && b < we;
+                        if (b >= we && b != kNoBucket) k2 = b < k2 ? b : k2;
+                        ring_push<K>(mv, b - wb, x, R, L);
+                    }
+                    k2 = wave_min_u32(k2);
+                    if ((tid & 63) == 0 && k2 != kNoBucket) {
+                        atomicMin(&L.ominb, k2);
+                        L.beyond = 1u;
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                n_refill++;
+                B.wbase = wb;
+                B.cb = wb - 1;
+                nq = 0;
+                t_split += wall_clock64() - ts0;
+            }
+        }
+        if (aborted) {
+            // iteration guard: leave the masks clean for the next batch and report
+            for (size_t i = tid; i < 2 * mbytes / 4; i += kSsspBlock)
+                reinterpret_cast<uint32_t*>(mA)[i] = 0u;
+            if (tid == 0) atomicOr(&stats[ST_OVERFLOW], 2ull);
+            __syncthreads();
+        }
+        if (tid == 0 && L.fover) {
+            atomicAdd(&stats[ST_FARSCAN], 1ull);
+            atomicOr(&stats[ST_OVERSITE], (unsigned long long)L.fover);
+        }
+        { unsigned long long t = wall_clock64(); t_sssp += t - tk; tk = t; }
+
+        // ---------------- parents + per-target epilogue, one source at a time -----------------
+        for (int jn = 0; jn < nk; jn++) {
+            const uint32_t j = (uint32_t)jn;
+            const uint32_t src = sources[r0 + jn];
+            const int s_idx = r0 + jn;
+            uint32_t* pcur = qa;
+            uint32_t* pnxt = qb;
+            // parents for the target chains (argmin d[u]): one adjacency pass per
+            // chain level finds min d[u] over the candidates fl(d[u] + w) == d[v] and counts them;
+            // vertices with several candidates get a recount at the minimum
+            mep++;
+            const unsigned long long mtag = (unsigned long long)mep << 32;
+            iter++;
+            if (tid == 0) L.qtail = 0;
+            __syncthreads();
+            for (uint32_t kb = 0; kb < (uint32_t)A; kb += kSsspBlock) {
+                const uint32_t k = kb + tid;
+                bool p = false;
+                uint32_t t = 0;
+                if (k < (uint32_t)A) {
+                    t = targets[k];
+                    p = (t != src) && (atomicExch(&stamp[t], iter) != iter);
+                    if (p) { best[t] = kInfBits; cntc[t] = 0; bslot[t] = 0xFFFFFFFFu; }
+                }
+                wave_push_t<uint32_t>(p, t, pcur, &L.qtail, cap, &L.fover, 128u);
+            }
+            __syncthreads();
+            uint32_t nF = min(L.qtail, cap);
+            __syncthreads();
+            while (nF > 0) {
+                n_par += nF;
+                // Heavy hubs first: the SSSP recorded which vertex last lowered each of the first
+                // P hubs for source j and whether any relaxation tied its value.  "No tie seen" +
+                // "the recorded u is a candidate" means u is the only candidate: the igraph
+                // parent, found without scanning the hub's row.  Anything else is scanned.
+                if (tid == 0) L.qtail = 0;
+                __syncthreads();
+                for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
+                    const uint32_t i = ib + tid;
+                    bool scan = false;
+                    uint32_t v = 0;
+                    if (i < nF) {
+                        v = pcur[i];
+                        scan = true;
+                        const size_t w = (size_t)v * K + j;
+                        if (g.rows_sorted && v < P && !((D.tb[w >> 5] >> (w & 31)) & 1u)) {
+                            const uint32_t u = D.hpar[w];
+                            if (u < (uint32_t)V) {
+                                uint32_t lo = g.rowptr[u], hi = g.rowptr[u + 1];
+                                while (lo < hi) {  // rows are sorted by neighbour
+                                    const uint32_t mid = (lo + hi) >> 1;
+                                    if (adj_col(g, mid) < v) lo = mid + 1; else hi = mid;
+                                }
+                                if (lo < g.rowptr[u + 1] && adj_col(g, lo) == v) {
+                                    uint32_t c;
+                                    double wt;
+                                    adj_load(g, lo, c, wt);
+                                    if (__dadd_rn(bits2d(D.get(u, j)), wt) == bits2d(D.get(v, j))) {
+                                        memo[v] = mtag | (unsigned long long)lo;
+                                        par[v] = u;
+                                        scan = false;
+                                    }
+                                }
+                            }
+                        }
+                    }
+                    wave_push_t<uint32_t>(scan, v, fscr, &L.qtail, cap, &L.fover, 128u);
+                }
+                __syncthreads();
+                const uint32_t nS = min(L.qtail, cap);
+                __syncthreads();
+                expand_list<K>(
+                    fscr, nS, g, L,
+                    [&](uint32_t v, double& val) {
+                        val = bits2d(D.get(v, j));
+                        return true;
+                    },
+                    [&](uint32_t v, double dv, uint32_t jr) {
+                        uint32_t u;
+                        double wt;
+                        adj_load(g, jr, u, wt);
+                        const unsigned long long du = D.get(u, j);
+                        if (__dadd_rn(bits2d(du), wt) == dv) {
+                            atomicMin(&best[v], du);
+                            atomicAdd(&cntc[v], 1u);
+                            atomicMin(&bslot[v], jr);
+                        }
+                    });
+                if (tid == 0) L.qtail = 0;
+                __syncthreads();
+                for (uint32_t ib = 0; ib < nS; ib += kSsspBlock) {
+                    const uint32_t i = ib + tid;
+                    bool multi = false;
+                    uint32_t v = 0;
+                    if (i < nS) {
+                        v = fscr[i];
+                        multi = ld_l2_u32(&cntc[v]) > 1u;
+                        if (multi) {
+                            atomicExch(&cntc[v], 0u);
+                            atomicExch(&bslot[v], 0xFFFFFFFFu);
+                        }
+                    }
+                    wave_push_t<uint32_t>(multi, v, pnxt, &L.qtail, cap, &L.fover, 128u);
+                }
+                __syncthreads();
+                const uint32_t nM = min(L.qtail, cap);
+                __syncthreads();
+                if (nM > 0) {
+                    expand_list<K>(
+                        pnxt, nM, g, L,
+                        [&](uint32_t v, double& val) {
+                            val = bits2d(D.get(v, j));
+                            return true;
+                        },
+                        [&](uint32_t v, double dv, uint32_t jr) {
+                            uint32_t u;
+                            double wt;
+                            adj_load(g, jr, u, wt);
+                            const unsigned long long du = D.get(u, j);
+                            if (__dadd_rn(bits2d(du), wt) == dv && du == ld_l2_u64(&best[v])) {
+                                atomicAdd(&cntc[v], 1u);
+                                atomicMin(&bslot[v], jr);
+                            }
+                        });
+                }
+                for (uint32_t i = tid; i < nS; i += kSsspBlock) {
+                    const uint32_t v = fscr[i];
+                    const uint32_t jr = ld_l2_u32(&bslot[v]);
+                    const uint32_t c = ld_l2_u32(&cntc[v]);
+                    if (jr == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
+                        atomicAdd(&stats[ST_ERRORS], 1ull);
+                        memo[v] = mtag | 0x7FFFFFFFull;
+                        par[v] = src;
+                    } else {
+                        memo[v] = mtag | (c > 1 ? 0x80000000ull : 0ull) | (unsigned long long)jr;
+                        par[v] = adj_col(g, jr);
+                    }
+                }
+                __syncthreads();
+                iter++;
+                if (tid == 0) L.qtail = 0;
+                __syncthreads();
+                for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
+                    const uint32_t i = ib + tid;
+                    bool p = false;
+                    uint32_t u = 0;
+                    if (i < nF) {
+                        u = par[pcur[i]];
+                        p = (u != src) && ((memo[u] & 0xFFFFFFFF00000000ull) != mtag) &&
+                            (atomicExch(&stamp[u], iter) != iter);
+                        if (p) { best[u] = kInfBits; cntc[u] = 0; bslot[u] = 0xFFFFFFFFu; }
+                    }
+                    wave_push_t<uint32_t>(p, u, pnxt, &L.qtail, cap, &L.fover, 128u);
+                }
+                __syncthreads();
+                nF = min(L.qtail, cap);
+                { uint32_t* t = pcur; pcur = pnxt; pnxt = t; }
+                __syncthreads();
+            }
+            { unsigned long long t = wall_clock64(); t_par += t - tk; tk = t; }
+
+            // per-target latency / reliability / hops (shd-topology.c:561-671)
+            double rmin = INFINITY;
+            const size_t rowbase = (size_t)s_idx * (size_t)A;
+            for (uint32_t k = tid; k < (uint32_t)A; k += kSsspBlock) {
+                const uint32_t t = targets[k];
+                double lat, rel;
+                uint32_t h = 0;
+                if (t == src) {
+                    // path [src]: the self loop (n == 1 branch), no destination loss
+                    const double sl = g.selfLat[src];
+                    if (isnan(sl)) {
+                        atomicAdd(&stats[ST_ERRORS], 1ull);
+                        lat = -1.0;
+                        rel = -1.0;
+                    } else {
+                        lat = 0.0 + sl;
+                        rel = 1.0;
+                        rel *= (1.0 - g.vloss[src]);
+                        rel *= (1.0 - g.selfLoss[src]);
+                        h = 1;
+                    }
+                } else {
+                    lat = bits2d(D.get(t, j));
+                    bool amb = false, bad = false;
+                    uint32_t v = t;
+                    while (v != src) {
+                        const unsigned long long m = memo[v];
+                        if ((m & 0xFFFFFFFF00000000ull) != mtag || (m & 0x7FFFFFFFull) == 0x7FFFFFFFull) {
+                            bad = true;
+                            break;
+                        }
+                        amb |= (m >> 31) & 1ull;
+                        if (h < kMaxHops) pbuf[(size_t)h * kSsspBlock + tid] = (uint32_t)(m & 0x7FFFFFFFull);
+                        h++;
+                        v = par[v];
+                        if (h > (uint32_t)V) { bad = true; break; }
+                    }
+                    rel = 1.0;
+                    rel *= (1.0 - g.vloss[src]);
+                    rel *= (1.0 - g.vloss[t]);
+                    if (bad) {
+                        atomicAdd(&stats[ST_ERRORS], 1ull);
+                        lat = -1.0;
+                        rel = -1.0;
+                    } else if (h <= (uint32_t)kMaxHops) {
+                        for (int i = (int)h - 1; i >= 0; --i)
+                            rel *= (1.0 - g.aloss[pbuf[(size_t)i * kSsspBlock + tid]]);
+                    } else {
+                        atomicAdd(&stats[ST_LONGPATH], 1ull);
+                        for (int i = (int)h - 1; i >= 0; --i) {  // edge at depth i from t
+                            uint32_t x = t;
+                            for (int q = 0; q < i; ++q) x = par[x];
+                            rel *= (1.0 - g.aloss[(uint32_t)(memo[x] & 0x7FFFFFFFull)]);
+                        }
+                    }
+                    if (amb) atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
+                    if (lat == 0.0) lat = 1.0;
+                }
+                out_lr[rowbase + k] = make_double2(lat, rel);
+                out_hops[rowbase + k] = (uint16_t)(h > 65535u ? 65535u : h);
+                if (lat >= 0.0) rmin = fmin(rmin, lat);
+            }
+            // row minimum (feeds the runahead, shd-topology.c:500-511)
+            {
+                const unsigned long long m = wave_min_u64(d2bits(rmin));
+                if (tid == 0) L.dmin = kInfBits;
+                __syncthreads();
+                if ((tid & 63) == 0) atomicMin(&L.dmin, m);
+                __syncthreads();
+                if (tid == 0) {
+                    if (out_rowmin) out_rowmin[s_idx] = bits2d(L.dmin);
+                    atomicMin(&stats[ST_GLOBAL_MIN], L.dmin);
+                }
+            }
+            __syncthreads();
+            { unsigned long long t = wall_clock64(); t_tgt += t - tk; tk = t; }
+        }
+    }
+    if (tid == 0) {
+        ctr[0] = iter;
+        ctr[2] = mep;
+        atomicAdd(&stats[ST_RELAX], L.cnt[0]);
+        atomicAdd(&stats[ST_T_INIT], t_init);
+        atomicAdd(&stats[ST_T_SSSP], t_sssp);
+        atomicAdd(&stats[ST_T_PARENT], t_par);
+        atomicAdd(&stats[ST_T_TARGET], t_tgt);
+        atomicAdd(&stats[ST_T_SPLIT], t_split);
+        atomicAdd(&stats[ST_NEAR_IT], n_near);
+        atomicAdd(&stats[ST_SPLITS], n_split + n_scan);
+        atomicAdd(&stats[ST_EV0 + 0], n_expand);
+        atomicAdd(&stats[ST_EV0 + 3], L.cnt[1]);
+        atomicAdd(&stats[ST_EV0 + 4], n_refill);
+        atomicAdd(&stats[ST_EV0 + 5], n_par);
+    }
+}
+
+SsspLdsPlan sssp_batch_lds_plan(int K, int64_t hub_limit, uint32_t par_hubs, int64_t V) {
+    auto bytes = [&](uint32_t H, uint32_t P) -> size_t {
+        switch (K) {
+            case 2: return blayout<2>(H, P).bytes;
+            case 4: return blayout<4>(H, P).bytes;
+            case 8: return blayout<8>(H, P).bytes;
+            case 16: return blayout<16>(H, P).bytes;
+        }
+        return (size_t)-1;
+    };
+    SsspLdsPlan p;
+    if (bytes(0, 0) == (size_t)-1) return p;
+    int64_t H = 0;
+    while (true) {  // largest H (multiple of 16) whose layout fits with P = min(par_hubs, H)
+        const int64_t h2 = H + 16;
+        const uint32_t P2 = (uint32_t)std::min<int64_t>(par_hubs, h2);
+        if (bytes((uint32_t)h2, P2) > kBMaxLds) break;
+        H = h2;
+    }
+    if (hub_limit >= 0 && hub_limit < H) H = hub_limit;
+    if (H > V) H = V;
+    p.H = (uint32_t)H;
+    p.P = (uint32_t)std::min<int64_t>(par_hubs, H);
+    p.bytes = bytes(p.H, p.P);
+    return p;
+}
+
+template <int K>
+static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
+                                 const double* d_srcsh, int nsrc, const uint32_t* d_targets, int A,
+                                 double delta, const SsspLdsPlan& plan, uint32_t far_cap,
+                                 double2* out_lr, uint16_t* out_hops, double* out_rowmin,
+                                 unsigned long long* d_stats, hipStream_t stream) {
+    const int nb = (nsrc + K - 1) / K;
+    const int grid = ws.slots < nb ? ws.slots : nb;
+    if (grid < 1) return hipSuccess;
+    if ((int64_t)plan.H > g.V || plan.P > plan.H || plan.bytes > kBMaxLds ||
+        blayout<K>(plan.H, plan.P).bytes != plan.bytes || ws.K != K)
+        return hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)sssp_batch_kernel<K>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)kBMaxLds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(sssp_batch_kernel<K>, dim3(grid), dim3(kSsspBlock), plan.bytes, stream, g,
+                       ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan.H, plan.P, far_cap,
+                       out_lr, out_hops, out_rowmin, d_stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
+                             const double* d_srcsh, int nsrc, const uint32_t* d_targets, int A,
+                             double delta, const SsspLdsPlan& plan, uint32_t far_cap,
+                             double2* out_lr, uint16_t* out_hops, double* out_rowmin,
+                             unsigned long long* d_stats, hipStream_t stream) {
+    switch (K) {
+        case 2: return launch_batch_k<2>(g, ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 4: return launch_batch_k<4>(g, ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 8: return launch_batch_k<8>(g, ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 16: return launch_batch_k<16>(g, ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace shdtopo

@@ -33,13 +33,16 @@ def test_complete_table_bundled(name):
     assert top.getMinimumLatency() == olat.min()
 
 
+@pytest.mark.parametrize("batch", [1, 8])
 @pytest.mark.parametrize("hubs", [-1, 0, 700])
 @pytest.mark.parametrize("integer", [False, True])
-def test_sssp_synthetic_table(integer, hubs):
-    """SSSP branch: sssp_rows_kernel vs igraph-0.7 Dijkstra + helper restatement.  `hubs` caps
-    the LDS-resident distance words: all (-1: the whole small graph fits), none, or mixed."""
+def test_sssp_synthetic_table(integer, hubs, batch):
+    """SSSP branch: sssp_rows_kernel (batch 1) / sssp_batch_kernel (8 sources per workgroup) vs
+    the igraph-0.7 Dijkstra + helper restatement.  `hubs` caps the LDS-resident distance rows:
+    all (-1: as many as fit), none, or mixed."""
     top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
     top.set_option("lds_hubs", hubs)
+    top.set_option("batch", batch)
     otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()
@@ -73,20 +76,38 @@ def test_sssp_synthetic_table(integer, hubs):
     assert top.getMinimumLatency() == olat.min()
 
 
-@pytest.mark.parametrize("which", ["far", "near"])
+@pytest.mark.parametrize("batch,which", [(1, "far"), (1, "near"), (8, "far")])
 @pytest.mark.parametrize("hubs", [-1, 0])
-def test_sssp_queue_overflow_fallback(hubs, which):
+def test_sssp_queue_overflow_fallback(hubs, which, batch):
     """A far pile / near queue too small for the source: entries are lost, the source switches
     to splits that scan every distance (re-expanding the current bucket after a near-queue
-    loss) with deduplicated pushes, and the table is still bit-exact."""
+    loss) with deduplicated pushes, and the table is still bit-exact.  (The batch kernel's near
+    queue is deduplicated by the source masks and cannot overflow.)"""
     top, g = synthetic_pair(seed=13, n_routers=2500, n_poi=120, n_edges=25000)
     top.set_option("lds_hubs", hubs)
+    top.set_option("batch", batch)
     top.set_option(which + "_cap", 48)
     otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay"])
     a, lat, rel, hops = top.table()
     st = top.stats()
     oa, olat, orel, ohops = g.table(verts)
     assert st["far_scan_sources"] > 0 and st["errors"] == 0
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+
+
+@pytest.mark.parametrize("batch", [2, 4, 16])
+def test_sssp_batch_widths(batch):
+    """Every batch width settles the same table (ragged last batch included: A % K != 0)."""
+    top, g = synthetic_pair(seed=17, n_routers=2000, n_poi=101, n_edges=20000)
+    top.set_option("batch", batch)
+    otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay", "server"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    oa, olat, orel, ohops = g.table(verts)
+    assert len(a) % batch != 0 or batch == 2
+    assert st["errors"] == 0 and st["ambiguous_pairs"] == 0
     assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
     assert np.array_equal(hops, ohops.astype(np.uint16))

@@ -13,6 +13,7 @@ cd "$ROOT/shadow_amd/csrc"
 /opt/rocm/bin/hipcc $FLAGS -x hip -c topo_core.cpp -o "$OUT/obj/core.o" &
 /opt/rocm/bin/hipcc $FLAGS -x hip -c topo_graph.cpp -o "$OUT/obj/graph.o" &
 /opt/rocm/bin/hipcc $FLAGS -c topo_kernels.hip -o "$OUT/obj/kernels.o" &
+/opt/rocm/bin/hipcc $FLAGS -c topo_sssp_batch.hip -o "$OUT/obj/batch.o" &
 wait
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libshdtopo.so" "$OUT"/obj/*.o -lpthread
 echo "$OUT/libshdtopo.so"

@@ -20,5 +20,6 @@ ARGS=("$@")
 run trace --kernel-trace --stats &&
 run fetch --pmc FETCH_SIZE &&
 run write --pmc WRITE_SIZE &&
+run req --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_ATOMIC_sum &&
 run hit --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_sum &&
 run sq --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_VALU SQ_BUSY_CYCLES
