@@ -106,8 +106,6 @@ struct _Topology {
     int64_t hubLimit = -1;  // LDS-cached hub distances (-1 = fill the LDS)
     int64_t parHubs = 2048; // hubs whose parent is hinted during the SSSP (0 = always scan)
     int wgPerCu = 1;        // SSSP workgroups per CU (each owns 1/wgPerCu of the LDS)
-    double ringPerVK = 12.0;  // batch mode: window entries per (vertex, source) per slot, split
-                              // evenly over the 48 buckets (C4 peak: 1.16M in one bucket)
     int batchK = 8;         // sources per SSSP workgroup (1 = sssp_rows_kernel, else
                             // sssp_batch_kernel with K in {2, 4, 8, 16})
     bool events = false;    // per-edge event counters (diagnostic kernel build)
@@ -468,10 +466,8 @@ int batch_k(Topology* top) {
     const int k = top->batchK;
     return (k == 2 || k == 4 || k == 8 || k == 16) ? k : 1;
 }
-int64_t ring_entries(Topology* top, int K) {
-    const int64_t V = top->g.V;
-    if (K <= 1) return (int64_t)kRingPerVertex * V;
-    return std::max<int64_t>(48 * 64, (int64_t)(top->ringPerVK * (double)V * K) / 48 * 48);
+int64_t ring_entries(Topology* top, int K) {  // the batch kernel keeps no bucket window
+    return K <= 1 ? (int64_t)kRingPerVertex * top->g.V : 0;
 }
 int64_t over_entries(Topology* top, int K) {  // the batch kernel keeps no overflow pile
     return K <= 1 ? (int64_t)kOverPerVertex * top->g.V : 0;
@@ -589,7 +585,9 @@ double default_delta(Topology* top) {
     for (int64_t e = 0; e < g.E; e++)
         if (g.eu[(size_t)e] != g.ev[(size_t)e]) { s += g.elat[(size_t)e]; n++; }
     double mean = n ? s / (double)n : 1.0;
-    return std::max(1e-9, 0.06 * mean);  // ~3 ms on the C4 topology (tuned, profiles/)
+    // tuned on C4: single-source 0.06 x mean (~3 ms); the batch kernel gains from
+    // wider buckets (sources of a batch share more expansions) up to 0.2 x mean (~10 ms)
+    return std::max(1e-9, (batch_k(top) > 1 ? 0.2 : 0.06) * mean);
 }
 
 // Enqueue rows [row0,row1) into out buffers (device pointers) on `st`.
@@ -1053,7 +1051,6 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "near_cap") top->nearCap = (int64_t)value;
     else if (k == "events") top->events = value != 0;
     else if (k == "batch") top->batchK = (int)value;
-    else if (k == "ring_per_vk") top->ringPerVK = value;
     else return -1;
     return 0;
 }

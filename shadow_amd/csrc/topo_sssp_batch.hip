@@ -23,11 +23,14 @@
 // Near-phase bookkeeping per vertex: a K-bit mask of the sources that must expand it in the next
 // iteration (double buffered by iteration parity; hubs' masks in LDS).  A vertex enters the next
 // near queue when its mask goes from 0 to non-zero, so the queue is deduplicated (<= V entries)
-// and an expansion serves every source of the mask.  Far improvements are (vertex, source)
-// entries in a 48-bucket window, merged into the masks when their bucket becomes current.
-// Improvements past the window are not stored: they only lower the smallest pending bucket, and
-// when the window is used up one streaming pass over the batch's distances (64 MB at K = 8, ~3
-// per batch) classifies every (vertex, source) into the next window -- no overflow pile.
+// and an expansion serves every source of the mask.
+//
+// Far improvements are not queued at all: they only lower L.fminb, the smallest pending bucket.
+// Each bucket starts with one streaming sweep over the batch's [V][K] rows (16-B loads, 64 MB at
+// K = 8) that classifies every (vertex, source) by its current bucket and builds the bucket's
+// near queue and masks.  With wide buckets (delta ~ 0.2 x mean edge latency, ~25 buckets per
+// batch on C4) the sweeps are cheaper than per-(vertex, source) queue entries, which cost random
+// reads and atomics to merge (measured: DESIGN.md 4).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -50,7 +53,6 @@ using namespace dev;
 #define SHD_BATCH_U 1  // edges per lane in flight (U = 2 spills at S = 8)
 #endif
 constexpr int kBChunk = 256;             // queue vertices per expansion chunk
-constexpr int kBRing = 48;               // buckets in the window (<= 64: one ballot scans them)
 constexpr uint32_t kNoBucket = 0xFFFFFFFFu;
 constexpr size_t kBMaxLds = 160 * 1024;  // LDS of one CU (one batch workgroup per CU)
 
@@ -83,15 +85,12 @@ struct LdsB {
     double val[kBChunk * K];  // the chunk's source distances, [vertex][source]
     double sh[K];             // per-source bucket shift sh_j = C - pi(s_j)
     uint32_t wave[kSsspBlock / 64];
-    uint32_t rtail[kBRing];   // entries pushed into each bucket of the window
     uint32_t qtail;
-    uint32_t beyond;   // an improvement landed past the window since the last refill
     uint32_t idx;      // batch taken by this workgroup
-    uint32_t fover;    // a window slot overflowed: scanning buckets from now on
-    uint32_t ominb;    // lower bound of the buckets past the window
-    uint32_t fminb;    // scanning mode: smallest bucket of the unexpanded far values
+    uint32_t fover;    // a (deduplicated, V-entry) queue overflowed: cannot happen, reported
+    uint32_t fminb;    // smallest bucket of the pending (vertex, source) pairs past cb
     unsigned long long dmin;
-    unsigned long long cnt[2];  // per-batch source-relaxations, window entries taken
+    unsigned long long cnt[2];  // source-relaxations, sweep entries
 };
 
 // Dynamic LDS after the control block: hub masks (two parities), parent-tie bits of the first P
@@ -133,42 +132,16 @@ struct BView {
 
 struct BBuckets {
     double inv_delta;
-    uint32_t cb, wbase;
-    uint32_t* ring;  // kBRing slots of slot_cap (vertex * K + source) entries
-    uint32_t slot_cap;
+    uint32_t cb;  // the bucket being settled
 };
-
-// Window push: lanes may target different slots; one LDS atomic per (wave, slot).
-template <int K>
-__device__ __forceinline__ void ring_push(bool pred, uint32_t slot, uint32_t val,
-                                          const BBuckets& B, LdsB<K>& L) {
-    unsigned long long m = __ballot(pred);
-    const int lane = threadIdx.x & 63;
-    while (m) {
-        const int leader = __ffsll((long long)m) - 1;
-        const uint32_t s = __shfl(slot, leader, 64);
-        const bool mine = pred && slot == s;
-        const unsigned long long mm = __ballot(mine);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&L.rtail[s], (uint32_t)__popcll(mm));
-        base = __shfl(base, leader, 64);
-        if (mine) {
-            const uint32_t pos = base + (uint32_t)__popcll(mm & ((1ull << lane) - 1ull));
-            if (pos < B.slot_cap) B.ring[(size_t)s * B.slot_cap + pos] = val;
-            else atomicOr(&L.fover, 2u);
-        }
-        m &= ~mm;
-    }
-}
 
 // One near iteration over queue Q (vertices; their source masks in mcur/hcur, cleared here).
 // G = K / S lanes per edge, each lane relaxing the edge for S consecutive sources (its S distance
 // words of the target's line are one vector load), U edges per lane in flight: 1024 * U / G edges
 // per pass keep enough requests in flight (the pass is a chain of dependent round trips).
 // Improvements of bucket cb set the target's mask in mnxt/hnxt (the group's bits OR-ed by its
-// first lane, one returning atomic) and push it to qout when the mask was empty; later buckets go
-// to the window as (vertex, source) entries when they move the vertex to an
-// earlier bucket than it had for that source; in scanning mode they only lower L.fminb.
+// first lane, one returning atomic) and push it to qout when the mask was empty; improvements to
+// later buckets only lower L.fminb (the next sweep finds them).
 template <int K, int S, int U>
 __device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, const DevCSR& g,
                                             LdsB<K>& L, const BView<K>& D,
@@ -176,7 +149,7 @@ __device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, cons
                                             typename MaskOps<K>::M* hcur,
                                             typename MaskOps<K>::M* mnxt,
                                             typename MaskOps<K>::M* hnxt, uint32_t* qout,
-                                            uint32_t qcap, const BBuckets& B, bool scan) {
+                                            uint32_t qcap, const BBuckets& B) {
     using MO = MaskOps<K>;
     static_assert(K % S == 0 && (S == 1 || S == 2 || S == 4 || S == 8), "sources per lane");
     constexpr int G = K / S;                  // lanes per edge
@@ -190,7 +163,6 @@ __device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, cons
     double shj[S];
 #pragma unroll
     for (int q = 0; q < S; q++) shj[q] = L.sh[j0 + q];
-    const uint32_t wend = B.wbase + (uint32_t)kBRing;
     for (uint32_t base = 0; base < nq; base += kBChunk) {
         const uint32_t cnt = min((uint32_t)kBChunk, nq - base);
         uint32_t deg = 0;
@@ -265,12 +237,11 @@ __device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, cons
                     cur[u][0] = t ? x : 0ull;
                 }
             }
-            uint32_t imp[U], nb[U];
-            uint32_t bk[U][S];
+            uint32_t nb[U];
+            uint32_t fm = kNoBucket;
             unsigned long long ab[U][S];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                imp[u] = 0u;
                 nb[u] = 0u;
                 const double w = rec_wt(rec[u]);
                 const bool hub = n[u] < D.H;
@@ -278,12 +249,10 @@ __device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, cons
                 for (int q = 0; q < S; q++) {
                     const bool on = (mk[u] >> q) & 1u;
                     ab[u][q] = on ? d2bits(__dadd_rn(L.val[los[u] * K + j0 + q], w)) : ~0ull;
-                    unsigned long long prev = cur[u][q];
                     bool im = false;
                     if (on && hub) {
                         const size_t wi = (size_t)n[u] * K + j0 + q;
                         const unsigned long long old = atomicMin(&D.hd[wi], ab[u][q]);
-                        prev = old;
                         im = ab[u][q] < old;
                         if (n[u] < D.P) {  // parent hint (see the parent pass)
                             if (im) D.hpar[wi] = from[u];
@@ -293,16 +262,13 @@ __device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, cons
                         (void)atomicMin(&D.dist[(size_t)n[u] * K + j0 + q], ab[u][q]);
                         im = true;
                     }
-                    bk[u][q] = kNoBucket;
                     if (im) {
                         const uint32_t b = bkt(bits2d(ab[u][q]), shj[q], B.inv_delta);
                         if (b <= B.cb) nb[u] |= 1u << q;
-                        else if (scan || b < bkt(bits2d(prev), shj[q], B.inv_delta)) bk[u][q] = b;
+                        else fm = b < fm ? b : fm;
                     }
-                    imp[u] |= im ? 1u << q : 0u;
                 }
             }
-            uint32_t om = kNoBucket, fm = kNoBucket;
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 // the group's near bits -> one mask OR by its first lane
@@ -315,27 +281,10 @@ __device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, cons
                     first = old == 0u;
                 }
                 wave_push_t<uint32_t>(first, n[u], qout, &L.qtail, qcap, &L.fover, 1u);
-#pragma unroll
-                for (int q = 0; q < S; q++) {
-                    const uint32_t b = bk[u][q];
-                    const bool far = b != kNoBucket;
-                    if (scan) {
-                        fm = b < fm ? b : fm;
-                        continue;
-                    }
-                    const bool pR = far && b < wend;
-                    if (far && !pR) om = b < om ? b : om;  // past the window: found by the refill
-                    ring_push<K>(pR, b - B.wbase, n[u] * K + j0 + q, B, L);
-                }
             }
-            if (__ballot(om != kNoBucket || fm != kNoBucket)) {
-                om = wave_min_u32(om);
+            if (__ballot(fm != kNoBucket)) {
                 fm = wave_min_u32(fm);
-                if (lane == 0 && om != kNoBucket) {
-                    atomicMin(&L.ominb, om);
-                    L.beyond = 1u;
-                }
-                if (lane == 0 && fm != kNoBucket) atomicMin(&L.fminb, fm);
+                if (lane == 0) atomicMin(&L.fminb, fm);
             }
         }
         // this wave's atomics and queue stores complete before any wave reads them after the
@@ -428,13 +377,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     const uint32_t cap = (uint32_t)V;
     BBuckets B;
     B.inv_delta = 1.0 / delta;
-    B.ring = reinterpret_cast<uint32_t*>(ws.ring) + (size_t)slot * ws.ring_entries;
-    B.slot_cap = (uint32_t)(ws.ring_entries / kBRing);
-    if (far_cap > 0) B.slot_cap = min(B.slot_cap, far_cap);
-    uint32_t* fscr = B.ring;  // parent-pass scratch list (the window is idle by then)
+    (void)far_cap;  // no bounded far structure to overflow (single-source kernel test hook)
+    uint32_t* fscr = qa + 2 * (size_t)V;  // parent-pass scratch list (upper half of qa)
 
     uint32_t iter = ctr[0], mep = ctr[2];
-    unsigned long long n_near = 0, n_split = 0, n_scan = 0, n_expand = 0, n_refill = 0, n_par = 0;
+    unsigned long long n_near = 0, n_sweep = 0, n_expand = 0, n_par = 0;
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, t_split = 0;
     if (tid < 2) L.cnt[tid] = 0;
     unsigned long long tk = wall_clock64();
@@ -456,7 +403,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             reinterpret_cast<uint32_t*>(hmB)[i] = 0u;
         }
         for (uint32_t i = tid; i < tbw; i += kSsspBlock) D.tb[i] = 0u;
-        for (uint32_t i = tid; i < (uint32_t)kBRing; i += kSsspBlock) L.rtail[i] = 0u;
         if (tid < (uint32_t)K) L.sh[tid] = (int)tid < nk ? srcsh[r0 + tid] : 0.0;
         {
             ulonglong2* d2 = reinterpret_cast<ulonglong2*>(D.dist);
@@ -464,41 +410,39 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             for (size_t i = lo + tid; i < hi; i += kSsspBlock) d2[i] = make_ulonglong2(kInfBits, kInfBits);
         }
         if (tid == 0) {
-            L.beyond = 1u;  // the sources: found by the first refill
-            L.ominb = kNoBucket;
             L.fminb = kNoBucket;
             L.fover = 0;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        // every source starts at its own (shifted) bucket, past the empty window
+        // every source starts at its own (shifted) bucket: found by the first sweep
         if ((int)tid < nk) {
             const uint32_t s = sources[r0 + tid];
             if (s < H) D.hd[(size_t)s * K + tid] = 0ull;
             else D.dist[(size_t)s * K + tid] = 0ull;
-            atomicMin(&L.ominb, bkt(0.0, L.sh[tid], B.inv_delta));
+            atomicMin(&L.fminb, bkt(0.0, L.sh[tid], B.inv_delta));
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         { unsigned long long t = wall_clock64(); t_init += t - tk; tk = t; }
 
         // ---------------- lock-step delta-stepping over the shifted buckets -------------------
-        B.cb = L.ominb - 1u;  // ominb >= 1: sh_j >= 2 delta (host)
-        B.wbase = 0;
+        // L.fminb is exact at every bucket change: the sweep sets it to the smallest pending
+        // bucket past the one it opens, and every improvement past cb lowers it.
+        B.cb = 0;
         M* mcur = mA; M* mnxt = mB;
         M* hcur = hmA; M* hnxt = hmB;
         uint32_t* qin = qa; uint32_t* qout = qb;
         uint32_t nq = 0;
         uint32_t guard = 0;
         bool aborted = false;
-        constexpr int FU = 4;
         for (;;) {
             while (nq > 0) {
                 if (tid == 0) L.qtail = 0;
                 __syncthreads();
                 n_expand += nq;
-                relax_batch<K, SHD_BATCH_S < K ? SHD_BATCH_S : K, SHD_BATCH_U>(qin, nq, g, L, D, mcur, hcur, mnxt, hnxt, qout, cap, B,
-                                  L.fover != 0u);
+                relax_batch<K, SHD_BATCH_S < K ? SHD_BATCH_S : K, SHD_BATCH_U>(
+                    qin, nq, g, L, D, mcur, hcur, mnxt, hnxt, qout, cap, B);
                 nq = min(L.qtail, cap);
                 { uint32_t* t = qin; qin = qout; qout = t; }
                 { M* t = mcur; mcur = mnxt; mnxt = t; }
@@ -511,163 +455,77 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 __syncthreads();
             }
             if (aborted) break;
+            const uint32_t nb = L.fminb;
+            if (nb == kNoBucket) break;  // nothing pending: the batch is settled
             const unsigned long long ts0 = wall_clock64();
-            if (L.fover != 0u) {
-                // Scanning mode: a window slot overflowed (entries were lost), so for
-                // the rest of this batch the next bucket is found by classifying every
-                // (vertex, source) distance.  L.fminb is exact after the first scanning pass.
-                const bool exact = (L.fover & 64u) != 0u;
-                const uint32_t fmb = L.fminb;
-                if (exact && fmb == kNoBucket) break;
-                uint32_t nb = B.cb + 1;
-                if (exact) nb = max(nb, fmb);
-                __syncthreads();
-                if (tid == 0) {
-                    L.qtail = 0;
-                    L.fminb = kNoBucket;
-                    L.fover |= 64u;
-                }
-                __syncthreads();
-                for (uint32_t vb = 0; vb < (uint32_t)V; vb += kSsspBlock) {
-                    const uint32_t v = vb + tid;
-                    uint32_t m = 0, km = kNoBucket;
-                    if (v < (uint32_t)V) {
-                        for (int jj = 0; jj < nk; jj++) {
-                            const unsigned long long d = D.get(v, (uint32_t)jj);
-                            if (d == kInfBits) continue;
-                            const uint32_t b = bkt(bits2d(d), L.sh[jj], B.inv_delta);
-                            if (b > B.cb && b <= nb) m |= 1u << jj;
-                            else if (b > nb && b < km) km = b;
-                        }
-                        if (m) {
-                            if (v < H) hcur[v] = (M)m;
-                            else mcur[v] = (M)m;
-                        }
-                    }
-                    wave_push_t<uint32_t>(m != 0u, v, qin, &L.qtail, cap, &L.fover, 32u);
-                    km = wave_min_u32(km);
-                    if ((tid & 63) == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                nq = min(L.qtail, cap);
-                B.cb = nb;
-                n_scan++;
-                t_split += wall_clock64() - ts0;
-                __syncthreads();
-                continue;
+            // Sweep: classify every (vertex, source) word by its bucket (K / 2 lanes per vertex,
+            // 16 B each); the pairs of bucket nb form the near queue with their masks in mcur /
+            // hcur (all zero here), the smallest bucket past nb becomes L.fminb.
+            __syncthreads();
+            if (tid == 0) {
+                L.qtail = 0;
+                L.fminb = kNoBucket;
             }
-            // next non-empty bucket of the window after cb (every wave scans the slot tails)
-            int s = -1;
+            __syncthreads();
             {
-                const int lane = (int)(tid & 63);
-                const int lo_slot = (int)B.cb - (int)B.wbase + 1;
-                const bool ne = lane < kBRing && lane >= lo_slot && L.rtail[lane] > 0u;
-                const unsigned long long m = __ballot(ne);
-                s = m ? __ffsll((long long)m) - 1 : -1;
-            }
-            if (s >= 0) {
-                // merge the slot's (vertex, source) entries into the masks: a vertex enters the
-                // near queue once, with every source whose entry is not stale
-                const uint32_t n = min(L.rtail[s], B.slot_cap);
-                if (tid == 0) atomicMax(&stats[ST_EV0 + 2], (unsigned long long)L.rtail[s]);
-                __syncthreads();
-                if (tid == 0) {
-                    L.rtail[s] = 0u;
-                    L.qtail = 0u;
-                }
-                B.cb = B.wbase + (uint32_t)s;
-                __syncthreads();
-                const uint32_t* ent = B.ring + (size_t)s * B.slot_cap;
-                for (uint32_t ib = 0; ib < n; ib += kSsspBlock * FU) {
-                    uint32_t v[FU], jj[FU];
-                    unsigned long long d[FU];
+                static_assert(K >= 2 && 64 % (K / 2) == 0, "lanes per vertex");
+                constexpr uint32_t LPV = K / 2;
+                const size_t npair = (size_t)V * K / 2;
+                const size_t hpair = (size_t)H * K / 2;
+                constexpr int SU = 4;  // 16-B loads in flight per lane
+                for (size_t ib = 0; ib < npair; ib += (size_t)kSsspBlock * SU) {
+                    unsigned long long d[SU][2];
 #pragma unroll
-                    for (int u = 0; u < FU; u++) {
-                        const uint32_t i = ib + (uint32_t)u * kSsspBlock + tid;
-                        const uint32_t x = i < n ? ent[i] : 0u;
-                        v[u] = x / K;
-                        jj[u] = x % K;
-                    }
-#pragma unroll
-                    for (int u = 0; u < FU; u++) d[u] = D.get(v[u], jj[u]);
-#pragma unroll
-                    for (int u = 0; u < FU; u++) {
-                        const uint32_t i = ib + (uint32_t)u * kSsspBlock + tid;
-                        bool first = false;
-                        if (i < n && bkt(bits2d(d[u]), L.sh[jj[u]], B.inv_delta) >= B.cb) {
-                            const uint32_t old = v[u] < H ? MO::set(hcur, v[u], 1u << jj[u])
-                                                          : MO::set(mcur, v[u], 1u << jj[u]);
-                            first = old == 0u;
-                        }
-                        wave_push_t<uint32_t>(first, v[u], qin, &L.qtail, cap, &L.fover, 16u);
-                    }
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                nq = min(L.qtail, cap);
-                if (tid == 0) L.cnt[1] += n;
-                n_split++;
-                t_split += wall_clock64() - ts0;
-                __syncthreads();
-                continue;
-            }
-            // window used up: refill it by one streaming pass over the batch's distances (or the
-            // batch is done).  No pending (vertex, source) lies in (cb, wb): the window's slots are
-            // empty and every improvement past it lowered ominb.
-            if (L.beyond == 0u) break;
-            {
-                const uint32_t wb = max(B.cb + 1, L.ominb);
-                const uint32_t we = wb + (uint32_t)kBRing;
-                __syncthreads();
-                if (tid == 0) {
-                    L.beyond = 0u;
-                    L.ominb = kNoBucket;
-                }
-                __syncthreads();
-                BBuckets R = B;
-                R.wbase = wb;
-                const size_t npair = (size_t)V * K / 2;  // two (vertex, source) words per lane
-                for (size_t ib = 0; ib < npair; ib += kSsspBlock) {
-                    const size_t i = ib + tid;
-                    unsigned long long d[2] = {kInfBits, kInfBits};
-                    if (i < npair) {
-                        if (2 * i < (size_t)H * K) {
-                            d[0] = D.hd[2 * i];
-                            d[1] = D.hd[2 * i + 1];
-                        } else {
+                    for (int u = 0; u < SU; u++) {
+                        const size_t i = ib + (size_t)u * kSsspBlock + tid;
+                        d[u][0] = d[u][1] = kInfBits;
+                        if (i < hpair) {
+                            d[u][0] = D.hd[2 * i];
+                            d[u][1] = D.hd[2 * i + 1];
+                        } else if (i < npair) {
                             // L1-bypassing 16-B load: the words were lowered by atomics
                             typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
                             const u64x2 x = __builtin_nontemporal_load(
                                 reinterpret_cast<const u64x2*>(D.dist) + i);
-                            d[0] = x.x;
-                            d[1] = x.y;
+                            d[u][0] = x.x;
+                            d[u][1] = x.y;
                         }
                     }
-                    uint32_t k2 = kNoBucket;
+                    uint32_t km = kNoBucket;
 #pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const uint32_t x = (uint32_t)(2 * i + h);
-                        const uint32_t b = d[h] == kInfBits ? kNoBucket
-                                                            : bkt(bits2d(d[h]), L.sh[x % K], B.inv_delta);
-                        const bool mv = b >= wb && b < we;
-                        if (b >= we && b != kNoBucket) k2 = b < k2 ? b : k2;
-                        ring_push<K>(mv, b - wb, x, R, L);
+                    for (int u = 0; u < SU; u++) {
+                        const size_t i = ib + (size_t)u * kSsspBlock + tid;
+                        const uint32_t jl = (uint32_t)((2 * i) % K);
+                        uint32_t m = 0;
+#pragma unroll
+                        for (int h = 0; h < 2; h++) {
+                            if (d[u][h] == kInfBits) continue;
+                            const uint32_t b = bkt(bits2d(d[u][h]), L.sh[jl + h], B.inv_delta);
+                            if (b == nb) m |= 1u << (jl + h);
+                            else if (b > nb && b < km) km = b;
+                        }
+#pragma unroll
+                        for (uint32_t o = 1; o < LPV; o <<= 1) m |= __shfl_xor(m, (int)o, 64);
+                        const uint32_t v = (uint32_t)(2 * i / K);
+                        const bool lead = (tid % LPV) == 0 && m != 0u && i < npair;
+                        if (lead) {
+                            if (v < H) hcur[v] = (M)m;
+                            else mcur[v] = (M)m;
+                        }
+                        wave_push_t<uint32_t>(lead, v, qin, &L.qtail, cap, &L.fover, 32u);
                     }
-                    k2 = wave_min_u32(k2);
-                    if ((tid & 63) == 0 && k2 != kNoBucket) {
-                        atomicMin(&L.ominb, k2);
-                        L.beyond = 1u;
-                    }
+                    km = wave_min_u32(km);
+                    if ((tid & 63) == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                n_refill++;
-                B.wbase = wb;
-                B.cb = wb - 1;
-                nq = 0;
-                t_split += wall_clock64() - ts0;
             }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            nq = min(L.qtail, cap);
+            if (tid == 0) L.cnt[1] += nq;
+            B.cb = nb;
+            n_sweep++;
+            t_split += wall_clock64() - ts0;
+            __syncthreads();
         }
         if (aborted) {
             // iteration guard: leave the masks clean for the next batch and report
@@ -931,10 +789,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         atomicAdd(&stats[ST_T_TARGET], t_tgt);
         atomicAdd(&stats[ST_T_SPLIT], t_split);
         atomicAdd(&stats[ST_NEAR_IT], n_near);
-        atomicAdd(&stats[ST_SPLITS], n_split + n_scan);
+        atomicAdd(&stats[ST_SPLITS], n_sweep);
         atomicAdd(&stats[ST_EV0 + 0], n_expand);
         atomicAdd(&stats[ST_EV0 + 3], L.cnt[1]);
-        atomicAdd(&stats[ST_EV0 + 4], n_refill);
         atomicAdd(&stats[ST_EV0 + 5], n_par);
     }
 }
