@@ -46,13 +46,22 @@ namespace {
 
 using namespace dev;
 
+#ifndef SHD_BATCH_T
+#define SHD_BATCH_T 1  // transposed relaxation (relax_batch_t); 0 = lane-per-edge relax_batch
+#endif
+#ifndef SHD_BATCH_RB
+#define SHD_BATCH_RB 8  // transposed relaxation: rounds whose loads are in flight together
+#endif
 #ifndef SHD_BATCH_S
 #define SHD_BATCH_S 8  // sources per lane in the relaxation (lanes per edge = K / S)
 #endif
 #ifndef SHD_BATCH_U
-#define SHD_BATCH_U 1  // edges per lane in flight (U = 2 spills at S = 8)
+#define SHD_BATCH_U 2  // phase-A edges per lane (lane-per-edge relax_batch: 1, U = 2 spills)
 #endif
-constexpr int kBChunk = 256;             // queue vertices per expansion chunk
+#ifndef SHD_BATCH_CHUNK
+#define SHD_BATCH_CHUNK 512
+#endif
+constexpr int kBChunk = SHD_BATCH_CHUNK;  // queue vertices per expansion chunk (<= kSsspBlock)
 constexpr uint32_t kNoBucket = 0xFFFFFFFFu;
 constexpr size_t kBMaxLds = 160 * 1024;  // LDS of one CU (one batch workgroup per CU)
 
@@ -90,7 +99,7 @@ struct LdsB {
     uint32_t fover;    // a (deduplicated, V-entry) queue overflowed: cannot happen, reported
     uint32_t fminb;    // smallest bucket of the pending (vertex, source) pairs past cb
     unsigned long long dmin;
-    unsigned long long cnt[2];  // source-relaxations, sweep entries
+    unsigned long long cnt[4];  // source-relaxations, sweep entries, edges, chunk-setup ticks
 };
 
 // Dynamic LDS after the control block: hub masks (two parities), parent-tie bits of the first P
@@ -135,6 +144,65 @@ struct BBuckets {
     uint32_t cb;  // the bucket being settled
 };
 
+// One chunk of a near queue: take each vertex's source mask (clearing it), its row bounds and
+// its K distances (K lanes per vertex read its line once) into LDS; a block scan of the degrees
+// flattens the chunk's edges.  Returns the chunk's edge count (uniform); ends with a barrier.
+template <int K>
+__device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, const DevCSR& g,
+                                               LdsB<K>& L, const BView<K>& D,
+                                               typename MaskOps<K>::M* mcur,
+                                               typename MaskOps<K>::M* hcur) {
+    using MO = MaskOps<K>;
+    const uint32_t tid = threadIdx.x;
+    const unsigned long long t0 = wall_clock64();
+    uint32_t deg = 0;
+    unsigned long long act = 0;
+    if (tid < cnt) {
+        const uint32_t v = Q[tid];
+        uint32_t m;
+        if (v < D.H) {
+            m = hcur[v];
+            hcur[v] = 0;
+        } else {
+            m = MO::get_l2(mcur, v);
+            mcur[v] = 0;
+        }
+        const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
+        deg = m ? r1 - r0 : 0u;
+        act = (unsigned long long)deg * (unsigned long long)__popc(m);
+        L.rs[tid] = r0;
+        L.vx[tid] = v;
+        L.msk[tid] = m;
+    }
+    uint32_t total;
+    const uint32_t off = block_excl_scan<kSsspBlock>(deg, L.wave, &total);
+    if (tid < cnt) L.off[tid] = off;
+    if (tid == 0) L.off[cnt] = total;
+    act = wave_sum_u64(act);
+    if ((tid & 63) == 0 && act) atomicAdd(&L.cnt[0], act);
+    for (uint32_t i = tid; i < cnt * K; i += kSsspBlock) {
+        const uint32_t vi = i / K, jj = i % K;
+        if ((L.msk[vi] >> jj) & 1u) L.val[i] = bits2d(D.get(L.vx[vi], jj));
+    }
+    __syncthreads();
+    if (tid == 0) {
+        L.cnt[2] += total;
+        L.cnt[3] += wall_clock64() - t0;
+    }
+    return total;
+}
+
+// Edge index e of the chunk -> its vertex slot in the chunk (binary search over L.off).
+template <int K>
+__device__ __forceinline__ int chunk_slot(const LdsB<K>& L, uint32_t cnt, uint32_t e) {
+    int lo = 0, hi = (int)cnt - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (L.off[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
 // One near iteration over queue Q (vertices; their source masks in mcur/hcur, cleared here).
 // G = K / S lanes per edge, each lane relaxing the edge for S consecutive sources (its S distance
 // words of the target's line are one vector load), U edges per lane in flight: 1024 * U / G edges
@@ -165,37 +233,7 @@ __device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, cons
     for (int q = 0; q < S; q++) shj[q] = L.sh[j0 + q];
     for (uint32_t base = 0; base < nq; base += kBChunk) {
         const uint32_t cnt = min((uint32_t)kBChunk, nq - base);
-        uint32_t deg = 0;
-        unsigned long long act = 0;
-        if (tid < cnt) {
-            const uint32_t v = Q[base + tid];
-            uint32_t m;
-            if (v < D.H) {
-                m = hcur[v];
-                hcur[v] = 0;
-            } else {
-                m = MO::get_l2(mcur, v);
-                mcur[v] = 0;
-            }
-            const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
-            deg = m ? r1 - r0 : 0u;
-            act = (unsigned long long)deg * (unsigned long long)__popc(m);
-            L.rs[tid] = r0;
-            L.vx[tid] = v;
-            L.msk[tid] = m;
-        }
-        uint32_t total;
-        const uint32_t off = block_excl_scan<kSsspBlock>(deg, L.wave, &total);
-        if (tid < cnt) L.off[tid] = off;
-        if (tid == 0) L.off[cnt] = total;
-        act = wave_sum_u64(act);
-        if (lane == 0 && act) atomicAdd(&L.cnt[0], act);
-        // the chunk's source distances: K lanes per vertex read its line once
-        for (uint32_t i = tid; i < cnt * K; i += kSsspBlock) {
-            const uint32_t vi = i / K, jj = i % K;
-            if ((L.msk[vi] >> jj) & 1u) L.val[i] = bits2d(D.get(L.vx[vi], jj));
-        }
-        __syncthreads();
+        const uint32_t total = load_chunk<K>(Q + base, cnt, g, L, D, mcur, hcur);
         for (uint32_t eb = 0; eb < total; eb += NG * U) {
             uint32_t n[U], from[U], mk[U];
             int los[U];
@@ -204,14 +242,7 @@ __device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, cons
             for (int u = 0; u < U; u++) {  // U searches, U record loads in flight
                 const uint32_t e = eb + (uint32_t)u * NG + grp;
                 const bool valid = e < total;
-                int lo = 0;
-                if (valid) {
-                    int hi = (int)cnt - 1;
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (L.off[mid] <= e) lo = mid; else hi = mid - 1;
-                    }
-                }
+                const int lo = valid ? chunk_slot<K>(L, cnt, e) : 0;
                 const uint32_t jr = valid ? L.rs[lo] + (e - L.off[lo]) : 0u;
                 rec[u] = *reinterpret_cast<const W3*>(g.adj + 3ull * jr);
                 mk[u] = valid ? (L.msk[lo] >> j0) & SM : 0u;
@@ -281,6 +312,121 @@ __device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, cons
                     first = old == 0u;
                 }
                 wave_push_t<uint32_t>(first, n[u], qout, &L.qtail, qcap, &L.fover, 1u);
+            }
+            if (__ballot(fm != kNoBucket)) {
+                fm = wave_min_u32(fm);
+                if (lane == 0) atomicMin(&L.fminb, fm);
+            }
+        }
+        // this wave's atomics and queue stores complete before any wave reads them after the
+        // barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+}
+
+// Transposed near iteration (default): phase A takes one edge per lane (UA per lane in flight:
+// row search + 12-B record load done once per edge, not once per source); phase B shuffles the
+// edges of a wave so that K consecutive lanes hold one edge, lane j = source j, for UA * K rounds.
+// The K lanes' pre-check loads and atomics then hit ONE 64-B line per edge in one instruction
+// (coalesced: one DRAM request instead of up to K), and every lane keeps UA * K loads in flight.
+template <int K, int UA>
+__device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, const DevCSR& g,
+                                              LdsB<K>& L, const BView<K>& D,
+                                              typename MaskOps<K>::M* mcur,
+                                              typename MaskOps<K>::M* hcur,
+                                              typename MaskOps<K>::M* mnxt,
+                                              typename MaskOps<K>::M* hnxt, uint32_t* qout,
+                                              uint32_t qcap, const BBuckets& B) {
+    using MO = MaskOps<K>;
+    static_assert(64 % K == 0, "a wave holds whole edge groups");
+    constexpr int EPW = 64 / K;          // edges per wave per round
+    constexpr int R = UA * K;            // rounds: the wave's 64 * UA edges, EPW at a time
+    constexpr int RB = R < SHD_BATCH_RB ? R : SHD_BATCH_RB;
+    static_assert(R % RB == 0, "rounds per load batch");
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    const uint32_t j = lane % K;         // phase B: this lane's source
+    const uint32_t ge = lane / K;        // phase B: this lane's edge within the round
+    const uint32_t wv = tid >> 6;
+    const double shj = L.sh[j];
+    for (uint32_t base = 0; base < nq; base += kBChunk) {
+        const uint32_t cnt = min((uint32_t)kBChunk, nq - base);
+        const uint32_t total = load_chunk<K>(Q + base, cnt, g, L, D, mcur, hcur);
+        for (uint32_t eb = 0; eb < total; eb += (uint32_t)kSsspBlock * UA) {
+            // phase A: edge e = eb + a * 1024 + wv * 64 + lane
+            uint32_t an[UA], amk[UA], alo[UA], awl[UA], awh[UA];
+#pragma unroll
+            for (int a = 0; a < UA; a++) {
+                const uint32_t e = eb + (uint32_t)a * kSsspBlock + wv * 64 + lane;
+                const bool valid = e < total;
+                const int lo = valid ? chunk_slot<K>(L, cnt, e) : 0;
+                const uint32_t jr = valid ? L.rs[lo] + (e - L.off[lo]) : 0u;
+                const W3 r = *reinterpret_cast<const W3*>(g.adj + 3ull * jr);
+                an[a] = r.a;
+                awl[a] = r.b;
+                awh[a] = r.c;
+                amk[a] = valid ? L.msk[lo] : 0u;
+                alo[a] = (uint32_t)lo;
+            }
+            // phase B: round r holds edges r * EPW .. r * EPW + EPW - 1 of the wave's 64 * UA;
+            // RB rounds at a time have their loads in flight
+            uint32_t fm = kNoBucket;
+#pragma unroll
+            for (int r0 = 0; r0 < R; r0 += RB) {
+            uint32_t n[RB], lo[RB];
+            unsigned long long ab[RB], cur[RB];  // ab = ~0: source inactive on this edge
+#pragma unroll
+            for (int rr = 0; rr < RB; rr++) {
+                const int r = r0 + rr;
+                const int a = (r * EPW) / 64;              // phase-A slot of this round's edges
+                const int src = (r * EPW) % 64 + (int)ge;  // lane holding the edge
+                // (shuffles only in uniform control flow: inactive source lanes read as 0)
+                n[rr] = __shfl(an[a], src, 64);
+                const uint32_t mk = __shfl(amk[a], src, 64);
+                lo[rr] = __shfl(alo[a], src, 64);
+                const double w = __hiloint2double((int)__shfl(awh[a], src, 64),
+                                                  (int)__shfl(awl[a], src, 64));
+                const bool on = (mk >> j) & 1u;
+                ab[rr] = on ? d2bits(__dadd_rn(L.val[lo[rr] * K + j], w)) : ~0ull;
+                // pre-check: the K lanes of the edge read its target's line in one request
+                const bool t = on && n[rr] >= D.H;
+                const unsigned long long x = D.dist[(t ? (size_t)n[rr] : (size_t)0) * K + j];
+                cur[rr] = t ? x : 0ull;
+            }
+#pragma unroll
+            for (int rr = 0; rr < RB; rr++) {
+                bool im = false;
+                const bool on = ab[rr] != ~0ull;
+                if (on && n[rr] < D.H) {
+                    const size_t wi = (size_t)n[rr] * K + j;
+                    const unsigned long long old = atomicMin(&D.hd[wi], ab[rr]);
+                    im = ab[rr] < old;
+                    if (n[rr] < D.P) {  // parent hint (see the parent pass)
+                        if (im) D.hpar[wi] = L.vx[lo[rr]];
+                        else if (ab[rr] == old) atomicOr(&D.tb[wi >> 5], 1u << (wi & 31));
+                    }
+                } else if (on && ab[rr] < cur[rr]) {
+                    // the edge's K lanes: one coalesced no-return atomic request per line
+                    (void)atomicMin(&D.dist[(size_t)n[rr] * K + j], ab[rr]);
+                    im = true;
+                }
+                bool nr = false;
+                if (im) {
+                    const uint32_t b = bkt(bits2d(ab[rr]), shj, B.inv_delta);
+                    if (b <= B.cb) nr = true;
+                    else fm = b < fm ? b : fm;
+                }
+                // the edge's near bits -> one mask OR by its first lane
+                const unsigned long long bal = __ballot(nr);
+                const uint32_t gm = (uint32_t)(bal >> (ge * K)) & MO::kFull;
+                bool first = false;
+                if (j == 0 && gm) {
+                    const uint32_t old = n[rr] < D.H ? MO::set(hnxt, n[rr], gm) : MO::set(mnxt, n[rr], gm);
+                    first = old == 0u;
+                }
+                wave_push_t<uint32_t>(first, n[rr], qout, &L.qtail, qcap, &L.fover, 1u);
+            }
             }
             if (__ballot(fm != kNoBucket)) {
                 fm = wave_min_u32(fm);
@@ -383,7 +529,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     uint32_t iter = ctr[0], mep = ctr[2];
     unsigned long long n_near = 0, n_sweep = 0, n_expand = 0, n_par = 0;
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, t_split = 0;
-    if (tid < 2) L.cnt[tid] = 0;
+    if (tid < 4) L.cnt[tid] = 0;
     unsigned long long tk = wall_clock64();
 
     for (;;) {
@@ -441,8 +587,12 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 if (tid == 0) L.qtail = 0;
                 __syncthreads();
                 n_expand += nq;
+#if SHD_BATCH_T
+                relax_batch_t<K, SHD_BATCH_U>(qin, nq, g, L, D, mcur, hcur, mnxt, hnxt, qout, cap, B);
+#else
                 relax_batch<K, SHD_BATCH_S < K ? SHD_BATCH_S : K, SHD_BATCH_U>(
                     qin, nq, g, L, D, mcur, hcur, mnxt, hnxt, qout, cap, B);
+#endif
                 nq = min(L.qtail, cap);
                 { uint32_t* t = qin; qin = qout; qout = t; }
                 { M* t = mcur; mcur = mnxt; mnxt = t; }
@@ -792,6 +942,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         atomicAdd(&stats[ST_SPLITS], n_sweep);
         atomicAdd(&stats[ST_EV0 + 0], n_expand);
         atomicAdd(&stats[ST_EV0 + 3], L.cnt[1]);
+        atomicAdd(&stats[ST_EV0 + 1], L.cnt[2]);
+        atomicAdd(&stats[ST_EV0 + 6], L.cnt[3]);
         atomicAdd(&stats[ST_EV0 + 5], n_par);
     }
 }
