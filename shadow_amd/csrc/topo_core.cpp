@@ -466,8 +466,12 @@ int batch_k(Topology* top) {
     const int k = top->batchK;
     return (k == 2 || k == 4 || k == 8 || k == 16) ? k : 1;
 }
-int64_t ring_entries(Topology* top, int K) {  // the batch kernel keeps no bucket window
-    return K <= 1 ? (int64_t)kRingPerVertex * top->g.V : 0;
+int64_t ring_entries(Topology* top, int K) {  // batch kernel: the parent pass' pair list
+    return K <= 1 ? (int64_t)kRingPerVertex * top->g.V : (int64_t)top->g.V * (K + 1);
+}
+int64_t queue_stride(Topology* top, int K) {  // u64 per slot of each near queue
+    const int64_t V = top->g.V;
+    return K <= 1 ? (int64_t)kNearPerVertex * V : std::max<int64_t>(kNearPerVertex * V, V * K / 2);
 }
 int64_t over_entries(Topology* top, int K) {  // the batch kernel keeps no overflow pile
     return K <= 1 ? (int64_t)kOverPerVertex * top->g.V : 0;
@@ -489,9 +493,10 @@ int ensure_workspace(Topology* top, int nsrc) {
     const int64_t ringE = ring_entries(top, K);
     const int64_t overE = over_entries(top, K);
     const size_t hparN = K > 1 ? (size_t)std::min<int64_t>(top->parHubs, 1 << 20) * K : 0;
-    // dist (K words/vertex), best/memo 16 B, stamp/cnt/bslot/par 16 B, near queues, window
-    // (u64 entries single-source, u32 batched), overflow piles (2 x 16 B)
-    size_t per_slot = (size_t)V * (8 * (size_t)K + 32 + 16 * kNearPerVertex) +
+    // dist (K words/vertex), per-(vertex, source) best/memo 16 B + stamp/cnt/bslot/par 16 B, near
+    // queues, window (u64 entries single-source, u32 pair list batched), overflow piles
+    const int64_t qs = queue_stride(top, K);
+    size_t per_slot = (size_t)V * (8 * (size_t)K + 32 * (size_t)K) + 16 * (size_t)qs +
                       (size_t)ringE * (K > 1 ? 4 : 8) + (size_t)overE * (K > 1 ? 16 : 32) + maskb + 4 * hparN +
                       (size_t)kMaxHops * kSsspBlock * 4 + 16;
     size_t freeb = 0, totalb = 0;
@@ -509,17 +514,18 @@ int ensure_workspace(Topology* top, int nsrc) {
         top->slots = 0;
     }
     const size_t n = (size_t)want * (size_t)V;
+    const size_t pn = n * (size_t)K;  // per-(vertex, source) arrays
     HIPCHK(top->d_dist.ensure(n * (size_t)K));
-    HIPCHK(top->d_best.ensure(n));
-    HIPCHK(top->d_memo.ensure(n));
-    HIPCHK(top->d_stamp.ensure(n));
-    HIPCHK(top->d_qa.ensure(n * kNearPerVertex));
-    HIPCHK(top->d_qb.ensure(n * kNearPerVertex));
+    HIPCHK(top->d_best.ensure(pn));
+    HIPCHK(top->d_memo.ensure(pn));
+    HIPCHK(top->d_stamp.ensure(pn));
+    HIPCHK(top->d_qa.ensure((size_t)want * (size_t)qs));
+    HIPCHK(top->d_qb.ensure((size_t)want * (size_t)qs));
     HIPCHK(top->d_ring.ensure((size_t)want * (size_t)ringE * (K > 1 ? 4 : 8) / 8));
     HIPCHK(top->d_over.ensure((size_t)want * (size_t)overE * (K > 1 ? 2 : 4)));
-    HIPCHK(top->d_cnt.ensure(n));
-    HIPCHK(top->d_bslot.ensure(n));
-    HIPCHK(top->d_par.ensure(n));
+    HIPCHK(top->d_cnt.ensure(pn));
+    HIPCHK(top->d_bslot.ensure(pn));
+    HIPCHK(top->d_par.ensure(pn));
     HIPCHK(top->d_pathbuf.ensure((size_t)want * kMaxHops * kSsspBlock));
     HIPCHK(top->d_counters.ensure((size_t)want * 4));
     if (K > 1) {
@@ -527,8 +533,8 @@ int ensure_workspace(Topology* top, int nsrc) {
         HIPCHK(top->d_hpar.ensure(std::max<size_t>(1, (size_t)want * hparN)));
         HIPCHK(hipMemsetAsync(top->d_mask.p, 0, (size_t)want * maskb, top->stream));
     }
-    HIPCHK(hipMemsetAsync(top->d_stamp.p, 0, sizeof(uint32_t) * n, top->stream));
-    HIPCHK(hipMemsetAsync(top->d_memo.p, 0, sizeof(unsigned long long) * n, top->stream));
+    HIPCHK(hipMemsetAsync(top->d_stamp.p, 0, sizeof(uint32_t) * pn, top->stream));
+    HIPCHK(hipMemsetAsync(top->d_memo.p, 0, sizeof(unsigned long long) * pn, top->stream));
     HIPCHK(hipMemsetAsync(top->d_counters.p, 0, sizeof(uint32_t) * (size_t)want * 4, top->stream));
     HIPCHK(hipStreamSynchronize(top->stream));
     top->slots = want;
@@ -550,6 +556,7 @@ SlotWs slot_ws(Topology* top) {
     w.counters = top->d_counters.p;
     w.K = top->wsK > 1 ? top->wsK : 1;
     w.ring_entries = top->wsRing;
+    w.q_stride = queue_stride(top, w.K);
     w.over_entries = top->wsOver;
     w.mask = top->d_mask.p;
     w.hpar = top->d_hpar.p;

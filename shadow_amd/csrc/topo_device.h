@@ -84,9 +84,12 @@ struct SlotWs {
     uint32_t* pathbuf = nullptr;         // [slot][kMaxHops][kSsspBlock]
     uint32_t* counters = nullptr;        // [slot][4]: iteration id, (unused), source epoch
     // batched kernel (sssp_batch_kernel, K sources per slot): dist is [V][K] per slot, ring holds
-    // ring_entries u32 (vertex * K + source) entries per slot (no overflow pile: over_entries is
-    // 0); mask = 2 parities of a K-bit mask per vertex; hpar [P][K] parent hints
+    // ring_entries u32 entries per slot (the parent pass' pair list; no overflow pile:
+    // over_entries is 0); qa / qb hold q_stride u64 per slot (near queues, parent pair lists of
+    // V * K u32); stamp/best/cnt/bslot/memo/par are per (vertex, source) pair, V * K per slot;
+    // mask = 2 parities of a K-bit mask per vertex; hpar [P][K] parent hints
     int K = 1;
+    int64_t q_stride = 0;
     int64_t ring_entries = 0;
     int64_t over_entries = 0;
     uint8_t* mask = nullptr;

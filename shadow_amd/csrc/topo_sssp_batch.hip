@@ -96,10 +96,12 @@ struct LdsB {
     uint32_t wave[kSsspBlock / 64];
     uint32_t qtail;
     uint32_t idx;      // batch taken by this workgroup
+    uint32_t src[K];   // the batch's source vertices
     uint32_t fover;    // a (deduplicated, V-entry) queue overflowed: cannot happen, reported
     uint32_t fminb;    // smallest bucket of the pending (vertex, source) pairs past cb
-    unsigned long long dmin;
+    unsigned long long rmin[K];  // per-source row minimum of the batch's table rows
     unsigned long long cnt[4];  // source-relaxations, sweep entries, edges, chunk-setup ticks
+    unsigned long long pt[5];   // parent-pass phase ticks (diagnostic)
 };
 
 // Dynamic LDS after the control block: hub masks (two parities), parent-tie bits of the first P
@@ -151,7 +153,7 @@ template <int K>
 __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, const DevCSR& g,
                                                LdsB<K>& L, const BView<K>& D,
                                                typename MaskOps<K>::M* mcur,
-                                               typename MaskOps<K>::M* hcur) {
+                                               typename MaskOps<K>::M* hcur, bool stats = true) {
     using MO = MaskOps<K>;
     const uint32_t tid = threadIdx.x;
     const unsigned long long t0 = wall_clock64();
@@ -179,13 +181,13 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
     if (tid < cnt) L.off[tid] = off;
     if (tid == 0) L.off[cnt] = total;
     act = wave_sum_u64(act);
-    if ((tid & 63) == 0 && act) atomicAdd(&L.cnt[0], act);
+    if (stats && (tid & 63) == 0 && act) atomicAdd(&L.cnt[0], act);
     for (uint32_t i = tid; i < cnt * K; i += kSsspBlock) {
         const uint32_t vi = i / K, jj = i % K;
         if ((L.msk[vi] >> jj) & 1u) L.val[i] = bits2d(D.get(L.vx[vi], jj));
     }
     __syncthreads();
-    if (tid == 0) {
+    if (stats && tid == 0) {
         L.cnt[2] += total;
         L.cnt[3] += wall_clock64() - t0;
     }
@@ -440,26 +442,23 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
     }
 }
 
-// Plain load-balanced expansion of vertex list Q (parent pass): VF(v, val) decides per vertex,
-// EF(v, val, adjacency slot) handles one edge.
+// Load-balanced expansion of a list of (vertex, source) pairs q = v * K + j (parent pass):
+// VF(q, val) gives the pair's value, EF(q, val, adjacency slot) handles one edge of v's row.
 template <int K, class VF, class EF>
-__device__ __forceinline__ void expand_list(const uint32_t* Q, uint32_t nq, const DevCSR& g,
-                                            LdsB<K>& L, VF&& vf, EF&& ef) {
+__device__ __forceinline__ void expand_pairs(const uint32_t* Q, uint32_t nq, const DevCSR& g,
+                                             LdsB<K>& L, VF&& vf, EF&& ef) {
     const uint32_t tid = threadIdx.x;
     for (uint32_t base = 0; base < nq; base += kBChunk) {
         const uint32_t cnt = min((uint32_t)kBChunk, nq - base);
         uint32_t deg = 0;
         if (tid < cnt) {
-            const uint32_t v = Q[base + tid];
+            const uint32_t q = Q[base + tid];
             double val = 0.0;
-            if (vf(v, val)) {
-                const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
-                deg = r1 - r0;
-                L.rs[tid] = r0;
-            } else {
-                L.rs[tid] = 0;
-            }
-            L.vx[tid] = v;
+            vf(q, val);
+            const uint32_t r0 = g.rowptr[q / K], r1 = g.rowptr[q / K + 1];
+            deg = r1 - r0;
+            L.rs[tid] = r0;
+            L.vx[tid] = q;
             L.val[tid] = val;
         }
         uint32_t total;
@@ -468,11 +467,7 @@ __device__ __forceinline__ void expand_list(const uint32_t* Q, uint32_t nq, cons
         if (tid == 0) L.off[cnt] = total;
         __syncthreads();
         for (uint32_t e = tid; e < total; e += kSsspBlock) {
-            int lo = 0, hi = (int)cnt - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (L.off[mid] <= e) lo = mid; else hi = mid - 1;
-            }
+            const int lo = chunk_slot<K>(L, cnt, e);
             ef(L.vx[lo], L.val[lo], L.rs[lo] + (e - L.off[lo]));
         }
         __syncthreads();
@@ -510,26 +505,32 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     const size_t mbytes = ((size_t)V * sizeof(M) + 255) / 256 * 256;
     M* mA = reinterpret_cast<M*>(ws.mask + (size_t)slot * 2 * mbytes);
     M* mB = reinterpret_cast<M*>(ws.mask + (size_t)slot * 2 * mbytes + mbytes);
-    uint32_t* qa = reinterpret_cast<uint32_t*>(ws.qa + (size_t)slot * kNearPerVertex * V);
-    uint32_t* qb = reinterpret_cast<uint32_t*>(ws.qb + (size_t)slot * kNearPerVertex * V);
-    uint32_t* stamp = ws.stamp + (size_t)slot * V;
-    unsigned long long* best = ws.best + (size_t)slot * V;
-    uint32_t* cntc = ws.cnt + (size_t)slot * V;
-    uint32_t* bslot = ws.bslot + (size_t)slot * V;
-    unsigned long long* memo = ws.memo + (size_t)slot * V;
-    uint32_t* par = ws.par + (size_t)slot * V;
+    uint32_t* qa = reinterpret_cast<uint32_t*>(ws.qa + (size_t)slot * ws.q_stride);
+    uint32_t* qb = reinterpret_cast<uint32_t*>(ws.qb + (size_t)slot * ws.q_stride);
+    // parent-pass state per (vertex, source) pair
+    uint32_t* stamp = ws.stamp + (size_t)slot * V * K;
+    unsigned long long* best = ws.best + (size_t)slot * V * K;
+    uint32_t* cntc = ws.cnt + (size_t)slot * V * K;
+    uint32_t* bslot = ws.bslot + (size_t)slot * V * K;
+    unsigned long long* memo = ws.memo + (size_t)slot * V * K;
+    uint32_t* par = ws.par + (size_t)slot * V * K;
     uint32_t* pbuf = ws.pathbuf + (size_t)slot * kMaxHops * kSsspBlock;
     uint32_t* ctr = ws.counters + (size_t)slot * 4;
     const uint32_t cap = (uint32_t)V;
     BBuckets B;
     B.inv_delta = 1.0 / delta;
     (void)far_cap;  // no bounded far structure to overflow (single-source kernel test hook)
-    uint32_t* fscr = qa + 2 * (size_t)V;  // parent-pass scratch list (upper half of qa)
+    // parent-pass pair lists: qa / qb (pcur / pnxt) and the ring memory (fscr), V * K entries each,
+    // then the merged vertex list
+    uint32_t* fscr = reinterpret_cast<uint32_t*>(ws.ring) + (size_t)slot * ws.ring_entries;
+    uint32_t* vscr = fscr + (size_t)V * K;  // parent-pass vertex list (V entries)
+    const uint32_t pcap = (uint32_t)(V * K);
 
     uint32_t iter = ctr[0], mep = ctr[2];
     unsigned long long n_near = 0, n_sweep = 0, n_expand = 0, n_par = 0;
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, t_split = 0;
     if (tid < 4) L.cnt[tid] = 0;
+    if (tid < 5) L.pt[tid] = 0;
     unsigned long long tk = wall_clock64();
 
     for (;;) {
@@ -690,244 +691,293 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         }
         { unsigned long long t = wall_clock64(); t_sssp += t - tk; tk = t; }
 
-        // ---------------- parents + per-target epilogue, one source at a time -----------------
-        for (int jn = 0; jn < nk; jn++) {
-            const uint32_t j = (uint32_t)jn;
-            const uint32_t src = sources[r0 + jn];
-            const int s_idx = r0 + jn;
-            uint32_t* pcur = qa;
-            uint32_t* pnxt = qb;
-            // parents for the target chains (argmin d[u]): one adjacency pass per
-            // chain level finds min d[u] over the candidates fl(d[u] + w) == d[v] and counts them;
-            // vertices with several candidates get a recount at the minimum
-            mep++;
-            const unsigned long long mtag = (unsigned long long)mep << 32;
-            iter++;
+        // ---------------- parents for the target chains of every source of the batch ---------
+        // One level-synchronous pass over (vertex, source) pairs p = v * K + j (SURVEY.md A.3:
+        // parent(v) = argmin d_j[u] over the candidates fl(d_j[u] + w) == d_j[v]).  A level finds
+        // the min d_j[u] over the candidates of each pair with one adjacency pass and counts them;
+        // pairs with several candidates get a recount at the minimum.  All K sources' chains run
+        // in the same levels, so the pass has K times the parallelism of one source's.
+        if ((int)tid < nk) L.src[tid] = sources[r0 + tid];
+        mep++;
+        const unsigned long long mtag = (unsigned long long)mep << 32;
+        iter++;
+        if (tid == 0) L.qtail = 0;
+        __syncthreads();
+        uint32_t* pcur = qa;
+        uint32_t* pnxt = qb;
+        for (uint32_t ib = 0; ib < (uint32_t)A * (uint32_t)nk; ib += kSsspBlock) {
+            const uint32_t i = ib + tid;
+            bool p = false;
+            uint32_t q = 0;
+            if (i < (uint32_t)A * (uint32_t)nk) {
+                const uint32_t j = i / (uint32_t)A;
+                const uint32_t t = targets[i - j * (uint32_t)A];
+                q = t * K + j;
+                p = (t != L.src[j]) && (atomicExch(&stamp[q], iter) != iter);
+                if (p) { best[q] = kInfBits; cntc[q] = 0; bslot[q] = 0xFFFFFFFFu; }
+            }
+            wave_push_t<uint32_t>(p, q, pcur, &L.qtail, pcap, &L.fover, 128u);
+        }
+        __syncthreads();
+        uint32_t nF = min(L.qtail, pcap);
+        __syncthreads();
+        while (nF > 0) {
+            n_par += nF;
+            unsigned long long tp0 = wall_clock64();
+            // Heavy hubs first: the SSSP recorded which vertex last lowered each of the first P
+            // hubs for source j and whether any relaxation tied its value.  "No tie seen" + "the
+            // recorded u is a candidate" means u is the only candidate: the igraph parent, found
+            // without scanning the hub's row.  Anything else is scanned.
             if (tid == 0) L.qtail = 0;
             __syncthreads();
-            for (uint32_t kb = 0; kb < (uint32_t)A; kb += kSsspBlock) {
-                const uint32_t k = kb + tid;
-                bool p = false;
-                uint32_t t = 0;
-                if (k < (uint32_t)A) {
-                    t = targets[k];
-                    p = (t != src) && (atomicExch(&stamp[t], iter) != iter);
-                    if (p) { best[t] = kInfBits; cntc[t] = 0; bslot[t] = 0xFFFFFFFFu; }
-                }
-                wave_push_t<uint32_t>(p, t, pcur, &L.qtail, cap, &L.fover, 128u);
-            }
-            __syncthreads();
-            uint32_t nF = min(L.qtail, cap);
-            __syncthreads();
-            while (nF > 0) {
-                n_par += nF;
-                // Heavy hubs first: the SSSP recorded which vertex last lowered each of the first
-                // P hubs for source j and whether any relaxation tied its value.  "No tie seen" +
-                // "the recorded u is a candidate" means u is the only candidate: the igraph
-                // parent, found without scanning the hub's row.  Anything else is scanned.
-                if (tid == 0) L.qtail = 0;
-                __syncthreads();
-                for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
-                    const uint32_t i = ib + tid;
-                    bool scan = false;
-                    uint32_t v = 0;
-                    if (i < nF) {
-                        v = pcur[i];
-                        scan = true;
-                        const size_t w = (size_t)v * K + j;
-                        if (g.rows_sorted && v < P && !((D.tb[w >> 5] >> (w & 31)) & 1u)) {
-                            const uint32_t u = D.hpar[w];
-                            if (u < (uint32_t)V) {
-                                uint32_t lo = g.rowptr[u], hi = g.rowptr[u + 1];
-                                while (lo < hi) {  // rows are sorted by neighbour
-                                    const uint32_t mid = (lo + hi) >> 1;
-                                    if (adj_col(g, mid) < v) lo = mid + 1; else hi = mid;
-                                }
-                                if (lo < g.rowptr[u + 1] && adj_col(g, lo) == v) {
-                                    uint32_t c;
-                                    double wt;
-                                    adj_load(g, lo, c, wt);
-                                    if (__dadd_rn(bits2d(D.get(u, j)), wt) == bits2d(D.get(v, j))) {
-                                        memo[v] = mtag | (unsigned long long)lo;
-                                        par[v] = u;
-                                        scan = false;
-                                    }
+            for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
+                const uint32_t i = ib + tid;
+                bool scan = false;
+                uint32_t q = 0;
+                if (i < nF) {
+                    q = pcur[i];
+                    scan = true;
+                    const uint32_t v = q / K, j = q % K;
+                    if (g.rows_sorted && v < P && !((D.tb[q >> 5] >> (q & 31)) & 1u)) {
+                        const uint32_t u = D.hpar[q];
+                        if (u < (uint32_t)V) {
+                            uint32_t lo = g.rowptr[u], hi = g.rowptr[u + 1];
+                            while (lo < hi) {  // rows are sorted by neighbour
+                                const uint32_t mid = (lo + hi) >> 1;
+                                if (adj_col(g, mid) < v) lo = mid + 1; else hi = mid;
+                            }
+                            if (lo < g.rowptr[u + 1] && adj_col(g, lo) == v) {
+                                uint32_t c;
+                                double wt;
+                                adj_load(g, lo, c, wt);
+                                if (__dadd_rn(bits2d(D.get(u, j)), wt) == bits2d(D.get(v, j))) {
+                                    memo[q] = mtag | (unsigned long long)lo;
+                                    par[q] = u;
+                                    scan = false;
                                 }
                             }
                         }
                     }
-                    wave_push_t<uint32_t>(scan, v, fscr, &L.qtail, cap, &L.fover, 128u);
                 }
+                wave_push_t<uint32_t>(scan, q, fscr, &L.qtail, pcap, &L.fover, 128u);
+            }
+            __syncthreads();
+            const uint32_t nS = min(L.qtail, pcap);
+            __syncthreads();
+            if (tid == 0) L.pt[1] += wall_clock64() - tp0;  // hint pass
+            tp0 = wall_clock64();
+            // merge the unresolved pairs by vertex (masks in mA / hmA, zero after the SSSP): a
+            // vertex's row is scanned once for every source whose chain needs it
+            if (tid == 0) L.qtail = 0;
+            __syncthreads();
+            for (uint32_t ib = 0; ib < nS; ib += kSsspBlock) {
+                const uint32_t i = ib + tid;
+                bool first = false;
+                uint32_t v = 0;
+                if (i < nS) {
+                    const uint32_t q = fscr[i];
+                    v = q / K;
+                    first = (v < H ? MO::set(hmA, v, 1u << (q % K)) : MO::set(mA, v, 1u << (q % K))) == 0u;
+                }
+                wave_push_t<uint32_t>(first, v, vscr, &L.qtail, cap, &L.fover, 128u);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const uint32_t nVs = min(L.qtail, cap);
+            __syncthreads();
+            // one pass over the merged rows: a lane per edge reads the neighbour's K distances
+            // (one line) and tests every source of the row's mask
+            for (uint32_t base = 0; base < nVs; base += kBChunk) {
+                const uint32_t cnt = min((uint32_t)kBChunk, nVs - base);
+                const uint32_t total = load_chunk<K>(vscr + base, cnt, g, L, D, mA, hmA, false);
+                for (uint32_t e = tid; e < total; e += kSsspBlock) {
+                    const int lo = chunk_slot<K>(L, cnt, e);
+                    const uint32_t jr = L.rs[lo] + (e - L.off[lo]);
+                    const uint32_t m = L.msk[lo];
+                    uint32_t u;
+                    double wt;
+                    adj_load(g, jr, u, wt);
+                    unsigned long long du[K];
+                    if (u < H) {
+#pragma unroll
+                        for (int q = 0; q < K; q++) du[q] = D.hd[(size_t)u * K + q];
+                    } else {
+                        // L1-bypassing 16-B loads of the line (lowered by atomics of other waves)
+                        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+                        const u64x2* p = reinterpret_cast<const u64x2*>(D.dist + (size_t)u * K);
+#pragma unroll
+                        for (int q = 0; q < K / 2; q++) {
+                            const u64x2 x = __builtin_nontemporal_load(p + q);
+                            du[2 * q] = x.x;
+                            du[2 * q + 1] = x.y;
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < K; q++) {
+                        if (((m >> q) & 1u) && __dadd_rn(bits2d(du[q]), wt) == L.val[lo * K + q]) {
+                            const uint32_t pq = L.vx[lo] * K + (uint32_t)q;
+                            atomicMin(&best[pq], du[q]);
+                            atomicAdd(&cntc[pq], 1u);
+                            atomicMin(&bslot[pq], jr);
+                        }
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
-                const uint32_t nS = min(L.qtail, cap);
-                __syncthreads();
-                expand_list<K>(
-                    fscr, nS, g, L,
-                    [&](uint32_t v, double& val) {
-                        val = bits2d(D.get(v, j));
-                        return true;
-                    },
-                    [&](uint32_t v, double dv, uint32_t jr) {
+            }
+            if (tid == 0) L.pt[2] += wall_clock64() - tp0;  // merged row scans
+            tp0 = wall_clock64();
+            // pairs with several candidates: recount at the minimum
+            if (tid == 0) L.qtail = 0;
+            __syncthreads();
+            for (uint32_t ib = 0; ib < nS; ib += kSsspBlock) {
+                const uint32_t i = ib + tid;
+                bool multi = false;
+                uint32_t q = 0;
+                if (i < nS) {
+                    q = fscr[i];
+                    multi = ld_l2_u32(&cntc[q]) > 1u;
+                    if (multi) {
+                        atomicExch(&cntc[q], 0u);
+                        atomicExch(&bslot[q], 0xFFFFFFFFu);
+                    }
+                }
+                wave_push_t<uint32_t>(multi, q, pnxt, &L.qtail, pcap, &L.fover, 128u);
+            }
+            __syncthreads();
+            const uint32_t nM = min(L.qtail, pcap);
+            __syncthreads();
+            if (nM > 0) {
+                expand_pairs<K>(
+                    pnxt, nM, g, L,
+                    [&](uint32_t q, double& val) { val = bits2d(D.get(q / K, q % K)); },
+                    [&](uint32_t q, double dv, uint32_t jr) {
                         uint32_t u;
                         double wt;
                         adj_load(g, jr, u, wt);
-                        const unsigned long long du = D.get(u, j);
-                        if (__dadd_rn(bits2d(du), wt) == dv) {
-                            atomicMin(&best[v], du);
-                            atomicAdd(&cntc[v], 1u);
-                            atomicMin(&bslot[v], jr);
+                        const unsigned long long du = D.get(u, q % K);
+                        if (__dadd_rn(bits2d(du), wt) == dv && du == ld_l2_u64(&best[q])) {
+                            atomicAdd(&cntc[q], 1u);
+                            atomicMin(&bslot[q], jr);
                         }
                     });
-                if (tid == 0) L.qtail = 0;
-                __syncthreads();
-                for (uint32_t ib = 0; ib < nS; ib += kSsspBlock) {
-                    const uint32_t i = ib + tid;
-                    bool multi = false;
-                    uint32_t v = 0;
-                    if (i < nS) {
-                        v = fscr[i];
-                        multi = ld_l2_u32(&cntc[v]) > 1u;
-                        if (multi) {
-                            atomicExch(&cntc[v], 0u);
-                            atomicExch(&bslot[v], 0xFFFFFFFFu);
-                        }
-                    }
-                    wave_push_t<uint32_t>(multi, v, pnxt, &L.qtail, cap, &L.fover, 128u);
-                }
-                __syncthreads();
-                const uint32_t nM = min(L.qtail, cap);
-                __syncthreads();
-                if (nM > 0) {
-                    expand_list<K>(
-                        pnxt, nM, g, L,
-                        [&](uint32_t v, double& val) {
-                            val = bits2d(D.get(v, j));
-                            return true;
-                        },
-                        [&](uint32_t v, double dv, uint32_t jr) {
-                            uint32_t u;
-                            double wt;
-                            adj_load(g, jr, u, wt);
-                            const unsigned long long du = D.get(u, j);
-                            if (__dadd_rn(bits2d(du), wt) == dv && du == ld_l2_u64(&best[v])) {
-                                atomicAdd(&cntc[v], 1u);
-                                atomicMin(&bslot[v], jr);
-                            }
-                        });
-                }
-                for (uint32_t i = tid; i < nS; i += kSsspBlock) {
-                    const uint32_t v = fscr[i];
-                    const uint32_t jr = ld_l2_u32(&bslot[v]);
-                    const uint32_t c = ld_l2_u32(&cntc[v]);
-                    if (jr == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
-                        atomicAdd(&stats[ST_ERRORS], 1ull);
-                        memo[v] = mtag | 0x7FFFFFFFull;
-                        par[v] = src;
-                    } else {
-                        memo[v] = mtag | (c > 1 ? 0x80000000ull : 0ull) | (unsigned long long)jr;
-                        par[v] = adj_col(g, jr);
-                    }
-                }
-                __syncthreads();
-                iter++;
-                if (tid == 0) L.qtail = 0;
-                __syncthreads();
-                for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
-                    const uint32_t i = ib + tid;
-                    bool p = false;
-                    uint32_t u = 0;
-                    if (i < nF) {
-                        u = par[pcur[i]];
-                        p = (u != src) && ((memo[u] & 0xFFFFFFFF00000000ull) != mtag) &&
-                            (atomicExch(&stamp[u], iter) != iter);
-                        if (p) { best[u] = kInfBits; cntc[u] = 0; bslot[u] = 0xFFFFFFFFu; }
-                    }
-                    wave_push_t<uint32_t>(p, u, pnxt, &L.qtail, cap, &L.fover, 128u);
-                }
-                __syncthreads();
-                nF = min(L.qtail, cap);
-                { uint32_t* t = pcur; pcur = pnxt; pnxt = t; }
-                __syncthreads();
             }
-            { unsigned long long t = wall_clock64(); t_par += t - tk; tk = t; }
-
-            // per-target latency / reliability / hops (shd-topology.c:561-671)
-            double rmin = INFINITY;
-            const size_t rowbase = (size_t)s_idx * (size_t)A;
-            for (uint32_t k = tid; k < (uint32_t)A; k += kSsspBlock) {
-                const uint32_t t = targets[k];
-                double lat, rel;
-                uint32_t h = 0;
-                if (t == src) {
-                    // path [src]: the self loop (n == 1 branch), no destination loss
-                    const double sl = g.selfLat[src];
-                    if (isnan(sl)) {
-                        atomicAdd(&stats[ST_ERRORS], 1ull);
-                        lat = -1.0;
-                        rel = -1.0;
-                    } else {
-                        lat = 0.0 + sl;
-                        rel = 1.0;
-                        rel *= (1.0 - g.vloss[src]);
-                        rel *= (1.0 - g.selfLoss[src]);
-                        h = 1;
-                    }
+            for (uint32_t i = tid; i < nS; i += kSsspBlock) {
+                const uint32_t q = fscr[i];
+                const uint32_t jr = ld_l2_u32(&bslot[q]);
+                const uint32_t c = ld_l2_u32(&cntc[q]);
+                if (jr == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
+                    atomicAdd(&stats[ST_ERRORS], 1ull);
+                    memo[q] = mtag | 0x7FFFFFFFull;
+                    par[q] = L.src[q % K];
                 } else {
-                    lat = bits2d(D.get(t, j));
-                    bool amb = false, bad = false;
-                    uint32_t v = t;
-                    while (v != src) {
-                        const unsigned long long m = memo[v];
-                        if ((m & 0xFFFFFFFF00000000ull) != mtag || (m & 0x7FFFFFFFull) == 0x7FFFFFFFull) {
-                            bad = true;
-                            break;
-                        }
-                        amb |= (m >> 31) & 1ull;
-                        if (h < kMaxHops) pbuf[(size_t)h * kSsspBlock + tid] = (uint32_t)(m & 0x7FFFFFFFull);
-                        h++;
-                        v = par[v];
-                        if (h > (uint32_t)V) { bad = true; break; }
-                    }
-                    rel = 1.0;
-                    rel *= (1.0 - g.vloss[src]);
-                    rel *= (1.0 - g.vloss[t]);
-                    if (bad) {
-                        atomicAdd(&stats[ST_ERRORS], 1ull);
-                        lat = -1.0;
-                        rel = -1.0;
-                    } else if (h <= (uint32_t)kMaxHops) {
-                        for (int i = (int)h - 1; i >= 0; --i)
-                            rel *= (1.0 - g.aloss[pbuf[(size_t)i * kSsspBlock + tid]]);
-                    } else {
-                        atomicAdd(&stats[ST_LONGPATH], 1ull);
-                        for (int i = (int)h - 1; i >= 0; --i) {  // edge at depth i from t
-                            uint32_t x = t;
-                            for (int q = 0; q < i; ++q) x = par[x];
-                            rel *= (1.0 - g.aloss[(uint32_t)(memo[x] & 0x7FFFFFFFull)]);
-                        }
-                    }
-                    if (amb) atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
-                    if (lat == 0.0) lat = 1.0;
-                }
-                out_lr[rowbase + k] = make_double2(lat, rel);
-                out_hops[rowbase + k] = (uint16_t)(h > 65535u ? 65535u : h);
-                if (lat >= 0.0) rmin = fmin(rmin, lat);
-            }
-            // row minimum (feeds the runahead, shd-topology.c:500-511)
-            {
-                const unsigned long long m = wave_min_u64(d2bits(rmin));
-                if (tid == 0) L.dmin = kInfBits;
-                __syncthreads();
-                if ((tid & 63) == 0) atomicMin(&L.dmin, m);
-                __syncthreads();
-                if (tid == 0) {
-                    if (out_rowmin) out_rowmin[s_idx] = bits2d(L.dmin);
-                    atomicMin(&stats[ST_GLOBAL_MIN], L.dmin);
+                    memo[q] = mtag | (c > 1 ? 0x80000000ull : 0ull) | (unsigned long long)jr;
+                    par[q] = adj_col(g, jr);
                 }
             }
             __syncthreads();
-            { unsigned long long t = wall_clock64(); t_tgt += t - tk; tk = t; }
+            if (tid == 0) L.pt[3] += wall_clock64() - tp0;  // recount + finalize
+            tp0 = wall_clock64();
+            iter++;
+            if (tid == 0) L.qtail = 0;
+            __syncthreads();
+            for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
+                const uint32_t i = ib + tid;
+                bool p = false;
+                uint32_t q = 0;
+                if (i < nF) {
+                    const uint32_t qc = pcur[i];
+                    const uint32_t j = qc % K;
+                    const uint32_t u = par[qc];
+                    q = u * K + j;
+                    p = (u != L.src[j]) && ((memo[q] & 0xFFFFFFFF00000000ull) != mtag) &&
+                        (atomicExch(&stamp[q], iter) != iter);
+                    if (p) { best[q] = kInfBits; cntc[q] = 0; bslot[q] = 0xFFFFFFFFu; }
+                }
+                wave_push_t<uint32_t>(p, q, pnxt, &L.qtail, pcap, &L.fover, 128u);
+            }
+            __syncthreads();
+            nF = min(L.qtail, pcap);
+            { uint32_t* t = pcur; pcur = pnxt; pnxt = t; }
+            __syncthreads();
+            if (tid == 0) L.pt[4] += wall_clock64() - tp0;  // next level
         }
+        { unsigned long long t = wall_clock64(); t_par += t - tk; tk = t; }
+
+        // ---------------- per-target latency / reliability / hops (shd-topology.c:561-671) ----
+        // items (source j, target k) of the whole batch; each thread walks its pairs' chains
+        if ((int)tid < K) L.rmin[tid] = kInfBits;
+        __syncthreads();
+        for (uint32_t i = tid; i < (uint32_t)A * (uint32_t)nk; i += kSsspBlock) {
+            const uint32_t j = i / (uint32_t)A;
+            const uint32_t k = i - j * (uint32_t)A;
+            const uint32_t t = targets[k];
+            const uint32_t src = L.src[j];
+            double lat, rel;
+            uint32_t h = 0;
+            if (t == src) {
+                // path [src]: the self loop (n == 1 branch), no destination loss
+                const double sl = g.selfLat[src];
+                if (isnan(sl)) {
+                    atomicAdd(&stats[ST_ERRORS], 1ull);
+                    lat = -1.0;
+                    rel = -1.0;
+                } else {
+                    lat = 0.0 + sl;
+                    rel = 1.0;
+                    rel *= (1.0 - g.vloss[src]);
+                    rel *= (1.0 - g.selfLoss[src]);
+                    h = 1;
+                }
+            } else {
+                lat = bits2d(D.get(t, j));
+                bool amb = false, bad = false;
+                uint32_t v = t;
+                while (v != src) {
+                    const unsigned long long m = memo[v * K + j];
+                    if ((m & 0xFFFFFFFF00000000ull) != mtag || (m & 0x7FFFFFFFull) == 0x7FFFFFFFull) {
+                        bad = true;
+                        break;
+                    }
+                    amb |= (m >> 31) & 1ull;
+                    if (h < kMaxHops) pbuf[(size_t)h * kSsspBlock + tid] = (uint32_t)(m & 0x7FFFFFFFull);
+                    h++;
+                    v = par[v * K + j];
+                    if (h > (uint32_t)V) { bad = true; break; }
+                }
+                rel = 1.0;
+                rel *= (1.0 - g.vloss[src]);
+                rel *= (1.0 - g.vloss[t]);
+                if (bad) {
+                    atomicAdd(&stats[ST_ERRORS], 1ull);
+                    lat = -1.0;
+                    rel = -1.0;
+                } else if (h <= (uint32_t)kMaxHops) {
+                    for (int x = (int)h - 1; x >= 0; --x)
+                        rel *= (1.0 - g.aloss[pbuf[(size_t)x * kSsspBlock + tid]]);
+                } else {
+                    atomicAdd(&stats[ST_LONGPATH], 1ull);
+                    for (int x = (int)h - 1; x >= 0; --x) {  // edge at depth x from t
+                        uint32_t y = t;
+                        for (int z = 0; z < x; ++z) y = par[y * K + j];
+                        rel *= (1.0 - g.aloss[(uint32_t)(memo[y * K + j] & 0x7FFFFFFFull)]);
+                    }
+                }
+                if (amb) atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
+                if (lat == 0.0) lat = 1.0;
+            }
+            const size_t o = (size_t)(r0 + (int)j) * (size_t)A + k;
+            out_lr[o] = make_double2(lat, rel);
+            out_hops[o] = (uint16_t)(h > 65535u ? 65535u : h);
+            if (lat >= 0.0) atomicMin(&L.rmin[j], d2bits(lat));  // row minimum (runahead)
+        }
+        __syncthreads();
+        if ((int)tid < nk) {
+            if (out_rowmin) out_rowmin[r0 + tid] = bits2d(L.rmin[tid]);
+            atomicMin(&stats[ST_GLOBAL_MIN], L.rmin[tid]);  // shd-topology.c:500-511
+        }
+        __syncthreads();
+        { unsigned long long t = wall_clock64(); t_tgt += t - tk; tk = t; }
     }
     if (tid == 0) {
         ctr[0] = iter;
@@ -944,6 +994,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         atomicAdd(&stats[ST_EV0 + 3], L.cnt[1]);
         atomicAdd(&stats[ST_EV0 + 1], L.cnt[2]);
         atomicAdd(&stats[ST_EV0 + 6], L.cnt[3]);
+        atomicAdd(&stats[ST_EV0 + 2], L.pt[1]);
+        atomicAdd(&stats[ST_EV0 + 4], L.pt[2]);
+        atomicAdd(&stats[ST_EV0 + 7], L.pt[3]);
         atomicAdd(&stats[ST_EV0 + 5], n_par);
     }
 }
