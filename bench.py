@@ -85,7 +85,9 @@ def main():
     ap.add_argument("--delta", type=float, default=0.0)
     ap.add_argument("--integer", action="store_true",
                     help="C4-int variant (integer latencies U{1..100}: heavy parent ties)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_sssp_pmc.json"))
+    ap.add_argument("--batch", type=int, default=8,
+                    help="sources per SSSP workgroup (1 = single-source sssp_rows_kernel)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01c_sssp_pmc.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -101,6 +103,7 @@ def main():
     top = sa.Topology.synthetic(seed=SEED, n_routers=args.routers, n_poi=args.poi,
                                 n_edges=args.edges, integer_latency=args.integer)
     top.set_option("device", local)
+    top.set_option("batch", args.batch)
     if args.delta:
         top.set_option("delta", args.delta)
     window0 = 10_000_000  # Shadow's default 10 ms window until the runahead is known
@@ -174,27 +177,36 @@ def main():
     routes_per_s = args.packets / t_window
 
     if rank == 0:
-        # roofline of the dominant kernel (sssp_rows_kernel), algorithmic bytes per source =
+        # roofline of the dominant kernel (the SSSP launch), algorithmic bytes per source =
         # 2E (4 B col + 8 B weight) + V (4 B rowptr + 8 B dist read + 8 B dist write)
         rows = table.r1 - table.r0
         b_src = 24 * E + 20 * V
         k_s = float(np.mean(kernel_ms)) / 1e3
         achieved = rows * b_src / k_s / 1e9
+        K = int(st["batch"])
+        kname = "sssp_batch_kernel<%d>" % K if K > 1 else "sssp_rows_kernel"
+        # the batch kernel's per-bucket sweeps stream the [V][K] rows past the LDS hubs (16-B
+        # loads); FETCH_SIZE counts such wide streaming reads at half (MI355X_MICROARCH.md)
+        sweeps = int(st["far_splits"]) if K > 1 else 0
+        sweep_bytes = sweeps * (V - int(st["lds_hubs"])) * K * 8
         traffic = None
         pmc_note = None
         if os.path.exists(args.pmc_json):
             try:
                 pm = json.load(open(args.pmc_json))
-                if not args.integer and pm.get("config_key") == "C4-%d-%d-%d-rows%d" % (
-                        V, E, A, rows):
+                if not args.integer and pm.get("config_key") == "C4-%d-%d-%d-rows%d-%s" % (
+                        V, E, A, rows, kname):
                     traffic = pm["hbm_bytes_per_launch"]
                     pmc_note = pm.get("source")
             except Exception:
                 traffic = None
         roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS,
                         unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic,
-                        kernel="sssp_rows_kernel", kernel_ms=round(k_s * 1e3, 3),
+                        kernel=kname, kernel_ms=round(k_s * 1e3, 3),
                         units_per_launch=rows, bytes_per_unit=b_src, pmc=pmc_note)
+        sssp = dict(kernel=kname, batch=K, lds_hubs=int(st["lds_hubs"]), sweeps=sweeps,
+                    sweep_bytes=sweep_bytes, slots=st["slots"],
+                    phase_ms_per_source=[round(x / max(1, rows), 3) for x in st["phase_ms"]])
         r_ms = float(np.mean(route_ms))
         route_roof = dict(bound="hbm", kernel="packet_route_kernel", kernel_ms=round(r_ms, 4),
                           achieved=round(n * 53 / (r_ms / 1e3) / 1e9, 1), peak=HBM_PEAK_GBS,
@@ -239,6 +251,7 @@ def main():
             "ms_per_window": round(t_window * 1e3, 4),
             "roofline": roofline,
             "route_roofline": route_roof,
+            "sssp": sssp,
             "cpu_baseline": cpu,
             "runahead_min_latency_ms": gmin,
             "ambiguous_pairs": st["ambiguous_pairs"],

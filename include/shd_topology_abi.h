@@ -169,6 +169,8 @@ typedef struct {
                                  entries skipped (events 1, 2, 6, 7 need option "events") */
     int64_t far_scan_sources; /* sources that overflowed a queue (scanning buckets instead) */
     double split_ms;          /* bucket changes + refills, summed over workgroups (in phase 1) */
+    int64_t batch;            /* sources per SSSP workgroup of the last build (1 = single-source) */
+    int64_t lds_hubs;         /* LDS-resident hub rows of the last SSSP launch */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -34,7 +34,8 @@ class ShdStats(ctypes.Structure):
                 ("sources", i64), ("targets", i64), ("ambiguous_pairs", i64),
                 ("relaxations", i64), ("long_paths", i64), ("errors", i64),
                 ("phase_ms", dbl * 4), ("near_iterations", i64), ("far_splits", i64),
-                ("slots", i64), ("events", i64 * 8), ("far_scan_sources", i64), ("split_ms", dbl)]
+                ("slots", i64), ("events", i64 * 8), ("far_scan_sources", i64), ("split_ms", dbl),
+                ("batch", i64), ("lds_hubs", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):

@@ -668,6 +668,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             const SsspLdsPlan bp = sssp_batch_lds_plan(
                 K, top->hubLimit, (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 20)),
                 top->g.V);
+            top->stats.lds_hubs = bp.H;
             HIPCHK(launch_sssp_batch(K, dev_csr(top), slot_ws(top), top->d_sources.p,
                                      top->d_srcsh.p, (int)rows, top->d_targets.p, (int)A,
                                      delta, bp, (uint32_t)top->farCap, out_lr, out_hops,
@@ -675,6 +676,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             HIPCHK(hipEventRecord(top->ev1, st));
             HIPCHK(hipStreamSynchronize(st));  // sh must outlive the async copy
         } else {
+            top->stats.lds_hubs = lds_plan(top).H;
             HIPCHK(launch_sssp_rows(dev_csr(top), slot_ws(top), top->d_sources.p, (int)rows,
                                     top->d_targets.p, (int)A, default_delta(top), lds_plan(top),
                                     (uint32_t)top->farCap,
@@ -686,6 +688,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         HIPCHK(hipStreamSynchronize(st));
     }
     top->rowsPending = true;
+    top->stats.batch = top->isComplete ? 0 : batch_k(top);
     top->stats.sources = rows;
     top->stats.targets = A;
     return 0;

@@ -19,7 +19,7 @@ def short(name):
     n = name.split("(")[0].replace("shdtopo::", "")
     if n.startswith("void "):
         n = n[5:]
-    return n.split("<")[0] if n.startswith("sssp_rows_kernel") else n
+    return n.split("<")[0] if n.startswith("sssp_rows_kernel") else n.split("(")[0]
 
 
 lines = ["# rocprofv3 summary %s (bench.py, C4/C5, 1 x MI355X)" % tag, ""]
@@ -50,8 +50,9 @@ for k, d in sorted(per.items()):
     for c, v in sorted(d.items()):
         lines.append("* %s = %.6g" % (c, v))
     lines.append("")
-k = "sssp_rows_kernel"
-if k in per:
+ks = [k for k in per if k.startswith("sssp_")]
+if ks:
+    k = ks[0]
     d = per[k]
     n = max(1, len(dur[k]))
     fetch = d.get("FETCH_SIZE", 0.0) * 1024 / n
@@ -59,24 +60,34 @@ if k in per:
     rd = d.get("TCC_EA0_RDREQ_sum", 0.0) / n
     wr = d.get("TCC_EA0_WRREQ_sum", 0.0) / n
     at = d.get("TCC_EA0_ATOMIC_sum", 0.0) / n
-    # config key as bench.py builds it (bench log line)
+    # config key and the batch kernel's streaming sweep bytes as bench.py reports them (its JSON
+    # line in the trace pass' log)
     log = open(os.path.join(src, "trace.log")).read() if os.path.exists(
         os.path.join(src, "trace.log")) else ""
     key = None
+    sweep_bytes = 0
     for line in log.splitlines():
         if line.startswith("{"):
             j = json.loads(line)
             c = j["config"]
-            key = "C4-%d-%d-%d-rows%d" % (c["vertices"], c["edges"], c["sources"],
-                                          j["roofline"]["units_per_launch"])
-    out = dict(config_key=key, hbm_bytes_per_launch=fetch + write,
-               fetch_bytes=fetch, write_bytes=write, rdreq=rd, wrreq=wr, atomic_req=at,
+            key = "C4-%d-%d-%d-rows%d-%s" % (c["vertices"], c["edges"], c["sources"],
+                                             j["roofline"]["units_per_launch"], k)
+            sweep_bytes = j.get("sssp", {}).get("sweep_bytes", 0)
+    # gfx950: FETCH_SIZE counts wide (16 B/lane) streaming reads at half -- the sweeps are such
+    # reads, so their missing half is added back (MI355X_MICROARCH.md, HBM/rocprofv3 section)
+    fetch_c = fetch + sweep_bytes / 2
+    out = dict(config_key=key, kernel=k, hbm_bytes_per_launch=fetch_c + write,
+               fetch_bytes=fetch, fetch_bytes_corrected=fetch_c, sweep_bytes=sweep_bytes,
+               write_bytes=write, rdreq=rd, wrreq=wr, atomic_req=at,
                source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), profiles/%s_summary.md; "
-                      "FETCH_SIZE per the gfx950 formula (64-B random requests are counted at 64 B; "
-                      "wide streaming reads would read 1/2, MI355X_MICROARCH.md)" % tag)
+                      "FETCH_SIZE per the gfx950 formula (64-B random requests counted at 64 B), "
+                      "plus half of the sweeps' streaming bytes (counted at 1/2 on gfx950)" % tag)
     json.dump(out, open(os.path.join(outdir, "%s_sssp_pmc.json" % tag), "w"), indent=1)
-    lines += ["## per-launch HBM traffic of sssp_rows_kernel", "",
-              "* FETCH_SIZE + WRITE_SIZE = %.4g B per launch" % (fetch + write),
+    lines += ["## per-launch HBM traffic of %s" % k, "",
+              "* FETCH_SIZE = %.4g B, + streaming-sweep correction %.4g B = %.4g B" %
+              (fetch, sweep_bytes / 2, fetch_c),
+              "* WRITE_SIZE = %.4g B" % write,
+              "* HBM traffic per launch = %.4g B" % (fetch_c + write),
               "* read requests %.4g, write requests %.4g, atomic requests %.4g per launch" %
               (rd, wr, at), ""]
 open(os.path.join(outdir, "%s_summary.md" % tag), "w").write("\n".join(lines) + "\n")
