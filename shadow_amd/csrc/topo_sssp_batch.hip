@@ -46,17 +46,14 @@ namespace {
 
 using namespace dev;
 
-#ifndef SHD_BATCH_T
-#define SHD_BATCH_T 1  // transposed relaxation (relax_batch_t); 0 = lane-per-edge relax_batch
-#endif
 #ifndef SHD_BATCH_RB
 #define SHD_BATCH_RB 8  // transposed relaxation: rounds whose loads are in flight together
 #endif
-#ifndef SHD_BATCH_S
-#define SHD_BATCH_S 8  // sources per lane in the relaxation (lanes per edge = K / S)
+#ifndef SHD_BATCH_SPEC
+#define SHD_BATCH_SPEC 1  // buckets past cb whose hub sources join a hub expansion speculatively
 #endif
 #ifndef SHD_BATCH_U
-#define SHD_BATCH_U 2  // phase-A edges per lane (lane-per-edge relax_batch: 1, U = 2 spills)
+#define SHD_BATCH_U 2  // phase-A edges per lane
 #endif
 #ifndef SHD_BATCH_CHUNK
 #define SHD_BATCH_CHUNK 512
@@ -93,8 +90,10 @@ struct LdsB {
     uint32_t msk[kBChunk];
     double val[kBChunk * K];  // the chunk's source distances, [vertex][source]
     double sh[K];             // per-source bucket shift sh_j = C - pi(s_j)
+    double invd;              // 1 / delta
     uint32_t wave[kSsspBlock / 64];
     uint32_t qtail;
+    uint32_t htail;    // hubs waiting in the deferred hub list
     uint32_t idx;      // batch taken by this workgroup
     uint32_t src[K];   // the batch's source vertices
     uint32_t fover;    // a (deduplicated, V-entry) queue overflowed: cannot happen, reported
@@ -102,12 +101,15 @@ struct LdsB {
     unsigned long long rmin[K];  // per-source row minimum of the batch's table rows
     unsigned long long cnt[4];  // source-relaxations, sweep entries, edges, chunk-setup ticks
     unsigned long long pt[5];   // parent-pass phase ticks (diagnostic)
+    unsigned long long dg[4];   // diagnostic: hub edges, hub source-relaxations, first-iteration
+                                // edges, first-iteration source-relaxations
 };
 
-// Dynamic LDS after the control block: hub masks (two parities), parent-tie bits of the first P
-// hubs (P*K bits), then the hub distances hd[H][K].
+// Dynamic LDS after the control block: the hubs' (deferred) source masks, parent-tie bits of the
+// first P hubs (P*K bits), "expanded at its current value" bits of every (hub, source), then the
+// hub distances hd[H][K].
 struct BLayout {
-    size_t hmA, hmB, tb, hd, bytes;
+    size_t hdef, tb, xb, hd, bytes;
 };
 template <int K>
 __host__ __device__ inline BLayout blayout(uint32_t H, uint32_t P) {
@@ -115,11 +117,12 @@ __host__ __device__ inline BLayout blayout(uint32_t H, uint32_t P) {
     BLayout l;
     const size_t ctrl = (sizeof(LdsB<K>) + 15) / 16 * 16;
     const size_t mb = ((size_t)H * sizeof(M) + 15) / 16 * 16;
-    l.hmA = ctrl;
-    l.hmB = ctrl + mb;
-    l.tb = ctrl + 2 * mb;
+    l.hdef = ctrl;
+    l.tb = ctrl + mb;
     const size_t tbw = ((size_t)P * K + 31) / 32;
-    l.hd = (l.tb + 4 * tbw + 15) / 16 * 16;
+    l.xb = l.tb + 4 * tbw;
+    const size_t xbw = ((size_t)H * K + 31) / 32;
+    l.hd = (l.xb + 4 * xbw + 15) / 16 * 16;
     l.bytes = l.hd + 8 * (size_t)H * K;
     return l;
 }
@@ -134,6 +137,7 @@ struct BView {
     unsigned long long* hd;    // LDS [H][K]
     unsigned long long* dist;  // HBM [V][K] (rows < H unused while the batch runs)
     uint32_t* tb;              // LDS parent-tie bits of (hub < P, source)
+    uint32_t* xb;              // LDS: (hub, source) expanded at its current distance
     uint32_t* hpar;            // HBM [P][K]: vertex whose relaxation last lowered hub v for j
     uint32_t H, P;
     __device__ __forceinline__ unsigned long long get(uint32_t v, uint32_t j) const {
@@ -153,7 +157,8 @@ template <int K>
 __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, const DevCSR& g,
                                                LdsB<K>& L, const BView<K>& D,
                                                typename MaskOps<K>::M* mcur,
-                                               typename MaskOps<K>::M* hcur, bool stats = true) {
+                                               typename MaskOps<K>::M* hcur, bool stats = true,
+                                               uint32_t spec_to = 0u) {
     using MO = MaskOps<K>;
     const uint32_t tid = threadIdx.x;
     const unsigned long long t0 = wall_clock64();
@@ -165,6 +170,19 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
         if (v < D.H) {
             m = hcur[v];
             hcur[v] = 0;
+            if (spec_to) {
+                // speculative co-expansion: the row also serves every source whose tentative
+                // distance lies in the next buckets (<= spec_to) and has not been expanded yet.
+                // Exact either way: a later improvement clears the source's x bit and queues the
+                // hub again; a final one is never expanded twice (the sweep skips x bits).
+                const uint32_t xw = D.xb[(v * K) >> 5] >> ((v * K) & 31);
+                for (int jj = 0; jj < K; jj++) {
+                    if (((m >> jj) & 1u) || ((xw >> jj) & 1u)) continue;
+                    const unsigned long long d = D.hd[(size_t)v * K + jj];
+                    if (d != kInfBits && bkt(bits2d(d), L.sh[jj], L.invd) <= spec_to) m |= 1u << jj;
+                }
+                if (m) atomicOr(&D.xb[(v * K) >> 5], m << ((v * K) & 31));
+            }
         } else {
             m = MO::get_l2(mcur, v);
             mcur[v] = 0;
@@ -175,6 +193,10 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
         L.rs[tid] = r0;
         L.vx[tid] = v;
         L.msk[tid] = m;
+        if (stats && v < D.H && deg) {
+            atomicAdd(&L.dg[0], (unsigned long long)deg);
+            atomicAdd(&L.dg[1], act);
+        }
     }
     uint32_t total;
     const uint32_t off = block_excl_scan<kSsspBlock>(deg, L.wave, &total);
@@ -205,141 +227,22 @@ __device__ __forceinline__ int chunk_slot(const LdsB<K>& L, uint32_t cnt, uint32
     return lo;
 }
 
-// One near iteration over queue Q (vertices; their source masks in mcur/hcur, cleared here).
-// G = K / S lanes per edge, each lane relaxing the edge for S consecutive sources (its S distance
-// words of the target's line are one vector load), U edges per lane in flight: 1024 * U / G edges
-// per pass keep enough requests in flight (the pass is a chain of dependent round trips).
-// Improvements of bucket cb set the target's mask in mnxt/hnxt (the group's bits OR-ed by its
-// first lane, one returning atomic) and push it to qout when the mask was empty; improvements to
-// later buckets only lower L.fminb (the next sweep finds them).
-template <int K, int S, int U>
-__device__ __forceinline__ void relax_batch(const uint32_t* Q, uint32_t nq, const DevCSR& g,
-                                            LdsB<K>& L, const BView<K>& D,
-                                            typename MaskOps<K>::M* mcur,
-                                            typename MaskOps<K>::M* hcur,
-                                            typename MaskOps<K>::M* mnxt,
-                                            typename MaskOps<K>::M* hnxt, uint32_t* qout,
-                                            uint32_t qcap, const BBuckets& B) {
-    using MO = MaskOps<K>;
-    static_assert(K % S == 0 && (S == 1 || S == 2 || S == 4 || S == 8), "sources per lane");
-    constexpr int G = K / S;                  // lanes per edge
-    constexpr uint32_t NG = kSsspBlock / G;   // edges per workgroup per unrolled step
-    constexpr uint32_t SM = (1u << S) - 1u;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63;
-    const uint32_t sub = tid % G;             // this lane's share of the sources: [j0, j0 + S)
-    const uint32_t j0 = sub * S;
-    const uint32_t grp = tid / G;
-    double shj[S];
-#pragma unroll
-    for (int q = 0; q < S; q++) shj[q] = L.sh[j0 + q];
-    for (uint32_t base = 0; base < nq; base += kBChunk) {
-        const uint32_t cnt = min((uint32_t)kBChunk, nq - base);
-        const uint32_t total = load_chunk<K>(Q + base, cnt, g, L, D, mcur, hcur);
-        for (uint32_t eb = 0; eb < total; eb += NG * U) {
-            uint32_t n[U], from[U], mk[U];
-            int los[U];
-            W3 rec[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {  // U searches, U record loads in flight
-                const uint32_t e = eb + (uint32_t)u * NG + grp;
-                const bool valid = e < total;
-                const int lo = valid ? chunk_slot<K>(L, cnt, e) : 0;
-                const uint32_t jr = valid ? L.rs[lo] + (e - L.off[lo]) : 0u;
-                rec[u] = *reinterpret_cast<const W3*>(g.adj + 3ull * jr);
-                mk[u] = valid ? (L.msk[lo] >> j0) & SM : 0u;
-                from[u] = L.vx[lo];
-                los[u] = lo;
-                n[u] = valid ? rec[u].a : 0u;
-            }
-            // tail pre-check: this lane's S words of the target's line (one vector load)
-            unsigned long long cur[U][S];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const bool t = mk[u] && n[u] >= D.H;
-                const unsigned long long* p = D.dist + (t ? (size_t)n[u] * K : (size_t)0) + j0;
-                if constexpr (S >= 2) {
-#pragma unroll
-                    for (int q = 0; q < S; q += 2) {
-                        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + q);
-                        cur[u][q] = t ? x.x : 0ull;
-                        cur[u][q + 1] = t ? x.y : 0ull;
-                    }
-                } else {
-                    const unsigned long long x = *p;
-                    cur[u][0] = t ? x : 0ull;
-                }
-            }
-            uint32_t nb[U];
-            uint32_t fm = kNoBucket;
-            unsigned long long ab[U][S];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                nb[u] = 0u;
-                const double w = rec_wt(rec[u]);
-                const bool hub = n[u] < D.H;
-#pragma unroll
-                for (int q = 0; q < S; q++) {
-                    const bool on = (mk[u] >> q) & 1u;
-                    ab[u][q] = on ? d2bits(__dadd_rn(L.val[los[u] * K + j0 + q], w)) : ~0ull;
-                    bool im = false;
-                    if (on && hub) {
-                        const size_t wi = (size_t)n[u] * K + j0 + q;
-                        const unsigned long long old = atomicMin(&D.hd[wi], ab[u][q]);
-                        im = ab[u][q] < old;
-                        if (n[u] < D.P) {  // parent hint (see the parent pass)
-                            if (im) D.hpar[wi] = from[u];
-                            else if (ab[u][q] == old) atomicOr(&D.tb[wi >> 5], 1u << (wi & 31));
-                        }
-                    } else if (on && ab[u][q] < cur[u][q]) {
-                        (void)atomicMin(&D.dist[(size_t)n[u] * K + j0 + q], ab[u][q]);
-                        im = true;
-                    }
-                    if (im) {
-                        const uint32_t b = bkt(bits2d(ab[u][q]), shj[q], B.inv_delta);
-                        if (b <= B.cb) nb[u] |= 1u << q;
-                        else fm = b < fm ? b : fm;
-                    }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                // the group's near bits -> one mask OR by its first lane
-                uint32_t gm = nb[u] << j0;
-#pragma unroll
-                for (int o = 1; o < G; o <<= 1) gm |= __shfl_xor(gm, o, 64);
-                bool first = false;
-                if (sub == 0 && gm) {
-                    const uint32_t old = n[u] < D.H ? MO::set(hnxt, n[u], gm) : MO::set(mnxt, n[u], gm);
-                    first = old == 0u;
-                }
-                wave_push_t<uint32_t>(first, n[u], qout, &L.qtail, qcap, &L.fover, 1u);
-            }
-            if (__ballot(fm != kNoBucket)) {
-                fm = wave_min_u32(fm);
-                if (lane == 0) atomicMin(&L.fminb, fm);
-            }
-        }
-        // this wave's atomics and queue stores complete before any wave reads them after the
-        // barrier
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-}
-
 // Transposed near iteration (default): phase A takes one edge per lane (UA per lane in flight:
 // row search + 12-B record load done once per edge, not once per source); phase B shuffles the
 // edges of a wave so that K consecutive lanes hold one edge, lane j = source j, for UA * K rounds.
 // The K lanes' pre-check loads and atomics then hit ONE 64-B line per edge in one instruction
 // (coalesced: one DRAM request instead of up to K), and every lane keeps UA * K loads in flight.
+// Hubs are deferred: a hub improved into bucket cb sets its bit in hdef (one mask per hub, no
+// parity) and joins the hub list hq once; the kernel expands the list only when the tail queue
+// is empty, so one hub expansion serves every source that reached it meanwhile (hub rows are
+// 41 % of the expanded edges; expanded at once they serve 2.3 sources each).
 template <int K, int UA>
 __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, const DevCSR& g,
                                               LdsB<K>& L, const BView<K>& D,
                                               typename MaskOps<K>::M* mcur,
-                                              typename MaskOps<K>::M* hcur,
-                                              typename MaskOps<K>::M* mnxt,
-                                              typename MaskOps<K>::M* hnxt, uint32_t* qout,
-                                              uint32_t qcap, const BBuckets& B) {
+                                              typename MaskOps<K>::M* hdef,
+                                              typename MaskOps<K>::M* mnxt, uint32_t* qout,
+                                              uint32_t qcap, uint32_t* hq, const BBuckets& B) {
     using MO = MaskOps<K>;
     static_assert(64 % K == 0, "a wave holds whole edge groups");
     constexpr int EPW = 64 / K;          // edges per wave per round
@@ -354,7 +257,8 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
     const double shj = L.sh[j];
     for (uint32_t base = 0; base < nq; base += kBChunk) {
         const uint32_t cnt = min((uint32_t)kBChunk, nq - base);
-        const uint32_t total = load_chunk<K>(Q + base, cnt, g, L, D, mcur, hcur);
+        const uint32_t total = load_chunk<K>(Q + base, cnt, g, L, D, mcur, hdef, true,
+                                             B.cb + (uint32_t)SHD_BATCH_SPEC);
         for (uint32_t eb = 0; eb < total; eb += (uint32_t)kSsspBlock * UA) {
             // phase A: edge e = eb + a * 1024 + wv * 64 + lane
             uint32_t an[UA], amk[UA], alo[UA], awl[UA], awh[UA];
@@ -404,6 +308,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     const size_t wi = (size_t)n[rr] * K + j;
                     const unsigned long long old = atomicMin(&D.hd[wi], ab[rr]);
                     im = ab[rr] < old;
+                    if (im) atomicAnd(&D.xb[wi >> 5], ~(1u << (wi & 31)));
                     if (n[rr] < D.P) {  // parent hint (see the parent pass)
                         if (im) D.hpar[wi] = L.vx[lo[rr]];
                         else if (ab[rr] == old) atomicOr(&D.tb[wi >> 5], 1u << (wi & 31));
@@ -422,12 +327,13 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 // the edge's near bits -> one mask OR by its first lane
                 const unsigned long long bal = __ballot(nr);
                 const uint32_t gm = (uint32_t)(bal >> (ge * K)) & MO::kFull;
-                bool first = false;
+                bool first = false, hfirst = false;
                 if (j == 0 && gm) {
-                    const uint32_t old = n[rr] < D.H ? MO::set(hnxt, n[rr], gm) : MO::set(mnxt, n[rr], gm);
-                    first = old == 0u;
+                    if (n[rr] < D.H) hfirst = MO::set(hdef, n[rr], gm) == 0u;
+                    else first = MO::set(mnxt, n[rr], gm) == 0u;
                 }
                 wave_push_t<uint32_t>(first, n[rr], qout, &L.qtail, qcap, &L.fover, 1u);
+                wave_push_t<uint32_t>(hfirst, n[rr], hq, &L.htail, D.H, &L.fover, 1u);
             }
             }
             if (__ballot(fm != kNoBucket)) {
@@ -488,15 +394,16 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     LdsB<K>& L = *reinterpret_cast<LdsB<K>*>(smem);
     const BLayout lay = blayout<K>(H, P);
-    M* hmA = reinterpret_cast<M*>(smem + lay.hmA);
-    M* hmB = reinterpret_cast<M*>(smem + lay.hmB);
-    const uint32_t hmw = (uint32_t)((lay.hmB - lay.hmA) / 4);  // u32 words per hub-mask array
+    M* hdef = reinterpret_cast<M*>(smem + lay.hdef);
+    const uint32_t hmw = (uint32_t)((lay.tb - lay.hdef) / 4);  // u32 words of the hub masks
     const uint32_t tbw = (uint32_t)(((size_t)P * K + 31) / 32);
     const int slot = blockIdx.x;
     const uint32_t tid = threadIdx.x;
     const int64_t V = ws.V;
     BView<K> D;
     D.tb = reinterpret_cast<uint32_t*>(smem + lay.tb);
+    D.xb = reinterpret_cast<uint32_t*>(smem + lay.xb);
+    const uint32_t xbw = (uint32_t)(((size_t)H * K + 31) / 32);
     D.hd = reinterpret_cast<unsigned long long*>(smem + lay.hd);
     D.dist = ws.dist + (size_t)slot * (size_t)V * K;
     D.hpar = ws.hpar + (size_t)slot * (size_t)P * K;
@@ -531,6 +438,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, t_split = 0;
     if (tid < 4) L.cnt[tid] = 0;
     if (tid < 5) L.pt[tid] = 0;
+    if (tid < 4) L.dg[tid] = 0;
     unsigned long long tk = wall_clock64();
 
     for (;;) {
@@ -546,11 +454,12 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // ---------------- init: hubs in LDS, the tail's K-wide rows in HBM --------------------
         for (uint32_t i = tid; i < H * K; i += kSsspBlock) D.hd[i] = kInfBits;
         for (uint32_t i = tid; i < hmw; i += kSsspBlock) {
-            reinterpret_cast<uint32_t*>(hmA)[i] = 0u;
-            reinterpret_cast<uint32_t*>(hmB)[i] = 0u;
+            reinterpret_cast<uint32_t*>(hdef)[i] = 0u;
         }
         for (uint32_t i = tid; i < tbw; i += kSsspBlock) D.tb[i] = 0u;
+        for (uint32_t i = tid; i < xbw; i += kSsspBlock) D.xb[i] = 0u;
         if (tid < (uint32_t)K) L.sh[tid] = (int)tid < nk ? srcsh[r0 + tid] : 0.0;
+        if (tid == 0) L.invd = B.inv_delta;
         {
             ulonglong2* d2 = reinterpret_cast<ulonglong2*>(D.dist);
             const size_t lo = (size_t)H * K / 2, hi = (size_t)V * K / 2;
@@ -578,30 +487,49 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // bucket past the one it opens, and every improvement past cb lowers it.
         B.cb = 0;
         M* mcur = mA; M* mnxt = mB;
-        M* hcur = hmA; M* hnxt = hmB;
         uint32_t* qin = qa; uint32_t* qout = qb;
+        uint32_t* hq[2] = {qa + V, qb + V};  // deferred hub lists (filling / being expanded)
+        int hsel = 0;
         uint32_t nq = 0;
         uint32_t guard = 0;
         bool aborted = false;
+        bool just_swept = false;
+        if (tid == 0) L.htail = 0;
+        __syncthreads();
         for (;;) {
-            while (nq > 0) {
-                if (tid == 0) L.qtail = 0;
+            // near phase of bucket cb: tail iterations until the tail queue is empty, then one
+            // iteration over the deferred hubs, until neither has work
+            for (;;) {
+                const uint32_t nh = L.htail;
+                const bool hubs = nq == 0;
+                if (hubs && nh == 0) break;
+                const uint32_t* src = hubs ? hq[hsel] : qin;
+                const uint32_t ns = hubs ? min(nh, H) : nq;
                 __syncthreads();
-                n_expand += nq;
-#if SHD_BATCH_T
-                relax_batch_t<K, SHD_BATCH_U>(qin, nq, g, L, D, mcur, hcur, mnxt, hnxt, qout, cap, B);
-#else
-                relax_batch<K, SHD_BATCH_S < K ? SHD_BATCH_S : K, SHD_BATCH_U>(
-                    qin, nq, g, L, D, mcur, hcur, mnxt, hnxt, qout, cap, B);
-#endif
+                if (tid == 0) {
+                    L.qtail = 0;
+                    if (hubs) L.htail = 0;
+                }
+                if (hubs) hsel ^= 1;
+                __syncthreads();
+                n_expand += ns;
+                const unsigned long long e0 = L.cnt[2], a0 = L.cnt[0];
+                const bool first_it = guard == 0 || just_swept;
+                relax_batch_t<K, SHD_BATCH_U>(src, ns, g, L, D, mcur, hdef, mnxt, qout, cap,
+                                              hq[hsel], B);
                 nq = min(L.qtail, cap);
+                if (tid == 0 && first_it) {
+                    L.dg[2] += L.cnt[2] - e0;
+                    L.dg[3] += L.cnt[0] - a0;
+                }
+                just_swept = false;
                 { uint32_t* t = qin; qin = qout; qout = t; }
                 { M* t = mcur; mcur = mnxt; mnxt = t; }
-                { M* t = hcur; hcur = hnxt; hnxt = t; }
                 n_near++;
                 if (++guard > 4000000u) {
                     aborted = true;
                     nq = 0;
+                    break;
                 }
                 __syncthreads();
             }
@@ -610,8 +538,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             if (nb == kNoBucket) break;  // nothing pending: the batch is settled
             const unsigned long long ts0 = wall_clock64();
             // Sweep: classify every (vertex, source) word by its bucket (K / 2 lanes per vertex,
-            // 16 B each); the pairs of bucket nb form the near queue with their masks in mcur /
-            // hcur (all zero here), the smallest bucket past nb becomes L.fminb.
+            // 16 B each); the pairs of bucket nb form the near queue with their masks in mcur
+            // (hubs: the deferred list, masks in hdef; all zero here), the smallest bucket past
+            // nb becomes L.fminb.
             __syncthreads();
             if (tid == 0) {
                 L.qtail = 0;
@@ -651,6 +580,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
 #pragma unroll
                         for (int h = 0; h < 2; h++) {
                             if (d[u][h] == kInfBits) continue;
+                            // a hub pair expanded (speculatively) at its current value is done
+                            if (i < hpair && ((D.xb[(2 * i + h) >> 5] >> ((2 * i + h) & 31)) & 1u))
+                                continue;
                             const uint32_t b = bkt(bits2d(d[u][h]), L.sh[jl + h], B.inv_delta);
                             if (b == nb) m |= 1u << (jl + h);
                             else if (b > nb && b < km) km = b;
@@ -660,10 +592,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         const uint32_t v = (uint32_t)(2 * i / K);
                         const bool lead = (tid % LPV) == 0 && m != 0u && i < npair;
                         if (lead) {
-                            if (v < H) hcur[v] = (M)m;
+                            if (v < H) hdef[v] = (M)m;
                             else mcur[v] = (M)m;
                         }
-                        wave_push_t<uint32_t>(lead, v, qin, &L.qtail, cap, &L.fover, 32u);
+                        wave_push_t<uint32_t>(lead && v >= H, v, qin, &L.qtail, cap, &L.fover, 32u);
+                        wave_push_t<uint32_t>(lead && v < H, v, hq[hsel], &L.htail, H, &L.fover, 32u);
                     }
                     km = wave_min_u32(km);
                     if ((tid & 63) == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
@@ -674,6 +607,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             nq = min(L.qtail, cap);
             if (tid == 0) L.cnt[1] += nq;
             B.cb = nb;
+            just_swept = true;
             n_sweep++;
             t_split += wall_clock64() - ts0;
             __syncthreads();
@@ -766,7 +700,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             __syncthreads();
             if (tid == 0) L.pt[1] += wall_clock64() - tp0;  // hint pass
             tp0 = wall_clock64();
-            // merge the unresolved pairs by vertex (masks in mA / hmA, zero after the SSSP): a
+            // merge the unresolved pairs by vertex (masks in mA / hdef, zero after the SSSP): a
             // vertex's row is scanned once for every source whose chain needs it
             if (tid == 0) L.qtail = 0;
             __syncthreads();
@@ -777,7 +711,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 if (i < nS) {
                     const uint32_t q = fscr[i];
                     v = q / K;
-                    first = (v < H ? MO::set(hmA, v, 1u << (q % K)) : MO::set(mA, v, 1u << (q % K))) == 0u;
+                    first = (v < H ? MO::set(hdef, v, 1u << (q % K)) : MO::set(mA, v, 1u << (q % K))) == 0u;
                 }
                 wave_push_t<uint32_t>(first, v, vscr, &L.qtail, cap, &L.fover, 128u);
             }
@@ -789,7 +723,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             // (one line) and tests every source of the row's mask
             for (uint32_t base = 0; base < nVs; base += kBChunk) {
                 const uint32_t cnt = min((uint32_t)kBChunk, nVs - base);
-                const uint32_t total = load_chunk<K>(vscr + base, cnt, g, L, D, mA, hmA, false);
+                const uint32_t total = load_chunk<K>(vscr + base, cnt, g, L, D, mA, hdef, false);
                 for (uint32_t e = tid; e < total; e += kSsspBlock) {
                     const int lo = chunk_slot<K>(L, cnt, e);
                     const uint32_t jr = L.rs[lo] + (e - L.off[lo]);
@@ -994,9 +928,12 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         atomicAdd(&stats[ST_EV0 + 3], L.cnt[1]);
         atomicAdd(&stats[ST_EV0 + 1], L.cnt[2]);
         atomicAdd(&stats[ST_EV0 + 6], L.cnt[3]);
-        atomicAdd(&stats[ST_EV0 + 2], L.pt[1]);
-        atomicAdd(&stats[ST_EV0 + 4], L.pt[2]);
-        atomicAdd(&stats[ST_EV0 + 7], L.pt[3]);
+        atomicAdd(&stats[ST_EV0 + 2], L.dg[0]);
+        atomicAdd(&stats[ST_EV0 + 4], L.dg[1]);
+        atomicAdd(&stats[ST_EV0 + 7], L.dg[2]);
+        atomicAdd(&stats[ST_NEAR_IT + 0], 0ull);
+        atomicAdd(&stats[ST_OVERSITE], 0ull);
+        atomicAdd(&stats[ST_EV0 + 5], 0ull);
         atomicAdd(&stats[ST_EV0 + 5], n_par);
     }
 }
