@@ -75,6 +75,12 @@ struct MaskOps {
         const uint32_t s = (v % kPer) * kBits;
         return (atomicOr(w, bits << s) >> s) & kFull;
     }
+    // atomic read-and-clear of v's mask (hub masks are OR-ed by other waves while they are read)
+    __device__ static __forceinline__ uint32_t take(M* m, uint32_t v) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(m) + v / kPer;
+        const uint32_t s = (v % kPer) * kBits;
+        return (atomicAnd(w, ~(kFull << s)) >> s) & kFull;
+    }
     // HBM mask read that bypasses L1 (the words are written by atomics of other waves)
     __device__ static __forceinline__ uint32_t get_l2(const M* m, uint32_t v) {
         const uint32_t w = ld_l2_u32(reinterpret_cast<const uint32_t*>(m) + v / kPer);
@@ -168,8 +174,7 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
         const uint32_t v = Q[tid];
         uint32_t m;
         if (v < D.H) {
-            m = hcur[v];
-            hcur[v] = 0;
+            m = MO::take(hcur, v);
             if (spec_to) {
                 // speculative co-expansion: the row also serves every source whose tentative
                 // distance lies in the next buckets (<= spec_to) and has not been expanded yet.
@@ -488,8 +493,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         B.cb = 0;
         M* mcur = mA; M* mnxt = mB;
         uint32_t* qin = qa; uint32_t* qout = qb;
-        uint32_t* hq[2] = {qa + V, qb + V};  // deferred hub lists (filling / being expanded)
-        int hsel = 0;
+        uint32_t* hfill = qa + V;  // deferred hub list being filled
+        uint32_t* hdrain = qb + V; // ... and the one being expanded
         uint32_t nq = 0;
         uint32_t guard = 0;
         bool aborted = false;
@@ -503,20 +508,20 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 const uint32_t nh = L.htail;
                 const bool hubs = nq == 0;
                 if (hubs && nh == 0) break;
-                const uint32_t* src = hubs ? hq[hsel] : qin;
+                if (hubs) { uint32_t* t = hfill; hfill = hdrain; hdrain = t; }
+                const uint32_t* src = hubs ? hdrain : qin;
                 const uint32_t ns = hubs ? min(nh, H) : nq;
                 __syncthreads();
                 if (tid == 0) {
                     L.qtail = 0;
                     if (hubs) L.htail = 0;
                 }
-                if (hubs) hsel ^= 1;
                 __syncthreads();
                 n_expand += ns;
                 const unsigned long long e0 = L.cnt[2], a0 = L.cnt[0];
                 const bool first_it = guard == 0 || just_swept;
                 relax_batch_t<K, SHD_BATCH_U>(src, ns, g, L, D, mcur, hdef, mnxt, qout, cap,
-                                              hq[hsel], B);
+                                              hfill, B);
                 nq = min(L.qtail, cap);
                 if (tid == 0 && first_it) {
                     L.dg[2] += L.cnt[2] - e0;
@@ -596,7 +601,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                             else mcur[v] = (M)m;
                         }
                         wave_push_t<uint32_t>(lead && v >= H, v, qin, &L.qtail, cap, &L.fover, 32u);
-                        wave_push_t<uint32_t>(lead && v < H, v, hq[hsel], &L.htail, H, &L.fover, 32u);
+                        wave_push_t<uint32_t>(lead && v < H, v, hfill, &L.htail, H, &L.fover, 32u);
                     }
                     km = wave_min_u32(km);
                     if ((tid & 63) == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
