@@ -467,7 +467,9 @@ int batch_k(Topology* top) {
     return (k == 2 || k == 4 || k == 8 || k == 16) ? k : 1;
 }
 int64_t ring_entries(Topology* top, int K) {  // batch kernel: the parent pass' pair list
-    return K <= 1 ? (int64_t)kRingPerVertex * top->g.V : (int64_t)top->g.V * (K + 1);
+    // batch: V * K pair list + V vertex list (parent pass), then the sweep's pending bitmap
+    return K <= 1 ? (int64_t)kRingPerVertex * top->g.V
+                  : (int64_t)top->g.V * (K + 1) + (top->g.V + 31) / 32 + 64;
 }
 int64_t queue_stride(Topology* top, int K) {  // u64 per slot of each near queue
     const int64_t V = top->g.V;
