@@ -417,22 +417,30 @@ int upload_csr(Topology* top) {
         }
     }
     HIPCHK(top->d_rowptr.ensure((size_t)V + 1));
-    HIPCHK(top->d_adj.ensure(3 * nadj));
+    HIPCHK(top->d_adj.ensure(4 * nadj));
     HIPCHK(top->d_aloss.ensure(nadj));
     HIPCHK(top->d_vloss.ensure((size_t)V));
     HIPCHK(top->d_selfLat.ensure((size_t)V));
     HIPCHK(top->d_selfLoss.ensure((size_t)V));
     HIPCHK(hipMemcpy(top->d_rowptr.p, rowptr.data(), sizeof(uint32_t) * ((size_t)V + 1), hipMemcpyHostToDevice));
     if (nadj) {
-        std::vector<uint32_t> adj(3 * nadj);
+        // 16-B records {col, pi(col) as f32 rounded up, f64 latency} (AdjRec)
+        std::vector<uint32_t> adj(4 * nadj);
         for (size_t k = 0; k < nadj; k++) {
             uint64_t wb;
             memcpy(&wb, &wt[k], 8);
-            adj[3 * k] = col[k];
-            adj[3 * k + 1] = (uint32_t)wb;
-            adj[3 * k + 2] = (uint32_t)(wb >> 32);
+            const double pv = top->pot[col[k]];
+            float pf = (float)pv;
+            if (std::isfinite(pv) && (double)pf < pv) pf = std::nextafter(pf, INFINITY);
+            if (!std::isfinite(pv)) pf = INFINITY;
+            uint32_t pb;
+            memcpy(&pb, &pf, 4);
+            adj[4 * k] = col[k];
+            adj[4 * k + 1] = pb;
+            adj[4 * k + 2] = (uint32_t)wb;
+            adj[4 * k + 3] = (uint32_t)(wb >> 32);
         }
-        HIPCHK(hipMemcpy(top->d_adj.p, adj.data(), sizeof(uint32_t) * 3 * nadj, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_adj.p, adj.data(), sizeof(uint32_t) * 4 * nadj, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_aloss.p, aloss.data(), sizeof(double) * nadj, hipMemcpyHostToDevice));
     }
     HIPCHK(hipMemcpy(top->d_vloss.p, vloss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
@@ -451,7 +459,7 @@ SsspLdsPlan lds_plan(Topology* top) {
 DevCSR dev_csr(Topology* top) {
     DevCSR c;
     c.V = top->g.V;
-    c.nadj = (int64_t)(top->d_adj.n / 3);
+    c.nadj = (int64_t)(top->d_adj.n / 4);
     c.rowptr = top->d_rowptr.p;
     c.adj = top->d_adj.p;
     c.aloss = top->d_aloss.p;
@@ -490,7 +498,7 @@ int ensure_workspace(Topology* top, int nsrc) {
     const int units = K > 1 ? (nsrc + K - 1) / K : nsrc;
     int want = top->slotsOpt > 0 ? top->slotsOpt
                                  : prop.multiProcessorCount *
-                                       (K > 1 ? 1 : sssp_max_blocks_per_cu(top->wgPerCu));
+                                       (K > 1 ? kBatchWgPerCu : sssp_max_blocks_per_cu(top->wgPerCu));
     const size_t maskb = K > 1 ? 2 * (((size_t)V * (K <= 8 ? 1 : 2) + 255) / 256 * 256) : 0;
     const int64_t ringE = ring_entries(top, K);
     const int64_t overE = over_entries(top, K);

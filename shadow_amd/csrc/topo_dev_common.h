@@ -29,17 +29,27 @@ __device__ __forceinline__ unsigned long long d2bits(double d) {
     return (unsigned long long)__double_as_longlong(d);
 }
 
-// adjacency record {u32 col, f64 latency} packed in 12 bytes (one 64-B line per short row)
-struct __attribute__((packed, aligned(4))) W3 {
-    uint32_t a, b, c;
+// adjacency record, 16 B (one aligned 16-B load): a = neighbour (column), p = f32 bits of
+// pi(a) = d(h0, a) rounded up (the landmark bound of the batch kernel's relaxation filter),
+// (b, c) = the f64 edge latency (low, high word)
+struct __attribute__((aligned(16))) AdjRec {
+    uint32_t a, p, b, c;
 };
-__device__ __forceinline__ uint32_t adj_col(const DevCSR& g, uint32_t j) { return g.adj[3ull * j]; }
+constexpr unsigned long long kAdjWords = 4;
+__device__ __forceinline__ uint32_t adj_col(const DevCSR& g, uint32_t j) {
+    return g.adj[kAdjWords * j];
+}
+__device__ __forceinline__ const AdjRec& adj_rec(const DevCSR& g, uint32_t j) {
+    return *reinterpret_cast<const AdjRec*>(g.adj + kAdjWords * j);
+}
 __device__ __forceinline__ void adj_load(const DevCSR& g, uint32_t j, uint32_t& col, double& wt) {
-    const W3 r = *reinterpret_cast<const W3*>(g.adj + 3ull * j);
+    const AdjRec r = adj_rec(g, j);
     col = r.a;
     wt = __hiloint2double((int)r.c, (int)r.b);
 }
-__device__ __forceinline__ double rec_wt(const W3& r) { return __hiloint2double((int)r.c, (int)r.b); }
+__device__ __forceinline__ double rec_wt(const AdjRec& r) {
+    return __hiloint2double((int)r.c, (int)r.b);
+}
 
 // Bucket of a distance: floor(x / delta) by one IEEE multiply, monotone non-decreasing in x (so a
 // bucket is an interval of distances); +inf and huge values land in the last bucket.

@@ -18,6 +18,10 @@ namespace shdtopo {
 #define SHD_SSSP_BLOCK 1024
 #endif
 constexpr int kSsspBlock = SHD_SSSP_BLOCK;  // threads per SSSP workgroup
+#ifndef SHD_BATCH_WGPCU
+#define SHD_BATCH_WGPCU 1
+#endif
+constexpr int kBatchWgPerCu = SHD_BATCH_WGPCU;  // batch-kernel workgroups per CU (share its LDS)
 constexpr int kMaxHops = 48;      // per-thread path buffer depth (longer paths: O(h^2) walk)
 #ifndef SHD_RING_PER_VERTEX
 #define SHD_RING_PER_VERTEX 16
@@ -57,7 +61,7 @@ struct DevCSR {
     int32_t V = 0;
     int64_t nadj = 0;
     const uint32_t* rowptr = nullptr;
-    const uint32_t* adj = nullptr;  // 12-B records {u32 col, f64 wt (two words)}: one line per short row
+    const uint32_t* adj = nullptr;  // 16-B AdjRec {u32 col, f32 pi(col) rounded up, f64 wt}
     const double* aloss = nullptr;
     const double* vloss = nullptr;
     const double* selfLat = nullptr;

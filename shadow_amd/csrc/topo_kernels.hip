@@ -349,7 +349,7 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
             uint32_t n[U], from[U];
             unsigned long long ab[U];
             bool valid[U];
-            W3 rec[U];
+            AdjRec rec[U];
             int los[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {  // U searches, U record loads in flight
@@ -365,7 +365,7 @@ __device__ __forceinline__ void relax_queue(const unsigned long long* Q, uint32_
                 }
                 los[u] = lo;
                 const uint32_t j = valid[u] ? L.rs[lo] + (e - L.off[lo]) : 0u;
-                rec[u] = *reinterpret_cast<const W3*>(g.adj + 3ull * j);
+                rec[u] = adj_rec(g, j);
             }
 #pragma unroll
             for (int u = 0; u < U; u++) {
