@@ -47,7 +47,7 @@ namespace {
 using namespace dev;
 
 #ifndef SHD_BATCH_RB
-#define SHD_BATCH_RB 8  // transposed relaxation: rounds whose loads are in flight together
+#define SHD_BATCH_RB 2  // transposed relaxation: rounds whose loads are in flight together
 #endif
 #ifndef SHD_BATCH_SPEC
 #define SHD_BATCH_SPEC 1  // buckets past cb whose hub sources join a hub expansion speculatively
@@ -96,6 +96,7 @@ struct LdsB {
     uint32_t msk[kBChunk];
     double val[kBChunk * K];  // the chunk's source distances, [vertex][source]
     double sh[K];             // per-source bucket shift sh_j = C - pi(s_j)
+    double dh0[K];            // per-source d_j(h0) (landmark filter; refreshed per chunk)
     double invd;              // 1 / delta
     uint32_t wave[kSsspBlock / 64];
     uint32_t qtail;
@@ -214,6 +215,7 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
         const uint32_t vi = i / K, jj = i % K;
         if ((L.msk[vi] >> jj) & 1u) L.val[i] = bits2d(D.get(L.vx[vi], jj));
     }
+    if (tid < (uint32_t)K) L.dh0[tid] = bits2d(D.get(0u, tid));
     __syncthreads();
     if (stats && tid == 0) {
         L.cnt[2] += total;
@@ -282,14 +284,84 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 amk[a] = valid ? L.msk[lo] : 0u;
                 alo[a] = (uint32_t)lo;
             }
-            // phase B: round r holds edges r * EPW .. r * EPW + EPW - 1 of the wave's 64 * UA;
-            // RB rounds at a time have their loads in flight
+            // Landmark filter, per (edge, source) of the lane's edges: the walk s_j -> h0 -> n
+            // gives d_j(n) <= d_j(h0) + pi(n) (up to rounding, far inside the 1e-6 margin;
+            // pi(n) is stored rounded up, d_j(h0) may be stale, i.e. larger), so a candidate
+            // above the bound can neither improve n's final distance nor tie it and the source
+            // is dropped from the edge (91 % of the tail relaxations on C4).  Every relaxation
+            // that sets or ties a final value is still performed: distances, parent hints and
+            // tie bits are unchanged.
+#pragma unroll
+            for (int a = 0; a < UA; a++) {
+                uint32_t mk = amk[a];
+                const double w = __hiloint2double((int)awh[a], (int)awl[a]);
+                const double pv = (double)__uint_as_float(apb[a]);
+                while (mk) {
+                    const uint32_t jj = (uint32_t)__ffs(mk) - 1u;
+                    mk &= mk - 1u;
+                    const double ad = __dadd_rn(L.val[alo[a] * K + jj], w);
+                    const double bnd = __dmul_rn(__dadd_rn(L.dh0[jj], pv), 1.000001);
+                    if (ad > bnd) amk[a] &= ~(1u << jj);
+                }
+            }
+            // Compaction: the wave's surviving edges (any source left) move to the front, so
+            // phase B runs only ceil(survivors / EPW) rounds.  Lane l pulls survivor
+            // a' * 64 + l (the q-th set bit of the slots' ballots, found by popcount bisection).
+            unsigned long long sb[UA];
+            uint32_t nsv = 0;
+#pragma unroll
+            for (int a = 0; a < UA; a++) {
+                sb[a] = __ballot(amk[a] != 0u);
+                nsv += (uint32_t)__popcll(sb[a]);
+            }
+            {
+                uint32_t cn[UA], cmk[UA], clo[UA], cwl[UA], cwh[UA];
+#pragma unroll
+                for (int a2 = 0; a2 < UA; a2++) {
+                    uint32_t q = (uint32_t)a2 * 64u + lane;
+                    const bool ok = q < nsv;
+                    int sa = 0;
+#pragma unroll
+                    for (int a = 0; a + 1 < UA; a++) {
+                        const uint32_t c = (uint32_t)__popcll(sb[a]);
+                        if (sa == a && q >= c) { q -= c; sa = a + 1; }
+                    }
+                    unsigned long long m = sb[0];
+#pragma unroll
+                    for (int a = 1; a < UA; a++) if (sa == a) m = sb[a];
+                    uint32_t pos = 0;
+#pragma unroll
+                    for (uint32_t wdt = 32; wdt >= 1; wdt >>= 1) {
+                        const uint32_t c = (uint32_t)__popcll(m & ((1ull << wdt) - 1ull));
+                        if (q >= c) { q -= c; pos += wdt; m >>= wdt; }
+                    }
+                    const int sl = ok ? (int)pos : (int)lane;
+                    cn[a2] = 0u; cmk[a2] = 0u; clo[a2] = 0u; cwl[a2] = 0u; cwh[a2] = 0u;
+#pragma unroll
+                    for (int a = 0; a < UA; a++) {
+                        const uint32_t xn = __shfl(an[a], sl, 64);
+                        const uint32_t xm = __shfl(amk[a], sl, 64);
+                        const uint32_t xl = __shfl(alo[a], sl, 64);
+                        const uint32_t xwl = __shfl(awl[a], sl, 64);
+                        const uint32_t xwh = __shfl(awh[a], sl, 64);
+                        if (ok && sa == a) {
+                            cn[a2] = xn; cmk[a2] = xm; clo[a2] = xl; cwl[a2] = xwl; cwh[a2] = xwh;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < UA; a++) {
+                    an[a] = cn[a]; amk[a] = cmk[a]; alo[a] = clo[a]; awl[a] = cwl[a];
+                    awh[a] = cwh[a];
+                }
+            }
+            // phase B: round r holds edges r * EPW .. r * EPW + EPW - 1 of the wave's compacted
+            // 64 * UA; RB rounds at a time have their loads in flight, rounds past the
+            // survivors are skipped (uniform per wave)
             uint32_t fm = kNoBucket;
-            // landmark bound of source j: d_j(h0) (current value: only ever larger than the
-            // final one, which keeps the filter safe)
-            const double dh0 = bits2d(D.get(0u, j));
 #pragma unroll
             for (int r0 = 0; r0 < R; r0 += RB) {
+            if ((uint32_t)(r0 * EPW) >= nsv) break;
             uint32_t n[RB], lo[RB];
             unsigned long long ab[RB], cur[RB];  // ab = ~0: source inactive on this edge
 #pragma unroll
@@ -303,18 +375,8 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 lo[rr] = __shfl(alo[a], src, 64);
                 const double w = __hiloint2double((int)__shfl(awh[a], src, 64),
                                                   (int)__shfl(awl[a], src, 64));
-                const double ad = __dadd_rn(L.val[lo[rr] * K + j], w);
-                // Landmark filter: the walk s_j -> h0 -> n gives d_j(n) <= d_j(h0) + pi(n) (up
-                // to rounding, far inside the 1e-6 margin; pi(n) is stored rounded up), so a
-                // candidate above the bound can neither improve n's final distance nor tie it:
-                // the relaxation is skipped (91 % of the tail relaxations on C4).  Every
-                // relaxation that sets or ties a final value is still performed, so distances,
-                // parent hints and tie bits are unchanged.
-                const double bnd = __dmul_rn(__dadd_rn(dh0, (double)__uint_as_float(
-                                                               __shfl(apb[a], src, 64))),
-                                             1.000001);
-                const bool on = ((mk >> j) & 1u) && !(ad > bnd);
-                ab[rr] = on ? d2bits(ad) : ~0ull;
+                const bool on = (mk >> j) & 1u;
+                ab[rr] = on ? d2bits(__dadd_rn(L.val[lo[rr] * K + j], w)) : ~0ull;
                 // pre-check: the K lanes of the edge read its target's line in one request
                 const bool t = on && n[rr] >= D.H;
                 const unsigned long long x = D.dist[(t ? (size_t)n[rr] : (size_t)0) * K + j];
