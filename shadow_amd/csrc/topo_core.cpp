@@ -141,6 +141,9 @@ struct _Topology {
     int wsK = 0;                // batch width the workspace was laid out for
     int64_t wsRing = 0, wsOver = 0;
     DevBuf<uint32_t> d_rowptr, d_adj;
+    DevBuf<uint32_t> d_adjk;  // rows re-sorted by kappa = w - pi(col) (batch relaxation copy)
+    DevBuf<float> d_kap, d_ksum;  // kappa of d_adjk (f32, rounded down), per-vertex probes
+    double piMax = 0.0;
     DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
     DevBuf<unsigned long long> d_dist, d_best, d_memo, d_ring, d_over, d_qa, d_qb;
     DevBuf<uint32_t> d_stamp, d_cnt, d_bslot, d_par, d_pathbuf,
@@ -442,6 +445,50 @@ int upload_csr(Topology* top) {
         }
         HIPCHK(hipMemcpy(top->d_adj.p, adj.data(), sizeof(uint32_t) * 4 * nadj, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_aloss.p, aloss.data(), sizeof(double) * nadj, hipMemcpyHostToDevice));
+        // Batch relaxation copy: each row re-sorted by kappa = w - pi(col).  The landmark filter
+        // keeps edge (u, v) for source j only if d_j(u) + w <= d_j(h0) + pi(v), i.e. kappa <=
+        // d_j(h0) - d_j(u) (+ margin): a prefix of the kappa-sorted row, whose end the kernel
+        // finds from 4 per-vertex probes (kappa at row positions 0, 1, 3, 7) and, past those,
+        // a binary search in d_kap.  kappa is stored rounded down, so a cut is never too early.
+        std::vector<uint32_t> adjk(4 * nadj);
+        std::vector<float> kap(nadj), ksum(4 * (size_t)V);
+        std::vector<uint32_t> ord;
+        std::vector<double> kd;
+        auto down = [](double x) {
+            if (std::isnan(x)) return -INFINITY;
+            float f = (float)x;
+            if ((double)f > x) f = std::nextafter(f, -INFINITY);
+            return f;
+        };
+        for (int32_t v = 0; v < V; v++) {
+            const uint32_t b = rowptr[(size_t)v], e = rowptr[(size_t)v + 1];
+            ord.resize(e - b);
+            kd.resize(e - b);
+            for (uint32_t k = b; k < e; k++) {
+                const double pv = top->pot[col[k]];
+                kd[k - b] = std::isfinite(pv) ? wt[k] - pv : -INFINITY;
+                ord[k - b] = k;
+            }
+            std::stable_sort(ord.begin(), ord.end(),
+                             [&](uint32_t x, uint32_t y) { return kd[x - b] < kd[y - b]; });
+            for (uint32_t i = 0; i < e - b; i++) {
+                const uint32_t k = ord[i];
+                std::copy(adj.begin() + 4 * (size_t)k, adj.begin() + 4 * (size_t)k + 4,
+                          adjk.begin() + 4 * (size_t)(b + i));
+                kap[b + i] = down(kd[k - b]);
+            }
+            static const uint32_t probe[4] = {0, 1, 3, 7};
+            for (int q = 0; q < 4; q++)
+                ksum[4 * (size_t)v + q] = probe[q] < e - b ? kap[b + probe[q]] : INFINITY;
+        }
+        top->piMax = 0.0;
+        for (double p : top->pot) if (std::isfinite(p)) top->piMax = std::max(top->piMax, p);
+        HIPCHK(top->d_adjk.ensure(4 * nadj));
+        HIPCHK(top->d_kap.ensure(nadj));
+        HIPCHK(top->d_ksum.ensure(4 * (size_t)V));
+        HIPCHK(hipMemcpy(top->d_adjk.p, adjk.data(), sizeof(uint32_t) * 4 * nadj, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_kap.p, kap.data(), sizeof(float) * nadj, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_ksum.p, ksum.data(), sizeof(float) * 4 * (size_t)V, hipMemcpyHostToDevice));
     }
     HIPCHK(hipMemcpy(top->d_vloss.p, vloss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(top->d_selfLat.p, selfLat.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
@@ -462,6 +509,10 @@ DevCSR dev_csr(Topology* top) {
     c.nadj = (int64_t)(top->d_adj.n / 4);
     c.rowptr = top->d_rowptr.p;
     c.adj = top->d_adj.p;
+    c.adjk = top->d_adjk.p;
+    c.kap = top->d_kap.p;
+    c.ksum = reinterpret_cast<const float4*>(top->d_ksum.p);
+    c.piMax = top->piMax;
     c.aloss = top->d_aloss.p;
     c.vloss = top->d_vloss.p;
     c.selfLat = top->d_selfLat.p;

@@ -62,6 +62,10 @@ struct DevCSR {
     int64_t nadj = 0;
     const uint32_t* rowptr = nullptr;
     const uint32_t* adj = nullptr;  // 16-B AdjRec {u32 col, f32 pi(col) rounded up, f64 wt}
+    const uint32_t* adjk = nullptr; // the same records, each row sorted by kappa = w - pi(col)
+    const float* kap = nullptr;     // kappa of adjk (f32 rounded down; -inf: pi unknown)
+    const float4* ksum = nullptr;   // per vertex: kappa at row positions 0, 1, 3, 7 (+inf past it)
+    double piMax = 0.0;             // largest finite pi
     const double* aloss = nullptr;
     const double* vloss = nullptr;
     const double* selfLat = nullptr;

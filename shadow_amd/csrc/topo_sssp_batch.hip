@@ -53,7 +53,7 @@ using namespace dev;
 #define SHD_BATCH_SPEC 1  // buckets past cb whose hub sources join a hub expansion speculatively
 #endif
 #ifndef SHD_BATCH_U
-#define SHD_BATCH_U 2  // phase-A edges per lane
+#define SHD_BATCH_U 4  // phase-A edges per lane
 #endif
 #ifndef SHD_BATCH_CHUNK
 #define SHD_BATCH_CHUNK 512
@@ -161,7 +161,11 @@ struct BBuckets {
 // One chunk of a near queue: take each vertex's source mask (clearing it), its row bounds and
 // its K distances (K lanes per vertex read its line once) into LDS; a block scan of the degrees
 // flattens the chunk's edges.  Returns the chunk's edge count (uniform); ends with a barrier.
-template <int K>
+// CUT (relaxation): rows are the kappa-sorted copy and only the prefix that can pass the
+// landmark filter for some source of the mask is taken (kappa <= max_j d_j(h0) - d_j(v) plus a
+// margin wider than the filter's); its K distances are read by the vertex's thread with the row
+// bounds.  Without CUT (parent pass) whole rows of the id-sorted adjacency.
+template <int K, bool CUT = false>
 __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, const DevCSR& g,
                                                LdsB<K>& L, const BView<K>& D,
                                                typename MaskOps<K>::M* mcur,
@@ -196,6 +200,48 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
         }
         const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
         deg = m ? r1 - r0 : 0u;
+        if (CUT && deg) {
+            const float4 ks = g.ksum[v];
+            double dv[K];
+            if (v < D.H) {
+#pragma unroll
+                for (int jj = 0; jj < K; jj++) dv[jj] = bits2d(D.hd[(size_t)v * K + jj]);
+            } else {
+                typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+                const u64x2* p = reinterpret_cast<const u64x2*>(D.dist + (size_t)v * K);
+#pragma unroll
+                for (int h = 0; h < K / 2; h++) {
+                    const u64x2 x = __builtin_nontemporal_load(p + h);
+                    dv[2 * h] = bits2d(x.x);
+                    dv[2 * h + 1] = bits2d(x.y);
+                }
+            }
+            // threshold: kappa <= d_j(h0) - d_j(v) + 1e-5 (d_j(h0) + d_j(v) + piMax) for some j
+            // of the mask (the filter's own margin is 1e-6 relative); +inf keeps the whole row
+            double T = -INFINITY;
+#pragma unroll
+            for (int jj = 0; jj < K; jj++) {
+                if (!((m >> jj) & 1u)) continue;
+                L.val[tid * K + jj] = dv[jj];
+                const double h = bits2d(D.get(0u, (uint32_t)jj));
+                const double t = (h - dv[jj]) + 1e-5 * (h + dv[jj] + g.piMax) + 1e-9;
+                T = t > T ? t : T;
+            }
+            uint32_t c;
+            if ((double)ks.x > T) c = 0;
+            else if ((double)ks.y > T) c = 1;
+            else if ((double)ks.z > T) c = 3;
+            else if ((double)ks.w > T) c = 7;
+            else {
+                uint32_t lo = 8, hi = deg;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if ((double)g.kap[r0 + mid] > T) hi = mid; else lo = mid + 1;
+                }
+                c = lo;
+            }
+            deg = c < deg ? c : deg;
+        }
         act = (unsigned long long)deg * (unsigned long long)__popc(m);
         L.rs[tid] = r0;
         L.vx[tid] = v;
@@ -211,9 +257,11 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
     if (tid == 0) L.off[cnt] = total;
     act = wave_sum_u64(act);
     if (stats && (tid & 63) == 0 && act) atomicAdd(&L.cnt[0], act);
-    for (uint32_t i = tid; i < cnt * K; i += kSsspBlock) {
-        const uint32_t vi = i / K, jj = i % K;
-        if ((L.msk[vi] >> jj) & 1u) L.val[i] = bits2d(D.get(L.vx[vi], jj));
+    if (!CUT) {
+        for (uint32_t i = tid; i < cnt * K; i += kSsspBlock) {
+            const uint32_t vi = i / K, jj = i % K;
+            if ((L.msk[vi] >> jj) & 1u) L.val[i] = bits2d(D.get(L.vx[vi], jj));
+        }
     }
     if (tid < (uint32_t)K) L.dh0[tid] = bits2d(D.get(0u, tid));
     __syncthreads();
@@ -265,7 +313,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
     const double shj = L.sh[j];
     for (uint32_t base = 0; base < nq; base += kBChunk) {
         const uint32_t cnt = min((uint32_t)kBChunk, nq - base);
-        const uint32_t total = load_chunk<K>(Q + base, cnt, g, L, D, mcur, hdef, true,
+        const uint32_t total = load_chunk<K, true>(Q + base, cnt, g, L, D, mcur, hdef, true,
                                              B.cb + (uint32_t)SHD_BATCH_SPEC);
         for (uint32_t eb = 0; eb < total; eb += (uint32_t)kSsspBlock * UA) {
             // phase A: edge e = eb + a * 1024 + wv * 64 + lane
@@ -276,7 +324,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 const bool valid = e < total;
                 const int lo = valid ? chunk_slot<K>(L, cnt, e) : 0;
                 const uint32_t jr = valid ? L.rs[lo] + (e - L.off[lo]) : 0u;
-                const AdjRec r = adj_rec(g, jr);
+                const AdjRec r = *reinterpret_cast<const AdjRec*>(g.adjk + kAdjWords * jr);
                 an[a] = r.a;
                 apb[a] = r.p;
                 awl[a] = r.b;
