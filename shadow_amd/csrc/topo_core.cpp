@@ -142,7 +142,7 @@ struct _Topology {
     int64_t wsRing = 0, wsOver = 0;
     DevBuf<uint32_t> d_rowptr, d_adj;
     DevBuf<uint32_t> d_adjk;  // rows re-sorted by kappa = w - pi(col) (batch relaxation copy)
-    DevBuf<float> d_kap, d_ksum;  // kappa of d_adjk (f32, rounded down), per-vertex probes
+    DevBuf<float> d_kap, d_ksum, d_kap0;  // kappa of d_adjk (f32, rounded down), per-vertex probes
     double piMax = 0.0;
     DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
     DevBuf<unsigned long long> d_dist, d_best, d_memo, d_ring, d_over, d_qa, d_qb;
@@ -486,6 +486,10 @@ int upload_csr(Topology* top) {
         HIPCHK(top->d_adjk.ensure(4 * nadj));
         HIPCHK(top->d_kap.ensure(nadj));
         HIPCHK(top->d_ksum.ensure(4 * (size_t)V));
+        HIPCHK(top->d_kap0.ensure((size_t)V));
+        std::vector<float> k0((size_t)V);
+        for (int32_t v = 0; v < V; v++) k0[(size_t)v] = ksum[4 * (size_t)v];
+        HIPCHK(hipMemcpy(top->d_kap0.p, k0.data(), sizeof(float) * (size_t)V, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_adjk.p, adjk.data(), sizeof(uint32_t) * 4 * nadj, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_kap.p, kap.data(), sizeof(float) * nadj, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_ksum.p, ksum.data(), sizeof(float) * 4 * (size_t)V, hipMemcpyHostToDevice));
@@ -512,6 +516,7 @@ DevCSR dev_csr(Topology* top) {
     c.adjk = top->d_adjk.p;
     c.kap = top->d_kap.p;
     c.ksum = reinterpret_cast<const float4*>(top->d_ksum.p);
+    c.kap0 = top->d_kap0.p;
     c.piMax = top->piMax;
     c.aloss = top->d_aloss.p;
     c.vloss = top->d_vloss.p;

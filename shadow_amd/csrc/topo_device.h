@@ -65,6 +65,7 @@ struct DevCSR {
     const uint32_t* adjk = nullptr; // the same records, each row sorted by kappa = w - pi(col)
     const float* kap = nullptr;     // kappa of adjk (f32 rounded down; -inf: pi unknown)
     const float4* ksum = nullptr;   // per vertex: kappa at row positions 0, 1, 3, 7 (+inf past it)
+    const float* kap0 = nullptr;    // per vertex: smallest kappa of its row (+inf: empty row)
     double piMax = 0.0;             // largest finite pi
     const double* aloss = nullptr;
     const double* vloss = nullptr;

@@ -272,6 +272,13 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
     return total;
 }
 
+// Can vertex v at distance d (source j, d_j(h0) = h) have an edge that passes the landmark
+// filter?  Only if kappa0(v) (its smallest kappa, f32 rounded down) lies under the CUT threshold of
+// load_chunk; h may be stale (larger), which only widens the test.
+__device__ __forceinline__ bool kappa_useful(float k0, double h, double d, double pimax) {
+    return (double)k0 <= (h - d) + 1e-5 * (h + d + pimax) + 1e-9;
+}
+
 // Edge index e of the chunk -> its vertex slot in the chunk (binary search over L.off).
 template <int K>
 __device__ __forceinline__ int chunk_slot(const LdsB<K>& L, uint32_t cnt, uint32_t e) {
@@ -412,6 +419,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             if ((uint32_t)(r0 * EPW) >= nsv) break;
             uint32_t n[RB], lo[RB];
             unsigned long long ab[RB], cur[RB];  // ab = ~0: source inactive on this edge
+            float kz[RB];                         // kappa0 of the edge's target
 #pragma unroll
             for (int rr = 0; rr < RB; rr++) {
                 const int r = r0 + rr;
@@ -428,6 +436,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 // pre-check: the K lanes of the edge read its target's line in one request
                 const bool t = on && n[rr] >= D.H;
                 const unsigned long long x = D.dist[(t ? (size_t)n[rr] : (size_t)0) * K + j];
+                kz[rr] = g.kap0[t ? n[rr] : 0u];
                 cur[rr] = t ? x : 0ull;
             }
 #pragma unroll
@@ -451,7 +460,10 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 bool nr = false, nf = false;
                 if (im) {
                     const uint32_t b = bkt(bits2d(ab[rr]), shj, B.inv_delta);
-                    if (b <= B.cb) nr = true;
+                    // a tail whose kappa-prefix is empty for this distance would expand no
+                    // edge (every one fails the landmark filter): settled without a queue entry
+                    if (b <= B.cb) nr = n[rr] < D.H || kappa_useful(kz[rr], L.dh0[j],
+                                                                    bits2d(ab[rr]), g.piMax);
                     else {
                         fm = b < fm ? b : fm;
                         // a tail pair reached for the first time past cb: its vertex joins the
@@ -600,6 +612,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         for (uint32_t i = tid; i < xbw; i += kSsspBlock) D.xb[i] = 0u;
         for (uint32_t i = tid; i < pw; i += kSsspBlock) D.pend[i] = 0u;
         if (tid < (uint32_t)K) L.sh[tid] = (int)tid < nk ? srcsh[r0 + tid] : 0.0;
+        // no landmark bound until h0 is reached (the sweeps test kappa0 against L.dh0)
+        if (tid < (uint32_t)K) L.dh0[tid] = INFINITY;
         if (tid == 0) L.invd = B.inv_delta;
         {
             ulonglong2* d2 = reinterpret_cast<ulonglong2*>(D.dist);
@@ -765,10 +779,12 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         for (uint32_t vb = 0; vb < n; vb += VPI * SU) {
                             unsigned long long d[SU][2];
                             uint32_t vv[SU];
+                            float k0[SU];
 #pragma unroll
                             for (int u = 0; u < SU; u++) {
                                 const uint32_t e = vb + (uint32_t)u * VPI + tid / LPV;
                                 vv[u] = e < n ? cl[e] : 0xFFFFFFFFu;
+                                k0[u] = g.kap0[e < n ? vv[u] : 0u];
                                 d[u][0] = d[u][1] = kInfBits;
                                 if (e < n) {
                                     // L1-bypassing 16-B load: the words were lowered by atomics
@@ -791,8 +807,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                     if (d[u][h] == kInfBits) continue;
                                     const uint32_t b = bkt(bits2d(d[u][h]), L.sh[jl + h],
                                                            B.inv_delta);
-                                    if (b == nb) m |= 1u << (jl + h);
-                                    else if (b > nb) {
+                                    if (b == nb) {
+                                        if (kappa_useful(k0[u], L.dh0[jl + h],
+                                                         bits2d(d[u][h]), g.piMax))
+                                            m |= 1u << (jl + h);
+                                    } else if (b > nb) {
                                         keep = 1u;
                                         if (b < km) km = b;
                                     }
