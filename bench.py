@@ -87,7 +87,7 @@ def main():
                     help="C4-int variant (integer latencies U{1..100}: heavy parent ties)")
     ap.add_argument("--batch", type=int, default=8,
                     help="sources per SSSP workgroup (1 = single-source sssp_rows_kernel)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01d_sssp_pmc.json"))
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01e_sssp_pmc.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -185,10 +185,11 @@ def main():
         achieved = rows * b_src / k_s / 1e9
         K = int(st["batch"])
         kname = "sssp_batch_kernel<%d>" % K if K > 1 else "sssp_rows_kernel"
-        # the batch kernel's per-bucket sweeps stream the [V][K] rows past the LDS hubs (16-B
-        # loads); FETCH_SIZE counts such wide streaming reads at half (MI355X_MICROARCH.md)
+        # the batch kernel's per-bucket sweeps read only the 64-B lines of vertices with a
+        # pending bit (random 64-B requests, which FETCH_SIZE counts at their size): no streaming
+        # correction (MI355X_MICROARCH.md: only wide coalesced 128-B reads are tallied at half)
         sweeps = int(st["far_splits"]) if K > 1 else 0
-        sweep_bytes = sweeps * (V - int(st["lds_hubs"])) * K * 8
+        sweep_bytes = 0
         traffic = None
         pmc_note = None
         if os.path.exists(args.pmc_json):
