@@ -138,6 +138,8 @@ struct _Topology {
     std::vector<int32_t> perm;  // new -> old
     std::vector<int32_t> inv;   // old -> new
     std::vector<double> pot;    // batch mode: d(h0, v) from the top hub (new ids), the bucket shift
+    std::vector<uint32_t> sptPar, sptSlot;  // h0 shortest-path tree: parent, its adjacency slot
+    DevBuf<uint32_t> d_spt;     // per vertex {parent, slot of (parent -> v), f64 latency}
     int wsK = 0;                // batch width the workspace was laid out for
     int64_t wsRing = 0, wsOver = 0;
     DevBuf<uint32_t> d_rowptr, d_adj;
@@ -402,6 +404,8 @@ int upload_csr(Topology* top) {
     // (see topo_sssp_batch.hip); only an estimate: any shift keeps the SSSP exact.
     {
         top->pot.assign((size_t)V, INFINITY);
+        top->sptPar.assign((size_t)V, 0xFFFFFFFFu);
+        top->sptSlot.assign((size_t)V, 0xFFFFFFFFu);
         using QE = std::pair<double, int32_t>;
         std::priority_queue<QE, std::vector<QE>, std::greater<QE>> pq;
         top->pot[0] = 0.0;
@@ -414,6 +418,8 @@ int upload_csr(Topology* top) {
                 const double a = t.first + wt[k];
                 if (a < top->pot[col[k]]) {
                     top->pot[col[k]] = a;
+                    top->sptPar[col[k]] = (uint32_t)t.second;  // h0-tree parent: the batch
+                    top->sptSlot[col[k]] = k;                  // parent pass' first guess
                     pq.push({a, (int32_t)col[k]});
                 }
             }
@@ -487,6 +493,22 @@ int upload_csr(Topology* top) {
         HIPCHK(top->d_kap.ensure(nadj));
         HIPCHK(top->d_ksum.ensure(4 * (size_t)V));
         HIPCHK(top->d_kap0.ensure((size_t)V));
+        {
+            std::vector<uint32_t> spt(4 * (size_t)V, 0xFFFFFFFFu);
+            for (int32_t v = 0; v < V; v++) {
+                const uint32_t k = top->sptSlot[(size_t)v];
+                if (k == 0xFFFFFFFFu) continue;
+                uint64_t wb;
+                memcpy(&wb, &wt[k], 8);
+                spt[4 * (size_t)v] = top->sptPar[(size_t)v];
+                spt[4 * (size_t)v + 1] = k;
+                spt[4 * (size_t)v + 2] = (uint32_t)wb;
+                spt[4 * (size_t)v + 3] = (uint32_t)(wb >> 32);
+            }
+            HIPCHK(top->d_spt.ensure(4 * (size_t)V));
+            HIPCHK(hipMemcpy(top->d_spt.p, spt.data(), sizeof(uint32_t) * 4 * (size_t)V,
+                             hipMemcpyHostToDevice));
+        }
         std::vector<float> k0((size_t)V);
         for (int32_t v = 0; v < V; v++) k0[(size_t)v] = ksum[4 * (size_t)v];
         HIPCHK(hipMemcpy(top->d_kap0.p, k0.data(), sizeof(float) * (size_t)V, hipMemcpyHostToDevice));
@@ -517,6 +539,7 @@ DevCSR dev_csr(Topology* top) {
     c.kap = top->d_kap.p;
     c.ksum = reinterpret_cast<const float4*>(top->d_ksum.p);
     c.kap0 = top->d_kap0.p;
+    c.spt = top->d_spt.p;
     c.piMax = top->piMax;
     c.aloss = top->d_aloss.p;
     c.vloss = top->d_vloss.p;
@@ -533,7 +556,8 @@ int batch_k(Topology* top) {
 int64_t ring_entries(Topology* top, int K) {  // batch kernel: the parent pass' pair list
     // batch: V * K pair list + V vertex list (parent pass), then the sweep's pending bitmap
     return K <= 1 ? (int64_t)kRingPerVertex * top->g.V
-                  : (int64_t)top->g.V * (K + 1) + (top->g.V + 31) / 32 + 64;
+                  : (int64_t)top->g.V * (K + 1) + (top->g.V + 31) / 32 + 64 +
+                        (top->g.V * K + 31) / 32 + 64;
 }
 int64_t queue_stride(Topology* top, int K) {  // u64 per slot of each near queue
     const int64_t V = top->g.V;

@@ -66,6 +66,7 @@ struct DevCSR {
     const float* kap = nullptr;     // kappa of adjk (f32 rounded down; -inf: pi unknown)
     const float4* ksum = nullptr;   // per vertex: kappa at row positions 0, 1, 3, 7 (+inf past it)
     const float* kap0 = nullptr;    // per vertex: smallest kappa of its row (+inf: empty row)
+    const uint32_t* spt = nullptr;  // per vertex {h0-tree parent, its slot of (parent, v), f64 w}
     double piMax = 0.0;             // largest finite pi
     const double* aloss = nullptr;
     const double* vloss = nullptr;

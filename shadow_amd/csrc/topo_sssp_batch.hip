@@ -47,7 +47,7 @@ namespace {
 using namespace dev;
 
 #ifndef SHD_BATCH_RB
-#define SHD_BATCH_RB 2  // transposed relaxation: rounds whose loads are in flight together
+#define SHD_BATCH_RB 4  // transposed relaxation: rounds whose loads are in flight together
 #endif
 #ifndef SHD_BATCH_SPEC
 #define SHD_BATCH_SPEC 1  // buckets past cb whose hub sources join a hub expansion speculatively
@@ -147,6 +147,7 @@ struct BView {
     uint32_t* xb;              // LDS: (hub, source) expanded at its current distance
     uint32_t* hpar;            // HBM [P][K]: vertex whose relaxation last lowered hub v for j
     uint32_t* pend;            // HBM, 1 bit per vertex: a tail vertex with a pair pending past cb
+    uint32_t* tie;             // HBM, 1 bit per (tail vertex, source): a relaxation tied its value
     uint32_t H, P;
     __device__ __forceinline__ unsigned long long get(uint32_t v, uint32_t j) const {
         return v < H ? hd[(size_t)v * K + j] : ld_l2_u64(&dist[(size_t)v * K + j]);
@@ -452,10 +453,16 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                         if (im) D.hpar[wi] = L.vx[lo[rr]];
                         else if (ab[rr] == old) atomicOr(&D.tb[wi >> 5], 1u << (wi & 31));
                     }
-                } else if (on && ab[rr] < cur[rr]) {
-                    // the edge's K lanes: one coalesced no-return atomic request per line
-                    (void)atomicMin(&D.dist[(size_t)n[rr] * K + j], ab[rr]);
-                    im = true;
+                } else if (on && ab[rr] <= cur[rr]) {
+                    // the edge's K lanes: one coalesced atomic request per line.  Returning, so
+                    // that exactly one relaxation per value counts as its improver and every
+                    // other one producing the same value as a tie (tie bit): "no tie bit" then
+                    // certifies a unique parent candidate for the parent pass.
+                    const size_t wi = (size_t)n[rr] * K + j;
+                    const unsigned long long old = atomicMin(&D.dist[wi], ab[rr]);
+                    im = ab[rr] < old;
+                    if (ab[rr] == old) atomicOr(&D.tie[wi >> 5], 1u << (wi & 31));
+                    cur[rr] = old;
                 }
                 bool nr = false, nf = false;
                 if (im) {
@@ -583,6 +590,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     uint32_t* vscr = fscr + (size_t)V * K;  // parent-pass vertex list (V entries)
     const uint32_t pw = (uint32_t)((V + 31) / 32);  // words of the pending bitmap
     D.pend = vscr + (size_t)V;
+    const uint32_t tw = (uint32_t)((V * K + 31) / 32);  // words of the tie bitmap
+    D.tie = D.pend + pw + 64;
     const uint32_t pcap = (uint32_t)(V * K);
 
     uint32_t iter = ctr[0], mep = ctr[2];
@@ -611,6 +620,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         for (uint32_t i = tid; i < tbw; i += kSsspBlock) D.tb[i] = 0u;
         for (uint32_t i = tid; i < xbw; i += kSsspBlock) D.xb[i] = 0u;
         for (uint32_t i = tid; i < pw; i += kSsspBlock) D.pend[i] = 0u;
+        for (uint32_t i = tid; i < tw; i += kSsspBlock) D.tie[i] = 0u;
         if (tid < (uint32_t)K) L.sh[tid] = (int)tid < nk ? srcsh[r0 + tid] : 0.0;
         // no landmark bound until h0 is reached (the sweeps test kappa0 against L.dh0)
         if (tid < (uint32_t)K) L.dh0[tid] = INFINITY;
@@ -907,7 +917,21 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     q = pcur[i];
                     scan = true;
                     const uint32_t v = q / K, j = q % K;
-                    if (g.rows_sorted && v < P && !((D.tb[q >> 5] >> (q & 31)) & 1u)) {
+                    if (v >= H && !((D.tie[q >> 5] >> (q & 31)) & 1u)) {
+                        // tail: guess the h0-tree parent; without a tie bit a candidate is the
+                        // only one (every tight edge's relaxation produced d_j(v): one improver,
+                        // the rest ties)
+                        const uint32_t pu = g.spt[4 * (size_t)v];
+                        if (pu < (uint32_t)V) {
+                            const double wt = __hiloint2double((int)g.spt[4 * (size_t)v + 3],
+                                                               (int)g.spt[4 * (size_t)v + 2]);
+                            if (__dadd_rn(bits2d(D.get(pu, j)), wt) == bits2d(D.get(v, j))) {
+                                memo[q] = mtag | (unsigned long long)g.spt[4 * (size_t)v + 1];
+                                par[q] = pu;
+                                scan = false;
+                            }
+                        }
+                    } else if (g.rows_sorted && v < P && !((D.tb[q >> 5] >> (q & 31)) & 1u)) {
                         const uint32_t u = D.hpar[q];
                         if (u < (uint32_t)V) {
                             uint32_t lo = g.rowptr[u], hi = g.rowptr[u + 1];
