@@ -880,6 +880,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         mep++;
         const unsigned long long mtag = (unsigned long long)mep << 32;
         iter++;
+        const uint32_t ep = iter;  // claim tag of this batch's pairs (stamp)
         if (tid == 0) L.qtail = 0;
         __syncthreads();
         uint32_t* pcur = qa;
@@ -892,72 +893,80 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 const uint32_t j = i / (uint32_t)A;
                 const uint32_t t = targets[i - j * (uint32_t)A];
                 q = t * K + j;
-                p = (t != L.src[j]) && (atomicExch(&stamp[q], iter) != iter);
-                if (p) { best[q] = kInfBits; cntc[q] = 0; bslot[q] = 0xFFFFFFFFu; }
+                p = t != L.src[j];
             }
             wave_push_t<uint32_t>(p, q, pcur, &L.qtail, pcap, &L.fover, 128u);
         }
         __syncthreads();
         uint32_t nF = min(L.qtail, pcap);
         __syncthreads();
+        // A guess certified without scanning a row: the first P hubs' recorded improver (LDS
+        // hint, no tie bit) or a tail's h0-tree parent (no tie bit, the edge is tight).  Sets
+        // memo / par; false: the pair needs a row scan.
+        auto try_hint = [&](uint32_t q) -> bool {
+            const uint32_t v = q / K, j = q % K;
+            if (v >= H) {
+                if ((D.tie[q >> 5] >> (q & 31)) & 1u) return false;
+                const uint32_t pu = g.spt[4 * (size_t)v];
+                if (pu >= (uint32_t)V) return false;
+                const double wt = __hiloint2double((int)g.spt[4 * (size_t)v + 3],
+                                                   (int)g.spt[4 * (size_t)v + 2]);
+                if (__dadd_rn(bits2d(D.get(pu, j)), wt) != bits2d(D.get(v, j))) return false;
+                memo[q] = mtag | (unsigned long long)g.spt[4 * (size_t)v + 1];
+                par[q] = pu;
+                return true;
+            }
+            if (!g.rows_sorted || v >= P || ((D.tb[q >> 5] >> (q & 31)) & 1u)) return false;
+            const uint32_t u = D.hpar[q];
+            if (u >= (uint32_t)V) return false;
+            uint32_t lo = g.rowptr[u], hi = g.rowptr[u + 1];
+            while (lo < hi) {  // rows are sorted by neighbour
+                const uint32_t mid = (lo + hi) >> 1;
+                if (adj_col(g, mid) < v) lo = mid + 1; else hi = mid;
+            }
+            if (lo >= g.rowptr[u + 1] || adj_col(g, lo) != v) return false;
+            uint32_t c;
+            double wt;
+            adj_load(g, lo, c, wt);
+            if (__dadd_rn(bits2d(D.get(u, j)), wt) != bits2d(D.get(v, j))) return false;
+            memo[q] = mtag | (unsigned long long)lo;
+            par[q] = u;
+            return true;
+        };
         while (nF > 0) {
             n_par += nF;
             unsigned long long tp0 = wall_clock64();
-            // Heavy hubs first: the SSSP recorded which vertex last lowered each of the first P
-            // hubs for source j and whether any relaxation tied its value.  "No tie seen" + "the
-            // recorded u is a candidate" means u is the only candidate: the igraph parent, found
-            // without scanning the hub's row.  Anything else is scanned.
+            // Walks: each thread follows its pairs' chains towards the source while the guesses
+            // certify parents (no level barriers); a chain stops at the source, at a pair another
+            // walk claimed first (stamp), or at a pair that needs a row scan (-> fscr).
             if (tid == 0) L.qtail = 0;
             __syncthreads();
-            for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
-                const uint32_t i = ib + tid;
-                bool scan = false;
-                uint32_t q = 0;
-                if (i < nF) {
-                    q = pcur[i];
-                    scan = true;
-                    const uint32_t v = q / K, j = q % K;
-                    if (v >= H && !((D.tie[q >> 5] >> (q & 31)) & 1u)) {
-                        // tail: guess the h0-tree parent; without a tie bit a candidate is the
-                        // only one (every tight edge's relaxation produced d_j(v): one improver,
-                        // the rest ties)
-                        const uint32_t pu = g.spt[4 * (size_t)v];
-                        if (pu < (uint32_t)V) {
-                            const double wt = __hiloint2double((int)g.spt[4 * (size_t)v + 3],
-                                                               (int)g.spt[4 * (size_t)v + 2]);
-                            if (__dadd_rn(bits2d(D.get(pu, j)), wt) == bits2d(D.get(v, j))) {
-                                memo[q] = mtag | (unsigned long long)g.spt[4 * (size_t)v + 1];
-                                par[q] = pu;
-                                scan = false;
-                            }
-                        }
-                    } else if (g.rows_sorted && v < P && !((D.tb[q >> 5] >> (q & 31)) & 1u)) {
-                        const uint32_t u = D.hpar[q];
-                        if (u < (uint32_t)V) {
-                            uint32_t lo = g.rowptr[u], hi = g.rowptr[u + 1];
-                            while (lo < hi) {  // rows are sorted by neighbour
-                                const uint32_t mid = (lo + hi) >> 1;
-                                if (adj_col(g, mid) < v) lo = mid + 1; else hi = mid;
-                            }
-                            if (lo < g.rowptr[u + 1] && adj_col(g, lo) == v) {
-                                uint32_t c;
-                                double wt;
-                                adj_load(g, lo, c, wt);
-                                if (__dadd_rn(bits2d(D.get(u, j)), wt) == bits2d(D.get(v, j))) {
-                                    memo[q] = mtag | (unsigned long long)lo;
-                                    par[q] = u;
-                                    scan = false;
-                                }
-                            }
-                        }
+            for (uint32_t i = tid; i < nF; i += kSsspBlock) {
+                uint32_t q = pcur[i];
+                if (atomicExch(&stamp[q], ep) == ep) continue;
+                for (;;) {
+                    const uint32_t j = q % K;
+                    if (!try_hint(q)) {
+                        best[q] = kInfBits;
+                        cntc[q] = 0;
+                        bslot[q] = 0xFFFFFFFFu;
+                        const uint32_t pos = atomicAdd(&L.qtail, 1u);
+                        if (pos < pcap) fscr[pos] = q;
+                        else atomicOr(&L.fover, 128u);
+                        break;
                     }
+                    const uint32_t u = par[q];
+                    if (u == L.src[j]) break;
+                    q = u * K + j;
+                    if (atomicExch(&stamp[q], ep) == ep) break;
                 }
-                wave_push_t<uint32_t>(scan, q, fscr, &L.qtail, pcap, &L.fover, 128u);
             }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             const uint32_t nS = min(L.qtail, pcap);
             __syncthreads();
-            if (tid == 0) L.pt[1] += wall_clock64() - tp0;  // hint pass
+            if (tid == 0) L.pt[1] += wall_clock64() - tp0;  // walks
+            if (nS == 0) break;
             tp0 = wall_clock64();
             // merge the unresolved pairs by vertex (masks in mA / hdef, zero after the SSSP): a
             // vertex's row is scanned once for every source whose chain needs it
@@ -1071,21 +1080,19 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             __syncthreads();
             if (tid == 0) L.pt[3] += wall_clock64() - tp0;  // recount + finalize
             tp0 = wall_clock64();
-            iter++;
+            // the scanned pairs' parents continue as walks
             if (tid == 0) L.qtail = 0;
             __syncthreads();
-            for (uint32_t ib = 0; ib < nF; ib += kSsspBlock) {
+            for (uint32_t ib = 0; ib < nS; ib += kSsspBlock) {
                 const uint32_t i = ib + tid;
                 bool p = false;
                 uint32_t q = 0;
-                if (i < nF) {
-                    const uint32_t qc = pcur[i];
+                if (i < nS) {
+                    const uint32_t qc = fscr[i];
                     const uint32_t j = qc % K;
                     const uint32_t u = par[qc];
                     q = u * K + j;
-                    p = (u != L.src[j]) && ((memo[q] & 0xFFFFFFFF00000000ull) != mtag) &&
-                        (atomicExch(&stamp[q], iter) != iter);
-                    if (p) { best[q] = kInfBits; cntc[q] = 0; bslot[q] = 0xFFFFFFFFu; }
+                    p = u != L.src[j];
                 }
                 wave_push_t<uint32_t>(p, q, pnxt, &L.qtail, pcap, &L.fover, 128u);
             }
