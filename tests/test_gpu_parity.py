@@ -263,3 +263,74 @@ def test_sssp_full_size_c4_sampled_rows():
     assert np.array_equal(glr[..., 0].view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(glr[..., 1].view(np.uint64), orel.view(np.uint64))
     assert np.array_equal(hp[rows].cpu().numpy().view(np.uint16), ohops.astype(np.uint16))
+
+
+def _grid_graphml(n=30, n_poi=60, seed=5):
+    """A 2-D grid of routers (random latencies) whose highest-degree vertex -- the batch kernel's
+    landmark h0 -- sits in a corner with long extra edges, so the landmark bound is loose and
+    the kappa-prefix cut keeps long rows: the filter must stay exact when h0 is not central."""
+    rng = np.random.default_rng(seed)
+    keys = ('<key attr.name="packetloss" attr.type="double" for="edge" id="d9" />'
+            '<key attr.name="jitter" attr.type="double" for="edge" id="d8" />'
+            '<key attr.name="latency" attr.type="double" for="edge" id="d7" />'
+            '<key attr.name="type" attr.type="string" for="node" id="d5" />'
+            '<key attr.name="bandwidthup" attr.type="int" for="node" id="d4" />'
+            '<key attr.name="bandwidthdown" attr.type="int" for="node" id="d3" />'
+            '<key attr.name="geocode" attr.type="string" for="node" id="d2" />'
+            '<key attr.name="ip" attr.type="string" for="node" id="d1" />'
+            '<key attr.name="packetloss" attr.type="double" for="node" id="d0" />')
+    out = ['<?xml version="1.0" encoding="utf-8"?><graphml '
+           'xmlns="http://graphml.graphdrawing.org/xmlns">', keys,
+           '<graph edgedefault="undirected">']
+
+    def node(name, typ, loss, bw):
+        out.append('<node id="%s"><data key="d0">%r</data><data key="d1">0.0.0.0</data>'
+                   '<data key="d2">US</data><data key="d3">%d</data><data key="d4">%d</data>'
+                   '<data key="d5">%s</data></node>' % (name, loss, bw, bw, typ))
+
+    def edge(a, b, lat, loss):
+        out.append('<edge source="%s" target="%s"><data key="d7">%r</data>'
+                   '<data key="d8">0</data><data key="d9">%r</data></edge>' % (a, b, lat, loss))
+
+    for i in range(n * n):
+        node("pop-%d" % i, "pop", 0.0, 0)
+    for k in range(n_poi):
+        node("poi-%d" % k, ("client", "relay", "server")[k % 3],
+             float(rng.uniform(0, 0.05)), 10240)
+    for r in range(n):
+        for c in range(n):
+            i = r * n + c
+            if c + 1 < n:
+                edge("pop-%d" % i, "pop-%d" % (i + 1), float(rng.uniform(1, 100)),
+                     float(rng.uniform(0, 0.01)))
+            if r + 1 < n:
+                edge("pop-%d" % i, "pop-%d" % (i + n), float(rng.uniform(1, 100)),
+                     float(rng.uniform(0, 0.01)))
+    for t in rng.choice(np.arange(1, n * n), 24, replace=False):  # corner hub, long edges
+        edge("pop-0", "pop-%d" % t, float(rng.uniform(150, 400)), 0.0)
+    for k in range(n_poi):
+        edge("poi-%d" % k, "pop-%d" % int(rng.integers(0, n * n)), 5.0, 0.0)
+        edge("poi-%d" % k, "poi-%d" % k, 1.0, 0.0)
+    out.append("</graph></graphml>")
+    return "".join(out).encode()
+
+
+@pytest.mark.parametrize("hubs", [-1, 0])
+def test_sssp_batch_peripheral_landmark(hubs):
+    """Landmark filter / kappa cut / tree-parent guesses on a grid whose landmark is peripheral:
+    every pair bit-exact against the oracle."""
+    data = _grid_graphml()
+    top = sa.Topology.from_buffer(data)
+    g = oracle.OGraph.from_graphml(data)
+    assert not top.is_complete
+    top.set_option("lds_hubs", hubs)
+    top.set_option("batch", 8)
+    otop, ips, verts = attach_hosts(top, g, 60, type_hints=["client", "relay", "server"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(a, oa)
+    assert st["errors"] == 0 and st["ambiguous_pairs"] == 0
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
