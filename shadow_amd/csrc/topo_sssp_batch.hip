@@ -100,6 +100,7 @@ struct LdsB {
     double invd;              // 1 / delta
     uint32_t wave[kSsspBlock / 64];
     uint32_t qtail;
+    uint32_t qhead;    // next queue entry taken by a wave (tail iterations, wave sub-chunks)
     uint32_t htail;    // hubs waiting in the deferred hub list
     uint32_t idx;      // batch taken by this workgroup
     uint32_t src[K];   // the batch's source vertices
@@ -291,6 +292,103 @@ __device__ __forceinline__ int chunk_slot(const LdsB<K>& L, uint32_t cnt, uint32
     return lo;
 }
 
+// Wave-wide exclusive prefix sum (no barrier); *total = the wave's sum.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t v = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(v, o, 64);
+        if (lane >= (uint32_t)o) v += y;
+    }
+    *total = __shfl(v, 63, 64);
+    return v - x;
+}
+
+// Slot of edge e in a (wave's) chunk slice: binary search over its cnt offsets.
+__device__ __forceinline__ uint32_t slice_slot(const uint32_t* off, uint32_t cnt, uint32_t e) {
+    uint32_t lo = 0, hi = cnt - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Wave sub-chunk of a TAIL queue (tail iterations): like load_chunk<K, true>, but one wave loads
+// up to kBSub vertices into its own slice [wb, wb + kBSub) of the chunk arrays and flattens
+// their cut rows with a wave scan, so the waves of a workgroup run their sub-chunks without
+// barriers.  Returns the slice's edge count (wave-uniform).
+constexpr uint32_t kBSub = kBChunk / (kSsspBlock / 64);
+template <int K>
+__device__ __forceinline__ uint32_t load_sub(const uint32_t* Q, uint32_t cnt, uint32_t wb,
+                                             const DevCSR& g, LdsB<K>& L, const BView<K>& D,
+                                             typename MaskOps<K>::M* mcur) {
+    using MO = MaskOps<K>;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t deg = 0;
+    unsigned long long act = 0;
+    if (lane < K) L.dh0[lane] = bits2d(D.get(0u, lane));  // any value read is a valid bound
+    if (lane < cnt) {
+        const uint32_t v = Q[lane];
+        const uint32_t m = MO::get_l2(mcur, v);
+        mcur[v] = 0;
+        const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
+        deg = m ? r1 - r0 : 0u;
+        if (deg) {
+            const float4 ks = g.ksum[v];
+            double dv[K];
+            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+            const u64x2* p = reinterpret_cast<const u64x2*>(D.dist + (size_t)v * K);
+#pragma unroll
+            for (int h = 0; h < K / 2; h++) {
+                const u64x2 x = __builtin_nontemporal_load(p + h);
+                dv[2 * h] = bits2d(x.x);
+                dv[2 * h + 1] = bits2d(x.y);
+            }
+            double T = -INFINITY;
+#pragma unroll
+            for (int jj = 0; jj < K; jj++) {
+                if (!((m >> jj) & 1u)) continue;
+                L.val[(wb + lane) * K + jj] = dv[jj];
+                const double h = bits2d(D.get(0u, (uint32_t)jj));
+                const double t = (h - dv[jj]) + 1e-5 * (h + dv[jj] + g.piMax) + 1e-9;
+                T = t > T ? t : T;
+            }
+            uint32_t c;
+            if ((double)ks.x > T) c = 0;
+            else if ((double)ks.y > T) c = 1;
+            else if ((double)ks.z > T) c = 3;
+            else if ((double)ks.w > T) c = 7;
+            else {
+                uint32_t lo = 8, hi = deg;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if ((double)g.kap[r0 + mid] > T) hi = mid; else lo = mid + 1;
+                }
+                c = lo;
+            }
+            deg = c < deg ? c : deg;
+        }
+        act = (unsigned long long)deg * (unsigned long long)__popc(m);
+        L.rs[wb + lane] = r0;
+        L.vx[wb + lane] = v;
+        L.msk[wb + lane] = m;
+    }
+    uint32_t total;
+    const uint32_t off = wave_excl_scan(deg, &total);
+    if (lane < cnt) L.off[wb + lane] = off;
+    act = wave_sum_u64(act);
+    if (lane == 0) {
+        if (act) atomicAdd(&L.cnt[0], act);
+        atomicAdd(&L.cnt[2], (unsigned long long)total);
+    }
+    // the slice's LDS writes are read by other lanes of this wave only
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    return total;
+}
+
 // Transposed near iteration (default): phase A takes one edge per lane (UA per lane in flight:
 // row search + 12-B record load done once per edge, not once per source); phase B shuffles the
 // edges of a wave so that K consecutive lanes hold one edge, lane j = source j, for UA * K rounds.
@@ -300,7 +398,7 @@ __device__ __forceinline__ int chunk_slot(const LdsB<K>& L, uint32_t cnt, uint32
 // parity) and joins the hub list hq once; the kernel expands the list only when the tail queue
 // is empty, so one hub expansion serves every source that reached it meanwhile (hub rows are
 // 41 % of the expanded edges; expanded at once they serve 2.3 sources each).
-template <int K, int UA>
+template <int K, int UA, bool WAVE = false>
 __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, const DevCSR& g,
                                               LdsB<K>& L, const BView<K>& D,
                                               typename MaskOps<K>::M* mcur,
@@ -319,18 +417,36 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
     const uint32_t ge = lane / K;        // phase B: this lane's edge within the round
     const uint32_t wv = tid >> 6;
     const double shj = L.sh[j];
-    for (uint32_t base = 0; base < nq; base += kBChunk) {
-        const uint32_t cnt = min((uint32_t)kBChunk, nq - base);
-        const uint32_t total = load_chunk<K, true>(Q + base, cnt, g, L, D, mcur, hdef, true,
-                                             B.cb + (uint32_t)SHD_BATCH_SPEC);
-        for (uint32_t eb = 0; eb < total; eb += (uint32_t)kSsspBlock * UA) {
-            // phase A: edge e = eb + a * 1024 + wv * 64 + lane
+    // WAVE (tail iterations): each wave takes kBSub-vertex sub-chunks of the queue from an LDS
+    // counter into its own slice of the chunk arrays; no barrier until the iteration ends.
+    // Otherwise (hub iterations: long rows) block-wide 512-vertex chunks.
+    const uint32_t wb = WAVE ? wv * kBSub : 0u;
+    for (uint32_t base = 0;; base += kBChunk) {
+        uint32_t cnt, total;
+        if (WAVE) {
+            uint32_t b0 = 0;
+            if (lane == 0) b0 = atomicAdd(&L.qhead, kBSub);
+            b0 = __shfl(b0, 0, 64);
+            if (b0 >= nq) break;
+            cnt = min(kBSub, nq - b0);
+            total = load_sub<K>(Q + b0, cnt, wb, g, L, D, mcur);
+        } else {
+            if (base >= nq) break;
+            cnt = min((uint32_t)kBChunk, nq - base);
+            total = load_chunk<K, true>(Q + base, cnt, g, L, D, mcur, hdef, true,
+                                        B.cb + (uint32_t)SHD_BATCH_SPEC);
+        }
+        constexpr uint32_t kStep = WAVE ? 64u : (uint32_t)kSsspBlock;  // lanes per phase-A slot
+        for (uint32_t eb = 0; eb < total; eb += kStep * UA) {
+            // phase A: edge e = eb + a * kStep (+ wv * 64 block-wide) + lane
             uint32_t an[UA], amk[UA], alo[UA], awl[UA], awh[UA], apb[UA];
 #pragma unroll
             for (int a = 0; a < UA; a++) {
-                const uint32_t e = eb + (uint32_t)a * kSsspBlock + wv * 64 + lane;
+                const uint32_t e = eb + (uint32_t)a * kStep + (WAVE ? 0u : wv * 64) + lane;
                 const bool valid = e < total;
-                const int lo = valid ? chunk_slot<K>(L, cnt, e) : 0;
+                const int lo = !valid ? 0
+                               : WAVE ? (int)(wb + slice_slot(L.off + wb, cnt, e))
+                                      : chunk_slot<K>(L, cnt, e);
                 const uint32_t jr = valid ? L.rs[lo] + (e - L.off[lo]) : 0u;
                 const AdjRec r = *reinterpret_cast<const AdjRec*>(g.adjk + kAdjWords * jr);
                 an[a] = r.a;
@@ -498,8 +614,18 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 if (lane == 0) atomicMin(&L.fminb, fm);
             }
         }
+        if (WAVE) {
+            // the next sub-chunk overwrites this wave's slice: its lanes' LDS reads are done
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
         // this wave's atomics and queue stores complete before any wave reads them after the
         // barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (WAVE) {
+        // the iteration's atomics and queue stores complete before the next iteration
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -677,14 +803,21 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 __syncthreads();
                 if (tid == 0) {
                     L.qtail = 0;
+                    L.qhead = 0;
                     if (hubs) L.htail = 0;
                 }
                 __syncthreads();
                 n_expand += ns;
                 const unsigned long long e0 = L.cnt[2], a0 = L.cnt[0];
                 const bool first_it = guard == 0 || just_swept;
-                relax_batch_t<K, SHD_BATCH_U>(src, ns, g, L, D, mcur, hdef, mnxt, qout, cap,
-                                              hfill, B);
+#ifndef SHD_BATCH_NOWAVE
+                if (!hubs)
+                    relax_batch_t<K, SHD_BATCH_U, true>(src, ns, g, L, D, mcur, hdef, mnxt, qout,
+                                                        cap, hfill, B);
+                else
+#endif
+                    relax_batch_t<K, SHD_BATCH_U>(src, ns, g, L, D, mcur, hdef, mnxt, qout, cap,
+                                                  hfill, B);
                 nq = min(L.qtail, cap);
                 if (tid == 0 && first_it) {
                     L.dg[2] += L.cnt[2] - e0;
