@@ -53,7 +53,7 @@ using namespace dev;
 #define SHD_BATCH_SPEC 1  // buckets past cb whose hub sources join a hub expansion speculatively
 #endif
 #ifndef SHD_BATCH_U
-#define SHD_BATCH_U 4  // phase-A edges per lane
+#define SHD_BATCH_U 2  // phase-A edges per lane
 #endif
 #ifndef SHD_BATCH_CHUNK
 #define SHD_BATCH_CHUNK 512
