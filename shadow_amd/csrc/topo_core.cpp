@@ -146,6 +146,8 @@ struct _Topology {
     DevBuf<uint32_t> d_adjk;  // rows re-sorted by kappa = w - pi(col) (batch relaxation copy)
     DevBuf<float> d_kap, d_ksum, d_kap0;  // kappa of d_adjk (f32, rounded down), per-vertex probes
     double piMax = 0.0;
+    double meanLat = -1.0;
+    uint64_t ipGen = 1, geomGen = 0;  // attach/detach generation; compute_geometry's copy  // mean non-loop edge latency (default delta), computed once
     DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
     DevBuf<unsigned long long> d_dist, d_best, d_memo, d_ring, d_over, d_qa, d_qb;
     DevBuf<uint32_t> d_stamp, d_cnt, d_bslot, d_par, d_pathbuf,
@@ -656,32 +658,45 @@ SlotWs slot_ws(Topology* top) {
 // columns = distinct attached vertices in ascending vertex order
 void compute_geometry(Topology* top) {
     std::vector<int32_t> vs;
+    bool same;
     {
         std::shared_lock<std::shared_mutex> lk(top->ipMu);
-        vs.reserve(top->virtualIP.size());
-        for (auto& kv : top->virtualIP)
-            if (kv.second >= 0) vs.push_back(kv.second);
+        same = top->geomGen == top->ipGen;  // no attach / detach since the last call
+        if (!same) {
+            top->geomGen = top->ipGen;
+            vs.reserve(top->virtualIP.size());
+            for (auto& kv : top->virtualIP)
+                if (kv.second >= 0) vs.push_back(kv.second);
+        }
     }
-    std::sort(vs.begin(), vs.end());
-    vs.erase(std::unique(vs.begin(), vs.end()), vs.end());
-    top->attached = vs;
-    top->A = (int64_t)vs.size();
-    top->colOf.assign((size_t)top->g.V, -1);
-    for (size_t i = 0; i < vs.size(); i++) top->colOf[(size_t)vs[i]] = (int32_t)i;
-    // complete branch materialisation bits are per (attached pair)
-    top->matPairWords = (size_t)((top->A * top->A + 63) / 64);
-    top->matPair.reset(new std::atomic<uint64_t>[top->matPairWords ? top->matPairWords : 1]);
-    for (size_t i = 0; i < top->matPairWords; i++) top->matPair[i].store(0);
+    if (!same) {
+        std::sort(vs.begin(), vs.end());
+        vs.erase(std::unique(vs.begin(), vs.end()), vs.end());
+        top->attached = vs;
+        top->A = (int64_t)vs.size();
+        top->colOf.assign((size_t)top->g.V, -1);
+        for (size_t i = 0; i < vs.size(); i++) top->colOf[(size_t)vs[i]] = (int32_t)i;
+    }
+    // complete branch materialisation bits are per (attached pair), cleared on every build
+    const size_t words = (size_t)((top->A * top->A + 63) / 64);
+    if (!top->matPair || words != top->matPairWords) {
+        top->matPairWords = words;
+        top->matPair.reset(new std::atomic<uint64_t>[words ? words : 1]);
+    }
+    for (size_t i = 0; i < top->matPairWords; i++) top->matPair[i].store(0, std::memory_order_relaxed);
 }
 
 double default_delta(Topology* top) {
     if (top->delta > 0) return top->delta;
-    const HostGraph& g = top->g;
-    double s = 0;
-    int64_t n = 0;
-    for (int64_t e = 0; e < g.E; e++)
-        if (g.eu[(size_t)e] != g.ev[(size_t)e]) { s += g.elat[(size_t)e]; n++; }
-    double mean = n ? s / (double)n : 1.0;
+    if (!(top->meanLat >= 0)) {  // the graph is immutable once loaded: one pass over the edges
+        const HostGraph& g = top->g;
+        double s = 0;
+        int64_t n = 0;
+        for (int64_t e = 0; e < g.E; e++)
+            if (g.eu[(size_t)e] != g.ev[(size_t)e]) { s += g.elat[(size_t)e]; n++; }
+        top->meanLat = n ? s / (double)n : 1.0;
+    }
+    const double mean = top->meanLat;
     // tuned on C4: single-source 0.06 x mean (~3 ms); the batch kernel gains from
     // wider buckets (sources of a batch share more expansions) up to 0.2 x mean (~10 ms)
     return std::max(1e-9, (batch_k(top) > 1 ? 0.2 : 0.06) * mean);
@@ -744,8 +759,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         if (K > 1) {
             // bucket shift per row: sh = C - pi(src) >= 2 delta (topo_sssp_batch.hip)
             const double delta = default_delta(top);
-            double pmax = 0.0;
-            for (double p : top->pot) if (std::isfinite(p)) pmax = std::max(pmax, p);
+            const double pmax = top->piMax;  // largest finite pi (upload_csr)
             std::vector<double> sh((size_t)rows);
             for (int64_t i = 0; i < rows; i++) {
                 const double p = top->pot[(size_t)src[(size_t)i]];
@@ -1061,6 +1075,7 @@ void do_attach(Topology* top, uint32_t ip, int32_t v, uint64_t* bwDownOut, uint6
     {
         std::unique_lock<std::shared_mutex> lk(top->ipMu);
         top->virtualIP[ip] = v;
+        top->ipGen++;
     }
     if (v >= 0) {
         if (bwUpOut) *bwUpOut = (uint64_t)top->g.vbwup[(size_t)v];
@@ -1183,7 +1198,7 @@ void topology_detach(Topology* top, Address* address) {
     if (!top || !address || !address_toNetworkIP) return;
     uint32_t ip = address_toNetworkIP(address);
     std::unique_lock<std::shared_mutex> lk(top->ipMu);
-    top->virtualIP.erase(ip);
+    if (top->virtualIP.erase(ip)) top->ipGen++;
 }
 
 double shdtopo_get_latency_ip(Topology* top, uint32_t srcIP, uint32_t dstIP) {
