@@ -80,8 +80,10 @@ if ks:
                fetch_bytes=fetch, fetch_bytes_corrected=fetch_c, sweep_bytes=sweep_bytes,
                write_bytes=write, rdreq=rd, wrreq=wr, atomic_req=at,
                source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), profiles/%s_summary.md; "
-                      "FETCH_SIZE per the gfx950 formula (64-B random requests counted at 64 B), "
-                      "plus half of the sweeps' streaming bytes (counted at 1/2 on gfx950)" % tag)
+                      "FETCH_SIZE per the gfx950 formula (64-B random requests counted at 64 B)%s"
+                      % (tag, ", plus half of the sweeps' streaming bytes (counted at 1/2 on gfx950)"
+                         if sweep_bytes else "; no streaming correction (sweeps read pending "
+                         "vertices' 64-B lines only)"))
     json.dump(out, open(os.path.join(outdir, "%s_sssp_pmc.json" % tag), "w"), indent=1)
     lines += ["## per-launch HBM traffic of %s" % k, "",
               "* FETCH_SIZE = %.4g B, + streaming-sweep correction %.4g B = %.4g B" %
