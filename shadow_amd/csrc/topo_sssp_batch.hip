@@ -321,7 +321,7 @@ __device__ __forceinline__ uint32_t slice_slot(const uint32_t* off, uint32_t cnt
 // barriers.  Returns the slice's edge count (wave-uniform).
 constexpr uint32_t kBSub = kBChunk / (kSsspBlock / 64);
 template <int K>
-__device__ __forceinline__ uint32_t load_sub(const uint32_t* Q, uint32_t cnt, uint32_t wb,
+__device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t wb,
                                              const DevCSR& g, LdsB<K>& L, const BView<K>& D,
                                              typename MaskOps<K>::M* mcur) {
     using MO = MaskOps<K>;
@@ -330,7 +330,7 @@ __device__ __forceinline__ uint32_t load_sub(const uint32_t* Q, uint32_t cnt, ui
     unsigned long long act = 0;
     if (lane < K) L.dh0[lane] = bits2d(D.get(0u, lane));  // any value read is a valid bound
     if (lane < cnt) {
-        const uint32_t v = Q[lane];
+        const uint32_t v = qv;  // this lane's queue entry (loaded by the caller)
         const uint32_t m = MO::get_l2(mcur, v);
         mcur[v] = 0;
         const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
@@ -421,15 +421,24 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
     // counter into its own slice of the chunk arrays; no barrier until the iteration ends.
     // Otherwise (hub iterations: long rows) block-wide 512-vertex chunks.
     const uint32_t wb = WAVE ? wv * kBSub : 0u;
+    // WAVE: the next sub-chunk is taken and its queue entries loaded before this one is
+    // expanded (one global round trip less on each sub-chunk's dependent chain)
+    uint32_t nb0 = 0, nqv = 0;
+    if (WAVE) {
+        if (lane == 0) nb0 = atomicAdd(&L.qhead, kBSub);
+        nb0 = __shfl(nb0, 0, 64);
+        nqv = nb0 + lane < nq ? Q[nb0 + lane] : 0u;
+    }
     for (uint32_t base = 0;; base += kBChunk) {
         uint32_t cnt, total;
         if (WAVE) {
-            uint32_t b0 = 0;
-            if (lane == 0) b0 = atomicAdd(&L.qhead, kBSub);
-            b0 = __shfl(b0, 0, 64);
+            const uint32_t b0 = nb0, qv = nqv;
             if (b0 >= nq) break;
             cnt = min(kBSub, nq - b0);
-            total = load_sub<K>(Q + b0, cnt, wb, g, L, D, mcur);
+            if (lane == 0) nb0 = atomicAdd(&L.qhead, kBSub);
+            nb0 = __shfl(nb0, 0, 64);
+            nqv = nb0 + lane < nq ? Q[nb0 + lane] : 0u;
+            total = load_sub<K>(qv, cnt, wb, g, L, D, mcur);
         } else {
             if (base >= nq) break;
             cnt = min((uint32_t)kBChunk, nq - base);
