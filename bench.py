@@ -87,7 +87,7 @@ def main():
                     help="C4-int variant (integer latencies U{1..100}: heavy parent ties)")
     ap.add_argument("--batch", type=int, default=8,
                     help="sources per SSSP workgroup (1 = single-source sssp_rows_kernel)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01h_sssp_pmc.json"))
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01i_sssp_pmc.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
