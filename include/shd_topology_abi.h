@@ -171,8 +171,21 @@ typedef struct {
     double split_ms;          /* bucket changes + refills, summed over workgroups (in phase 1) */
     int64_t batch;            /* sources per SSSP workgroup of the last build (1 = single-source) */
     int64_t lds_hubs;         /* LDS-resident hub rows of the last SSSP launch */
+    int64_t replay_rows;      /* rows recomputed by the exact igraph heap replay (rows with a
+                                 d-tied parent on a target chain; every row of a directed graph) */
+    double replay_ms;         /* event-timed duration of the heap-replay launch */
+    int64_t replay_pops;      /* heap operations of the replay, summed over its rows: pops, */
+    int64_t replay_pushes;    /*   pushes (first reach) and */
+    int64_t replay_modifies;  /*   modifies (strict improvement of a queued vertex) */
+    int64_t replay_slots;     /* concurrent replay wavefronts of the last launch */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
+
+/* Test hook: run the exact heap replay (igraph_get_shortest_paths_dijkstra restated on the GPU)
+ * from vertex `src` over the current attached set.  full = 1 runs to an empty heap instead of
+ * stopping when every attached vertex is popped.  dist f64[V] (-1 = unreached) and parent int32[V]
+ * (-1 = none) receive the replay's result in original vertex ids.  Returns 0 or an error. */
+int shdtopo_replay_source(Topology* top, int32_t src, int full, double* dist, int32_t* parent);
 
 /* Copy the parsed graph into host arrays (document order; any pointer may be NULL):
  * eu, ev int32[E]; elat, eloss f64[E]; vloss f64[V].  Used by tools and oracle cross-checks. */

@@ -35,7 +35,9 @@ class ShdStats(ctypes.Structure):
                 ("relaxations", i64), ("long_paths", i64), ("errors", i64),
                 ("phase_ms", dbl * 4), ("near_iterations", i64), ("far_splits", i64),
                 ("slots", i64), ("events", i64 * 8), ("far_scan_sources", i64), ("split_ms", dbl),
-                ("batch", i64), ("lds_hubs", i64)]
+                ("batch", i64), ("lds_hubs", i64), ("replay_rows", i64), ("replay_ms", dbl),
+                ("replay_pops", i64), ("replay_pushes", i64), ("replay_modifies", i64),
+                ("replay_slots", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):
@@ -77,6 +79,7 @@ SIGNATURES = {
     "shdtopo_get_lazy_minimum_latency": (dbl, [P]),
     "shdtopo_get_stats": (ctypes.c_int, [P, P]),
     "shdtopo_write_graphml": (ctypes.c_int, [P, cstr]),
+    "shdtopo_replay_source": (ctypes.c_int, [P, i32, ctypes.c_int, P, P]),
     "shdtopo_export_graph": (ctypes.c_int, [P, P, P, P, P, P]),
     "shdtopo_new_synthetic": (P, [P]),
     "shdtopo_synth_packets": (ctypes.c_int, [P, u64, i64, i64, u64, u64, P, P, P, P, P, P, P]),

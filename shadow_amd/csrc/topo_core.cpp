@@ -168,6 +168,23 @@ struct _Topology {
     DevBuf<uint64_t> b_now, b_time;
     DevBuf<uint8_t> b_dl;
 
+    // exact heap replay (topo_replay.hip): igraph's pop order for rows whose target chains cross
+    // a d-tied parent, and every row of a directed topology
+    bool tieReplay = true;    // option "tie_replay" (0: report ambiguous pairs only)
+    bool replayAll = false;   // option "replay_all" (test hook: every row through the replay)
+    int replaySlotsOpt = 0;   // option "replay_slots" (0 = sized from the CUs and free HBM)
+    bool replayUploaded = false;
+    DevBuf<uint32_t> d_rrow;
+    DevBuf<uint4> d_rrec;
+    DevBuf<double2> d_rhop;
+    DevBuf<uint32_t> d_tbits;
+    DevBuf<double> d_rdist, d_rkey;
+    DevBuf<uint32_t> d_rvert, d_rhpos, d_rpar, d_rpath, d_rrows;
+    DevBuf<uint8_t> d_rowflag;
+    int rslots = 0;
+    hipEvent_t evr0 = nullptr, evr1 = nullptr;
+    bool replayPending = false;
+
     // host mirror of the table (for the per-call getters)
     std::vector<double> hlat, hrel, hrowmin;
     std::vector<uint16_t> hhops;
@@ -260,12 +277,21 @@ bool check_graph(Topology* top) {
         }
         std::sort(keys.begin(), keys.end());
         size_t uniq = (size_t)(std::unique(keys.begin(), keys.end()) - keys.begin());
-        top->hasMultiEdges = (uniq != keys.size()) && !g.directed;
+        top->hasMultiEdges = uniq != keys.size();
+        if (g.directed && top->hasMultiEdges) {  // directed: only same-direction duplicates
+            keys.clear();
+            for (int64_t e = 0; e < g.E; e++)
+                if (g.eu[(size_t)e] != g.ev[(size_t)e])
+                    keys.push_back((uint64_t)g.eu[(size_t)e] * (uint64_t)g.V + (uint64_t)g.ev[(size_t)e]);
+            std::sort(keys.begin(), keys.end());
+            top->hasMultiEdges = std::unique(keys.begin(), keys.end()) != keys.end();
+        }
         top->isComplete = (uint64_t)uniq == (uint64_t)g.V * (uint64_t)(g.V - 1) / 2;
     }
     if (top->hasMultiEdges)
         WARNING("topology has parallel edges: igraph_get_eid picks one of them "
-                "(implementation-defined); the lowest edge id is used here");
+                "(implementation-defined); the lowest edge id is used here, and every row is "
+                "computed by the exact heap replay");
     // edge latency > 0 (:312-317; the reference calls error() here)
     for (int64_t e = 0; e < g.E; e++) {
         if (g.elat[(size_t)e] <= 0) {
@@ -309,6 +335,8 @@ int dev_init(Topology* top) {
     HIPCHK(hipEventCreate(&top->ev1));
     HIPCHK(hipEventCreate(&top->ev2));
     HIPCHK(hipEventCreate(&top->ev3));
+    HIPCHK(hipEventCreate(&top->evr0));
+    HIPCHK(hipEventCreate(&top->evr1));
     HIPCHK(top->d_stats.ensure(ST_COUNT));
     top->devInit = true;
     return 0;
@@ -323,6 +351,29 @@ int upload_csr(Topology* top) {
     if (top->csrUploaded) return 0;
     HostGraph& g = top->g;
     const int32_t V = g.V;
+    if (top->isDirected) {
+        // Directed topologies run only the heap replay (its out-edge rows: upload_replay); the
+        // batch kernel's undirected CSR, relabel and landmark are not built.  Identity labels.
+        top->perm.resize((size_t)V);
+        std::iota(top->perm.begin(), top->perm.end(), 0);
+        top->inv = top->perm;
+        std::vector<double> selfLat((size_t)V, NAN), selfLoss((size_t)V, 0.0);
+        for (int64_t e = 0; e < g.E; e++) {
+            const int32_t a = g.eu[(size_t)e];
+            if (a == g.ev[(size_t)e] && std::isnan(selfLat[(size_t)a])) {
+                selfLat[(size_t)a] = g.elat[(size_t)e];
+                selfLoss[(size_t)a] = g.eloss[(size_t)e];
+            }
+        }
+        HIPCHK(top->d_vloss.ensure((size_t)V));
+        HIPCHK(top->d_selfLat.ensure((size_t)V));
+        HIPCHK(top->d_selfLoss.ensure((size_t)V));
+        HIPCHK(hipMemcpy(top->d_vloss.p, g.vloss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_selfLat.p, selfLat.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_selfLoss.p, selfLoss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
+        top->csrUploaded = true;
+        return 0;
+    }
     std::vector<uint32_t> deg((size_t)V, 0);
     for (int64_t e = 0; e < g.E; e++) {
         int32_t a = g.eu[(size_t)e], b = g.ev[(size_t)e];
@@ -655,6 +706,151 @@ SlotWs slot_ws(Topology* top) {
     return w;
 }
 
+// Incidence-order CSR of the heap replay (ReplayCSR in topo_device.h).  Row x (relabelled id)
+// lists x's igraph_incident edges (type_indexededgelist.c): undirected = out-list (from == x,
+// i.e. neighbours <= x) then in-list (neighbours >= x), each by (neighbour, edge id) -> ascending
+// original neighbour id; directed (mode OUT) = out-neighbours ascending.  Self loops never relax
+// and are dropped; a parallel group becomes one entry with the group's minimum latency (same
+// heap history, topo_replay.hip) and the lowest edge id's latency/loss for the hop
+// (igraph_get_eid as orc_get_eid).  Needs perm/inv (upload_csr).
+int upload_replay(Topology* top) {
+    if (top->replayUploaded) return 0;
+    const HostGraph& g = top->g;
+    const int32_t V = g.V;
+    const bool dir = top->isDirected;
+    // entries (x, y, e) in edge-id order, then stable counting sorts by y and by x
+    std::vector<int32_t> ex, ey, ee;
+    ex.reserve((size_t)g.E * (dir ? 1 : 2));
+    ey.reserve(ex.capacity());
+    ee.reserve(ex.capacity());
+    for (int64_t e = 0; e < g.E; e++) {
+        const int32_t a = g.eu[(size_t)e], b = g.ev[(size_t)e];
+        if (a == b) continue;
+        ex.push_back(a); ey.push_back(b); ee.push_back((int32_t)e);
+        if (!dir) { ex.push_back(b); ey.push_back(a); ee.push_back((int32_t)e); }
+    }
+    const size_t n = ex.size();
+    std::vector<uint32_t> o1(n), o2(n);
+    std::vector<int64_t> cnt((size_t)V + 1);
+    auto csort = [&](const std::vector<int32_t>& key, const std::vector<uint32_t>* in,
+                     std::vector<uint32_t>& out) {
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (size_t i = 0; i < n; i++) cnt[(size_t)key[in ? (*in)[i] : i] + 1]++;
+        for (int32_t k = 0; k < V; k++) cnt[(size_t)k + 1] += cnt[(size_t)k];
+        for (size_t i = 0; i < n; i++) {
+            const uint32_t id = in ? (*in)[i] : (uint32_t)i;
+            out[(size_t)cnt[(size_t)key[id]]++] = id;
+        }
+    };
+    csort(ey, nullptr, o1);  // by neighbour (edge ids ascending within)
+    csort(ex, &o1, o2);      // by row, stable: (x, y, e)
+    // merge parallel groups; count entries per relabelled row
+    std::vector<uint32_t> rowptr((size_t)V + 1, 0);
+    std::vector<size_t> gstart;
+    gstart.reserve(n);
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t id = o2[i];
+        if (i == 0 || ex[id] != ex[o2[i - 1]] || ey[id] != ey[o2[i - 1]]) {
+            gstart.push_back(i);
+            rowptr[(size_t)top->inv[(size_t)ex[id]] + 1]++;
+        }
+    }
+    for (int32_t k = 0; k < V; k++) rowptr[(size_t)k + 1] += rowptr[(size_t)k];
+    const size_t nr = gstart.size();
+    std::vector<uint4> rec(nr);
+    std::vector<double2> hop(nr);
+    std::vector<uint32_t> fill(rowptr.begin(), rowptr.end() - 1);
+    for (size_t gi = 0; gi < nr; gi++) {
+        const size_t b = gstart[gi], e = gi + 1 < nr ? gstart[gi + 1] : n;
+        const uint32_t id0 = o2[b];  // lowest edge id of the group: igraph_get_eid's edge
+        double w = g.elat[(size_t)ee[id0]];
+        for (size_t i = b + 1; i < e; i++) w = std::min(w, g.elat[(size_t)ee[o2[i]]]);
+        const uint32_t x = (uint32_t)top->inv[(size_t)ex[id0]];
+        const uint32_t k = fill[x]++;
+        uint64_t wb;
+        memcpy(&wb, &w, 8);
+        rec[k] = make_uint4((uint32_t)top->inv[(size_t)ey[id0]], x, (uint32_t)wb,
+                            (uint32_t)(wb >> 32));
+        hop[k] = make_double2(g.elat[(size_t)ee[id0]], g.eloss[(size_t)ee[id0]]);
+    }
+    HIPCHK(top->d_rrow.ensure((size_t)V + 1));
+    HIPCHK(top->d_rrec.ensure(std::max<size_t>(1, nr)));
+    HIPCHK(top->d_rhop.ensure(std::max<size_t>(1, nr)));
+    HIPCHK(hipMemcpy(top->d_rrow.p, rowptr.data(), sizeof(uint32_t) * ((size_t)V + 1), hipMemcpyHostToDevice));
+    if (nr) {
+        HIPCHK(hipMemcpy(top->d_rrec.p, rec.data(), sizeof(uint4) * nr, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_rhop.p, hop.data(), sizeof(double2) * nr, hipMemcpyHostToDevice));
+    }
+    top->replayUploaded = true;
+    return 0;
+}
+
+ReplayCSR replay_csr(Topology* top) {
+    ReplayCSR c;
+    c.V = top->g.V;
+    c.nadj = (int64_t)top->d_rrec.n;
+    c.rowptr = top->d_rrow.p;
+    c.rec = top->d_rrec.p;
+    c.hop = top->d_rhop.p;
+    c.vloss = top->d_vloss.p;
+    c.selfLat = top->d_selfLat.p;
+    c.selfLoss = top->d_selfLoss.p;
+    c.tbits = top->d_tbits.p;
+    c.ntargets = top->A;
+    return c;
+}
+
+// Replay workspace: 28 B x V + the path buffer per slot (one wavefront each), as many slots as
+// the rows need, 16 per CU, and 3/5 of the free HBM allow.
+int ensure_replay_ws(Topology* top, int nrows) {
+    const size_t V = (size_t)top->g.V;
+    const size_t per_slot = 28 * V + (size_t)kMaxHops * 64 * 4 + 64;
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, top->device));
+    int want = top->replaySlotsOpt > 0 ? top->replaySlotsOpt : prop.multiProcessorCount * 16;
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    const size_t held = (size_t)top->rslots * per_slot;
+    want = std::min(want, (int)std::max<size_t>(1, ((freeb + held) * 3 / 5) / per_slot));
+    want = std::max(1, std::min(want, nrows));
+    if (top->rslots >= want) return 0;
+    top->d_rdist.release(); top->d_rkey.release(); top->d_rvert.release();
+    top->d_rhpos.release(); top->d_rpar.release(); top->d_rpath.release();
+    top->rslots = 0;
+    const size_t n = (size_t)want * V;
+    HIPCHK(top->d_rdist.ensure(n));
+    HIPCHK(top->d_rkey.ensure(n));
+    HIPCHK(top->d_rvert.ensure(n));
+    HIPCHK(top->d_rhpos.ensure(n));
+    HIPCHK(top->d_rpar.ensure(n));
+    HIPCHK(top->d_rpath.ensure((size_t)want * kMaxHops * 64));
+    top->rslots = want;
+    return 0;
+}
+
+ReplayWs replay_ws(Topology* top) {
+    ReplayWs w;
+    w.slots = top->rslots;
+    w.dist = top->d_rdist.p;
+    w.key = top->d_rkey.p;
+    w.vert = top->d_rvert.p;
+    w.hpos = top->d_rhpos.p;
+    w.par = top->d_rpar.p;
+    w.pathbuf = top->d_rpath.p;
+    return w;
+}
+
+// target bitmap over V (relabelled ids) for the replay's early exit
+int upload_target_bits(Topology* top, const std::vector<uint32_t>& tgt, hipStream_t st) {
+    const size_t words = ((size_t)top->g.V + 31) / 32;
+    std::vector<uint32_t> tb(words, 0u);
+    for (uint32_t t : tgt) tb[t >> 5] |= 1u << (t & 31u);
+    HIPCHK(top->d_tbits.ensure(words));
+    HIPCHK(hipMemcpyAsync(top->d_tbits.p, tb.data(), 4 * words, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));  // tb must outlive the async copy
+    return 0;
+}
+
 // columns = distinct attached vertices in ascending vertex order
 void compute_geometry(Topology* top) {
     std::vector<int32_t> vs;
@@ -739,14 +935,13 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         // the host vectors must outlive the async copies
         HIPCHK(hipStreamSynchronize(st));
     } else {
-        if (top->isDirected) {
-            CRITICAL("directed non-complete topologies are not supported by the GPU SSSP yet");
-            return -3;
-        }
         int r = upload_csr(top);
         if (r) return r;
-        r = ensure_workspace(top, (int)rows);
-        if (r) return r;
+        // directed topologies (and the "replay_all" test hook) run every row through the exact
+        // heap replay; otherwise the batch kernel runs and flags the rows that need it
+        // multigraphs too: the reference sums the igraph_get_eid edge of each hop, which the batch
+        // epilogue (latency = distance) does not reproduce when parallel edges differ
+        const bool allReplay = top->isDirected || top->replayAll || top->hasMultiEdges;
         std::vector<uint32_t> src((size_t)rows), tgt((size_t)A);
         for (int64_t i = 0; i < rows; i++) src[(size_t)i] = (uint32_t)top->inv[(size_t)top->attached[(size_t)(row0 + i)]];
         for (int64_t i = 0; i < A; i++) tgt[(size_t)i] = (uint32_t)top->inv[(size_t)top->attached[(size_t)i]];
@@ -756,40 +951,78 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         HIPCHK(hipMemcpyAsync(top->d_targets.p, tgt.data(), sizeof(uint32_t) * (size_t)A, hipMemcpyHostToDevice, st));
         const int K = batch_k(top);
         HIPCHK(hipEventRecord(top->ev0, st));
-        if (K > 1) {
-            // bucket shift per row: sh = C - pi(src) >= 2 delta (topo_sssp_batch.hip)
-            const double delta = default_delta(top);
-            const double pmax = top->piMax;  // largest finite pi (upload_csr)
-            std::vector<double> sh((size_t)rows);
-            for (int64_t i = 0; i < rows; i++) {
-                const double p = top->pot[(size_t)src[(size_t)i]];
-                sh[(size_t)i] = (pmax - (std::isfinite(p) ? p : pmax)) + 2.0 * delta;
+        if (!allReplay) {
+            r = ensure_workspace(top, (int)rows);
+            if (r) return r;
+            HIPCHK(top->d_rowflag.ensure((size_t)rows));
+            HIPCHK(hipMemsetAsync(top->d_rowflag.p, 0, (size_t)rows, st));
+            SlotWs ws = slot_ws(top);
+            ws.rowflag = top->d_rowflag.p;
+            if (K > 1) {
+                // bucket shift per row: sh = C - pi(src) >= 2 delta (topo_sssp_batch.hip)
+                const double delta = default_delta(top);
+                const double pmax = top->piMax;  // largest finite pi (upload_csr)
+                std::vector<double> sh((size_t)rows);
+                for (int64_t i = 0; i < rows; i++) {
+                    const double p = top->pot[(size_t)src[(size_t)i]];
+                    sh[(size_t)i] = (pmax - (std::isfinite(p) ? p : pmax)) + 2.0 * delta;
+                }
+                HIPCHK(top->d_srcsh.ensure((size_t)rows));
+                HIPCHK(hipMemcpyAsync(top->d_srcsh.p, sh.data(), sizeof(double) * (size_t)rows,
+                                      hipMemcpyHostToDevice, st));
+                HIPCHK(hipEventRecord(top->ev0, st));
+                const SsspLdsPlan bp = sssp_batch_lds_plan(
+                    K, top->hubLimit, (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 20)),
+                    top->g.V);
+                top->stats.lds_hubs = bp.H;
+                HIPCHK(launch_sssp_batch(K, dev_csr(top), ws, top->d_sources.p,
+                                         top->d_srcsh.p, (int)rows, top->d_targets.p, (int)A,
+                                         delta, bp, (uint32_t)top->farCap, out_lr, out_hops,
+                                         out_rowmin, top->d_stats.p, st));
+                HIPCHK(hipEventRecord(top->ev1, st));
+                HIPCHK(hipStreamSynchronize(st));  // sh must outlive the async copy
+            } else {
+                top->stats.lds_hubs = lds_plan(top).H;
+                HIPCHK(launch_sssp_rows(dev_csr(top), ws, top->d_sources.p, (int)rows,
+                                        top->d_targets.p, (int)A, default_delta(top), lds_plan(top),
+                                        (uint32_t)top->farCap,
+                                        (uint32_t)top->nearCap, top->events,
+                                        out_lr, out_hops,
+                                        out_rowmin, top->d_stats.p, st));
             }
-            HIPCHK(top->d_srcsh.ensure((size_t)rows));
-            HIPCHK(hipMemcpyAsync(top->d_srcsh.p, sh.data(), sizeof(double) * (size_t)rows,
-                                  hipMemcpyHostToDevice, st));
-            HIPCHK(hipEventRecord(top->ev0, st));
-            const SsspLdsPlan bp = sssp_batch_lds_plan(
-                K, top->hubLimit, (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 20)),
-                top->g.V);
-            top->stats.lds_hubs = bp.H;
-            HIPCHK(launch_sssp_batch(K, dev_csr(top), slot_ws(top), top->d_sources.p,
-                                     top->d_srcsh.p, (int)rows, top->d_targets.p, (int)A,
-                                     delta, bp, (uint32_t)top->farCap, out_lr, out_hops,
-                                     out_rowmin, top->d_stats.p, st));
-            HIPCHK(hipEventRecord(top->ev1, st));
-            HIPCHK(hipStreamSynchronize(st));  // sh must outlive the async copy
-        } else {
-            top->stats.lds_hubs = lds_plan(top).H;
-            HIPCHK(launch_sssp_rows(dev_csr(top), slot_ws(top), top->d_sources.p, (int)rows,
-                                    top->d_targets.p, (int)A, default_delta(top), lds_plan(top),
-                                    (uint32_t)top->farCap,
-                                    (uint32_t)top->nearCap, top->events,
-                                    out_lr, out_hops,
-                                    out_rowmin, top->d_stats.p, st));
         }
         HIPCHK(hipEventRecord(top->ev1, st));
         HIPCHK(hipStreamSynchronize(st));
+        // rows that need igraph's heap pop order: replayed exactly on the GPU
+        std::vector<uint32_t> rlist;
+        if (allReplay) {
+            rlist.resize((size_t)rows);
+            std::iota(rlist.begin(), rlist.end(), 0u);
+        } else if (top->tieReplay) {
+            std::vector<uint8_t> fl((size_t)rows);
+            HIPCHK(hipMemcpy(fl.data(), top->d_rowflag.p, (size_t)rows, hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < rows; i++)
+                if (fl[(size_t)i]) rlist.push_back((uint32_t)i);
+        }
+        top->replayPending = false;
+        if (!rlist.empty()) {
+            r = upload_replay(top);
+            if (r) return r;
+            r = ensure_replay_ws(top, (int)rlist.size());
+            if (r) return r;
+            r = upload_target_bits(top, tgt, st);
+            if (r) return r;
+            HIPCHK(top->d_rrows.ensure(rlist.size()));
+            HIPCHK(hipMemcpy(top->d_rrows.p, rlist.data(), 4 * rlist.size(), hipMemcpyHostToDevice));
+            HIPCHK(hipEventRecord(top->evr0, st));
+            HIPCHK(launch_heap_replay(replay_csr(top), replay_ws(top), top->d_sources.p,
+                                      top->d_rrows.p, (int)rlist.size(), top->d_targets.p, (int)A,
+                                      0, out_lr, out_hops, out_rowmin, top->d_stats.p, nullptr,
+                                      nullptr, st));
+            HIPCHK(hipEventRecord(top->evr1, st));
+            HIPCHK(hipStreamSynchronize(st));
+            top->replayPending = true;
+        }
     }
     top->rowsPending = true;
     top->stats.batch = top->isComplete ? 0 : batch_k(top);
@@ -807,6 +1040,15 @@ int collect_row_stats(Topology* top) {
     HIPCHK(hipMemcpy(h, top->d_stats.p, sizeof h, hipMemcpyDeviceToHost));
     top->stats.sssp_kernel_ms = ms;
     top->stats.build_ms = ms;
+    top->stats.replay_ms = 0.0;
+    if (top->replayPending) {
+        float rms = 0;
+        HIPCHK(hipEventSynchronize(top->evr1));
+        HIPCHK(hipEventElapsedTime(&rms, top->evr0, top->evr1));
+        top->stats.replay_ms = rms;
+        top->stats.build_ms += rms;
+        top->replayPending = false;
+    }
     top->stats.ambiguous_pairs = (int64_t)h[ST_AMBIGUOUS];
     top->stats.relaxations = (int64_t)h[ST_RELAX];
     top->stats.long_paths = (int64_t)h[ST_LONGPATH];
@@ -829,6 +1071,11 @@ int collect_row_stats(Topology* top) {
         MESSAGE("%llu sources overflowed the far pile and finished with scanning splits",
                 h[ST_FARSCAN]);
     top->stats.far_scan_sources = (int64_t)h[ST_FARSCAN];
+    top->stats.replay_rows = (int64_t)h[ST_RP_ROWS];
+    top->stats.replay_pops = (int64_t)h[ST_RP_POPS];
+    top->stats.replay_pushes = (int64_t)h[ST_RP_PUSH];
+    top->stats.replay_modifies = (int64_t)h[ST_RP_MOD];
+    top->stats.replay_slots = top->stats.replay_rows ? top->rslots : 0;
     {
         int khz = 0;
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->device) != hipSuccess || khz <= 0)
@@ -836,9 +1083,9 @@ int collect_row_stats(Topology* top) {
         top->stats.split_ms = (double)h[ST_T_SPLIT] / (double)khz;
     }
     if (h[ST_OVERFLOW]) CRITICAL("SSSP queue overflow / iteration guard (code %llu)", h[ST_OVERFLOW]);
-    if (top->stats.ambiguous_pairs)
+    if (top->stats.ambiguous_pairs && !top->tieReplay)
         WARNING("%lld pairs cross a parent tie (equal d[u]): igraph's heap pop order decides them "
-                "in the reference; the lowest adjacency slot is used here",
+                "in the reference; tie_replay is off, so the lowest adjacency slot is used here",
                 (long long)top->stats.ambiguous_pairs);
     top->rowsPending = false;
     return (h[ST_OVERFLOW] ? -4 : 0);
@@ -1146,6 +1393,8 @@ void topology_free(Topology* top) {
         (void)hipEventDestroy(top->ev1);
         (void)hipEventDestroy(top->ev2);
         (void)hipEventDestroy(top->ev3);
+        (void)hipEventDestroy(top->evr0);
+        (void)hipEventDestroy(top->evr1);
         (void)hipStreamDestroy(top->stream);
     }
     delete top;
@@ -1166,6 +1415,9 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "near_cap") top->nearCap = (int64_t)value;
     else if (k == "events") top->events = value != 0;
     else if (k == "batch") top->batchK = (int)value;
+    else if (k == "tie_replay") top->tieReplay = value != 0;
+    else if (k == "replay_all") top->replayAll = value != 0;
+    else if (k == "replay_slots") top->replaySlotsOpt = (int)value;
     else return -1;
     return 0;
 }
@@ -1420,6 +1672,56 @@ int shdtopo_get_stats(Topology* top, ShdStats* out) {
         top->routePending = false;
     }
     *out = top->stats;
+    return 0;
+}
+
+int shdtopo_replay_source(Topology* top, int32_t srcv, int full, double* dist, int32_t* parent) {
+    if (!top || !dist || !parent) return -1;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    if (srcv < 0 || srcv >= top->g.V || top->isComplete) return -2;
+    int r = dev_init(top);
+    if (r) return r;
+    compute_geometry(top);
+    const int64_t A = top->A;
+    if (A <= 0) return -2;
+    r = upload_csr(top);
+    if (r) return r;
+    r = upload_replay(top);
+    if (r) return r;
+    r = ensure_replay_ws(top, 1);
+    if (r) return r;
+    hipStream_t st = top->stream;
+    std::vector<uint32_t> tgt((size_t)A);
+    for (int64_t i = 0; i < A; i++) tgt[(size_t)i] = (uint32_t)top->inv[(size_t)top->attached[(size_t)i]];
+    r = upload_target_bits(top, tgt, st);
+    if (r) return r;
+    const uint32_t s = (uint32_t)top->inv[(size_t)srcv], row = 0;
+    const size_t V = (size_t)top->g.V;
+    DevBuf<uint32_t> d_s, d_row, d_tg;
+    DevBuf<double2> d_lr;
+    DevBuf<uint16_t> d_h;
+    DevBuf<double> d_dist;
+    DevBuf<int32_t> d_par;
+    HIPCHK(d_s.ensure(1)); HIPCHK(d_row.ensure(1)); HIPCHK(d_tg.ensure((size_t)A));
+    HIPCHK(d_lr.ensure((size_t)A)); HIPCHK(d_h.ensure((size_t)A));
+    HIPCHK(d_dist.ensure(V)); HIPCHK(d_par.ensure(V));
+    HIPCHK(hipMemcpy(d_s.p, &s, 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_row.p, &row, 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_tg.p, tgt.data(), 4 * (size_t)A, hipMemcpyHostToDevice));
+    HIPCHK(hipMemsetAsync(top->d_stats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
+    HIPCHK(launch_fill_u64(top->d_stats.p + ST_GLOBAL_MIN, 0x7FF0000000000000ull, 1, st));
+    HIPCHK(launch_heap_replay(replay_csr(top), replay_ws(top), d_s.p, d_row.p, 1, d_tg.p, (int)A,
+                              full, d_lr.p, d_h.p, nullptr, top->d_stats.p, d_dist.p, d_par.p, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<double> hd(V);
+    std::vector<int32_t> hp(V);
+    HIPCHK(hipMemcpy(hd.data(), d_dist.p, 8 * V, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hp.data(), d_par.p, 4 * V, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < V; i++) {  // relabelled -> original ids
+        const size_t o = (size_t)top->perm[i];
+        dist[o] = hd[i];
+        parent[o] = hp[i] < 0 ? -1 : top->perm[(size_t)hp[i]];
+    }
     return 0;
 }
 

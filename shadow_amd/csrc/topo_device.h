@@ -54,7 +54,12 @@ enum StatIdx {
     ST_FARSCAN = 21,    // sources that overflowed a queue (finished with scanning buckets)
     ST_T_SPLIT = 22,    // wall-clock ticks summed over workgroups: bucket changes + refills
     ST_OVERSITE = 23,   // OR of the push sites that overflowed (diagnostic)
-    ST_COUNT = 24
+    ST_RP_DEQUEUE = 24, // heap replay: next row to take (persistent wavefronts)
+    ST_RP_POPS = 25,    //   heap pops (delete_max) summed over replayed rows
+    ST_RP_PUSH = 26,    //   pushes (first reach)
+    ST_RP_MOD = 27,     //   modifies (strict improvement of a queued vertex)
+    ST_RP_ROWS = 28,    //   rows replayed
+    ST_COUNT = 29
 };
 
 struct DevCSR {
@@ -104,6 +109,41 @@ struct SlotWs {
     int64_t over_entries = 0;
     uint8_t* mask = nullptr;
     uint32_t* hpar = nullptr;
+    // per row of the launch: set to 1 when a pair of the row crosses a d-tied parent (its parent
+    // chain needs igraph's heap pop order: the row is recomputed by heap_replay_kernel)
+    uint8_t* rowflag = nullptr;
+};
+
+// Incidence-order CSR of the heap replay (topo_replay.hip), relabelled vertex ids: row x holds
+// x's neighbours in igraph_incident order (ascending ORIGINAL neighbour id; directed graphs:
+// out-neighbours), self loops dropped, parallel edges merged.
+//   rec  {u32 col, u32 row vertex x, f64 latency (min over a parallel group)}   16 B
+//   hop  {f64 latency, f64 packet loss} of the igraph_get_eid edge (lowest edge id)  16 B
+struct ReplayCSR {
+    int32_t V = 0;
+    int64_t nadj = 0;
+    const uint32_t* rowptr = nullptr;
+    const uint4* rec = nullptr;
+    const double2* hop = nullptr;
+    const double* vloss = nullptr;
+    const double* selfLat = nullptr;
+    const double* selfLoss = nullptr;
+    const uint32_t* tbits = nullptr;  // target (attached vertex) bitmap over V
+    int64_t ntargets = 0;             // distinct targets (igraph's to_reach)
+};
+
+// per-slot workspace of the heap replay (one wavefront = one slot), slot-major [slot][V]:
+// dist f64 (-1 = unreached), heap keys f64 + vertices u32 (positions >= the LDS part), hpos u32
+// (heap position of a queued vertex), par u32 (replay-CSR slot of the parent edge), and a path
+// buffer [kMaxHops][64] per slot.  28 B x V + 12 KiB per slot.
+struct ReplayWs {
+    int slots = 0;
+    double* dist = nullptr;
+    double* key = nullptr;
+    uint32_t* vert = nullptr;
+    uint32_t* hpos = nullptr;
+    uint32_t* par = nullptr;
+    uint32_t* pathbuf = nullptr;
 };
 
 // LDS plan of one SSSP workgroup: H hub distance words (+ their queue bitmaps) and P parent
@@ -132,6 +172,16 @@ hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uin
                              double delta, const SsspLdsPlan& plan, uint32_t far_cap,
                              double2* out_lr, uint16_t* out_hops, double* out_rowmin,
                              unsigned long long* d_stats, hipStream_t stream);
+
+// Exact igraph-0.7 Dijkstra replay, one wavefront per row (topo_replay.hip): rows[0..nrows) index
+// d_sources / the output rows.  full = 1 ignores the early exit (test hook); dbg_dist / dbg_par
+// (V entries, nrows == 1) receive the replay's distances and parent vertices (relabelled ids).
+hipError_t launch_heap_replay(const ReplayCSR& g, const ReplayWs& ws, const uint32_t* d_sources,
+                              const uint32_t* d_rows, int nrows, const uint32_t* d_targets, int A,
+                              int full, double2* out_lr, uint16_t* out_hops, double* out_rowmin,
+                              unsigned long long* d_stats, double* dbg_dist, int32_t* dbg_par,
+                              hipStream_t stream);
+int replay_lds_levels();
 
 hipError_t launch_pair_table_complete(int A, int64_t row0, int64_t rows, const double* elatAA,
                                       const double* elossAA, const double* vlossA, double2* out_lr,

@@ -935,7 +935,10 @@ sssp_rows_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources, int 
                         rel *= (1.0 - g.aloss[(uint32_t)(memo[x] & 0x7FFFFFFFull)]);
                     }
                 }
-                if (amb) atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
+                if (amb) {
+                    atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
+                    if (ws.rowflag) ws.rowflag[s_idx] = 1;  // tie replay (topo_replay.hip)
+                }
                 if (lat == 0.0) lat = 1.0;
             }
             out_lr[rowbase + k] = make_double2(lat, rel);

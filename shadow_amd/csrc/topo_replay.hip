@@ -1,0 +1,380 @@
+// topo_replay.hip -- exact igraph-0.7 Dijkstra replay for gfx950: one wavefront per source runs
+// the reference's heap algorithm operation for operation, so that parents on equal-distance ties
+// (igraph's pop order among equal keys) come out exactly as the reference's.
+//
+// Why.  The batched delta-stepping kernel (topo_sssp_batch.hip) computes every distance bit-exact
+// and every parent that has a single candidate.  Where a vertex v has several candidates u with
+// the same minimal d[u] (integer latencies: common), igraph's parent is the candidate popped
+// first from its two-way heap, and that order is a sequential heap history.  The
+// batch kernel flags every such row (memo bit 31 -> rowflag); this kernel recomputes exactly
+// those rows (and every row of a directed topology, where the batch kernel does not run).
+//
+// What is replayed (igraph 0.7.1, restated in oracle/oracle.c:146-305 and SURVEY.md A.3):
+//   * igraph_get_shortest_paths_dijkstra (structural_properties.c): dist = -1, push(src, 0);
+//     while (size > 0 && to_reach > 0): pop max; to_reach -= is_target; relax the incident
+//     edges in igraph_incident order: dist < 0 -> dist = alt, parent = e, push(-alt);
+//     alt < dist (strict) -> dist = alt, parent = e, modify(-alt);
+//   * igraph_2wheap_t (indheap.c): max-heap on -dist, PARENT(x) = (x+1)/2-1;
+//     shift_up swaps while data[x] >= data[parent]; delete_max swaps root and last, pops, sinks;
+//     sink takes the left child if right == size || data[L] >= data[R], swaps if
+//     data[head] < data[child]; modify = set, sink (a no-op for a larger key), shift_up;
+//   * the per-target helper shd-topology.c:561-671 for the epilogue (reliability product in
+//     path order from the source, latency = left-to-right sum of the igraph_get_eid edges).
+// Incidence order (type_indexededgelist.c): for an undirected graph out-list (neighbours <= x)
+// then in-list (neighbours >= x), i.e. ascending neighbour id (original numbering) with self
+// loops in the middle (they never relax); directed, mode OUT: out-neighbours ascending.  The
+// host builds rows in that order (relabelled ids, parallel edges merged: see below).
+//
+// Parallel edges.  igraph relaxes them one after another; for a group of parallel edges the
+// heap ends in the same state as one relaxation with the group's minimum latency (a shift-up
+// from a position on the ancestor chain stops where the largest key stops, keys being monotone
+// along the chain), so the host merges them.  The epilogue uses the igraph_get_eid edge of each
+// hop (lowest edge id, as the oracle) for latency and loss.
+//
+// Wavefront mapping.  Heap operations are inherently sequential; the 64 lanes make each one
+// short instead: a sink loads the 62-node subtree five levels below the current node in one
+// round trip (positions of a level are contiguous: a few cache lines) and walks it in
+// registers; a shift-up loads the whole ancestor chain (<= 20 lanes) in one round trip and
+// finds its stop by a ballot; the relaxation of a row takes 64 edges per step.  The top
+// kRpLdsLevels levels of the heap live in LDS (the positions every sink starts from).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "topo_dev_common.h"
+
+namespace shdtopo {
+
+namespace {
+
+using namespace dev;
+
+#ifndef SHD_RP_LDS_LEVELS
+#define SHD_RP_LDS_LEVELS 9
+#endif
+constexpr uint32_t kRpT = (1u << SHD_RP_LDS_LEVELS) - 1u;  // heap positions held in LDS
+
+__device__ __forceinline__ uint32_t rl_u32(uint32_t x, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+}
+__device__ __forceinline__ double rl_f64(double x, int l) {
+    const unsigned long long b = d2bits(x);
+    const uint32_t lo = rl_u32((uint32_t)b, l), hi = rl_u32((uint32_t)(b >> 32), l);
+    return bits2d(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t uni_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+__device__ __forceinline__ double uni_f64(double x) { return rl_f64(x, 0); }
+
+// The heap of one source: keys (igraph's data = -dist) and vertices, positions < kRpT in LDS,
+// the rest in this slot's HBM arrays; hpos[v] = position of v (igraph's index2 - 2).
+struct RpHeap {
+    double* gk;
+    uint32_t* gv;
+    uint32_t* hpos;
+    double* sk;
+    uint32_t* sv;
+    __device__ __forceinline__ double key(uint32_t p) const { return p < kRpT ? sk[p] : gk[p]; }
+    __device__ __forceinline__ uint32_t vtx(uint32_t p) const { return p < kRpT ? sv[p] : gv[p]; }
+    __device__ __forceinline__ void put(uint32_t p, double k, uint32_t v) const {
+        if (p < kRpT) {
+            sk[p] = k;
+            sv[p] = v;
+        } else {
+            gk[p] = k;
+            gv[p] = v;
+        }
+        hpos[v] = p;
+    }
+};
+
+// igraph_2wheap_sink of element (xk, xv) from position `head` (a hole) in a heap of `size`.
+// The path of larger children does not depend on x, so the subtree five levels below the hole is
+// loaded at once; x stops where it is not smaller than the chosen child.
+__device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t size, double xk,
+                                        uint32_t xv, int lane) {
+    const uint32_t rr = (uint32_t)lane + 2u;  // BFS index + 1 of this lane's subtree node
+    const int dl = 31 - __clz(rr);            // its depth below the hole (1..5 for lanes < 62)
+    const uint32_t off = rr - (1u << dl);
+    for (;;) {
+        const uint32_t p = ((head + 1u) << dl) - 1u + off;
+        double k = -INFINITY;
+        uint32_t v = 0;
+        if (lane < 62 && p < size) {
+            k = H.key(p);
+            v = H.vtx(p);
+        }
+        uint32_t cur = head, q = 0;
+        bool stop = false;
+        unsigned long long path = 0;
+#pragma unroll
+        for (int s = 0; s < 5; ++s) {
+            const uint32_t L = 2u * cur + 1u;
+            if (L >= size) {
+                stop = true;
+                break;
+            }
+            const int li = (int)(2u * q);  // lane of the left child (BFS 2q+1)
+            const double kL = rl_f64(k, li);
+            int ci = li;
+            uint32_t c = L;
+            double kc = kL;
+            if (L + 1u < size) {
+                const double kR = rl_f64(k, li + 1);
+                if (!(kL >= kR)) {
+                    ci = li + 1;
+                    c = L + 1u;
+                    kc = kR;
+                }
+            }
+            if (xk < kc) {
+                path |= 1ull << ci;
+                cur = c;
+                q = (uint32_t)ci + 1u;
+            } else {
+                stop = true;
+                break;
+            }
+        }
+        // every chosen child moves up to its parent's position
+        if ((path >> lane) & 1ull) H.put((p - 1u) >> 1, k, v);
+        head = cur;
+        if (stop) break;
+    }
+    if (lane == 0) H.put(head, xk, xv);
+}
+
+// igraph_2wheap_shift_up of element (xk, xv) from position `pos` (a hole).  Returns the number f
+// of ancestors moved down one level; lane i < f holds the moved vertex (mv) and its new position.
+__device__ __forceinline__ int rp_shift_up(const RpHeap& H, uint32_t pos, double xk, uint32_t xv,
+                                           int lane, uint32_t& mv, uint32_t& mp) {
+    const uint32_t depth = (uint32_t)(31 - __clz(pos + 1u));  // ancestors of pos
+    const bool valid = (uint32_t)lane < depth;
+    const uint32_t sh = valid ? (uint32_t)lane + 1u : 0u;
+    const uint32_t a = ((pos + 1u) >> sh) - 1u;
+    double ak = INFINITY;
+    uint32_t av = 0;
+    if (valid) {
+        ak = H.key(a);
+        av = H.vtx(a);
+    }
+    // x rises past every ancestor with key <= x and stops below the first one with key > x
+    const unsigned long long stopm = __ballot(valid && xk < ak);
+    const int f = stopm ? __ffsll((long long)stopm) - 1 : (int)depth;
+    const uint32_t c = lane == 0 ? pos : (valid ? ((pos + 1u) >> (uint32_t)lane) - 1u : 0u);
+    if (lane < f) H.put(c, ak, av);
+    const uint32_t fp = f == 0 ? pos : ((pos + 1u) >> (uint32_t)f) - 1u;
+    if (lane == 0) H.put(fp, xk, xv);
+    mv = av;
+    mp = c;
+    return f;
+}
+
+__global__ void __launch_bounds__(64, 4)
+heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ sources,
+                   const uint32_t* __restrict__ rows, int nrows,
+                   const uint32_t* __restrict__ targets, int A, int full, double2* out_lr,
+                   uint16_t* out_hops, double* out_rowmin, unsigned long long* stats,
+                   double* dbg_dist, int32_t* dbg_par) {
+    __shared__ double sk[kRpT];
+    __shared__ uint32_t sv[kRpT];
+    const int lane = (int)threadIdx.x;
+    const size_t V = (size_t)g.V;
+    const size_t slot = blockIdx.x;
+    double* dist = ws.dist + slot * V;
+    uint32_t* par = ws.par + slot * V;
+    RpHeap H{ws.key + slot * V, ws.vert + slot * V, ws.hpos + slot * V, sk, sv};
+    uint32_t* pbuf = ws.pathbuf + slot * (size_t)kMaxHops * 64;
+    unsigned long long n_pop = 0, n_push = 0, n_mod = 0, n_rows = 0;
+
+    for (;;) {
+        uint32_t item = 0;
+        if (lane == 0) item = (uint32_t)atomicAdd(&stats[ST_RP_DEQUEUE], 1ull);
+        item = rl_u32(item, 0);
+        if (item >= (uint32_t)nrows) break;
+        const uint32_t row = rows[item];
+        const uint32_t src = uni_u32(sources[row]);
+        n_rows++;
+
+        // ---- igraph_get_shortest_paths_dijkstra ----
+        for (size_t i = (size_t)lane; i < V; i += 64) dist[i] = -1.0;
+        uint32_t size = 1;
+        if (lane == 0) {
+            dist[src] = 0.0;
+            H.put(0, 0.0, src);
+        }
+        int64_t to_reach = full ? (int64_t)V + 1 : (int64_t)g.ntargets;
+        while (size > 0 && to_reach > 0) {
+            // igraph_2wheap_delete_max
+            const uint32_t u = uni_u32(sv[0]);
+            const double du = -uni_f64(sk[0]);  // mindist = -data[0]
+            const uint32_t lastp = size - 1u;
+            const double xk = uni_f64(H.key(lastp));
+            const uint32_t xv = uni_u32(H.vtx(lastp));
+            size = lastp;
+            if (size > 0) rp_sink(H, 0, size, xk, xv, lane);
+            n_pop++;
+            if ((g.tbits[u >> 5] >> (u & 31u)) & 1u) {
+                to_reach--;
+                // every target is popped: its parent chain is final (relaxing u's edges, as
+                // igraph still does, cannot change a popped vertex)
+                if (to_reach == 0) break;
+            }
+            const uint32_t rb = uni_u32(g.rowptr[u]), re = uni_u32(g.rowptr[u + 1]);
+            for (uint32_t base = rb; base < re; base += 64) {
+                const uint32_t j = base + (uint32_t)lane;
+                const bool act = j < re;
+                uint32_t t = 0, mypos = 0;
+                double w = 0.0, cur = 0.0;
+                if (act) {
+                    const uint4 r = g.rec[j];
+                    t = r.x;
+                    w = __hiloint2double((int)r.w, (int)r.z);
+                    cur = dist[t];
+                    mypos = H.hpos[t];
+                }
+                const double alt = __dadd_rn(du, w);
+                const bool first = act && cur < 0.0;
+                const bool impr = act && !first && alt < cur;
+                if (first || impr) {
+                    dist[t] = alt;
+                    par[t] = j;
+                }
+                unsigned long long m = __ballot(first || impr);
+                const unsigned long long fm = __ballot(first);
+                while (m) {
+                    const int l = __ffsll((long long)m) - 1;
+                    m &= m - 1ull;
+                    const uint32_t tv = rl_u32(t, l);
+                    const double xkey = -rl_f64(alt, l);
+                    uint32_t pos;
+                    if ((fm >> l) & 1ull) {  // igraph_2wheap_push_with_index
+                        if (size >= (uint32_t)V) {  // cannot happen (each vertex queued once)
+                            if (lane == 0) atomicAdd(&stats[ST_OVERFLOW], 1ull);
+                            continue;
+                        }
+                        pos = size++;
+                        n_push++;
+                    } else {  // igraph_2wheap_modify (its sink is a no-op for a larger key)
+                        pos = rl_u32(mypos, l);
+                        n_mod++;
+                    }
+                    uint32_t mv, mp;
+                    const int f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp);
+                    // later lanes whose vertex was moved down by this shift-up
+                    for (int i = 0; i < f; ++i) {
+                        const uint32_t vi = rl_u32(mv, i), pi = rl_u32(mp, i);
+                        if (t == vi) mypos = pi;
+                    }
+                }
+            }
+        }
+
+        if (dbg_dist) {  // test hook: the replay's dist / parent vertex in relabelled ids
+            for (size_t i = (size_t)lane; i < V; i += 64) {
+                const double d = dist[i];
+                dbg_dist[i] = d;
+                dbg_par[i] = (d >= 0.0 && i != src) ? (int32_t)g.rec[par[i]].y : -1;
+            }
+        }
+
+        // ---- per-target helper (shd-topology.c:561-671) ----
+        double rmin = INFINITY;
+        const size_t rowbase = (size_t)row * (size_t)A;
+        for (int k = lane; k < A; k += 64) {
+            const uint32_t t = targets[k];
+            double lat, rel;
+            uint32_t h = 0;
+            if (t == src) {
+                // path [src]: the self loop (n == 1 branch), no destination loss
+                const double sl = g.selfLat[src];
+                if (isnan(sl)) {
+                    atomicAdd(&stats[ST_ERRORS], 1ull);
+                    lat = -1.0;
+                    rel = -1.0;
+                } else {
+                    lat = 0.0 + sl;
+                    rel = 1.0;
+                    rel *= (1.0 - g.vloss[src]);
+                    rel *= (1.0 - g.selfLoss[src]);
+                    h = 1;
+                }
+            } else {
+                bool bad = !(dist[t] >= 0.0);
+                uint32_t v = t;
+                while (!bad && v != src) {
+                    const uint32_t j = par[v];
+                    if ((int64_t)j >= g.nadj) {
+                        bad = true;
+                        break;
+                    }
+                    if (h < (uint32_t)kMaxHops) pbuf[(size_t)h * 64 + lane] = j;
+                    h++;
+                    v = g.rec[j].y;
+                    if (h > (uint32_t)V) bad = true;
+                }
+                lat = 0.0;
+                rel = 1.0;
+                rel *= (1.0 - g.vloss[src]);
+                rel *= (1.0 - g.vloss[t]);
+                if (bad) {
+                    atomicAdd(&stats[ST_ERRORS], 1ull);
+                    lat = -1.0;
+                    rel = -1.0;
+                } else {
+                    if (h > (uint32_t)kMaxHops) atomicAdd(&stats[ST_LONGPATH], 1ull);
+                    for (int x = (int)h - 1; x >= 0; --x) {  // hop x from the target, forwards
+                        uint32_t j;
+                        if (x < kMaxHops) {
+                            j = pbuf[(size_t)x * 64 + lane];
+                        } else {
+                            uint32_t y = t;  // the chain was validated by the walk above
+                            for (int z = 0; z < x; ++z) y = g.rec[par[y]].y;
+                            j = par[y];
+                        }
+                        const double2 hp = g.hop[j];
+                        lat = __dadd_rn(lat, hp.x);
+                        rel *= (1.0 - hp.y);
+                    }
+                    if (lat == 0.0) lat = 1.0;
+                }
+            }
+            out_lr[rowbase + (size_t)k] = make_double2(lat, rel);
+            out_hops[rowbase + (size_t)k] = (uint16_t)(h > 65535u ? 65535u : h);
+            if (lat >= 0.0) rmin = fmin(rmin, lat);
+        }
+        const unsigned long long mb = wave_min_u64(d2bits(rmin));
+        if (lane == 0) {
+            if (out_rowmin) out_rowmin[row] = bits2d(mb);
+            atomicMin(&stats[ST_GLOBAL_MIN], mb);  // shd-topology.c:500-511
+        }
+    }
+    if (lane == 0) {
+        atomicAdd(&stats[ST_RP_POPS], n_pop);
+        atomicAdd(&stats[ST_RP_PUSH], n_push);
+        atomicAdd(&stats[ST_RP_MOD], n_mod);
+        atomicAdd(&stats[ST_RP_ROWS], n_rows);
+    }
+}
+
+}  // namespace
+
+int replay_lds_levels() { return SHD_RP_LDS_LEVELS; }
+
+hipError_t launch_heap_replay(const ReplayCSR& g, const ReplayWs& ws, const uint32_t* d_sources,
+                              const uint32_t* d_rows, int nrows, const uint32_t* d_targets, int A,
+                              int full, double2* out_lr, uint16_t* out_hops, double* out_rowmin,
+                              unsigned long long* d_stats, double* dbg_dist, int32_t* dbg_par,
+                              hipStream_t stream) {
+    const int grid = ws.slots < nrows ? ws.slots : nrows;
+    if (grid < 1) return hipSuccess;
+    if (g.V <= 0 || (dbg_dist && nrows != 1)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(heap_replay_kernel, dim3(grid), dim3(64), 0, stream, g, ws, d_sources,
+                       d_rows, nrows, d_targets, A, full, out_lr, out_hops, out_rowmin, d_stats,
+                       dbg_dist, dbg_par);
+    return hipGetLastError();
+}
+
+}  // namespace shdtopo

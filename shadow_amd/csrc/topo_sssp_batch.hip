@@ -1308,7 +1308,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         rel *= (1.0 - g.aloss[(uint32_t)(memo[y * K + j] & 0x7FFFFFFFull)]);
                     }
                 }
-                if (amb) atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
+                if (amb) {
+                    atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
+                    if (ws.rowflag) ws.rowflag[r0 + (int)j] = 1;  // tie replay (topo_replay.hip)
+                }
                 if (lat == 0.0) lat = 1.0;
             }
             const size_t o = (size_t)(r0 + (int)j) * (size_t)A + k;

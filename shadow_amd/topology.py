@@ -253,6 +253,17 @@ class Topology:
             raise RuntimeError("export_graph failed")
         return V, eu, ev, el, lo, vl
 
+    def replay_source(self, src, full=True):
+        """Test hook (shdtopo_replay_source): the exact heap replay's (dist, parent vertex) from
+        vertex `src`, original ids; full=False stops when every attached vertex is popped."""
+        V = self.num_vertices
+        dist = np.empty(V, np.float64)
+        par = np.empty(V, np.int32)
+        r = self._lib.shdtopo_replay_source(self._h, int(src), int(bool(full)), _p(dist), _p(par))
+        if r != 0:
+            raise RuntimeError("shdtopo_replay_source failed: %d" % r)
+        return dist, par
+
     def write_graphml(self, path):
         if self._lib.shdtopo_write_graphml(self._h, path.encode()) != 0:
             raise RuntimeError("write_graphml failed")

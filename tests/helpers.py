@@ -61,3 +61,70 @@ def rel_close(a, b, tol=1e-12):
     a = np.asarray(a)
     b = np.asarray(b)
     return np.all(np.abs(a - b) <= tol * np.maximum(np.abs(b), 1e-300))
+
+
+_KEYS = ('<key attr.name="packetloss" attr.type="double" for="edge" id="d9" />'
+         '<key attr.name="jitter" attr.type="double" for="edge" id="d8" />'
+         '<key attr.name="latency" attr.type="double" for="edge" id="d7" />'
+         '<key attr.name="type" attr.type="string" for="node" id="d5" />'
+         '<key attr.name="bandwidthup" attr.type="int" for="node" id="d4" />'
+         '<key attr.name="bandwidthdown" attr.type="int" for="node" id="d3" />'
+         '<key attr.name="geocode" attr.type="string" for="node" id="d2" />'
+         '<key attr.name="ip" attr.type="string" for="node" id="d1" />'
+         '<key attr.name="packetloss" attr.type="double" for="node" id="d0" />')
+
+
+def graphml_doc(nodes, edges, directed=False):
+    """GraphML text in the bundled files' key schema.  nodes: (id, type, loss);
+    edges: (src, dst, latency, loss)."""
+    out = ['<?xml version="1.0" encoding="utf-8"?><graphml '
+           'xmlns="http://graphml.graphdrawing.org/xmlns">', _KEYS,
+           '<graph edgedefault="%s">' % ("directed" if directed else "undirected")]
+    for nid, typ, loss in nodes:
+        out.append('<node id="%s"><data key="d0">%r</data><data key="d1">0.0.0.0</data>'
+                   '<data key="d2">US</data><data key="d3">10240</data>'
+                   '<data key="d4">10240</data><data key="d5">%s</data></node>'
+                   % (nid, float(loss), typ))
+    for a, b, lat, loss in edges:
+        out.append('<edge source="%s" target="%s"><data key="d7">%r</data>'
+                   '<data key="d8">0</data><data key="d9">%r</data></edge>'
+                   % (a, b, float(lat), float(loss)))
+    out.append("</graph></graphml>")
+    return "".join(out).encode()
+
+
+def random_topology_graphml(n_routers=600, n_poi=60, extra=2400, seed=3, integer=False,
+                            directed=False, parallel=0):
+    """A connected router graph (a cycle, both directions when directed, plus `extra` random
+    edges), poi vertices with an uplink (a pair of opposite edges when directed) and a self loop.
+    `parallel` extra edges duplicate existing router edges with other latencies (multigraph)."""
+    rng = np.random.default_rng(seed)
+    lat = (lambda: int(rng.integers(1, 101))) if integer else (lambda: rng.uniform(1, 100))
+    nodes = [("pop-%d" % i, "pop", 0.0) for i in range(n_routers)]
+    nodes += [("poi-%d" % k, ("client", "relay", "server")[k % 3], rng.uniform(0, 0.05))
+              for k in range(n_poi)]
+    edges = []
+    for i in range(n_routers):
+        j = (i + 1) % n_routers
+        edges.append(("pop-%d" % i, "pop-%d" % j, lat(), rng.uniform(0, 0.01)))
+        if directed:
+            edges.append(("pop-%d" % j, "pop-%d" % i, lat(), rng.uniform(0, 0.01)))
+    seen = set()
+    while len(seen) < extra:
+        a, b = (int(x) for x in rng.integers(0, n_routers, 2))
+        key = (a, b) if directed else (min(a, b), max(a, b))
+        if a == b or abs(a - b) in (1, n_routers - 1) or key in seen:
+            continue
+        seen.add(key)
+        edges.append(("pop-%d" % a, "pop-%d" % b, lat(), rng.uniform(0, 0.01)))
+    for _ in range(parallel):
+        a, b, _, _ = edges[int(rng.integers(0, len(edges)))]
+        edges.append((a, b, lat(), rng.uniform(0, 0.01)))
+    for k in range(n_poi):
+        r = "pop-%d" % int(rng.integers(0, n_routers))
+        edges.append(("poi-%d" % k, r, 5.0, 0.0))
+        if directed:
+            edges.append((r, "poi-%d" % k, float(lat()), 0.0))
+        edges.append(("poi-%d" % k, "poi-%d" % k, 1.0, 0.0))
+    order = rng.permutation(len(edges))  # edge ids not grouped by vertex
+    return graphml_doc(nodes, [edges[i] for i in order], directed)

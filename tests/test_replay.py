@@ -1,0 +1,142 @@
+"""GPU parity of the exact heap replay (topo_replay.hip) against the igraph-0.7 restatement.
+
+The replay runs igraph_get_shortest_paths_dijkstra with its two-way heap operation for operation
+(oracle/oracle.c:146-305 is the restated spec), so on integer latencies -- where many vertices
+have several candidate parents at the same d[u] and igraph's pop order decides -- every
+distance AND every parent must equal the oracle's.  Through the table path this resolves the rows
+the batch kernel flags (ambiguous_pairs), directed topologies and multigraphs.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import shadow_amd as sa
+from helpers import attach_hosts, random_topology_graphml, synthetic_pair
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("integer", [True, False])
+def test_replay_full_dijkstra_parents_match_oracle(integer):
+    """Full Dijkstra (no early exit): dist bit-exact and the parent of EVERY vertex equal to the
+    oracle heap's, ties included."""
+    top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
+    otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay", "server"])
+    srcs = sorted(set(verts))[:4] + [0, g.V // 2]
+    nties = 0
+    for s in srcs:
+        d, p = top.replay_source(s, full=True)
+        od, opv, _, _ = g.dijkstra(s)
+        assert np.array_equal(d.view(np.uint64), od.view(np.uint64)), s
+        assert np.array_equal(p, opv), (s, int(np.sum(p != opv)))
+        nties += int(np.sum(g.parent_ties(od, s) >= 2))
+    if integer:
+        assert nties > 50  # the case the replay exists for
+
+
+def test_replay_early_exit_matches_oracle():
+    """The reference's early exit (all attached targets popped): every vertex popped before it
+    has the oracle's parent."""
+    top, g = synthetic_pair(seed=12, n_routers=2500, n_poi=120, n_edges=25000, integer=True)
+    otop, ips, verts = attach_hosts(top, g, 200, type_hints=["client", "relay"])
+    targets = np.asarray(sorted(set(verts)), np.int32)
+    for s in targets[:5]:
+        d, p = top.replay_source(int(s), full=False)
+        od, opv, _, rank = g.dijkstra(int(s), targets)
+        popped = rank >= 0
+        assert popped[targets].all()
+        assert np.array_equal(d[popped].view(np.uint64), od[popped].view(np.uint64))
+        assert np.array_equal(p[popped], opv[popped])
+
+
+@pytest.mark.parametrize("batch", [8, 1])
+def test_integer_ties_table_bit_exact(batch):
+    """Integer latencies U{1..100}: every pair of the table -- hops and reliability included --
+    bit-exact against the oracle; the tie rows went through the replay."""
+    top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=True)
+    top.set_option("batch", batch)
+    otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(a, oa)
+    assert st["errors"] == 0
+    assert st["ambiguous_pairs"] > 0 and st["replay_rows"] > 0
+    assert st["replay_pops"] > 0 and st["replay_ms"] > 0
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert top.getMinimumLatency() == olat.min()
+
+
+def test_tie_replay_off_reports_only():
+    """tie_replay = 0: the batch kernel's table stands (latencies exact), nothing replayed."""
+    top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=True)
+    top.set_option("tie_replay", 0)
+    otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    oa, olat, orel, ohops = g.table(verts)
+    assert st["ambiguous_pairs"] > 0 and st["replay_rows"] == 0
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+
+
+def test_replay_all_equals_oracle_continuous():
+    """replay_all: the replay alone builds the whole table (continuous latencies)."""
+    top, g = synthetic_pair(seed=5, n_routers=1500, n_poi=80, n_edges=15000)
+    top.set_option("replay_all", 1)
+    otop, ips, verts = attach_hosts(top, g, 200, type_hints=["client", "relay"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    oa, olat, orel, ohops = g.table(verts)
+    assert st["replay_rows"] == len(a) and st["errors"] == 0
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+
+
+@pytest.mark.parametrize("integer", [False, True])
+def test_directed_topology_table(integer):
+    """Directed non-complete topology (igraph mode OUT, shd-topology.c:153,762-763): the table
+    is built by the replay over out-edge rows, bit-exact against the oracle; getters answer
+    forward rows only (no reverse lookup for directed graphs, shd-topology.c:896-898)."""
+    data = random_topology_graphml(n_routers=500, n_poi=50, extra=2500, seed=7, integer=integer,
+                                   directed=True)
+    top = sa.Topology.from_buffer(data)
+    g = oracle.OGraph.from_graphml(data)
+    assert top.is_directed and g.directed and not top.is_complete
+    otop, ips, verts = attach_hosts(top, g, 120, type_hints=["client", "relay", "server"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(a, oa)
+    assert st["errors"] == 0 and st["replay_rows"] == len(a)
+    assert not np.array_equal(lat, lat.T)  # really directed
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    # lazy getters against the reference cache (forward rows only)
+    rng = np.random.default_rng(2)
+    for _ in range(200):
+        x, y = (int(v) for v in rng.choice(ips, 2))
+        assert top.latency_ip(x, y) == otop.get_latency(x, y)
+        assert top.reliability_ip(x, y) == otop.get_reliability(x, y)
+    assert top.lazyMinimumLatency() == otop.minimum_path_latency
+
+
+@pytest.mark.parametrize("directed", [False, True])
+def test_multigraph_table(directed):
+    """Parallel edges with different latencies: the reference sums the igraph_get_eid edge of
+    each hop (lowest edge id, as the oracle); every row goes through the replay."""
+    data = random_topology_graphml(n_routers=400, n_poi=40, extra=1600, seed=9, integer=True,
+                                   directed=directed, parallel=300)
+    top = sa.Topology.from_buffer(data)
+    g = oracle.OGraph.from_graphml(data)
+    otop, ips, verts = attach_hosts(top, g, 80, type_hints=["client", "relay"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    oa, olat, orel, ohops = g.table(verts)
+    assert st["errors"] == 0 and st["replay_rows"] == len(a)
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
