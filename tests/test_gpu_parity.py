@@ -214,12 +214,17 @@ def test_minimum_latency_simple_config1():
     assert data_top.getMinimumLatency() == 20.0
 
 
+def _oracle_threads():
+    import os
+    return max(1, min(64, (os.cpu_count() or 8)))
+
+
 def test_sssp_full_size_c4_sampled_rows():
-    """BASELINE config 4 at full size (1M vertices / 10M edges, the bench workload): three rows
-    (first, middle, last source) bit-exact against the oracle's Dijkstra + helper, and
-    size-independent properties of the whole 9,999 x 9,999 table: every latency finite and
-    > 0, reliability in (0, 1], the diagonal is the self loop (1 hop), no overflow fallback,
-    and the kernel's row minima equal the table's."""
+    """BASELINE config 4 at full size (1M vertices / 10M edges, the bench workload): 128 seeded
+    rows bit-exact against the oracle's Dijkstra + helper (the box's host cores run them in a few
+    seconds), and size-independent properties of the whole 9,999 x 9,999 table: every latency
+    finite and > 0, reliability in (0, 1], the diagonal is the self loop (1 hop), no overflow
+    fallback, nothing to replay, and the kernel's row minima equal the table's."""
     import torch
     top = sa.Topology.synthetic(seed=20261015)
     assert top.num_vertices == 1_000_000 and top.num_edges == 10_000_000
@@ -233,6 +238,7 @@ def test_sssp_full_size_c4_sampled_rows():
     torch.cuda.synchronize()
     st = top.stats()
     assert st["errors"] == 0 and st["ambiguous_pairs"] == 0 and st["far_scan_sources"] == 0
+    assert st["replay_rows"] == 0
     lat = lr[..., 0]
     rel = lr[..., 1]
     assert bool(torch.isfinite(lat).all()) and bool((lat > 0).all())
@@ -240,14 +246,40 @@ def test_sssp_full_size_c4_sampled_rows():
     diag = torch.arange(A, device="cuda")
     assert bool((hp[diag, diag] == 1).all()) and bool((hp >= 1).all())
     assert torch.equal(rm, lat.min(dim=1).values)
-    rows = [0, A // 2, A - 1]
+    rows = np.sort(np.random.default_rng(20261015).choice(A, 128, replace=False))
     V, eu, ev, elat, eloss, vloss = top.export_graph()
     g = oracle.OGraph(V, eu, ev, elat, eloss, vloss)
-    olat, orel, ohops = g.source_rows(att[rows], att, nthreads=3)
-    glr = lr[rows].cpu().numpy()
+    olat, orel, ohops = g.source_rows(att[rows], att, nthreads=_oracle_threads())
+    glr = lr[torch.from_numpy(rows).cuda()].cpu().numpy()
     assert np.array_equal(glr[..., 0].view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(glr[..., 1].view(np.uint64), orel.view(np.uint64))
-    assert np.array_equal(hp[rows].cpu().numpy().view(np.uint16), ohops.astype(np.uint16))
+    ghp = hp[torch.from_numpy(rows).cuda()].cpu().numpy().view(np.uint16)
+    assert np.array_equal(ghp, ohops.astype(np.uint16))
+
+
+def test_sssp_full_size_c4_int_rows():
+    """C4-int at full size (1M vertices / 10M edges, integer latencies U{1..100}: 45 % of the
+    table's pairs cross a d-tied parent): 64 consecutive rows through the batch kernel + heap
+    replay, every pair bit-exact against the oracle (latency, reliability, hops)."""
+    import torch
+    top = sa.Topology.synthetic(seed=20261015, integer_latency=True)
+    top.synth_packets(20261015, 100_000, 1000, 10**9, 10**7)
+    att = top.attached_vertices()
+    A = len(att)
+    r0, r1 = 4000, 4064
+    lr = torch.empty((r1 - r0, A, 2), dtype=torch.float64, device="cuda")
+    hp = torch.empty((r1 - r0, A), dtype=torch.int16, device="cuda")
+    top.build_rows_into(r0, r1, lr, hp)
+    torch.cuda.synchronize()
+    st = top.stats()
+    assert st["errors"] == 0 and st["ambiguous_pairs"] > 0 and st["replay_rows"] > 0
+    V, eu, ev, elat, eloss, vloss = top.export_graph()
+    g = oracle.OGraph(V, eu, ev, elat, eloss, vloss)
+    olat, orel, ohops = g.source_rows(att[r0:r1], att, nthreads=_oracle_threads())
+    glr = lr.cpu().numpy()
+    assert np.array_equal(glr[..., 0].view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(glr[..., 1].view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hp.cpu().numpy().view(np.uint16), ohops.astype(np.uint16))
 
 
 def _grid_graphml(n=30, n_poi=60, seed=5):

@@ -1,0 +1,33 @@
+"""Probe: heap-replay cost on C4-int (integer latencies) for a row range, per row and per heap op.
+usage: python tools/replay_probe.py ROWS [SLOTS]"""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+import shadow_amd as sa  # noqa: E402
+
+rows = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+slots = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+t0 = time.time()
+top = sa.Topology.synthetic(seed=20261015, integer_latency=True)
+top.synth_packets(20261015, 100_000, 1000, 10**9, 10**7)
+A = len(top.attached_vertices())
+print("gen %.1fs A=%d" % (time.time() - t0, A), flush=True)
+if slots:
+    top.set_option("replay_slots", slots)
+lr = torch.empty((rows, A, 2), dtype=torch.float64, device="cuda")
+hp = torch.empty((rows, A), dtype=torch.int16, device="cuda")
+for mode in ("batch+replay", "replay_all"):
+    top.set_option("replay_all", 1 if mode == "replay_all" else 0)
+    t0 = time.time()
+    top.build_rows_into(0, rows, lr, hp)
+    torch.cuda.synchronize()
+    st = top.stats()
+    r = max(1, st["replay_rows"])
+    print("%s: wall %.2fs sssp %.1f ms replay %.1f ms rows %d slots %d ambiguous %d | per row: "
+          "pops %.0f pushes %.0f mods %.0f" % (
+              mode, time.time() - t0, st["sssp_kernel_ms"], st["replay_ms"], st["replay_rows"],
+              st["replay_slots"], st["ambiguous_pairs"], st["replay_pops"] / r,
+              st["replay_pushes"] / r, st["replay_modifies"] / r), flush=True)
