@@ -110,6 +110,8 @@ int shdtopo_set_option(Topology* top, const char* key, double value);
 int32_t shdtopo_attach_ip(Topology* top, uint32_t ip, uint32_t* rngState, const char* ipHint,
                           const char* geocodeHint, const char* typeHint, uint64_t* bwDownOut,
                           uint64_t* bwUpOut);
+/* topology_detach by raw IP (shd-topology.c:1190-1197: the mapping goes, cached paths stay) */
+void shdtopo_detach_ip(Topology* top, uint32_t ip);
 double shdtopo_get_latency_ip(Topology* top, uint32_t srcIP, uint32_t dstIP);
 double shdtopo_get_reliability_ip(Topology* top, uint32_t srcIP, uint32_t dstIP);
 
@@ -178,6 +180,8 @@ typedef struct {
     int64_t replay_pushes;    /*   pushes (first reach) and */
     int64_t replay_modifies;  /*   modifies (strict improvement of a queued vertex) */
     int64_t replay_slots;     /* concurrent replay wavefronts of the last launch */
+    int64_t route_bad_packets; /* packets with a column outside [0, A), not routed (delivered 0,
+                                  time 0, state unchanged), since the last table build */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -37,7 +37,7 @@ class ShdStats(ctypes.Structure):
                 ("slots", i64), ("events", i64 * 8), ("far_scan_sources", i64), ("split_ms", dbl),
                 ("batch", i64), ("lds_hubs", i64), ("replay_rows", i64), ("replay_ms", dbl),
                 ("replay_pops", i64), ("replay_pushes", i64), ("replay_modifies", i64),
-                ("replay_slots", i64)]
+                ("replay_slots", i64), ("route_bad_packets", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):
@@ -60,6 +60,7 @@ SIGNATURES = {
     "shdtopo_new_from_buffer": (P, [cstr, ctypes.c_size_t]),
     "shdtopo_set_option": (ctypes.c_int, [P, cstr, dbl]),
     "shdtopo_attach_ip": (i32, [P, u32, P, cstr, cstr, cstr, P, P]),
+    "shdtopo_detach_ip": (None, [P, u32]),
     "shdtopo_get_latency_ip": (dbl, [P, u32, u32]),
     "shdtopo_get_reliability_ip": (dbl, [P, u32, u32]),
     "shdtopo_num_vertices": (i64, [P]),

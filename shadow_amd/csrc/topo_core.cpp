@@ -123,8 +123,6 @@ struct _Topology {
     // table geometry
     std::mutex buildMu;
     std::atomic<bool> tableValid{false};
-    std::atomic<bool> hostValid{false};
-    std::atomic<bool> rowminValid{false};  // hrowmin mirrors d_rowmin (lazy batch orientation)
     std::vector<int32_t> attached;  // columns: distinct attached vertices, ascending
     std::vector<int32_t> colOf;     // vertex -> column
     int64_t A = 0;
@@ -185,14 +183,29 @@ struct _Topology {
     hipEvent_t evr0 = nullptr, evr1 = nullptr;
     bool replayPending = false;
 
-    // host mirror of the table (for the per-call getters)
-    std::vector<double> hlat, hrel, hrowmin;
-    std::vector<uint16_t> hhops;
+    // host mirror of the table for the per-call getters: an immutable snapshot swapped atomically
+    // (getters on worker threads never see a table being rebuilt)
+    std::shared_ptr<const HostTable> snap;
     double eagerMin = -1.0;
 
-    // lazy emulation
-    std::unique_ptr<std::atomic<uint8_t>[]> matRow;    // per vertex (SSSP branch)
-    std::unique_ptr<std::atomic<uint64_t>[]> matPair;  // per (vertex pair) bit (complete branch)
+    // attached-set generations: setGen bumps whenever a vertex gains its first or loses its last
+    // host (the table's columns change); tableGen = the setGen the device table was built for
+    std::atomic<uint64_t> setGen{1};
+    uint64_t tableGen = 0;
+    std::atomic<uint64_t> tableSerial{0};  // bumps on every device table build / bind
+    bool geomInit = false;
+
+    // lazy emulation.  SSSP branch: the reference's cache holds (s, t) iff
+    // row s was computed (computeSourcePaths) at a moment t was attached; rows are recomputed on
+    // a miss.  Epochs are ipGen values: per vertex the attach intervals [start, end) of "at
+    // least one host on it", per source vertex the epochs it was materialised at.
+    std::vector<uint32_t> hostsOn;                             // hosts per vertex (ipMu)
+    std::unordered_map<int32_t, std::vector<std::pair<uint64_t, uint64_t>>> ivals;  // (ipMu)
+    std::atomic<uint64_t> lastNewEpoch{0};                     // latest interval start
+    std::unique_ptr<std::atomic<uint64_t>[]> matGen;          // per vertex: latest epoch
+    std::unordered_map<int32_t, std::vector<uint64_t>> matEpochs;  // all epochs (lazyMu)
+    std::mutex lazyMu;
+    std::unique_ptr<std::atomic<uint64_t>[]> matPair;  // per (column pair) bit (complete branch)
     size_t matPairWords = 0;
     std::mutex minMu;
     double lazyMin = 0.0;  // top->minimumPathLatency
@@ -303,8 +316,9 @@ bool check_graph(Topology* top) {
             top->isComplete ? "complete" : "incomplete",
             top->isDirected ? "directed" : "undirected", g.V, (long long)g.E);
     top->aidx.build(g);
-    top->matRow.reset(new std::atomic<uint8_t>[(size_t)g.V]);
-    for (int32_t v = 0; v < g.V; v++) top->matRow[(size_t)v].store(0);
+    top->matGen.reset(new std::atomic<uint64_t>[(size_t)g.V]);
+    for (int32_t v = 0; v < g.V; v++) top->matGen[(size_t)v].store(0);
+    top->hostsOn.assign((size_t)g.V, 0u);
     return true;
 }
 
@@ -851,35 +865,36 @@ int upload_target_bits(Topology* top, const std::vector<uint32_t>& tgt, hipStrea
     return 0;
 }
 
-// columns = distinct attached vertices in ascending vertex order
-void compute_geometry(Topology* top) {
+// columns = distinct attached vertices in ascending vertex order.  Caller holds buildMu.
+// Returns the setGen the geometry corresponds to; a changed attached set invalidates the table.
+uint64_t compute_geometry(Topology* top) {
     std::vector<int32_t> vs;
-    bool same;
+    uint64_t sg;
     {
         std::shared_lock<std::shared_mutex> lk(top->ipMu);
-        same = top->geomGen == top->ipGen;  // no attach / detach since the last call
-        if (!same) {
-            top->geomGen = top->ipGen;
-            vs.reserve(top->virtualIP.size());
-            for (auto& kv : top->virtualIP)
-                if (kv.second >= 0) vs.push_back(kv.second);
-        }
+        sg = top->setGen.load();
+        if (top->geomInit && top->geomGen == top->ipGen) return sg;  // no attach / detach since
+        top->geomGen = top->ipGen;
+        vs.reserve(top->virtualIP.size());
+        for (auto& kv : top->virtualIP)
+            if (kv.second >= 0) vs.push_back(kv.second);
     }
-    if (!same) {
-        std::sort(vs.begin(), vs.end());
-        vs.erase(std::unique(vs.begin(), vs.end()), vs.end());
-        top->attached = vs;
-        top->A = (int64_t)vs.size();
-        top->colOf.assign((size_t)top->g.V, -1);
-        for (size_t i = 0; i < vs.size(); i++) top->colOf[(size_t)vs[i]] = (int32_t)i;
-    }
-    // complete branch materialisation bits are per (attached pair), cleared on every build
+    std::sort(vs.begin(), vs.end());
+    vs.erase(std::unique(vs.begin(), vs.end()), vs.end());
+    if (top->geomInit && vs == top->attached) return sg;
+    top->geomInit = true;
+    top->attached = vs;
+    top->A = (int64_t)vs.size();
+    top->colOf.assign((size_t)top->g.V, -1);
+    for (size_t i = 0; i < vs.size(); i++) top->colOf[(size_t)vs[i]] = (int32_t)i;
+    top->tableValid.store(false);
+    // complete-branch materialisation bits are per column pair: a new geometry starts them over
+    // (a re-touched pair re-offers a latency >= the running minimum: a no-op, shd-topology.c:501)
     const size_t words = (size_t)((top->A * top->A + 63) / 64);
-    if (!top->matPair || words != top->matPairWords) {
-        top->matPairWords = words;
-        top->matPair.reset(new std::atomic<uint64_t>[words ? words : 1]);
-    }
-    for (size_t i = 0; i < top->matPairWords; i++) top->matPair[i].store(0, std::memory_order_relaxed);
+    top->matPairWords = words;
+    top->matPair.reset(new std::atomic<uint64_t>[words ? words : 1]);
+    for (size_t i = 0; i < std::max<size_t>(1, words); i++) top->matPair[i].store(0, std::memory_order_relaxed);
+    return sg;
 }
 
 double default_delta(Topology* top) {
@@ -1095,76 +1110,88 @@ void push_min_to_engine(double m) {
     if (worker_updateMinTimeJump && m > 0) worker_updateMinTimeJump(m);
 }
 
-// whole-table build on this GPU
+bool table_current(Topology* top) {
+    return top->tableValid.load(std::memory_order_acquire) && top->tableGen == top->setGen.load();
+}
+
+// whole-table build on this GPU (for the current attached set)
 int ensure_table(Topology* top) {
-    if (top->tableValid.load(std::memory_order_acquire)) return 0;
+    if (table_current(top)) return 0;
     std::lock_guard<std::mutex> lk(top->buildMu);
-    if (top->tableValid.load()) return 0;
+    if (table_current(top)) return 0;
     int r = dev_init(top);
     if (r) return r;
-    compute_geometry(top);
+    const uint64_t sg = compute_geometry(top);
     const int64_t A = top->A;
-    if (A == 0) {
-        top->tableValid.store(true);
+    if (A > 0) {
+        HIPCHK(top->d_lr.ensure((size_t)(A * A)));
+        HIPCHK(top->d_hops.ensure((size_t)(A * A)));
+        HIPCHK(top->d_rowmin.ensure((size_t)A));
+        r = enqueue_rows(top, 0, A, top->d_lr.p, top->d_hops.p, top->d_rowmin.p, top->stream);
+        if (r) return r;
+        r = collect_row_stats(top);
+        if (r) return r;
+        if (top->stats.errors) {
+            CRITICAL("%lld attached pairs have no path/edge (e.g. a vertex without self loop)",
+                     (long long)top->stats.errors);
+        }
+    }
+    top->tableGen = sg;
+    top->tableSerial.fetch_add(1);
+    top->tableValid.store(true, std::memory_order_release);
+    if (!top->lazy && A > 0) push_min_to_engine(top->eagerMin);
+    return 0;
+}
+
+// Host snapshot of the current device table: column map + row minima, and (full) the whole
+// A x A lat / rel / hops mirror.  Published atomically; readers keep the old one alive.
+int ensure_snapshot(Topology* top, bool full, std::shared_ptr<const HostTable>* out) {
+    for (int attempt = 0; attempt < 4; attempt++) {
+        int r = ensure_table(top);
+        if (r) return r;
+        std::shared_ptr<const HostTable> cur = std::atomic_load(&top->snap);
+        if (cur && cur->serial == top->tableSerial.load() && (cur->full || !full) &&
+            table_current(top)) {
+            *out = cur;
+            return 0;
+        }
+        std::lock_guard<std::mutex> lk(top->buildMu);
+        if (!table_current(top)) continue;  // an attach / detach raced: rebuild first
+        cur = std::atomic_load(&top->snap);
+        if (cur && cur->serial == top->tableSerial.load() && (cur->full || !full)) {
+            *out = cur;
+            return 0;
+        }
+        auto h = std::make_shared<HostTable>();
+        h->gen = top->tableGen;
+        h->serial = top->tableSerial.load();
+        h->A = top->A;
+        h->colOf = top->colOf;
+        const size_t A = (size_t)top->A, n = A * A;
+        h->rowmin.resize(A);
+        if (A) HIPCHK(hipMemcpy(h->rowmin.data(), top->d_rowmin.p, sizeof(double) * A, hipMemcpyDeviceToHost));
+        if (full) {
+            h->full = true;
+            std::vector<double2> lr(n);
+            h->hops.resize(n);
+            if (n) {
+                HIPCHK(hipMemcpy(lr.data(), top->d_lr.p, sizeof(double2) * n, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(h->hops.data(), top->d_hops.p, sizeof(uint16_t) * n, hipMemcpyDeviceToHost));
+            }
+            h->lat.resize(n);
+            h->rel.resize(n);
+            for (size_t i = 0; i < n; i++) {
+                h->lat[i] = lr[i].x;
+                h->rel[i] = lr[i].y;
+            }
+        }
+        std::shared_ptr<const HostTable> hc = h;
+        std::atomic_store(&top->snap, hc);
+        *out = hc;
         return 0;
     }
-    HIPCHK(top->d_lr.ensure((size_t)(A * A)));
-    HIPCHK(top->d_hops.ensure((size_t)(A * A)));
-    HIPCHK(top->d_rowmin.ensure((size_t)A));
-    r = enqueue_rows(top, 0, A, top->d_lr.p, top->d_hops.p, top->d_rowmin.p, top->stream);
-    if (r) return r;
-    r = collect_row_stats(top);
-    if (r) return r;
-    if (top->stats.errors) {
-        CRITICAL("%lld attached pairs have no path/edge (e.g. a vertex without self loop)",
-                 (long long)top->stats.errors);
-    }
-    top->hostValid.store(false);
-    top->rowminValid.store(false);
-    top->tableValid.store(true, std::memory_order_release);
-    if (!top->lazy) push_min_to_engine(top->eagerMin);
-    return 0;
-}
-
-int ensure_host(Topology* top) {
-    int r = ensure_table(top);
-    if (r) return r;
-    if (top->hostValid.load(std::memory_order_acquire)) return 0;
-    std::lock_guard<std::mutex> lk(top->buildMu);
-    if (top->hostValid.load()) return 0;
-    const size_t n = (size_t)(top->A * top->A);
-    std::vector<double2> lr(n);
-    top->hhops.resize(n);
-    top->hrowmin.resize((size_t)top->A);
-    if (n) {
-        HIPCHK(hipMemcpy(lr.data(), top->d_lr.p, sizeof(double2) * n, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(top->hhops.data(), top->d_hops.p, sizeof(uint16_t) * n, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(top->hrowmin.data(), top->d_rowmin.p, sizeof(double) * (size_t)top->A, hipMemcpyDeviceToHost));
-    }
-    top->hlat.resize(n);
-    top->hrel.resize(n);
-    for (size_t i = 0; i < n; i++) {
-        top->hlat[i] = lr[i].x;
-        top->hrel[i] = lr[i].y;
-    }
-    top->hostValid.store(true, std::memory_order_release);
-    top->rowminValid.store(true, std::memory_order_release);
-    return 0;
-}
-
-// Row minima on the host without the full table mirror (lazy min pushes of batched routes).
-int ensure_rowmin_host(Topology* top) {
-    int r = ensure_table(top);
-    if (r) return r;
-    if (top->rowminValid.load(std::memory_order_acquire)) return 0;
-    std::lock_guard<std::mutex> lk(top->buildMu);
-    if (top->rowminValid.load()) return 0;
-    top->hrowmin.resize((size_t)top->A);
-    if (top->A)
-        HIPCHK(hipMemcpy(top->hrowmin.data(), top->d_rowmin.p, sizeof(double) * (size_t)top->A,
-                         hipMemcpyDeviceToHost));
-    top->rowminValid.store(true, std::memory_order_release);
-    return 0;
+    CRITICAL("the attached set keeps changing while the routing table is built");
+    return -5;
 }
 
 int32_t vertex_of_ip(Topology* top, uint32_t ip) {
@@ -1182,31 +1209,67 @@ void lazy_store_min(Topology* top, double lat) {
     }
 }
 
+// Does the reference's cache hold (s, t)?  Only if row s was computed at an epoch when t was
+// attached (shd-topology.c:690-744 build the targets from the attached set of that moment).
+// Fast path: s materialised after the latest attach interval started covers every vertex
+// attached now (the only ones a query can name).
+bool lazy_covered(Topology* top, int32_t s, int32_t t) {
+    const uint64_t g = top->matGen[(size_t)s].load(std::memory_order_acquire);
+    if (g == 0) return false;
+    if (g >= top->lastNewEpoch.load(std::memory_order_acquire)) return true;
+    std::lock_guard<std::mutex> lk(top->lazyMu);
+    std::shared_lock<std::shared_mutex> lk2(top->ipMu);
+    auto m = top->matEpochs.find(s);
+    auto iv = top->ivals.find(t);
+    if (m == top->matEpochs.end() || iv == top->ivals.end()) return false;
+    for (uint64_t e : m->second)
+        for (const auto& p : iv->second)
+            if (p.first <= e && e < p.second) return true;
+    return false;
+}
+
+// computeSourcePaths(s) now: row s over the current targets enters the cache and its minimum the
+// running minimum (shd-topology.c:808-823, :500-511)
+void lazy_materialise(Topology* top, int32_t s, double rowmin) {
+    uint64_t e;
+    {
+        std::shared_lock<std::shared_mutex> lk(top->ipMu);
+        e = top->ipGen;
+    }
+    {
+        std::lock_guard<std::mutex> lk(top->lazyMu);
+        auto& v = top->matEpochs[s];
+        if (v.empty() || v.back() != e) v.push_back(e);
+    }
+    uint64_t old = top->matGen[(size_t)s].load();
+    while (old < e && !top->matGen[(size_t)s].compare_exchange_weak(old, e)) {
+    }
+    if (rowmin > 0 && !std::isinf(rowmin)) lazy_store_min(top, rowmin);
+}
+
 // First-rooted-wins orientation of the SSSP branch (shd-topology.c:894-915):
-// (s,d) is answered from row s if s's paths are materialised, else from row d if d's are and
-// the graph is undirected, else s's row is materialised now (its minimum enters the running
-// minimum, shd-topology.c:500-511).  Returns true when the answer comes from row d.
-bool lazy_orient_row(Topology* top, int32_t s, int32_t d, int64_t cs, int64_t cd) {
-    (void)cd;
-    if (top->matRow[(size_t)s].load(std::memory_order_acquire)) return false;
-    if (!top->isDirected && top->matRow[(size_t)d].load(std::memory_order_acquire)) return true;
-    uint8_t was = top->matRow[(size_t)s].exchange(1);
-    if (!was && top->hrowmin[(size_t)cs] > 0 && !std::isinf(top->hrowmin[(size_t)cs]))
-        lazy_store_min(top, top->hrowmin[(size_t)cs]);
+// (s,d) is answered from row s if the cache holds (s,d), else from row d if it holds (d,s) and
+// the graph is undirected, else s's row is computed now.  Returns true when the answer comes
+// from row d.
+bool lazy_orient_row(Topology* top, const HostTable& h, int32_t s, int32_t d) {
+    if (lazy_covered(top, s, d)) return false;
+    if (!top->isDirected && lazy_covered(top, d, s)) return true;
+    lazy_materialise(top, s, h.rowmin[(size_t)h.colOf[(size_t)s]]);
     return false;
 }
 
 // Per-pair first touch of the complete branch (shd-topology.c:894-915 + :835-873): the pair's
 // values are symmetric bit for bit, only the running minimum depends on the order.
-void lazy_touch_pair(Topology* top, int64_t cs, int64_t cd) {
-    const int64_t A = top->A;
+void lazy_touch_pair(Topology* top, const HostTable& h, int64_t cs, int64_t cd) {
+    const int64_t A = h.A;
     const size_t b1 = (size_t)(cs * A + cd), b2 = (size_t)(cd * A + cs);
+    if (top->matPairWords * 64 < (size_t)(A * A)) return;  // geometry moved on (raced)
     bool have = (top->matPair[b1 >> 6].load(std::memory_order_relaxed) >> (b1 & 63)) & 1;
     if (!have && !top->isDirected)
         have = (top->matPair[b2 >> 6].load(std::memory_order_relaxed) >> (b2 & 63)) & 1;
     if (!have) {
         uint64_t old = top->matPair[b1 >> 6].fetch_or(1ull << (b1 & 63));
-        if (!((old >> (b1 & 63)) & 1) && top->hlat[b1] > 0) lazy_store_min(top, top->hlat[b1]);
+        if (!((old >> (b1 & 63)) & 1) && h.lat[b1] > 0) lazy_store_min(top, h.lat[b1]);
     }
 }
 
@@ -1222,23 +1285,28 @@ bool get_path_entry(Topology* top, uint32_t srcIP, uint32_t dstIP, double* lat, 
         CRITICAL("invalid vertex %d, destination address is not connected to topology", d);
         return false;
     }
-    int r = ensure_host(top);
+    std::shared_ptr<const HostTable> h;
+    int r = ensure_snapshot(top, true, &h);
     if (r) {
         fatal_or_continue(top, "unable to build the routing table");
         return false;
     }
-    const int64_t A = top->A;
-    int64_t cs = top->colOf[(size_t)s], cd = top->colOf[(size_t)d];
+    const int64_t A = h->A;
+    const int64_t cs = h->colOf[(size_t)s], cd = h->colOf[(size_t)d];
+    if (cs < 0 || cd < 0) {  // detached / re-attached while this call ran
+        CRITICAL("address is not connected to the current routing table");
+        return false;
+    }
     size_t k;
     if (top->isComplete) {
         k = (size_t)(cs * A + cd);
-        if (top->lazy) lazy_touch_pair(top, cs, cd);
+        if (top->lazy) lazy_touch_pair(top, *h, cs, cd);
     } else if (!top->lazy) {
         k = (size_t)(cs * A + cd);
     } else {
-        k = lazy_orient_row(top, s, d, cs, cd) ? (size_t)(cd * A + cs) : (size_t)(cs * A + cd);
+        k = lazy_orient_row(top, *h, s, d) ? (size_t)(cd * A + cs) : (size_t)(cs * A + cd);
     }
-    double L = top->hlat[k], R = top->hrel[k];
+    double L = h->lat[k], R = h->rel[k];
     if (L < 0) {
         // the reference error()s: "unable to find path between node ..." (shd-topology.c:924)
         fatal_or_continue(top, "unable to find path between attached vertices");
@@ -1318,23 +1386,52 @@ int32_t find_attachment_vertex(Topology* top, const char* ipHint, const char* ge
     return (*cands)[(size_t)chosen];
 }
 
+// hosts-per-vertex bookkeeping (caller holds ipMu exclusively, ipGen already advanced): a vertex
+// gaining its first host opens an attach interval, losing its last closes it; both change the
+// table's columns (setGen)
+void host_on(Topology* top, int32_t v) {
+    if (top->hostsOn[(size_t)v]++ == 0) {
+        top->ivals[v].push_back({top->ipGen, UINT64_MAX});
+        top->lastNewEpoch.store(top->ipGen);
+        top->setGen.fetch_add(1);
+    }
+}
+void host_off(Topology* top, int32_t v) {
+    if (--top->hostsOn[(size_t)v] == 0) {
+        auto& iv = top->ivals[v];
+        if (!iv.empty()) iv.back().second = top->ipGen;
+        top->setGen.fetch_add(1);
+    }
+}
+
+// shd-topology.c:1154-1166: g_hash_table_replace(virtualIP, ip, vertex)
 void do_attach(Topology* top, uint32_t ip, int32_t v, uint64_t* bwDownOut, uint64_t* bwUpOut) {
     {
         std::unique_lock<std::shared_mutex> lk(top->ipMu);
+        auto it = top->virtualIP.find(ip);
+        const int32_t old = it == top->virtualIP.end() ? -1 : it->second;
         top->virtualIP[ip] = v;
         top->ipGen++;
+        if (old != v) {
+            if (old >= 0) host_off(top, old);
+            if (v >= 0) host_on(top, v);
+        }
     }
     if (v >= 0) {
         if (bwUpOut) *bwUpOut = (uint64_t)top->g.vbwup[(size_t)v];
         if (bwDownOut) *bwDownOut = (uint64_t)top->g.vbwdown[(size_t)v];
-        // an attach onto a vertex outside the current columns invalidates the table
-        if (top->tableValid.load() && ((size_t)v >= top->colOf.size() || top->colOf[(size_t)v] < 0)) {
-            std::lock_guard<std::mutex> lk(top->buildMu);
-            top->tableValid.store(false);
-            top->hostValid.store(false);
-    top->rowminValid.store(false);
-        }
     }
+}
+
+// shd-topology.c:1190-1197: only the IP mapping goes; cached paths stay
+void do_detach(Topology* top, uint32_t ip) {
+    std::unique_lock<std::shared_mutex> lk(top->ipMu);
+    auto it = top->virtualIP.find(ip);
+    if (it == top->virtualIP.end()) return;
+    const int32_t v = it->second;
+    top->virtualIP.erase(it);
+    top->ipGen++;
+    if (v >= 0) host_off(top, v);
 }
 
 }  // namespace
@@ -1448,9 +1545,11 @@ int32_t shdtopo_attach_ip(Topology* top, uint32_t ip, uint32_t* rngState, const 
 
 void topology_detach(Topology* top, Address* address) {
     if (!top || !address || !address_toNetworkIP) return;
-    uint32_t ip = address_toNetworkIP(address);
-    std::unique_lock<std::shared_mutex> lk(top->ipMu);
-    if (top->virtualIP.erase(ip)) top->ipGen++;
+    do_detach(top, address_toNetworkIP(address));
+}
+
+void shdtopo_detach_ip(Topology* top, uint32_t ip) {
+    if (top) do_detach(top, ip);
 }
 
 double shdtopo_get_latency_ip(Topology* top, uint32_t srcIP, uint32_t dstIP) {
@@ -1499,14 +1598,14 @@ int shdtopo_is_directed(Topology* top) { return top ? (int)top->isDirected : -1;
 int64_t shdtopo_num_attached(Topology* top) {
     if (!top) return -1;
     std::lock_guard<std::mutex> lk(top->buildMu);
-    if (!top->tableValid.load()) compute_geometry(top);
+    compute_geometry(top);
     return top->A;
 }
 
 int64_t shdtopo_attached_vertices(Topology* top, int32_t* out, int64_t cap) {
     if (!top) return -1;
     std::lock_guard<std::mutex> lk(top->buildMu);
-    if (!top->tableValid.load()) compute_geometry(top);
+    compute_geometry(top);
     int64_t n = std::min<int64_t>(cap, top->A);
     for (int64_t i = 0; i < n; i++) out[i] = top->attached[(size_t)i];
     return top->A;
@@ -1519,8 +1618,7 @@ int32_t shdtopo_column_of_ip(Topology* top, uint32_t ip) {
     int32_t v = vertex_of_ip(top, ip);
     if (v < 0) return -1;
     std::lock_guard<std::mutex> lk(top->buildMu);
-    if (!top->tableValid.load() && (top->colOf.size() != (size_t)top->g.V || top->colOf[(size_t)v] < 0))
-        compute_geometry(top);
+    compute_geometry(top);
     return top->colOf[(size_t)v];
 }
 
@@ -1549,7 +1647,7 @@ int shdtopo_bind_table(Topology* top, const void* d_lr, const void* d_hops, doub
     std::lock_guard<std::mutex> lk(top->buildMu);
     int r = dev_init(top);
     if (r) return r;
-    compute_geometry(top);
+    const uint64_t sg = compute_geometry(top);
     const size_t n = (size_t)(top->A * top->A);
     hipStream_t st = stream ? (hipStream_t)stream : top->stream;
     HIPCHK(top->d_lr.ensure(n));
@@ -1560,22 +1658,43 @@ int shdtopo_bind_table(Topology* top, const void* d_lr, const void* d_hops, doub
     if (top->A) HIPCHK(launch_row_min(top->A, top->A, top->d_lr.p, top->d_rowmin.p, st));
     HIPCHK(hipStreamSynchronize(st));
     top->eagerMin = globalMin;
-    top->hostValid.store(false);
-    top->rowminValid.store(false);
-    top->tableValid.store(true);
+    top->tableGen = sg;
+    top->tableSerial.fetch_add(1);
+    top->tableValid.store(true, std::memory_order_release);
     return 0;
 }
 
 int shdtopo_table_to_host(Topology* top, double* lat, double* rel, uint16_t* hops) {
     if (!top) return -1;
-    int r = ensure_host(top);
+    std::shared_ptr<const HostTable> h;
+    int r = ensure_snapshot(top, true, &h);
     if (r) return r;
-    const size_t n = (size_t)(top->A * top->A);
-    if (lat) memcpy(lat, top->hlat.data(), sizeof(double) * n);
-    if (rel) memcpy(rel, top->hrel.data(), sizeof(double) * n);
-    if (hops) memcpy(hops, top->hhops.data(), sizeof(uint16_t) * n);
+    const size_t n = (size_t)(h->A * h->A);
+    if (lat) memcpy(lat, h->lat.data(), sizeof(double) * n);
+    if (rel) memcpy(rel, h->rel.data(), sizeof(double) * n);
+    if (hops) memcpy(hops, h->hops.data(), sizeof(uint16_t) * n);
     return 0;
 }
+
+}  // extern "C"
+
+namespace {
+// packet_route_kernel over the installed table; caller holds buildMu (no rebuild in between)
+int route_locked(Topology* top, const int32_t* d_srcCol, const int32_t* d_dstCol,
+                 const uint32_t* d_payload, const uint32_t* d_stateIn, const uint64_t* d_now,
+                 int64_t n, uint64_t jumpNs, int clamp, uint64_t* d_time, uint32_t* d_stateOut,
+                 uint8_t* d_delivered, hipStream_t st) {
+    HIPCHK(hipEventRecord(top->ev2, st));
+    HIPCHK(launch_packet_route(n, d_srcCol, d_dstCol, d_payload, d_stateIn, d_now, top->d_lr.p,
+                               top->A, jumpNs, clamp, d_time, d_stateOut, d_delivered,
+                               top->d_stats.p + ST_ROUTE_BAD, st));
+    HIPCHK(hipEventRecord(top->ev3, st));
+    top->routePending = true;
+    return 0;
+}
+}  // namespace
+
+extern "C" {
 
 int shdtopo_route_batch_device(Topology* top, const int32_t* d_srcCol, const int32_t* d_dstCol,
                                const uint32_t* d_payload, const uint32_t* d_stateIn,
@@ -1585,32 +1704,20 @@ int shdtopo_route_batch_device(Topology* top, const int32_t* d_srcCol, const int
     if (!top) return -1;
     int r = ensure_table(top);
     if (r) return r;
+    std::lock_guard<std::mutex> lk(top->buildMu);
     hipStream_t st = stream ? (hipStream_t)stream : top->stream;
-    HIPCHK(hipEventRecord(top->ev2, st));
-    HIPCHK(launch_packet_route(n, d_srcCol, d_dstCol, d_payload, d_stateIn, d_now, top->d_lr.p,
-                               top->A, jumpNs, clamp, d_time, d_stateOut, d_delivered, st));
-    HIPCHK(hipEventRecord(top->ev3, st));
-    top->routePending = true;
-    return 0;
+    return route_locked(top, d_srcCol, d_dstCol, d_payload, d_stateIn, d_now, n, jumpNs, clamp,
+                        d_time, d_stateOut, d_delivered, st);
 }
 
 int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketOut* out, size_t n,
                               uint64_t jumpNs, int clampInterHost) {
     if (!top || (!in && n) || (!out && n)) return -1;
-    int r = ensure_table(top);
-    if (r) return r;
-    if (n == 0) return 0;
-    std::vector<int32_t> sc(n), dc(n);
+    if (n == 0) return ensure_table(top);
+    std::vector<int32_t> sv(n), dv(n), sc(n), dc(n);
     std::vector<uint32_t> pay(n), sin(n), sout(n);
     std::vector<uint64_t> now(n), tim(n);
     std::vector<uint8_t> dl(n);
-    // Lazy mode answers every packet as the reference's getReliability/getLatency pair would in
-    // emission order (first-rooted-wins orientation, running-minimum pushes): the orientation
-    // is resolved here, sequentially, and the kernel reads the chosen row.
-    if (top->lazy) {
-        r = top->isComplete ? ensure_host(top) : ensure_rowmin_host(top);
-        if (r) return r;
-    }
     {
         std::shared_lock<std::shared_mutex> lk(top->ipMu);
         for (size_t i = 0; i < n; i++) {
@@ -1620,37 +1727,61 @@ int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketO
                 CRITICAL("packet %zu: address is not connected to the topology", i);
                 return -2;
             }
-            sc[i] = top->colOf[(size_t)a->second];
-            dc[i] = top->colOf[(size_t)b->second];
-            if (top->lazy) {
-                if (top->isComplete) {
-                    lazy_touch_pair(top, sc[i], dc[i]);
-                } else if (lazy_orient_row(top, a->second, b->second, sc[i], dc[i])) {
-                    std::swap(sc[i], dc[i]);
-                }
-            }
+            sv[i] = a->second;
+            dv[i] = b->second;
             pay[i] = in[i].payloadLength;
             sin[i] = in[i].rngState;
             now[i] = in[i].now;
         }
     }
-    hipStream_t st = top->stream;
-    HIPCHK(top->b_src.ensure(n)); HIPCHK(top->b_dst.ensure(n)); HIPCHK(top->b_pay.ensure(n));
-    HIPCHK(top->b_sin.ensure(n)); HIPCHK(top->b_sout.ensure(n)); HIPCHK(top->b_now.ensure(n));
-    HIPCHK(top->b_time.ensure(n)); HIPCHK(top->b_dl.ensure(n));
-    HIPCHK(hipMemcpyAsync(top->b_src.p, sc.data(), 4 * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(top->b_dst.p, dc.data(), 4 * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(top->b_pay.p, pay.data(), 4 * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(top->b_sin.p, sin.data(), 4 * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(top->b_now.p, now.data(), 8 * n, hipMemcpyHostToDevice, st));
-    r = shdtopo_route_batch_device(top, top->b_src.p, top->b_dst.p, top->b_pay.p, top->b_sin.p,
-                                   top->b_now.p, (int64_t)n, jumpNs, clampInterHost, top->b_time.p,
-                                   top->b_sout.p, top->b_dl.p, st);
-    if (r) return r;
-    HIPCHK(hipMemcpyAsync(tim.data(), top->b_time.p, 8 * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(sout.data(), top->b_sout.p, 4 * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(dl.data(), top->b_dl.p, n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    // the snapshot and the device table must be the same build: retry if a rebuild intervened
+    for (int attempt = 0;; attempt++) {
+        std::shared_ptr<const HostTable> h;
+        int r = ensure_snapshot(top, top->lazy && top->isComplete, &h);
+        if (r) return r;
+        std::unique_lock<std::mutex> lk(top->buildMu);
+        if (!table_current(top) || h->serial != top->tableSerial.load()) {
+            if (attempt < 4) continue;
+            CRITICAL("the routing table keeps changing under a packet batch");
+            return -5;
+        }
+        // Lazy mode answers every packet as the reference's getReliability/getLatency pair would
+        // in emission order (cache orientation, running-minimum pushes): resolved here,
+        // sequentially; the kernel reads the chosen row.
+        for (size_t i = 0; i < n; i++) {
+            sc[i] = h->colOf[(size_t)sv[i]];
+            dc[i] = h->colOf[(size_t)dv[i]];
+            if (sc[i] < 0 || dc[i] < 0 || sc[i] >= h->A || dc[i] >= h->A) {
+                CRITICAL("packet %zu: address is not connected to the current routing table", i);
+                return -2;
+            }
+            if (top->lazy) {
+                if (top->isComplete) {
+                    lazy_touch_pair(top, *h, sc[i], dc[i]);
+                } else if (lazy_orient_row(top, *h, sv[i], dv[i])) {
+                    std::swap(sc[i], dc[i]);
+                }
+            }
+        }
+        hipStream_t st = top->stream;
+        HIPCHK(top->b_src.ensure(n)); HIPCHK(top->b_dst.ensure(n)); HIPCHK(top->b_pay.ensure(n));
+        HIPCHK(top->b_sin.ensure(n)); HIPCHK(top->b_sout.ensure(n)); HIPCHK(top->b_now.ensure(n));
+        HIPCHK(top->b_time.ensure(n)); HIPCHK(top->b_dl.ensure(n));
+        HIPCHK(hipMemcpyAsync(top->b_src.p, sc.data(), 4 * n, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(top->b_dst.p, dc.data(), 4 * n, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(top->b_pay.p, pay.data(), 4 * n, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(top->b_sin.p, sin.data(), 4 * n, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(top->b_now.p, now.data(), 8 * n, hipMemcpyHostToDevice, st));
+        r = route_locked(top, top->b_src.p, top->b_dst.p, top->b_pay.p, top->b_sin.p,
+                         top->b_now.p, (int64_t)n, jumpNs, clampInterHost, top->b_time.p,
+                         top->b_sout.p, top->b_dl.p, st);
+        if (r) return r;
+        HIPCHK(hipMemcpyAsync(tim.data(), top->b_time.p, 8 * n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(sout.data(), top->b_sout.p, 4 * n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(dl.data(), top->b_dl.p, n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        break;
+    }
     for (size_t i = 0; i < n; i++) {
         out[i].time = tim[i];
         out[i].rngState = sout[i];
@@ -1669,6 +1800,9 @@ int shdtopo_get_stats(Topology* top, ShdStats* out) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, top->ev2, top->ev3));
         top->stats.route_kernel_ms = ms;
+        unsigned long long nb = 0;
+        HIPCHK(hipMemcpy(&nb, top->d_stats.p + ST_ROUTE_BAD, sizeof nb, hipMemcpyDeviceToHost));
+        top->stats.route_bad_packets = (int64_t)nb;
         top->routePending = false;
     }
     *out = top->stats;
@@ -1773,7 +1907,7 @@ int shdtopo_synth_packets(Topology* top, uint64_t seed, int64_t n_hosts, int64_t
     if (servers.empty()) servers = relays;
     {
         std::lock_guard<std::mutex> lk(top->buildMu);
-        if (!top->tableValid.load()) compute_geometry(top);
+        compute_geometry(top);
     }
     SplitMix rng(seed ^ 0x5eed5eed5eedull);
     for (int64_t k = 0; k < n_packets; k++) {

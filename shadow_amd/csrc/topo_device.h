@@ -59,7 +59,8 @@ enum StatIdx {
     ST_RP_PUSH = 26,    //   pushes (first reach)
     ST_RP_MOD = 27,     //   modifies (strict improvement of a queued vertex)
     ST_RP_ROWS = 28,    //   rows replayed
-    ST_COUNT = 29
+    ST_ROUTE_BAD = 29,  // packets with a column outside [0, A) (not routed) since the last build
+    ST_COUNT = 30
 };
 
 struct DevCSR {
@@ -192,7 +193,7 @@ hipError_t launch_packet_route(int64_t n, const int32_t* src, const int32_t* dst
                                const uint32_t* payload, const uint32_t* state_in,
                                const uint64_t* now, const double2* table, int64_t A,
                                uint64_t jump, int clamp, uint64_t* t_out, uint32_t* state_out,
-                               uint8_t* delivered, hipStream_t stream);
+                               uint8_t* delivered, unsigned long long* d_bad, hipStream_t stream);
 
 hipError_t launch_row_min(int64_t rows, int64_t A, const double2* lr, double* out_rowmin,
                           hipStream_t stream);

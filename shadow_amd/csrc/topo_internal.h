@@ -69,7 +69,20 @@ inline int32_t glibc_rand_r(uint32_t* seed) {
 }
 inline double rand_r_double(uint32_t* seed) { return (double)glibc_rand_r(seed) / 2147483647.0; }
 
-uint32_t string_to_ip(const char* s);  // inet_pton(AF_INET) as shd-address.c:137-144
+uint32_t string_to_ip(const char* s);
+
+// Immutable host mirror of one device routing table (the per-call getters' view): the column
+// map it was built for, row minima, and (full) the A x A latency / reliability / hop arrays.
+struct HostTable {
+    uint64_t gen = 0;     // attached-set generation (Topology::setGen) of the table
+    uint64_t serial = 0;  // Topology::tableSerial of the table (every build / bind bumps it)
+    int64_t A = 0;
+    std::vector<int32_t> colOf;
+    std::vector<double> rowmin;
+    bool full = false;
+    std::vector<double> lat, rel;
+    std::vector<uint16_t> hops;
+};  // inet_pton(AF_INET) as shd-address.c:137-144
 
 // Index of the attachment candidates (the "poi" vertices) so that attaching H hosts costs
 // O(H + V) instead of the reference's O(H * V) string scan (shd-topology.c:1087); candidate

@@ -1062,41 +1062,75 @@ __global__ void row_min_kernel(int64_t rows, int64_t A, const double2* __restric
 // ------------------------------------------------------------------------------------------
 // packet route: worker_schedulePacket (shd-worker.c:332-370) + clamp (shd-worker.c:310-324).
 // 53 B per packet: 24 B of inputs, one 16-B {lat, rel} record gather, 13 B of outputs.
+// Each thread takes kRouteU packets of a 256 x kRouteU tile (coalesced column / state loads) and
+// issues all of their record gathers before using any: the gathers are random 16-B reads of a
+// table far larger than the caches, so the kernel lives on memory-level parallelism.
+// A column outside [0, A) is not routed (delivered 0, time 0, state unchanged) and counted.
 // ------------------------------------------------------------------------------------------
+constexpr int kRouteU = 8;
+
 __global__ void __launch_bounds__(256)
 packet_route_kernel(int64_t n, const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                     const uint32_t* __restrict__ payload, const uint32_t* __restrict__ state_in,
                     const uint64_t* __restrict__ now, const double2* __restrict__ table, int64_t A,
                     uint64_t jump, int clamp, uint64_t* __restrict__ t_out,
-                    uint32_t* __restrict__ state_out, uint8_t* __restrict__ delivered) {
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-         k += (int64_t)gridDim.x * blockDim.x) {
-        const double2 rec = table[(int64_t)src[k] * A + dst[k]];
-        uint32_t next = state_in[k];
-        // glibc rand_r: three LCG steps, 11 + 10 + 10 bits
-        next = next * 1103515245u + 12345u;
-        uint32_t r = (next / 65536u) % 2048u;
-        next = next * 1103515245u + 12345u;
-        r = (r << 10) ^ ((next / 65536u) % 1024u);
-        next = next * 1103515245u + 12345u;
-        r = (r << 10) ^ ((next / 65536u) % 1024u);
-        const double chance = (double)(int32_t)r / 2147483647.0;
-        const uint64_t tnow = now[k];
+                    uint32_t* __restrict__ state_out, uint8_t* __restrict__ delivered,
+                    unsigned long long* __restrict__ bad) {
+    const int64_t tile = (int64_t)blockIdx.x * 256 * kRouteU + threadIdx.x;
+    int64_t idx[kRouteU];
+    bool ok[kRouteU];
+#pragma unroll
+    for (int j = 0; j < kRouteU; j++) {
+        const int64_t k = tile + (int64_t)j * 256;
+        int64_t x = -1;
+        if (k < n) {
+            const uint32_t a = (uint32_t)__builtin_nontemporal_load(src + k);
+            const uint32_t b = (uint32_t)__builtin_nontemporal_load(dst + k);
+            if ((int64_t)a < A && (int64_t)b < A) x = (int64_t)a * A + b;
+        }
+        idx[j] = x;
+        ok[j] = x >= 0;
+    }
+    double2 rec[kRouteU];
+#pragma unroll
+    for (int j = 0; j < kRouteU; j++) rec[j] = ok[j] ? table[idx[j]] : make_double2(0.0, -1.0);
+    uint32_t nbad = 0;
+#pragma unroll
+    for (int j = 0; j < kRouteU; j++) {
+        const int64_t k = tile + (int64_t)j * 256;
+        if (k >= n) break;
+        const uint32_t s0 = __builtin_nontemporal_load(state_in + k);
+        const uint32_t pay = __builtin_nontemporal_load(payload + k);
+        const uint64_t tnow = __builtin_nontemporal_load(now + k);
         uint64_t t = 0;
         uint8_t dl = 0;
-        if (chance <= rec.y || payload[k] == 0u) {
-            const uint64_t delay = (uint64_t)ceil(rec.x * 1000000.0);
-            t = tnow + delay;
-            if (clamp) {
-                const uint64_t minTime = tnow + jump;
-                if (t < minTime) t = minTime;
+        uint32_t next = s0;
+        if (ok[j]) {
+            // glibc rand_r: three LCG steps, 11 + 10 + 10 bits
+            next = next * 1103515245u + 12345u;
+            uint32_t r = (next / 65536u) % 2048u;
+            next = next * 1103515245u + 12345u;
+            r = (r << 10) ^ ((next / 65536u) % 1024u);
+            next = next * 1103515245u + 12345u;
+            r = (r << 10) ^ ((next / 65536u) % 1024u);
+            const double chance = (double)(int32_t)r / 2147483647.0;
+            if (chance <= rec[j].y || pay == 0u) {
+                const uint64_t delay = (uint64_t)ceil(rec[j].x * 1000000.0);
+                t = tnow + delay;
+                if (clamp) {
+                    const uint64_t minTime = tnow + jump;
+                    if (t < minTime) t = minTime;
+                }
+                dl = 1;
             }
-            dl = 1;
+        } else {
+            nbad++;
         }
-        t_out[k] = t;
-        state_out[k] = next;
+        __builtin_nontemporal_store(t, t_out + k);
+        __builtin_nontemporal_store(next, state_out + k);
         delivered[k] = dl;
     }
+    if (nbad && bad) atomicAdd(bad, (unsigned long long)nbad);
 }
 
 __global__ void fill_u64_kernel(unsigned long long* p, unsigned long long v, int64_t n) {
@@ -1185,11 +1219,13 @@ hipError_t launch_packet_route(int64_t n, const int32_t* src, const int32_t* dst
                                const uint32_t* payload, const uint32_t* state_in,
                                const uint64_t* now, const double2* table, int64_t A,
                                uint64_t jump, int clamp, uint64_t* t_out, uint32_t* state_out,
-                               uint8_t* delivered, hipStream_t stream) {
+                               uint8_t* delivered, unsigned long long* d_bad, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(packet_route_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, src,
+    const int64_t tiles = (n + 256 * kRouteU - 1) / (256 * kRouteU);
+    if (tiles > INT32_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(packet_route_kernel, dim3((unsigned)tiles), dim3(256), 0, stream, n, src,
                        dst, payload, state_in, now, table, A, jump, clamp, t_out, state_out,
-                       delivered);
+                       delivered, d_bad);
     return hipGetLastError();
 }
 

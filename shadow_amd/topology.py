@@ -178,6 +178,9 @@ class Topology:
                                         _b(geocodeHint), _b(typeHint), None, None)
         return v, st.value
 
+    def detach_ip(self, ip):
+        self._lib.shdtopo_detach_ip(self._h, int(ip))
+
     def latency_ip(self, s, d):
         return self._lib.shdtopo_get_latency_ip(self._h, int(s), int(d))
 
