@@ -212,7 +212,8 @@ Topology* shdtopo_new_synthetic(const ShdSynthParams* p);
 
 /* Attach n_hosts hosts with Tor-like type hints (94 % client, 5 % relay, 1 % server) following
  * Shadow's seed chain (master --seed -> slave seed -> per-host nodeSeed), IPs
- * 11.0.0.1 + k; then emit n_packets packets of one window: src uniform over hosts, dst by role,
+ * 11.0.0.1 + k; host k < (number of poi with a usable ip) is pinned to the k-th poi by an exact
+ * ipHint (so every poi of a synthetic topology is attached); then emit n_packets packets of one window: src uniform over hosts, dst by role,
  * payload 1448 w.p. 0.8 else 0, pre-draw rand_r state from each host's stream, now ~
  * U[t0, t0 + jump).  Output arrays are host memory of length n_packets (hostState: n_hosts,
  * the hosts' states after attach). */

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1448,12 +1449,18 @@ Topology* topology_new(const char* graphPath) {
     Topology* top = new Topology();
     std::string err;
     MESSAGE("reading graphml topology graph at '%s'...", graphPath);
+    const auto t0 = std::chrono::steady_clock::now();
     if (!graphml_load_file(graphPath, top->g, err)) {
         CRITICAL("reading graphml topology '%s' failed: %s", graphPath, err.c_str());
         delete top;
         return nullptr;
     }
-    return finish_new(top);
+    const auto t1 = std::chrono::steady_clock::now();
+    Topology* r = finish_new(top);
+    const auto t2 = std::chrono::steady_clock::now();
+    MESSAGE("graphml parsed in %.3f s, checked in %.3f s",
+            std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count());
+    return r;
 }
 
 Topology* shdtopo_new_from_buffer(const char* graphml, size_t len) {
@@ -1898,8 +1905,16 @@ int shdtopo_synth_packets(Topology* top, uint64_t seed, int64_t n_hosts, int64_t
         if (role[(size_t)h] == 2) servers.push_back(h);
         hostState[(size_t)h] = (uint32_t)glibc_rand_r(&slave);
         hostIP[(size_t)h] = htonl(0x0B000001u + (uint32_t)h);
+        // the first hosts are pinned one per poi by an exact ipHint (shd-topology.c:1087-1100,
+        // no random draw), so every poi is attached (A = n_poi); the rest attach by type hint
+        const char* iphint = nullptr;
+        std::string hs;
+        if (h < (int64_t)top->aidx.all.size() && top->aidx.usable[(size_t)top->aidx.all[(size_t)h]]) {
+            hs = top->g.vip[(size_t)top->aidx.all[(size_t)h]];
+            iphint = hs.c_str();
+        }
         hostVertex[(size_t)h] = shdtopo_attach_ip(top, hostIP[(size_t)h], &hostState[(size_t)h],
-                                                  nullptr, nullptr, kRole[role[(size_t)h]],
+                                                  iphint, nullptr, kRole[role[(size_t)h]],
                                                   nullptr, nullptr);
         if (hostVertex[(size_t)h] < 0) return -2;
     }

@@ -7,7 +7,7 @@ set -u
 OUT=$1; shift
 ROOT=$(pwd)
 mkdir -p "$OUT"
-BENCH_ARGS=(--steps 1 --warmup 0 --no-cpu-baseline --route-steps 5 "$@")
+BENCH_ARGS=(--steps 1 --warmup 0 --no-cpu-baseline --no-graphml --no-complete --route-steps 5 "$@")
 cd /tmp && export TMPDIR=/tmp
 pass() {
   local name=$1; shift

@@ -77,6 +77,7 @@ if ks:
     # reads, so their missing half is added back (MI355X_MICROARCH.md, HBM/rocprofv3 section)
     fetch_c = fetch + sweep_bytes / 2
     out = dict(config_key=key, kernel=k, hbm_bytes_per_launch=fetch_c + write,
+               dram_requests_per_launch=rd + wr,
                fetch_bytes=fetch, fetch_bytes_corrected=fetch_c, sweep_bytes=sweep_bytes,
                write_bytes=write, rdreq=rd, wrreq=wr, atomic_req=at,
                source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), profiles/%s_summary.md; "
@@ -92,5 +93,19 @@ if ks:
               "* HBM traffic per launch = %.4g B" % (fetch_c + write),
               "* read requests %.4g, write requests %.4g, atomic requests %.4g per launch" %
               (rd, wr, at), ""]
+rk = [k for k in per if k.startswith("packet_route")]
+if rk:
+    k = rk[0]
+    d = per[k]
+    n = max(1, len(dur[k]))
+    fetch = d.get("FETCH_SIZE", 0.0) * 1024 / n
+    write = d.get("WRITE_SIZE", 0.0) * 1024 / n
+    json.dump(dict(kernel=k, hbm_bytes_per_launch=fetch + write, fetch_bytes=fetch,
+                   write_bytes=write, dispatches=n,
+                   source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, profiles/%s_summary.md" % tag),
+              open(os.path.join(outdir, "%s_route_pmc.json" % tag), "w"), indent=1)
+    lines += ["## per-launch HBM traffic of %s" % k, "",
+              "* FETCH_SIZE = %.4g B, WRITE_SIZE = %.4g B, total %.4g B per launch" %
+              (fetch, write, fetch + write), ""]
 open(os.path.join(outdir, "%s_summary.md" % tag), "w").write("\n".join(lines) + "\n")
 print("\n".join(lines))
