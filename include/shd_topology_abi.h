@@ -103,7 +103,12 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * -1 = fill), "par_hubs" (hubs with SSSP parent hints), "wg_per_cu" (SSSP workgroups sharing a
  * CU's LDS), "far_cap" / "near_cap" (entries per window bucket and overflow pile / per near
  * queue, 0 = sized from V; small values force the scanning fallback), "events" (1 = diagnostic
- * kernel with event counters).  Returns 0 or -1 for an unknown key. */
+ * kernel with event counters), "tie_replay" (1: rows whose target chains cross a d-tied parent
+ * are recomputed by the exact heap replay; 0: reported only), "replay_all" (test hook: every row
+ * through the replay), "replay_slots" (concurrent replay wavefronts, 0 = auto), "devices" (N:
+ * the table is built by N GPUs of this process -- rows sharded, RCCL all-gather of the rows and
+ * all-reduce(MIN) of the minimum; devices device..device+N-1), "rccl" (1: use that exchange even
+ * with one device).  Returns 0 or -1 for an unknown key / bad value. */
 int shdtopo_set_option(Topology* top, const char* key, double value);
 
 /* attach by raw IP and a rand_r state (same algorithm and RNG use as topology_attach) */
@@ -127,8 +132,11 @@ int64_t shdtopo_attached_vertices(Topology* top, int32_t* out, int64_t cap);
 int32_t shdtopo_column_of_ip(Topology* top, uint32_t ip);          /* -1 if unattached */
 int32_t shdtopo_vertex_of_ip(Topology* top, uint32_t ip);          /* -1 if unattached */
 
-/* Build the whole A x A table on this process's GPU (SSSP or complete-pair kernel). */
+/* Build the whole A x A table on this process's GPU(s) (SSSP or complete-pair kernel). */
 int shdtopo_build(Topology* top);
+/* Row shard [*r0, *r1) of device d out of n for A rows: ceil(A / n) rows each, the last shards
+ * possibly short or empty (the split of option "devices" and of shadow_amd.sharding). */
+void shdtopo_shard_rows(int64_t A, int n, int d, int64_t* r0, int64_t* r1);
 /* Build rows [row0,row1) into caller-owned HBM: lr = {f64 lat, f64 rel}[rows][A],
  * hops = u16[rows][A], rowmin = f64[rows] (may be NULL).  Enqueued on `stream`. */
 int shdtopo_build_rows(Topology* top, int64_t row0, int64_t row1, void* d_lr, void* d_hops,
@@ -182,6 +190,8 @@ typedef struct {
     int64_t replay_slots;     /* concurrent replay wavefronts of the last launch */
     int64_t route_bad_packets; /* packets with a column outside [0, A), not routed (delivered 0,
                                   time 0, state unchanged), since the last table build */
+    int64_t devices;          /* GPUs that built the last table (option "devices") */
+    double exchange_ms;       /* RCCL all-gather + all-reduce(min) of that build (wall) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

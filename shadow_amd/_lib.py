@@ -37,7 +37,8 @@ class ShdStats(ctypes.Structure):
                 ("slots", i64), ("events", i64 * 8), ("far_scan_sources", i64), ("split_ms", dbl),
                 ("batch", i64), ("lds_hubs", i64), ("replay_rows", i64), ("replay_ms", dbl),
                 ("replay_pops", i64), ("replay_pushes", i64), ("replay_modifies", i64),
-                ("replay_slots", i64), ("route_bad_packets", i64)]
+                ("replay_slots", i64), ("route_bad_packets", i64), ("devices", i64),
+                ("exchange_ms", dbl)]
 
 
 class ShdSynthParams(ctypes.Structure):
@@ -72,6 +73,7 @@ SIGNATURES = {
     "shdtopo_column_of_ip": (i32, [P, u32]),
     "shdtopo_vertex_of_ip": (i32, [P, u32]),
     "shdtopo_build": (ctypes.c_int, [P]),
+    "shdtopo_shard_rows": (None, [i64, ctypes.c_int, ctypes.c_int, P, P]),
     "shdtopo_build_rows": (ctypes.c_int, [P, i64, i64, P, P, P, P]),
     "shdtopo_bind_table": (ctypes.c_int, [P, P, P, dbl, P]),
     "shdtopo_table_to_host": (ctypes.c_int, [P, P, P, P]),

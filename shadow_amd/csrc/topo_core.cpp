@@ -10,7 +10,9 @@
 //     for the same query sequence;
 //   * attach uses a candidate index built once instead of an O(V) scan per host.
 #include <arpa/inet.h>
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -23,6 +25,7 @@
 #include <functional>
 #include <numeric>
 #include <queue>
+#include <thread>
 #include <vector>
 
 #include "../../include/shd_topology_abi.h"
@@ -183,6 +186,16 @@ struct _Topology {
     int rslots = 0;
     hipEvent_t evr0 = nullptr, evr1 = nullptr;
     bool replayPending = false;
+
+    // multi-GPU build inside the library (one Shadow process): device d builds
+    // rows [d*R, (d+1)*R) with its own stream / workspace (a peer Topology on that device),
+    // RCCL all-gathers the rows into every device's table and all-reduces the minimum
+    int devicesOpt = 1;        // option "devices"
+    bool forceRccl = false;    // option "rccl": the RCCL exchange even with one device (tests)
+    std::vector<Topology*> peers;      // devices 1..N-1
+    std::vector<ncclComm_t> comms;     // one per device, ncclCommInitAll
+    std::vector<int> commDevs;
+    int64_t shardRows = 0;
 
     // host mirror of the table for the per-call getters: an immutable snapshot swapped atomically
     // (getters on worker threads never see a table being rebuilt)
@@ -1115,6 +1128,232 @@ bool table_current(Topology* top) {
     return top->tableValid.load(std::memory_order_acquire) && top->tableGen == top->setGen.load();
 }
 
+// ---------------------------------------------------------------------------------------------
+// multi-GPU build inside one process: no Python, no torch.distributed
+// ---------------------------------------------------------------------------------------------
+// RCCL is loaded on first use (dlopen by soname: a process that already holds RCCL, e.g. through
+// torch, shares that copy; a single-GPU user never needs it).
+struct RcclApi {
+    bool ok = false;
+    std::string why;
+    ncclResult_t (*commInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*allGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*allReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    ncclResult_t (*groupStart)() = nullptr;
+    ncclResult_t (*groupEnd)() = nullptr;
+    const char* (*errStr)(ncclResult_t) = nullptr;
+};
+
+RcclApi& rccl() {
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = nullptr;
+        for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+            if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
+        if (!h) {
+            api.why = dlerror() ? dlerror() : "librccl.so.1 not found";
+            return;
+        }
+        auto sym = [&](const char* n) { return dlsym(h, n); };
+        api.commInitAll = (decltype(api.commInitAll))sym("ncclCommInitAll");
+        api.commDestroy = (decltype(api.commDestroy))sym("ncclCommDestroy");
+        api.allGather = (decltype(api.allGather))sym("ncclAllGather");
+        api.allReduce = (decltype(api.allReduce))sym("ncclAllReduce");
+        api.groupStart = (decltype(api.groupStart))sym("ncclGroupStart");
+        api.groupEnd = (decltype(api.groupEnd))sym("ncclGroupEnd");
+        api.errStr = (decltype(api.errStr))sym("ncclGetErrorString");
+        api.ok = api.commInitAll && api.commDestroy && api.allGather && api.allReduce &&
+                 api.groupStart && api.groupEnd && api.errStr;
+        if (!api.ok) api.why = "RCCL symbols missing";
+    });
+    return api;
+}
+
+#define NCCLCHK(expr)                                                                        \
+    do {                                                                                     \
+        ncclResult_t _r = (expr);                                                            \
+        if (_r != ncclSuccess) {                                                             \
+            CRITICAL("RCCL error %s at %s:%d (%s)", rccl().errStr(_r), __FILE__, __LINE__, #expr); \
+            return -200 - (int)_r;                                                           \
+        }                                                                                    \
+    } while (0)
+
+int num_devices() {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
+// The engine of device slot d: slot 0 is the Topology itself, the others are peers holding the
+// same graph and columns on their own device (stream, CSR copy, workspaces, table).
+Topology* slot_engine(Topology* top, int d) { return d == 0 ? top : top->peers[(size_t)d - 1]; }
+
+Topology* make_peer(Topology* top, int phys) {
+    Topology* p = new Topology();
+    p->g = top->g;
+    p->isComplete = top->isComplete;
+    p->isDirected = top->isDirected;
+    p->hasMultiEdges = top->hasMultiEdges;
+    p->abortOnError = top->abortOnError;
+    p->lazy = false;
+    p->device = phys;
+    return p;
+}
+
+// options and columns of the owner, copied before every multi-device build
+void sync_peer(Topology* top, Topology* p) {
+    p->delta = top->delta;
+    p->slotsOpt = top->slotsOpt;
+    p->hubLimit = top->hubLimit;
+    p->parHubs = top->parHubs;
+    p->wgPerCu = top->wgPerCu;
+    p->batchK = top->batchK;
+    p->events = top->events;
+    p->nearCap = top->nearCap;
+    p->farCap = top->farCap;
+    p->tieReplay = top->tieReplay;
+    p->replayAll = top->replayAll;
+    p->replaySlotsOpt = top->replaySlotsOpt;
+    p->attached = top->attached;
+    p->colOf = top->colOf;
+    p->A = top->A;
+    p->geomInit = true;
+}
+
+// N devices: slot d builds rows [d*R, min(A, (d+1)*R)) into its own full-size buffers (R*N rows,
+// padded), then the rows are exchanged so that every device holds the whole table:
+// ncclAllGather (in place) of the {lat, rel} rows, the u16 hop rows and the row minima, and
+// ncclAllReduce(MIN) of the per-device minimum (u64 bits of a non-negative f64 order like the
+// values) -> topology_getMinimumLatency / the runahead (shd-master.c:113-124).  Several slots on
+// one physical device (a test configuration: RCCL refuses duplicate devices) exchange with
+// device copies instead.
+int build_multi(Topology* top) {
+    const int N = std::max(1, top->devicesOpt);
+    const int ndev = num_devices();
+    if (ndev <= 0) {
+        CRITICAL("no HIP device available: the routing engine runs on the GPU only");
+        return -1;
+    }
+    while ((int)top->peers.size() < N - 1)
+        top->peers.push_back(make_peer(top, (top->device + (int)top->peers.size() + 1) % ndev));
+    for (int d = 1; d < N; d++) sync_peer(top, slot_engine(top, d));
+    const int64_t A = top->A;
+    const int64_t R = (A + N - 1) / N;
+    top->shardRows = R;
+    std::vector<int> phys(N);
+    bool distinct = true;
+    for (int d = 0; d < N; d++) {
+        phys[(size_t)d] = slot_engine(top, d)->device % ndev;
+        for (int e = 0; e < d; e++) distinct = distinct && phys[(size_t)e] != phys[(size_t)d];
+    }
+    // 1) rows, one host thread per device
+    std::vector<int> rc(N, 0);
+    std::vector<std::thread> th;
+    for (int d = 0; d < N; d++)
+        th.emplace_back([&, d]() {
+            Topology* T = slot_engine(top, d);
+            auto run = [&]() -> int {
+                HIPCHK(hipSetDevice(phys[(size_t)d]));
+                int r = dev_init(T);
+                if (r) return r;
+                HIPCHK(hipSetDevice(phys[(size_t)d]));
+                HIPCHK(T->d_lr.ensure((size_t)(R * N * A)));
+                HIPCHK(T->d_hops.ensure((size_t)(R * N * A)));
+                HIPCHK(T->d_rowmin.ensure((size_t)(R * N)));
+                const int64_t r0 = std::min(A, d * R), r1 = std::min(A, r0 + R);
+                if (r1 > r0) {
+                    r = enqueue_rows(T, r0, r1, T->d_lr.p + r0 * A, T->d_hops.p + r0 * A,
+                                     T->d_rowmin.p + r0, T->stream);
+                    if (r) return r;
+                    r = collect_row_stats(T);
+                    if (r) return r;
+                } else {  // an empty shard: its minimum is +inf
+                    HIPCHK(launch_fill_u64(T->d_stats.p + ST_GLOBAL_MIN, 0x7FF0000000000000ull, 1, T->stream));
+                    HIPCHK(hipStreamSynchronize(T->stream));
+                }
+                return 0;
+            };
+            rc[(size_t)d] = run();
+        });
+    for (auto& x : th) x.join();
+    for (int d = 0; d < N; d++)
+        if (rc[(size_t)d]) return rc[(size_t)d];
+    // 2) exchange
+    HIPCHK(hipSetDevice(phys[0]));
+    HIPCHK(hipEventRecord(top->ev2, top->stream));
+    const auto tx0 = std::chrono::steady_clock::now();
+    if (distinct) {
+        RcclApi& api = rccl();
+        if (!api.ok) {
+            CRITICAL("multi-GPU build needs RCCL: %s", api.why.c_str());
+            return -6;
+        }
+        if (top->commDevs != phys) {
+            for (ncclComm_t c : top->comms) (void)api.commDestroy(c);
+            top->comms.assign((size_t)N, nullptr);
+            NCCLCHK(api.commInitAll(top->comms.data(), N, phys.data()));
+            top->commDevs = phys;
+        }
+        NCCLCHK(api.groupStart());
+        for (int d = 0; d < N; d++) {
+            Topology* T = slot_engine(top, d);
+            ncclComm_t c = top->comms[(size_t)d];
+            const size_t lrB = (size_t)(R * A) * sizeof(double2), hB = (size_t)(R * A) * 2;
+            NCCLCHK(api.allGather((const char*)T->d_lr.p + (size_t)d * lrB, T->d_lr.p, lrB, ncclUint8, c, T->stream));
+            NCCLCHK(api.allGather((const char*)T->d_hops.p + (size_t)d * hB, T->d_hops.p, hB, ncclUint8, c, T->stream));
+            NCCLCHK(api.allGather(T->d_rowmin.p + (size_t)d * (size_t)R, T->d_rowmin.p, (size_t)R, ncclFloat64, c, T->stream));
+            NCCLCHK(api.allReduce(T->d_stats.p + ST_GLOBAL_MIN, T->d_stats.p + ST_GLOBAL_MIN, 1, ncclUint64, ncclMin, c, T->stream));
+        }
+        NCCLCHK(api.groupEnd());
+    } else {
+        unsigned long long gmin = 0x7FF0000000000000ull;
+        for (int d = 0; d < N; d++) {
+            unsigned long long m = 0;
+            Topology* T = slot_engine(top, d);
+            HIPCHK(hipMemcpy(&m, T->d_stats.p + ST_GLOBAL_MIN, 8, hipMemcpyDeviceToHost));
+            gmin = std::min(gmin, m);
+        }
+        for (int d = 0; d < N; d++) {
+            Topology* T = slot_engine(top, d);
+            for (int e = 0; e < N; e++) {
+                if (e == d) continue;
+                Topology* S = slot_engine(top, e);
+                const int64_t r0 = std::min(A, e * R), r1 = std::min(A, r0 + R);
+                if (r1 <= r0) continue;
+                HIPCHK(hipMemcpyAsync(T->d_lr.p + r0 * A, S->d_lr.p + r0 * A, sizeof(double2) * (size_t)((r1 - r0) * A), hipMemcpyDefault, T->stream));
+                HIPCHK(hipMemcpyAsync(T->d_hops.p + r0 * A, S->d_hops.p + r0 * A, 2 * (size_t)((r1 - r0) * A), hipMemcpyDefault, T->stream));
+                HIPCHK(hipMemcpyAsync(T->d_rowmin.p + r0, S->d_rowmin.p + r0, 8 * (size_t)(r1 - r0), hipMemcpyDefault, T->stream));
+            }
+            HIPCHK(hipMemcpyAsync(T->d_stats.p + ST_GLOBAL_MIN, &gmin, 8, hipMemcpyHostToDevice, T->stream));
+            HIPCHK(hipStreamSynchronize(T->stream));
+        }
+    }
+    for (int d = 0; d < N; d++) HIPCHK(hipStreamSynchronize(slot_engine(top, d)->stream));
+    HIPCHK(hipSetDevice(phys[0]));
+    top->stats.exchange_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tx0).count();
+    unsigned long long gm = 0;
+    HIPCHK(hipMemcpy(&gm, top->d_stats.p + ST_GLOBAL_MIN, 8, hipMemcpyDeviceToHost));
+    double g;
+    memcpy(&g, &gm, 8);
+    top->eagerMin = std::isinf(g) ? -1.0 : g;
+    // whole-job statistics: the slowest device's kernels, every device's counts
+    top->stats.devices = N;
+    top->stats.sources = A;
+    for (int d = 1; d < N; d++) {
+        const ShdStats& o = slot_engine(top, d)->stats;
+        top->stats.sssp_kernel_ms = std::max(top->stats.sssp_kernel_ms, o.sssp_kernel_ms);
+        top->stats.replay_ms = std::max(top->stats.replay_ms, o.replay_ms);
+        top->stats.build_ms = std::max(top->stats.build_ms, o.build_ms);
+        top->stats.ambiguous_pairs += o.ambiguous_pairs;
+        top->stats.replay_rows += o.replay_rows;
+        top->stats.errors += o.errors;
+        top->stats.relaxations += o.relaxations;
+    }
+    return 0;
+}
+
 // whole-table build on this GPU (for the current attached set)
 int ensure_table(Topology* top) {
     if (table_current(top)) return 0;
@@ -1124,7 +1363,16 @@ int ensure_table(Topology* top) {
     if (r) return r;
     const uint64_t sg = compute_geometry(top);
     const int64_t A = top->A;
-    if (A > 0) {
+    top->stats.devices = 1;
+    top->stats.exchange_ms = 0.0;
+    if (A > 0 && (top->devicesOpt > 1 || top->forceRccl)) {
+        r = build_multi(top);
+        if (r) return r;
+        if (top->stats.errors) {
+            CRITICAL("%lld attached pairs have no path/edge (e.g. a vertex without self loop)",
+                     (long long)top->stats.errors);
+        }
+    } else if (A > 0) {
         HIPCHK(top->d_lr.ensure((size_t)(A * A)));
         HIPCHK(top->d_hops.ensure((size_t)(A * A)));
         HIPCHK(top->d_rowmin.ensure((size_t)A));
@@ -1491,6 +1739,11 @@ Topology* shdtopo_new_synthetic(const ShdSynthParams* p) {
 
 void topology_free(Topology* top) {
     if (!top) return;
+    for (Topology* p : top->peers) topology_free(p);
+    top->peers.clear();
+    if (!top->comms.empty() && rccl().ok)
+        for (ncclComm_t c : top->comms) (void)rccl().commDestroy(c);
+    top->comms.clear();
     if (top->devInit) {
         (void)hipStreamSynchronize(top->stream);
         (void)hipEventDestroy(top->ev0);
@@ -1522,6 +1775,17 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "tie_replay") top->tieReplay = value != 0;
     else if (k == "replay_all") top->replayAll = value != 0;
     else if (k == "replay_slots") top->replaySlotsOpt = (int)value;
+    else if (k == "devices") {
+        const int n = (int)value;
+        if (n < 1 || n > 64) return -1;
+        std::lock_guard<std::mutex> lk(top->buildMu);
+        if (n != top->devicesOpt) top->tableValid.store(false);
+        top->devicesOpt = n;
+    } else if (k == "rccl") {
+        std::lock_guard<std::mutex> lk(top->buildMu);
+        top->forceRccl = value != 0;
+        top->tableValid.store(false);
+    }
     else return -1;
     return 0;
 }
@@ -1627,6 +1891,13 @@ int32_t shdtopo_column_of_ip(Topology* top, uint32_t ip) {
     std::lock_guard<std::mutex> lk(top->buildMu);
     compute_geometry(top);
     return top->colOf[(size_t)v];
+}
+
+void shdtopo_shard_rows(int64_t A, int n, int d, int64_t* r0, int64_t* r1) {
+    const int64_t R = n > 0 ? (A + n - 1) / n : 0;
+    const int64_t a = std::min(A, (int64_t)d * R), b = std::min(A, a + R);
+    if (r0) *r0 = a;
+    if (r1) *r1 = b;
 }
 
 int shdtopo_build(Topology* top) {

@@ -1181,15 +1181,13 @@ hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d
         return hipErrorInvalidValue;
     const uint32_t hubs = plan.H, par_hubs = plan.P;
     const size_t lds = plan.bytes;
-    static bool attr_set = false;
-    if (!attr_set) {
+    {  // per device (multi-GPU builds launch on several): set before every launch
         for (const void* k : {(const void*)sssp_rows_kernel<false>,
                               (const void*)sssp_rows_kernel<true>}) {
             hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)kSsspMaxLds);
             if (e != hipSuccess) return e;
         }
-        attr_set = true;
     }
     hipLaunchKernelGGL(events ? sssp_rows_kernel<true> : sssp_rows_kernel<false>, dim3(grid),
                        dim3(kSsspBlock), lds, stream, g, ws,

@@ -1391,13 +1391,11 @@ static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32
     if ((int64_t)plan.H > g.V || plan.P > plan.H || plan.bytes > kBMaxLds ||
         blayout<K>(plan.H, plan.P).bytes != plan.bytes || ws.K != K)
         return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
+    {  // per device (multi-GPU builds launch on several): set before every launch
         hipError_t e = hipFuncSetAttribute((const void*)sssp_batch_kernel<K>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)kBMaxLds);
         if (e != hipSuccess) return e;
-        attr_set = true;
     }
     hipLaunchKernelGGL(sssp_batch_kernel<K>, dim3(grid), dim3(kSsspBlock), plan.bytes, stream, g,
                        ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan.H, plan.P, far_cap,

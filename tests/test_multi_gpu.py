@@ -1,0 +1,83 @@
+"""Multi-GPU build inside libshdtopo (option "devices"): one Shadow process, no
+Python in the loop -- rows sharded over devices, RCCL all-gather of the rows and all-reduce(MIN)
+of the runahead minimum.
+
+CPU: the row split (shdtopo_shard_rows) for N = 1, 2, 3, 8 covers every row exactly once and
+agrees with the multi-process harness (shadow_amd.sharding).  GPU (one MI355X on the test box):
+the RCCL exchange with one device, and 2 / 3 engines on the same device (RCCL refuses duplicate
+devices, so those exchange by device copies), each bit-equal to the single-device table and to
+the oracle.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+import shadow_amd as sa
+from shadow_amd import sharding
+from helpers import attach_hosts, synthetic_pair
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+@pytest.mark.parametrize("A", [1, 7, 37, 10000])
+def test_shard_rows_cover_each_row_once(n, A):
+    lib, _ = sa._lib.load()
+    seen = np.zeros(A, np.int32)
+    prev = 0
+    for d in range(n):
+        r0, r1 = ctypes.c_int64(), ctypes.c_int64()
+        lib.shdtopo_shard_rows(A, n, d, ctypes.byref(r0), ctypes.byref(r1))
+        assert r0.value == prev and r0.value <= r1.value
+        assert (r1.value - r0.value) <= -(-A // n)
+        assert (r0.value, r1.value) == sharding.shard_range(A, d, n)
+        seen[r0.value:r1.value] += 1
+        prev = r1.value
+    assert prev == A and np.all(seen == 1)
+
+
+def _table_with(devices, rccl, integer, seed=21):
+    top, g = synthetic_pair(seed=seed, n_routers=2000, n_poi=101, n_edges=20000, integer=integer)
+    top.set_option("devices", devices)
+    top.set_option("rccl", int(rccl))
+    otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay", "server"])
+    a, lat, rel, hops = top.table()
+    return top, g, otop, ips, verts, a, lat, rel, hops
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("integer", [False, True])
+@pytest.mark.parametrize("devices,rccl", [(1, True), (2, False), (3, False)])
+def test_multi_device_table_equals_single_and_oracle(devices, rccl, integer):
+    top1, g, _, _, verts, a1, lat1, rel1, hops1 = _table_with(1, False, integer)
+    topN, _, otop, ips, _, aN, latN, relN, hopsN = _table_with(devices, rccl, integer)
+    st = topN.stats()
+    assert st["devices"] == devices and st["errors"] == 0
+    if rccl:
+        assert st["exchange_ms"] > 0
+    assert np.array_equal(a1, aN)
+    assert np.array_equal(lat1.view(np.uint64), latN.view(np.uint64))
+    assert np.array_equal(rel1.view(np.uint64), relN.view(np.uint64))
+    assert np.array_equal(hops1, hopsN)
+    assert topN.getMinimumLatency() == top1.getMinimumLatency()
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(latN.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(relN.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hopsN, ohops.astype(np.uint16))
+    assert topN.getMinimumLatency() == olat.min()
+
+
+@pytest.mark.gpu
+def test_getters_trigger_multi_device_build():
+    """topology_getLatency on a topology with devices = 2: the lazy getter builds the table on
+    both engines itself (no Python sharding) and answers as the reference cache does."""
+    top, g = synthetic_pair(seed=23, n_routers=1500, n_poi=70, n_edges=15000, integer=True)
+    top.set_option("devices", 2)
+    otop, ips, verts = attach_hosts(top, g, 150, type_hints=["client", "relay"])
+    rng = np.random.default_rng(4)
+    for _ in range(300):
+        x, y = (int(v) for v in rng.choice(ips, 2))
+        assert top.latency_ip(x, y) == otop.get_latency(x, y)
+        assert top.reliability_ip(x, y) == otop.get_reliability(x, y)
+    assert top.stats()["devices"] == 2
+    assert top.lazyMinimumLatency() == otop.minimum_path_latency
