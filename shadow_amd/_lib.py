@@ -88,6 +88,19 @@ SIGNATURES = {
     "shdtopo_synth_packets": (ctypes.c_int, [P, u64, i64, i64, u64, u64, P, P, P, P, P, P, P]),
 }
 
+# include/shd_topology_window.h
+WINDOW_DELIVER = ctypes.CFUNCTYPE(None, P, P, ctypes.c_int, u64)
+SIGNATURES.update({
+    "topowindow_new": (P, [P]),
+    "topowindow_free": (None, [P]),
+    "topowindow_emit": (i64, [P, P, P, u32, P, u64, P]),
+    "topowindow_emit_state": (i64, [P, u32, u32, u32, u32, u64, P]),
+    "topowindow_pending": (i64, [P]),
+    "topowindow_flush": (ctypes.c_int, [P, u64, ctypes.c_int, WINDOW_DELIVER, P]),
+    "topowindow_jump_ns": (u64, [P, u64]),
+    "topowindow_serial_window_ns": (u64, [P]),
+})
+
 SHIM_SIGNATURES = {
     "shim_address_new": (P, [u32]),
     "shim_address_free": (None, [P]),

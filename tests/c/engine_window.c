@@ -9,16 +9,19 @@
  *                                          delay = ceil(topology_getLatency(src, dst) * 1e6)
  *                                          time = max(now + delay, now + jump)   (multi-threaded)
  *                                      }
- *   adapter (at emit):                 record {src, dst, payload, sender state BEFORE the draw,
- *                                      now}; advance the sender's Random by the one draw
- *   adapter (at the window barrier):   topology_routePacketBatch(...) -> delivered, time, state
+ *   adapter (at emit):                 topowindow_emit(): records {src, dst, payload, sender
+ *                                      state BEFORE the draw, now}, advances the sender's Random
+ *                                      by the one draw
+ *   adapter (at the window barrier):   topowindow_flush() -> deliver(packet, delivered, time)
+ * Multi-threaded windows (jump = the runahead, clamp on) and serial-mode windows
+ * (topowindow_serial_window_ns, no clamp: shd-master.c:220-224 runs serial mode unwindowed).
  *
  * Senders also draw from their host stream between packets (Shadow's process emulation uses
  * the host Random), so the captured state is not a simple function of the window start.
  * Both topologies run in lazy mode: the batch must reproduce the first-rooted-wins orientation
  * and the running-minimum trajectory (worker_updateMinTimeJump) of the per-packet getters.
  *
- * usage: engine_window [windows packets_per_window]      exit 0 = identical, 1 = mismatch
+ * usage: engine_window [windows packets_per_window [serial]]   exit 0 = identical, 1 = mismatch
  * Test infrastructure: links libshdtopo.so + libshdtopo_shim.so only (no oracle).
  */
 #include <math.h>
@@ -27,6 +30,7 @@
 #include <stdlib.h>
 
 #include "../../include/shd_topology_abi.h"
+#include "../../include/shd_topology_window.h"
 
 /* libshdtopo_shim.so (restatements of Shadow's Address / Random) */
 Address* shim_address_new(uint32_t networkIP);
@@ -48,6 +52,20 @@ static uint32_t pick(uint32_t n) {
     return (uint32_t)((lcg >> 33) % n);
 }
 
+typedef struct {
+    uint8_t* dl;
+    uint64_t* t;
+    long calls;
+} Got;
+
+static void deliver(void* ctx, void* packet, int delivered, uint64_t time) {
+    Got* g = (Got*)ctx;
+    const long k = (long)(intptr_t)packet;
+    g->dl[k] = (uint8_t)delivered;
+    g->t[k] = time;
+    g->calls++;
+}
+
 static Topology* make_topology(void) {
     ShdSynthParams p = {20261016ull, 3000, 150, 30000, 0, 1.0 / 1.1};
     Topology* t = shdtopo_new_synthetic(&p);
@@ -58,6 +76,7 @@ static Topology* make_topology(void) {
 int main(int argc, char** argv) {
     const int windows = argc > 1 ? atoi(argv[1]) : 4;
     const int perWindow = argc > 2 ? atoi(argv[2]) : 20000;
+    const int serial = argc > 3 ? atoi(argv[3]) : 0;
     const int nHosts = 400;
     Topology* ref = make_topology();
     Topology* bat = make_topology();
@@ -87,9 +106,13 @@ int main(int argc, char** argv) {
     /* runahead: shd-master.c:113-124 truncates the minimum latency to whole ms */
     const double gmin = topology_getMinimumLatency(bat);
     if (topology_getMinimumLatency(ref) != gmin) return 1;
-    const uint64_t jump = (uint64_t)gmin * 1000000ull;
-    TopoPacketIn* in = (TopoPacketIn*)calloc((size_t)perWindow, sizeof(TopoPacketIn));
-    TopoPacketOut* out = (TopoPacketOut*)calloc((size_t)perWindow, sizeof(TopoPacketOut));
+    const uint64_t jump = serial ? topowindow_serial_window_ns(bat) : topowindow_jump_ns(bat, 0);
+    if (!serial && jump != (uint64_t)gmin * 1000000ull) return 1;
+    TopoWindow* win = topowindow_new(bat);
+    Got got;
+    got.dl = (uint8_t*)calloc((size_t)perWindow, 1);
+    got.t = (uint64_t*)calloc((size_t)perWindow, 8);
+    uint32_t* batS = (uint32_t*)calloc((size_t)perWindow, 4);
     uint8_t* refDl = (uint8_t*)calloc((size_t)perWindow, 1);
     uint64_t* refT = (uint64_t*)calloc((size_t)perWindow, 8);
     uint32_t* refS = (uint32_t*)calloc((size_t)perWindow, 4);
@@ -116,32 +139,38 @@ int main(int argc, char** argv) {
             if (refDl[n]) {
                 const double lat = topology_getLatency(ref, h[s].addr, h[d].addr);
                 uint64_t t = now + (uint64_t)ceil(lat * 1000000.0);
-                if (t < now + jump) t = now + jump;
+                if (!serial && t < now + jump) t = now + jump;
+                if (serial && t < t0 + jump) {
+                    fprintf(stderr, "serial window: arrival %llu before the window end\n",
+                            (unsigned long long)t);
+                    mism++;
+                }
                 refT[n] = t;
             }
             refS[n] = shim_random_state(h[s].rngRef);
-            /* ---- adapter, emit half: capture the pre-draw state, advance by the one draw ---- */
-            in[n].srcIP = h[s].ip;
-            in[n].dstIP = h[d].ip;
-            in[n].payloadLength = payload;
-            in[n].rngState = shim_random_state(h[s].rngBat);
-            in[n].now = now;
-            random_nextDouble(h[s].rngBat);
+            /* ---- adapter, emit half (the product's topowindow_emit) ---- */
+            if (topowindow_emit(win, h[s].addr, h[d].addr, payload, h[s].rngBat, now,
+                                (void*)(intptr_t)n) != n) {
+                fprintf(stderr, "topowindow_emit failed\n");
+                return 2;
+            }
+            batS[n] = shim_random_state(h[s].rngBat);
             n++;
         }
         /* ---- adapter, barrier half (shd-slave.c:415): one batch for the window ---- */
-        if (topology_routePacketBatch(bat, in, out, (size_t)n, jump, 1) != 0) {
-            fprintf(stderr, "routePacketBatch failed\n");
+        got.calls = 0;
+        if (topowindow_pending(win) != n ||
+            topowindow_flush(win, jump, serial ? 0 : 1, deliver, &got) != 0 || got.calls != n) {
+            fprintf(stderr, "topowindow_flush failed\n");
             return 2;
         }
         for (int k = 0; k < n; k++) {
             total++;
-            delivered += out[k].delivered;
-            if (out[k].delivered != refDl[k] || out[k].time != refT[k] ||
-                out[k].rngState != refS[k]) {
+            delivered += got.dl[k];
+            if (got.dl[k] != refDl[k] || got.t[k] != refT[k] || batS[k] != refS[k]) {
                 if (mism < 5)
                     fprintf(stderr, "window %d packet %d: batch (%u, %llu, %u) reference (%u, %llu, %u)\n",
-                            w, k, out[k].delivered, (unsigned long long)out[k].time, out[k].rngState,
+                            w, k, got.dl[k], (unsigned long long)got.t[k], batS[k],
                             refDl[k], (unsigned long long)refT[k], refS[k]);
                 mism++;
             }
@@ -156,8 +185,9 @@ int main(int argc, char** argv) {
             fprintf(stderr, "window %d: lazy minimum %.17g vs %.17g\n", w, m1, m2);
             mism++;
         }
-        t0 += jump ? jump : 10000000ull;
+        t0 += jump;
     }
+    topowindow_free(win);
     /* orientation matters on this graph: pairs whose two rows disagree in the last bits */
     const int64_t A = shdtopo_num_attached(bat);
     double* lat = (double*)malloc(sizeof(double) * (size_t)(A * A));
@@ -165,9 +195,9 @@ int main(int argc, char** argv) {
         for (int64_t i = 0; i < A; i++)
             for (int64_t j = i + 1; j < A; j++)
                 if (lat[i * A + j] != lat[j * A + i]) reversed++;
-    printf("engine_window: %ld packets in %d windows, %ld delivered, %ld mismatches, jump %llu ns, "
-           "%ld of %lld attached pairs orientation-dependent\n",
-           total, windows, delivered, mism, (unsigned long long)jump, reversed,
-           (long long)(A * (A - 1) / 2));
+    printf("engine_window: %s, %ld packets in %d windows, %ld delivered, %ld mismatches, "
+           "window %llu ns, %ld of %lld attached pairs orientation-dependent\n",
+           serial ? "serial" : "multi-threaded", total, windows, delivered, mism,
+           (unsigned long long)jump, reversed, (long long)(A * (A - 1) / 2));
     return mism ? 1 : 0;
 }

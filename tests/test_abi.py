@@ -22,9 +22,12 @@ from shadow_amd import _lib
 
 
 def header_functions():
-    txt = open(os.path.join(ROOT, "include", "shd_topology_abi.h")).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b((?:topology|shdtopo)_\w+)\s*\(", txt)))
+    names = set()
+    for h in ("shd_topology_abi.h", "shd_topology_window.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names |= set(re.findall(r"\b((?:topology|shdtopo|topowindow)_\w+)\s*\(", txt))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():

@@ -1,0 +1,85 @@
+"""The product window adapter (include/shd_topology_window.h) against the reference's per-packet
+worker_schedulePacket (src/engine/shd-worker.c:332-370) over the reference Topology restatement
+(oracle.OracleTopology), in multi-threaded windows (runahead clamp) and serial-mode windows.
+
+Hosts carry Shadow Random streams (libshdtopo_shim.so); packets go through topowindow_emit, which
+captures the pre-draw state and takes the draw, and come back through topowindow_flush's deliver
+callback.  The reference side replays the same emission order with getReliability, the draw,
+getLatency and the clamp.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+import shadow_amd as sa
+from shadow_amd import _lib
+from helpers import host_ip, synthetic_pair
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("serial", [False, True])
+def test_window_adapter_vs_reference(serial):
+    top, g = synthetic_pair(seed=31, n_routers=1500, n_poi=80, n_edges=15000, integer=True)
+    lib, shim = _lib.load()
+    otop = oracle.OracleTopology(g)
+    nh = 150
+    hosts = []
+    st = 5
+    for k in range(nh):
+        st = (st * 1103515245 + 12345) & 0xFFFFFFFF
+        ip = host_ip(k + 1)
+        v1, s1 = top.attach_ip(ip, st, typeHint=("client", "relay", "server")[k % 3])
+        v2, s2 = otop.attach(ip, st, type_hint=("client", "relay", "server")[k % 3])
+        assert v1 == v2 and s1 == s2
+        hosts.append((ip, sa.Address(ip), sa.Random(s1)))
+    ref_state = [h[2].state for h in hosts]
+    w = lib.topowindow_new(top._h)
+    jump = lib.topowindow_serial_window_ns(top._h) if serial else lib.topowindow_jump_ns(top._h, 0)
+    gmin = top.getMinimumLatency()
+    if serial:
+        assert jump == math.floor(gmin * 1e6)
+    else:
+        assert jump == int(gmin) * 1_000_000
+    got = {}
+
+    @_lib.WINDOW_DELIVER
+    def deliver(ctx, packet, delivered, time):
+        got[int(packet)] = (delivered, time)
+
+    rng = np.random.default_rng(8)
+    t0 = 10**9
+    for win in range(3):
+        ref = []
+        for k in range(1500):
+            s, d = (int(x) for x in rng.choice(nh, 2, replace=False))
+            pay = 1448 if rng.random() < 0.8 else 0
+            now = t0 + int(rng.integers(0, jump))
+            # reference, shd-worker.c:345-369 at emit
+            rel = otop.get_reliability(hosts[s][0], hosts[d][0])
+            r, ref_state[s] = oracle.next_double(ref_state[s])
+            dl = r <= rel or pay == 0
+            t = 0
+            if dl:
+                lat = otop.get_latency(hosts[s][0], hosts[d][0])
+                t = now + int(math.ceil(lat * 1e6))
+                if not serial:
+                    t = max(t, now + jump)
+                else:
+                    assert t >= t0 + jump  # the deferral changes no arrival time
+            ref.append((int(dl), t))
+            # adapter
+            idx = lib.topowindow_emit(w, hosts[s][1]._p, hosts[d][1]._p, pay, hosts[s][2]._p, now,
+                                      k + 1)
+            assert idx == k
+            assert hosts[s][2].state == ref_state[s]
+        got.clear()
+        assert lib.topowindow_pending(w) == len(ref)
+        assert lib.topowindow_flush(w, jump, 0 if serial else 1, deliver, None) == 0
+        assert lib.topowindow_pending(w) == 0
+        assert [got[k + 1] for k in range(len(ref))] == ref
+        assert top.lazyMinimumLatency() == otop.minimum_path_latency
+        t0 += jump
+    lib.topowindow_free(w)
