@@ -175,6 +175,9 @@ struct _Topology {
     bool tieReplay = true;    // option "tie_replay" (0: report ambiguous pairs only)
     bool replayAll = false;   // option "replay_all" (test hook: every row through the replay)
     int replaySlotsOpt = 0;   // option "replay_slots" (0 = sized from the CUs and free HBM)
+    int sourceOrder = 1;      // option "source_order": batch kernel source grouping (0 = row
+                              // order, 1 = by the hub their h0-tree path enters the core, then pi)
+    DevBuf<uint32_t> d_rowmap;
     bool replayUploaded = false;
     DevBuf<uint32_t> d_rrow;
     DevBuf<uint4> d_rrec;
@@ -375,6 +378,29 @@ int dev_init(Topology* top) {
 // at hubs).  Self loops go to selfLat/selfLoss (first = lowest edge id, as orc_get_eid).
 SsspLdsPlan lds_plan(Topology* top);
 
+// IEEE half bits of x rounded up (up) or down (!up): directed rounding, so a stored bound never
+// tightens (+-inf for NaN).  Exact search over the finite halves, sorted once.
+uint16_t f16_directed(double x, bool up) {
+    static const std::vector<std::pair<double, uint16_t>> tab = [] {
+        std::vector<std::pair<double, uint16_t>> t;
+        for (uint32_t b = 0; b < 0x10000u; b++) {
+            const uint32_t e = (b >> 10) & 31u, m = b & 1023u;
+            if (e == 31u) continue;  // inf / NaN
+            const double mag = e == 0 ? std::ldexp((double)m, -24) : std::ldexp((double)(1024 + m), (int)e - 25);
+            t.push_back({(b & 0x8000u) ? -mag : mag, (uint16_t)b});
+        }
+        std::sort(t.begin(), t.end());
+        return t;
+    }();
+    if (std::isnan(x)) return up ? 0x7C00 : 0xFC00;
+    if (up) {
+        auto it = std::lower_bound(tab.begin(), tab.end(), std::make_pair(x, (uint16_t)0));
+        return it == tab.end() ? (uint16_t)0x7C00 : it->second;  // smallest half >= x
+    }
+    auto it = std::upper_bound(tab.begin(), tab.end(), std::make_pair(x, (uint16_t)0xFFFF));
+    return it == tab.begin() ? (uint16_t)0xFC00 : std::prev(it)->second;  // largest half <= x
+}
+
 int upload_csr(Topology* top) {
     if (top->csrUploaded) return 0;
     HostGraph& g = top->g;
@@ -514,17 +540,30 @@ int upload_csr(Topology* top) {
     HIPCHK(top->d_selfLoss.ensure((size_t)V));
     HIPCHK(hipMemcpy(top->d_rowptr.p, rowptr.data(), sizeof(uint32_t) * ((size_t)V + 1), hipMemcpyHostToDevice));
     if (nadj) {
-        // 16-B records {col, pi(col) as f32 rounded up, f64 latency} (AdjRec)
+        // kappa0 of every vertex: the smallest kappa = w - pi(col) of its row (+inf: empty row,
+        // -inf: pi unknown), as the kappa-sorted copy below computes it
+        std::vector<double> kmin((size_t)V, INFINITY);
+        for (int32_t v = 0; v < V; v++)
+            for (uint32_t k = rowptr[(size_t)v]; k < rowptr[(size_t)v + 1]; k++) {
+                const double pv = top->pot[col[k]];
+                kmin[(size_t)v] = std::min(kmin[(size_t)v], std::isfinite(pv) ? wt[k] - pv : -INFINITY);
+            }
+        // 16-B records {col, pi(col) as f32 rounded up | {f16 pi up, f16 kappa0 down}, f64 w}
         std::vector<uint32_t> adj(4 * nadj);
         for (size_t k = 0; k < nadj; k++) {
             uint64_t wb;
             memcpy(&wb, &wt[k], 8);
             const double pv = top->pot[col[k]];
-            float pf = (float)pv;
-            if (std::isfinite(pv) && (double)pf < pv) pf = std::nextafter(pf, INFINITY);
-            if (!std::isfinite(pv)) pf = INFINITY;
             uint32_t pb;
-            memcpy(&pb, &pf, 4);
+            if (kKapInRec) {
+                pb = ((uint32_t)f16_directed(std::isfinite(pv) ? pv : INFINITY, true) << 16) |
+                     (uint32_t)f16_directed(kmin[col[k]], false);
+            } else {
+                float pf = (float)pv;
+                if (std::isfinite(pv) && (double)pf < pv) pf = std::nextafter(pf, INFINITY);
+                if (!std::isfinite(pv)) pf = INFINITY;
+                memcpy(&pb, &pf, 4);
+            }
             adj[4 * k] = col[k];
             adj[4 * k + 1] = pb;
             adj[4 * k + 2] = (uint32_t)wb;
@@ -988,12 +1027,43 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             SlotWs ws = slot_ws(top);
             ws.rowflag = top->d_rowflag.p;
             if (K > 1) {
+                // Batches of K sources settle in lock-step and share an expansion when their
+                // shifted distances to a vertex fall in one bucket: sources whose shortest paths
+                // enter the hub core through the same hub share the most.  Batch position p takes
+                // source perm[p]; the kernel writes its row at rowmap[p] = perm[p].
+                std::vector<uint32_t> perm((size_t)rows);
+                std::iota(perm.begin(), perm.end(), 0u);
+                if (top->sourceOrder == 1) {
+                    const uint32_t Hc = (uint32_t)lds_plan(top).H;
+                    std::vector<uint64_t> key((size_t)rows);
+                    for (int64_t i = 0; i < rows; i++) {
+                        uint32_t v = src[(size_t)i];
+                        for (int hop = 0; v >= Hc && hop < 64; hop++) {  // up the h0 tree
+                            const uint32_t p = top->sptPar[(size_t)v];
+                            if (p == 0xFFFFFFFFu) break;
+                            v = p;
+                        }
+                        const double pi = top->pot[(size_t)src[(size_t)i]];
+                        const float pf = std::isfinite(pi) ? (float)pi : INFINITY;
+                        uint32_t pb;
+                        memcpy(&pb, &pf, 4);
+                        key[(size_t)i] = ((uint64_t)v << 32) | pb;  // pi >= 0: bits order as values
+                    }
+                    std::stable_sort(perm.begin(), perm.end(),
+                                     [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+                }
+                std::vector<uint32_t> psrc((size_t)rows);
+                for (int64_t i = 0; i < rows; i++) psrc[(size_t)i] = src[(size_t)perm[(size_t)i]];
+                HIPCHK(top->d_rowmap.ensure((size_t)rows));
+                HIPCHK(hipMemcpyAsync(top->d_rowmap.p, perm.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
+                HIPCHK(hipMemcpyAsync(top->d_sources.p, psrc.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
+                ws.rowmap = top->d_rowmap.p;
                 // bucket shift per row: sh = C - pi(src) >= 2 delta (topo_sssp_batch.hip)
                 const double delta = default_delta(top);
                 const double pmax = top->piMax;  // largest finite pi (upload_csr)
                 std::vector<double> sh((size_t)rows);
                 for (int64_t i = 0; i < rows; i++) {
-                    const double p = top->pot[(size_t)src[(size_t)i]];
+                    const double p = top->pot[(size_t)psrc[(size_t)i]];
                     sh[(size_t)i] = (pmax - (std::isfinite(p) ? p : pmax)) + 2.0 * delta;
                 }
                 HIPCHK(top->d_srcsh.ensure((size_t)rows));
@@ -1041,6 +1111,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             if (r) return r;
             r = upload_target_bits(top, tgt, st);
             if (r) return r;
+            // the batch kernel took its sources in locality order: the replay indexes by row
+            HIPCHK(hipMemcpy(top->d_sources.p, src.data(), sizeof(uint32_t) * (size_t)rows, hipMemcpyHostToDevice));
             HIPCHK(top->d_rrows.ensure(rlist.size()));
             HIPCHK(hipMemcpy(top->d_rrows.p, rlist.data(), 4 * rlist.size(), hipMemcpyHostToDevice));
             HIPCHK(hipEventRecord(top->evr0, st));
@@ -1216,6 +1288,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->tieReplay = top->tieReplay;
     p->replayAll = top->replayAll;
     p->replaySlotsOpt = top->replaySlotsOpt;
+    p->sourceOrder = top->sourceOrder;
     p->attached = top->attached;
     p->colOf = top->colOf;
     p->A = top->A;
@@ -1775,6 +1848,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "tie_replay") top->tieReplay = value != 0;
     else if (k == "replay_all") top->replayAll = value != 0;
     else if (k == "replay_slots") top->replaySlotsOpt = (int)value;
+    else if (k == "source_order") top->sourceOrder = (int)value;
     else if (k == "devices") {
         const int n = (int)value;
         if (n < 1 || n > 64) return -1;

@@ -31,6 +31,13 @@ constexpr int kRingPerVertex = SHD_RING_PER_VERTEX;  // bucket-window entries pe
 constexpr int kOverPerVertex = 2;  // overflow-pile capacity per slot, in 16-B entries per vertex
                                    // (double buffered: a refill streams the kept entries over)
 constexpr int kNearPerVertex = 2; // near-queue capacity per slot, in entries per vertex
+#ifndef SHD_KAP_IN_REC
+#define SHD_KAP_IN_REC 1
+#endif
+// 1: the adjacency record's 32-bit field holds {f16 pi(col) rounded up, f16 kappa0(col) rounded
+// down} (high, low half), so the batch relaxation gets the target's kappa0 with the record
+// instead of a random 4-B load per surviving edge; 0: f32 pi(col) rounded up, kappa0 from g.kap0
+constexpr bool kKapInRec = SHD_KAP_IN_REC != 0;
 
 // indices into the device stats block (unsigned long long[16])
 enum StatIdx {
@@ -113,6 +120,9 @@ struct SlotWs {
     // per row of the launch: set to 1 when a pair of the row crosses a d-tied parent (its parent
     // chain needs igraph's heap pop order: the row is recomputed by heap_replay_kernel)
     uint8_t* rowflag = nullptr;
+    // batch kernel: output row of batch position p (sources are taken in a locality order, the
+    // table keeps row order); nullptr = identity
+    const uint32_t* rowmap = nullptr;
 };
 
 // Incidence-order CSR of the heap replay (topo_replay.hip), relabelled vertex ids: row x holds

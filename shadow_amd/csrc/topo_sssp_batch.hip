@@ -277,6 +277,15 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
 // Can vertex v at distance d (source j, d_j(h0) = h) have an edge that passes the landmark
 // filter?  Only if kappa0(v) (its smallest kappa, f32 rounded down) lies under the CUT threshold of
 // load_chunk; h may be stale (larger), which only widens the test.
+// the record's pi(col) (rounded up) and the target's kappa0 (rounded down), kKapInRec layout
+__device__ __forceinline__ double rec_pi(uint32_t p) {
+    if (kKapInRec) return (double)(float)__builtin_bit_cast(_Float16, (unsigned short)(p >> 16));
+    return (double)__uint_as_float(p);
+}
+__device__ __forceinline__ float rec_kap0(uint32_t p) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(p & 0xFFFFu));
+}
+
 __device__ __forceinline__ bool kappa_useful(float k0, double h, double d, double pimax) {
     return (double)k0 <= (h - d) + 1e-5 * (h + d + pimax) + 1e-9;
 }
@@ -476,7 +485,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             for (int a = 0; a < UA; a++) {
                 uint32_t mk = amk[a];
                 const double w = __hiloint2double((int)awh[a], (int)awl[a]);
-                const double pv = (double)__uint_as_float(apb[a]);
+                const double pv = rec_pi(apb[a]);
                 while (mk) {
                     const uint32_t jj = (uint32_t)__ffs(mk) - 1u;
                     mk &= mk - 1u;
@@ -496,7 +505,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 nsv += (uint32_t)__popcll(sb[a]);
             }
             {
-                uint32_t cn[UA], cmk[UA], clo[UA], cwl[UA], cwh[UA];
+                uint32_t cn[UA], cmk[UA], clo[UA], cwl[UA], cwh[UA], cpb[UA];
 #pragma unroll
                 for (int a2 = 0; a2 < UA; a2++) {
                     uint32_t q = (uint32_t)a2 * 64u + lane;
@@ -518,6 +527,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     }
                     const int sl = ok ? (int)pos : (int)lane;
                     cn[a2] = 0u; cmk[a2] = 0u; clo[a2] = 0u; cwl[a2] = 0u; cwh[a2] = 0u;
+                    cpb[a2] = 0u;
 #pragma unroll
                     for (int a = 0; a < UA; a++) {
                         const uint32_t xn = __shfl(an[a], sl, 64);
@@ -525,15 +535,17 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                         const uint32_t xl = __shfl(alo[a], sl, 64);
                         const uint32_t xwl = __shfl(awl[a], sl, 64);
                         const uint32_t xwh = __shfl(awh[a], sl, 64);
+                        const uint32_t xpb = kKapInRec ? __shfl(apb[a], sl, 64) : 0u;
                         if (ok && sa == a) {
                             cn[a2] = xn; cmk[a2] = xm; clo[a2] = xl; cwl[a2] = xwl; cwh[a2] = xwh;
+                            cpb[a2] = xpb;
                         }
                     }
                 }
 #pragma unroll
                 for (int a = 0; a < UA; a++) {
                     an[a] = cn[a]; amk[a] = cmk[a]; alo[a] = clo[a]; awl[a] = cwl[a];
-                    awh[a] = cwh[a];
+                    awh[a] = cwh[a]; apb[a] = cpb[a];
                 }
             }
             // phase B: round r holds edges r * EPW .. r * EPW + EPW - 1 of the wave's compacted
@@ -562,7 +574,8 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 // pre-check: the K lanes of the edge read its target's line in one request
                 const bool t = on && n[rr] >= D.H;
                 const unsigned long long x = D.dist[(t ? (size_t)n[rr] : (size_t)0) * K + j];
-                kz[rr] = g.kap0[t ? n[rr] : 0u];
+                if (kKapInRec) kz[rr] = rec_kap0(__shfl(apb[a], src, 64));
+                else kz[rr] = g.kap0[t ? n[rr] : 0u];
                 cur[rr] = t ? x : 0ull;
             }
 #pragma unroll
@@ -1310,18 +1323,18 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 }
                 if (amb) {
                     atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
-                    if (ws.rowflag) ws.rowflag[r0 + (int)j] = 1;  // tie replay (topo_replay.hip)
+                    if (ws.rowflag) ws.rowflag[ws.rowmap ? ws.rowmap[r0 + (int)j] : r0 + (int)j] = 1;  // tie replay (topo_replay.hip)
                 }
                 if (lat == 0.0) lat = 1.0;
             }
-            const size_t o = (size_t)(r0 + (int)j) * (size_t)A + k;
+            const size_t o = (size_t)(ws.rowmap ? (int)ws.rowmap[r0 + (int)j] : r0 + (int)j) * (size_t)A + k;
             out_lr[o] = make_double2(lat, rel);
             out_hops[o] = (uint16_t)(h > 65535u ? 65535u : h);
             if (lat >= 0.0) atomicMin(&L.rmin[j], d2bits(lat));  // row minimum (runahead)
         }
         __syncthreads();
         if ((int)tid < nk) {
-            if (out_rowmin) out_rowmin[r0 + tid] = bits2d(L.rmin[tid]);
+            if (out_rowmin) out_rowmin[ws.rowmap ? (int)ws.rowmap[r0 + tid] : r0 + (int)tid] = bits2d(L.rmin[tid]);
             atomicMin(&stats[ST_GLOBAL_MIN], L.rmin[tid]);  // shd-topology.c:500-511
         }
         __syncthreads();

@@ -10,10 +10,12 @@ OUT=$ROOT/abtest/$NAME
 mkdir -p "$OUT/obj"
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-result $*"
 cd "$ROOT/shadow_amd/csrc"
-/opt/rocm/bin/hipcc $FLAGS -x hip -c topo_core.cpp -o "$OUT/obj/core.o" &
-/opt/rocm/bin/hipcc $FLAGS -x hip -c topo_graph.cpp -o "$OUT/obj/graph.o" &
-/opt/rocm/bin/hipcc $FLAGS -c topo_kernels.hip -o "$OUT/obj/kernels.o" &
-/opt/rocm/bin/hipcc $FLAGS -c topo_sssp_batch.hip -o "$OUT/obj/batch.o" &
+for f in topo_core.cpp topo_graph.cpp topo_window.cpp; do
+  /opt/rocm/bin/hipcc $FLAGS -x hip -c $f -o "$OUT/obj/${f%.cpp}.o" &
+done
+for f in topo_kernels.hip topo_sssp_batch.hip topo_replay.hip; do
+  /opt/rocm/bin/hipcc $FLAGS -c $f -o "$OUT/obj/${f%.hip}.o" &
+done
 wait
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libshdtopo.so" "$OUT"/obj/*.o -lpthread
 echo "$OUT/libshdtopo.so"
