@@ -141,6 +141,7 @@ struct _Topology {
     std::vector<int32_t> inv;   // old -> new
     std::vector<double> pot;    // batch mode: d(h0, v) from the top hub (new ids), the bucket shift
     std::vector<uint32_t> sptPar, sptSlot;  // h0 shortest-path tree: parent, its adjacency slot
+    std::vector<uint32_t> sptPre;           // preorder number in that tree (source_order 2)
     DevBuf<uint32_t> d_spt;     // per vertex {parent, slot of (parent -> v), f64 latency}
     int wsK = 0;                // batch width the workspace was laid out for
     int64_t wsRing = 0, wsOver = 0;
@@ -175,8 +176,11 @@ struct _Topology {
     bool tieReplay = true;    // option "tie_replay" (0: report ambiguous pairs only)
     bool replayAll = false;   // option "replay_all" (test hook: every row through the replay)
     int replaySlotsOpt = 0;   // option "replay_slots" (0 = sized from the CUs and free HBM)
-    int sourceOrder = 1;      // option "source_order": batch kernel source grouping (0 = row
-                              // order, 1 = by the hub their h0-tree path enters the core, then pi)
+    int sourceOrder = 2;      // option "source_order": batch kernel source grouping (0 = row
+                              // order, 1 = by the hub their h0-tree path enters the core, then
+                              // pi, 2 = preorder of the h0 shortest-path tree)
+    int batchOrder = 2;       // option "batch_order": 0 grouped order, 1 shuffled, 2 / 3 by mean
+                              // pi descending / ascending
     DevBuf<uint32_t> d_rowmap;
     bool replayUploaded = false;
     DevBuf<uint32_t> d_rrow;
@@ -1033,7 +1037,32 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 // source perm[p]; the kernel writes its row at rowmap[p] = perm[p].
                 std::vector<uint32_t> perm((size_t)rows);
                 std::iota(perm.begin(), perm.end(), 0u);
-                if (top->sourceOrder == 1) {
+                if (top->sourceOrder == 2) {
+                    // preorder of the h0 shortest-path tree: sources in one subtree (sharing the
+                    // longest path prefix from h0) are adjacent
+                    if (top->sptPre.empty()) {
+                        const size_t Vn = (size_t)top->g.V;
+                        std::vector<uint32_t> cnt(Vn + 1, 0), ch(Vn);
+                        for (size_t v = 0; v < Vn; v++)
+                            if (top->sptPar[v] != 0xFFFFFFFFu) cnt[top->sptPar[v] + 1]++;
+                        for (size_t v = 0; v < Vn; v++) cnt[v + 1] += cnt[v];
+                        std::vector<uint32_t> fillc(cnt.begin(), cnt.end() - 1);
+                        for (size_t v = 0; v < Vn; v++)
+                            if (top->sptPar[v] != 0xFFFFFFFFu) ch[fillc[top->sptPar[v]]++] = (uint32_t)v;
+                        top->sptPre.assign(Vn, 0xFFFFFFFFu);
+                        std::vector<uint32_t> stk{0u};
+                        uint32_t next = 0;
+                        while (!stk.empty()) {
+                            const uint32_t v = stk.back();
+                            stk.pop_back();
+                            top->sptPre[v] = next++;
+                            for (uint32_t k = cnt[v + 1]; k > cnt[v]; k--) stk.push_back(ch[k - 1]);
+                        }
+                    }
+                    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
+                        return top->sptPre[src[a]] < top->sptPre[src[b]];
+                    });
+                } else if (top->sourceOrder == 1) {
                     const uint32_t Hc = (uint32_t)lds_plan(top).H;
                     std::vector<uint64_t> key((size_t)rows);
                     for (int64_t i = 0; i < rows; i++) {
@@ -1051,6 +1080,44 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     }
                     std::stable_sort(perm.begin(), perm.end(),
                                      [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+                }
+                // order of the batches (groups of K consecutive positions) in the dequeue: the
+                // kernel ends with the slowest slot, so the last batches decide its tail
+                if (top->batchOrder != 0 && rows > K) {
+                    const int64_t nb = (rows + K - 1) / K;
+                    std::vector<uint32_t> bo((size_t)nb);
+                    std::iota(bo.begin(), bo.end(), 0u);
+                    if (top->batchOrder == 1) {
+                        SplitMix rng(0x5eedull);
+                        for (int64_t i = nb - 1; i > 0; i--) std::swap(bo[(size_t)i], bo[(size_t)rng.below((uint64_t)i + 1)]);
+                    } else {
+                        std::vector<double> mp((size_t)nb, 0.0);
+                        for (int64_t b = 0; b < nb; b++) {
+                            int64_t c = 0;
+                            for (int64_t i = b * K; i < std::min(rows, (b + 1) * K); i++, c++) {
+                                const double p = top->pot[(size_t)src[(size_t)perm[(size_t)i]]];
+                                mp[(size_t)b] += std::isfinite(p) ? p : 0.0;
+                            }
+                            mp[(size_t)b] /= (double)std::max<int64_t>(1, c);
+                        }
+                        const bool desc = top->batchOrder == 2;
+                        std::stable_sort(bo.begin(), bo.end(), [&](uint32_t a, uint32_t b) {
+                            return desc ? mp[a] > mp[b] : mp[a] < mp[b];
+                        });
+                    }
+                    // the ragged batch (if any) stays last
+                    const int64_t last = nb - 1;
+                    if (rows % K) {
+                        auto it = std::find(bo.begin(), bo.end(), (uint32_t)last);
+                        bo.erase(it);
+                        bo.push_back((uint32_t)last);
+                    }
+                    std::vector<uint32_t> p2;
+                    p2.reserve((size_t)rows);
+                    for (uint32_t b : bo)
+                        for (int64_t i = (int64_t)b * K; i < std::min(rows, ((int64_t)b + 1) * K); i++)
+                            p2.push_back(perm[(size_t)i]);
+                    perm.swap(p2);
                 }
                 std::vector<uint32_t> psrc((size_t)rows);
                 for (int64_t i = 0; i < rows; i++) psrc[(size_t)i] = src[(size_t)perm[(size_t)i]];
@@ -1289,6 +1356,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->replayAll = top->replayAll;
     p->replaySlotsOpt = top->replaySlotsOpt;
     p->sourceOrder = top->sourceOrder;
+    p->batchOrder = top->batchOrder;
     p->attached = top->attached;
     p->colOf = top->colOf;
     p->A = top->A;
@@ -1849,6 +1917,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "replay_all") top->replayAll = value != 0;
     else if (k == "replay_slots") top->replaySlotsOpt = (int)value;
     else if (k == "source_order") top->sourceOrder = (int)value;
+    else if (k == "batch_order") top->batchOrder = (int)value;
     else if (k == "devices") {
         const int n = (int)value;
         if (n < 1 || n > 64) return -1;
