@@ -192,6 +192,8 @@ typedef struct {
                                   time 0, state unchanged), since the last table build */
     int64_t devices;          /* GPUs that built the last table (option "devices") */
     double exchange_ms;       /* RCCL all-gather + all-reduce(min) of that build (wall) */
+    double parent_phase_ms[4]; /* batch kernel parent pass, summed over workgroups: walks, merged
+                                  row scans, recount + finalize, next level */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -605,6 +605,9 @@ int upload_csr(Topology* top) {
                 const uint32_t k = ord[i];
                 std::copy(adj.begin() + 4 * (size_t)k, adj.begin() + 4 * (size_t)k + 4,
                           adjk.begin() + 4 * (size_t)(b + i));
+                // bit 31 of the relaxation copy's column: this edge is the h0-tree edge into
+                // the column (its parent pass finds it without a recorded hint)
+                if (top->sptPar[col[k]] == (uint32_t)v) adjk[4 * (size_t)(b + i)] |= 0x80000000u;
                 kap[b + i] = down(kd[k - b]);
             }
             static const uint32_t probe[4] = {0, 1, 3, 7};
@@ -1226,6 +1229,7 @@ int collect_row_stats(Topology* top) {
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->device) != hipSuccess || khz <= 0)
             khz = 100000;
         for (int i = 0; i < 4; i++) top->stats.phase_ms[i] = (double)h[ST_T_INIT + i] / (double)khz;
+        for (int i = 0; i < 4; i++) top->stats.parent_phase_ms[i] = (double)h[ST_PT0 + i] / (double)khz;
     }
     top->stats.near_iterations = (int64_t)h[ST_NEAR_IT];
     top->stats.far_splits = (int64_t)h[ST_SPLITS];

@@ -67,7 +67,9 @@ enum StatIdx {
     ST_RP_MOD = 27,     //   modifies (strict improvement of a queued vertex)
     ST_RP_ROWS = 28,    //   rows replayed
     ST_ROUTE_BAD = 29,  // packets with a column outside [0, A) (not routed) since the last build
-    ST_COUNT = 30
+    ST_PT0 = 30,        // batch kernel parent pass, wall ticks summed over workgroups: walks,
+                        //   merged row scans, recount + finalize, next level (4 slots)
+    ST_COUNT = 34
 };
 
 struct DevCSR {

@@ -55,6 +55,9 @@ using namespace dev;
 #ifndef SHD_BATCH_U
 #define SHD_BATCH_U 2  // phase-A edges per lane
 #endif
+#ifndef SHD_TAIL_HINT
+#define SHD_TAIL_HINT 1  // record each tail pair's improver during the SSSP (parent-pass guess)
+#endif
 #ifndef SHD_BATCH_CHUNK
 #define SHD_BATCH_CHUNK 512
 #endif
@@ -149,6 +152,8 @@ struct BView {
     uint32_t* hpar;            // HBM [P][K]: vertex whose relaxation last lowered hub v for j
     uint32_t* pend;            // HBM, 1 bit per vertex: a tail vertex with a pair pending past cb
     uint32_t* tie;             // HBM, 1 bit per (tail vertex, source): a relaxation tied its value
+    uint32_t* tpar;            // HBM [V][K]: vertex whose relaxation last lowered the tail pair
+                               // (SHD_TAIL_HINT; the parent pass' par array, free during the SSSP)
     uint32_t H, P;
     __device__ __forceinline__ unsigned long long get(uint32_t v, uint32_t j) const {
         return v < H ? hd[(size_t)v * K + j] : ld_l2_u64(&dist[(size_t)v * K + j]);
@@ -558,13 +563,16 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             uint32_t n[RB], lo[RB];
             unsigned long long ab[RB], cur[RB];  // ab = ~0: source inactive on this edge
             float kz[RB];                         // kappa0 of the edge's target
+            uint32_t tree[RB];
 #pragma unroll
             for (int rr = 0; rr < RB; rr++) {
                 const int r = r0 + rr;
                 const int a = (r * EPW) / 64;              // phase-A slot of this round's edges
                 const int src = (r * EPW) % 64 + (int)ge;  // lane holding the edge
                 // (shuffles only in uniform control flow: inactive source lanes read as 0)
-                n[rr] = __shfl(an[a], src, 64);
+                const uint32_t nt = __shfl(an[a], src, 64);
+                n[rr] = nt & 0x7FFFFFFFu;
+                tree[rr] = nt >> 31;  // the h0-tree edge into n
                 const uint32_t mk = __shfl(amk[a], src, 64);
                 lo[rr] = __shfl(alo[a], src, 64);
                 const double w = __hiloint2double((int)__shfl(awh[a], src, 64),
@@ -600,6 +608,10 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     const unsigned long long old = atomicMin(&D.dist[wi], ab[rr]);
                     im = ab[rr] < old;
                     if (ab[rr] == old) atomicOr(&D.tie[wi >> 5], 1u << (wi & 31));
+                    // the improver as the parent pass' second guess (a later improver's hint may
+                    // be overwritten by an earlier one's store: the pass verifies tightness)
+                    // (the h0-tree edge needs no record: it is the pass' first guess)
+                    if (SHD_TAIL_HINT && im && !tree[rr]) D.tpar[wi] = L.vx[lo[rr]];
                     cur[rr] = old;
                 }
                 bool nr = false, nf = false;
@@ -726,6 +738,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     uint32_t* bslot = ws.bslot + (size_t)slot * V * K;
     unsigned long long* memo = ws.memo + (size_t)slot * V * K;
     uint32_t* par = ws.par + (size_t)slot * V * K;
+    D.tpar = par;
     uint32_t* pbuf = ws.pathbuf + (size_t)slot * kMaxHops * kSsspBlock;
     uint32_t* ctr = ws.counters + (size_t)slot * 4;
     const uint32_t cap = (uint32_t)V;
@@ -1066,12 +1079,35 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             if (v >= H) {
                 if ((D.tie[q >> 5] >> (q & 31)) & 1u) return false;
                 const uint32_t pu = g.spt[4 * (size_t)v];
-                if (pu >= (uint32_t)V) return false;
-                const double wt = __hiloint2double((int)g.spt[4 * (size_t)v + 3],
-                                                   (int)g.spt[4 * (size_t)v + 2]);
-                if (__dadd_rn(bits2d(D.get(pu, j)), wt) != bits2d(D.get(v, j))) return false;
-                memo[q] = mtag | (unsigned long long)g.spt[4 * (size_t)v + 1];
-                par[q] = pu;
+                const unsigned long long dv = D.get(v, j);
+                if (pu < (uint32_t)V) {
+                    const double wt = __hiloint2double((int)g.spt[4 * (size_t)v + 3],
+                                                       (int)g.spt[4 * (size_t)v + 2]);
+                    if (__dadd_rn(bits2d(D.get(pu, j)), wt) == bits2d(dv)) {
+                        memo[q] = mtag | (unsigned long long)g.spt[4 * (size_t)v + 1];
+                        par[q] = pu;
+                        return true;
+                    }
+                }
+                if (!SHD_TAIL_HINT || !g.rows_sorted) return false;
+                // second guess: the recorded improver u; the edge is found in v's own row (a
+                // tail: short) -- the same undirected edge, same latency and loss as u's slot
+                const uint32_t u = par[q];
+                if (u >= (uint32_t)V || u == v) return false;
+                const unsigned long long du = D.get(u, j);
+                uint32_t lo = g.rowptr[v], hi = g.rowptr[v + 1];
+                const uint32_t end = hi;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (adj_col(g, mid) < u) lo = mid + 1; else hi = mid;
+                }
+                if (lo >= end || adj_col(g, lo) != u) return false;
+                uint32_t c;
+                double wt;
+                adj_load(g, lo, c, wt);
+                if (__dadd_rn(bits2d(du), wt) != bits2d(dv)) return false;
+                memo[q] = mtag | (unsigned long long)lo;
+                par[q] = u;
                 return true;
             }
             if (!g.rows_sorted || v >= P || ((D.tb[q >> 5] >> (q & 31)) & 1u)) return false;
@@ -1362,6 +1398,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         atomicAdd(&stats[ST_OVERSITE], 0ull);
         atomicAdd(&stats[ST_EV0 + 5], 0ull);
         atomicAdd(&stats[ST_EV0 + 5], n_par);
+        for (int i = 0; i < 4; i++) atomicAdd(&stats[ST_PT0 + i], L.pt[1 + i]);
     }
 }
 

@@ -55,6 +55,8 @@ for rep in range(args.reps):
           "splits/src %.0f slots %d" % tuple([x / rows for x in ph] +
                                             [st["near_iterations"] / rows,
                                              st["far_splits"] / rows, st["slots"]]), flush=True)
+    print("   parent phases ms/src: walks %.3f scans %.3f recount %.3f next %.3f" %
+          tuple(x / rows for x in st["parent_phase_ms"]), flush=True)
     print("   split ms/src %.2f  far-scan sources %d" % (st["split_ms"] / rows,
                                                       st["far_scan_sources"]), flush=True)
     print("   per-source events:", {k: "%.3g" % (v / rows) for k, v in st["events"].items()},
