@@ -1067,7 +1067,10 @@ __global__ void row_min_kernel(int64_t rows, int64_t A, const double2* __restric
 // table far larger than the caches, so the kernel lives on memory-level parallelism.
 // A column outside [0, A) is not routed (delivered 0, time 0, state unchanged) and counted.
 // ------------------------------------------------------------------------------------------
-constexpr int kRouteU = 8;
+#ifndef SHD_ROUTE_U
+#define SHD_ROUTE_U 1
+#endif
+constexpr int kRouteU = SHD_ROUTE_U;  // packets per thread (gathers in flight)
 
 __global__ void __launch_bounds__(256)
 packet_route_kernel(int64_t n, const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
