@@ -194,6 +194,9 @@ typedef struct {
     double exchange_ms;       /* RCCL all-gather + all-reduce(min) of that build (wall) */
     double parent_phase_ms[4]; /* batch kernel parent pass, summed over workgroups: walks, merged
                                   row scans, recount + finalize, next level */
+    int64_t replay_lines[6];  /* profiling builds (-DSHD_RP_LINES=1) only, else 0: 64-B lines the
+                                 replay touched in HBM -- sink loads, sink stores, shift-up loads,
+                                 shift-up stores, relaxation loads, relaxation stores */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

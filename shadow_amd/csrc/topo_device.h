@@ -69,7 +69,9 @@ enum StatIdx {
     ST_ROUTE_BAD = 29,  // packets with a column outside [0, A) (not routed) since the last build
     ST_PT0 = 30,        // batch kernel parent pass, wall ticks summed over workgroups: walks,
                         //   merged row scans, recount + finalize, next level (4 slots)
-    ST_COUNT = 34
+    ST_RP_L0 = 34,      // replay 64-B lines (SHD_RP_LINES builds): sink ld/st, shift-up ld/st,
+                        // relaxation ld/st
+    ST_COUNT = 40
 };
 
 struct DevCSR {
@@ -146,16 +148,14 @@ struct ReplayCSR {
 };
 
 // per-slot workspace of the heap replay (one wavefront = one slot), slot-major [slot][V]:
-// dist f64 (-1 = unreached), heap keys f64 + vertices u32 (positions >= the LDS part), hpos u32
-// (heap position of a queued vertex), par u32 (replay-CSR slot of the parent edge), and a path
-// buffer [kMaxHops][64] per slot.  28 B x V + 12 KiB per slot.
+// vertex records {f64 dist (-1 = unreached), u32 parent (replay-CSR slot of the parent edge),
+// u32 heap position} and heap nodes {f64 key, u32 vertex, pad} (positions >= the LDS part),
+// 16 B each (one line per access), and a path buffer [kMaxHops][64] per slot.
+// 32 B x V + 12 KiB per slot.
 struct ReplayWs {
     int slots = 0;
-    double* dist = nullptr;
-    double* key = nullptr;
-    uint32_t* vert = nullptr;
-    uint32_t* hpos = nullptr;
-    uint32_t* par = nullptr;
+    uint4* vrec = nullptr;
+    uint4* node = nullptr;
     uint32_t* pathbuf = nullptr;
 };
 

@@ -53,7 +53,19 @@ using namespace dev;
 #ifndef SHD_RP_LDS_LEVELS
 #define SHD_RP_LDS_LEVELS 9
 #endif
+#ifndef SHD_RP_PROG
+#define SHD_RP_PROG 1  // shift-up reads the parent first, the whole ancestor chain only if x rises
+#endif
+#ifndef SHD_RP_LINES
+#define SHD_RP_LINES 0  // profiling build: count the 64-B lines each part of the replay touches
+#endif
+#ifndef SHD_RP_LA
+#define SHD_RP_LA 5  // sink lookahead: heap levels loaded per round trip (<= 5: 62 nodes)
+#endif
 constexpr uint32_t kRpT = (1u << SHD_RP_LDS_LEVELS) - 1u;  // heap positions held in LDS
+constexpr int kRpLA = SHD_RP_LA;
+constexpr int kRpLaNodes = (2 << kRpLA) - 2;               // subtree nodes below the hole
+static_assert(kRpLA >= 1 && kRpLaNodes <= 64, "one node per lane");
 
 __device__ __forceinline__ uint32_t rl_u32(uint32_t x, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
@@ -68,49 +80,78 @@ __device__ __forceinline__ uint32_t uni_u32(uint32_t x) {
 }
 __device__ __forceinline__ double uni_f64(double x) { return rl_f64(x, 0); }
 
+// 64-B lines touched by one wave-wide access (active lanes, addresses ascending in lane order
+// for the heap's subtree / chain accesses; a random gather counts one line per lane).
+enum { RPL_SINK_LD, RPL_SINK_ST, RPL_SHIFT_LD, RPL_SHIFT_ST, RPL_RELAX_LD, RPL_RELAX_ST };
+__device__ __forceinline__ void rp_lines(unsigned long long* nl, int cat, bool act, const void* a) {
+#if SHD_RP_LINES
+    const unsigned long long line = (unsigned long long)a >> 6;
+    const unsigned long long am = __ballot(act);
+    const int lane = (int)__lane_id();
+    const unsigned long long prev = __shfl_up(line, 1);
+    const bool dup = lane > 0 && ((am >> (lane - 1)) & 1ull) && prev == line;
+    const unsigned long long nm = __ballot(act && !dup);
+    if (lane == __ffsll((long long)am) - 1) nl[cat] += (unsigned long long)__popcll(nm);
+#else
+    (void)nl; (void)cat; (void)act; (void)a;
+#endif
+}
+
 // The heap of one source: keys (igraph's data = -dist) and vertices, positions < kRpT in LDS,
-// the rest in this slot's HBM arrays; hpos[v] = position of v (igraph's index2 - 2).
+// the rest as 16-B nodes {f64 key, u32 vertex, pad} in this slot's HBM (one line per node
+// access); the position of a queued vertex lives in its 16-B vertex record
+// {f64 dist, u32 parent slot, u32 heap position} (one line per relaxation target).
 struct RpHeap {
-    double* gk;
-    uint32_t* gv;
-    uint32_t* hpos;
+    uint4* gn;
+    uint4* vr;
     double* sk;
     uint32_t* sv;
-    __device__ __forceinline__ double key(uint32_t p) const { return p < kRpT ? sk[p] : gk[p]; }
-    __device__ __forceinline__ uint32_t vtx(uint32_t p) const { return p < kRpT ? sv[p] : gv[p]; }
-    __device__ __forceinline__ void put(uint32_t p, double k, uint32_t v) const {
+    unsigned long long* nl;
+    __device__ __forceinline__ void node(uint32_t p, double& k, uint32_t& v, int cat) const {
+        rp_lines(nl, cat, p >= kRpT, gn + p);
+        if (p < kRpT) {
+            k = sk[p];
+            v = sv[p];
+        } else {
+            const uint4 q = gn[p];
+            k = __hiloint2double((int)q.y, (int)q.x);
+            v = q.z;
+        }
+    }
+    __device__ __forceinline__ void put(uint32_t p, double k, uint32_t v, int cat) const {
+        rp_lines(nl, cat, p >= kRpT, gn + p);
+        rp_lines(nl, cat, true, vr + 4 * (size_t)__lane_id() + v);  // random: one line each
         if (p < kRpT) {
             sk[p] = k;
             sv[p] = v;
         } else {
-            gk[p] = k;
-            gv[p] = v;
+            const unsigned long long b = d2bits(k);
+            gn[p] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), v, 0u);
         }
-        hpos[v] = p;
+        reinterpret_cast<uint32_t*>(vr + v)[3] = p;
     }
 };
 
-// igraph_2wheap_sink of element (xk, xv) from position `head` (a hole) in a heap of `size`.
-// The path of larger children does not depend on x, so the subtree five levels below the hole is
-// loaded at once; x stops where it is not smaller than the chosen child.
-__device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t size, double xk,
-                                        uint32_t xv, int lane) {
+// Heap position of this lane's node in the subtree kRpLA levels below `head` (BFS order).
+__device__ __forceinline__ uint32_t rp_sub_pos(uint32_t head, int lane) {
     const uint32_t rr = (uint32_t)lane + 2u;  // BFS index + 1 of this lane's subtree node
-    const int dl = 31 - __clz(rr);            // its depth below the hole (1..5 for lanes < 62)
-    const uint32_t off = rr - (1u << dl);
+    const int dl = 31 - __clz(rr);            // its depth below the hole (1..kRpLA)
+    return ((head + 1u) << dl) - 1u + (rr - (1u << dl));
+}
+
+// igraph_2wheap_sink of element (xk, xv) from position `head` (a hole) in a heap of `size`.
+// The path of larger children does not depend on x, so the subtree kRpLA levels below the hole
+// is loaded in one round trip; x stops where it is not smaller than the chosen child.  (k, v):
+// the first round's subtree, loaded by the caller together with its other loads.
+__device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t size, double xk,
+                                        uint32_t xv, int lane, double k, uint32_t v) {
     for (;;) {
-        const uint32_t p = ((head + 1u) << dl) - 1u + off;
-        double k = -INFINITY;
-        uint32_t v = 0;
-        if (lane < 62 && p < size) {
-            k = H.key(p);
-            v = H.vtx(p);
-        }
+        const uint32_t p = rp_sub_pos(head, lane);
         uint32_t cur = head, q = 0;
         bool stop = false;
         unsigned long long path = 0;
 #pragma unroll
-        for (int s = 0; s < 5; ++s) {
+        for (int s = 0; s < kRpLA; ++s) {
             const uint32_t L = 2u * cur + 1u;
             if (L >= size) {
                 stop = true;
@@ -139,38 +180,52 @@ __device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t
             }
         }
         // every chosen child moves up to its parent's position
-        if ((path >> lane) & 1ull) H.put((p - 1u) >> 1, k, v);
+        if ((path >> lane) & 1ull) H.put((p - 1u) >> 1, k, v, RPL_SINK_ST);
         head = cur;
         if (stop) break;
+        const uint32_t pn = rp_sub_pos(head, lane);  // below the last moved node: not written above
+        k = -INFINITY;
+        v = 0;
+        if (lane < kRpLaNodes && pn < size) H.node(pn, k, v, RPL_SINK_LD);
     }
-    if (lane == 0) H.put(head, xk, xv);
+    if (lane == 0) H.put(head, xk, xv, RPL_SINK_ST);
 }
 
 // igraph_2wheap_shift_up of element (xk, xv) from position `pos` (a hole).  Returns the number f
 // of ancestors moved down one level; lane i < f holds the moved vertex (mv) and its new position.
+// Most shift-ups stop below the parent: it is read first (one node), the whole chain only when x
+// rises past it.
 __device__ __forceinline__ int rp_shift_up(const RpHeap& H, uint32_t pos, double xk, uint32_t xv,
                                            int lane, uint32_t& mv, uint32_t& mp) {
+    if (SHD_RP_PROG && pos > 0) {
+        double k0;
+        uint32_t v0;
+        H.node((pos - 1u) >> 1, k0, v0, RPL_SHIFT_LD);
+        if (xk < uni_f64(k0)) {  // data[x] < data[parent]: stays
+            if (lane == 0) H.put(pos, xk, xv, RPL_SHIFT_ST);
+            return 0;
+        }
+    }
     const uint32_t depth = (uint32_t)(31 - __clz(pos + 1u));  // ancestors of pos
     const bool valid = (uint32_t)lane < depth;
     const uint32_t sh = valid ? (uint32_t)lane + 1u : 0u;
     const uint32_t a = ((pos + 1u) >> sh) - 1u;
     double ak = INFINITY;
     uint32_t av = 0;
-    if (valid) {
-        ak = H.key(a);
-        av = H.vtx(a);
-    }
+    if (valid) H.node(a, ak, av, RPL_SHIFT_LD);
     // x rises past every ancestor with key <= x and stops below the first one with key > x
     const unsigned long long stopm = __ballot(valid && xk < ak);
     const int f = stopm ? __ffsll((long long)stopm) - 1 : (int)depth;
     const uint32_t c = lane == 0 ? pos : (valid ? ((pos + 1u) >> (uint32_t)lane) - 1u : 0u);
-    if (lane < f) H.put(c, ak, av);
+    if (lane < f) H.put(c, ak, av, RPL_SHIFT_ST);
     const uint32_t fp = f == 0 ? pos : ((pos + 1u) >> (uint32_t)f) - 1u;
-    if (lane == 0) H.put(fp, xk, xv);
+    if (lane == 0) H.put(fp, xk, xv, RPL_SHIFT_ST);
     mv = av;
     mp = c;
     return f;
 }
+
+__device__ __forceinline__ uint32_t vr_par(const uint4* vr, uint32_t v) { return vr[v].z; }
 
 __global__ void __launch_bounds__(64, 4)
 heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ sources,
@@ -183,9 +238,9 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
     const int lane = (int)threadIdx.x;
     const size_t V = (size_t)g.V;
     const size_t slot = blockIdx.x;
-    double* dist = ws.dist + slot * V;
-    uint32_t* par = ws.par + slot * V;
-    RpHeap H{ws.key + slot * V, ws.vert + slot * V, ws.hpos + slot * V, sk, sv};
+    uint4* vr = ws.vrec + slot * V;
+    unsigned long long nl[6] = {0, 0, 0, 0, 0, 0};
+    RpHeap H{ws.node + slot * V, vr, sk, sv, nl};
     uint32_t* pbuf = ws.pathbuf + slot * (size_t)kMaxHops * 64;
     unsigned long long n_pop = 0, n_push = 0, n_mod = 0, n_rows = 0;
 
@@ -199,11 +254,15 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
         n_rows++;
 
         // ---- igraph_get_shortest_paths_dijkstra ----
-        for (size_t i = (size_t)lane; i < V; i += 64) dist[i] = -1.0;
+        {
+            const unsigned long long m1 = d2bits(-1.0);
+            for (size_t i = (size_t)lane; i < V; i += 64)
+                *reinterpret_cast<unsigned long long*>(vr + i) = m1;  // dist = -1
+        }
         uint32_t size = 1;
         if (lane == 0) {
-            dist[src] = 0.0;
-            H.put(0, 0.0, src);
+            *reinterpret_cast<double*>(vr + src) = 0.0;
+            H.put(0, 0.0, src, RPL_SINK_ST);
         }
         int64_t to_reach = full ? (int64_t)V + 1 : (int64_t)g.ntargets;
         while (size > 0 && to_reach > 0) {
@@ -211,36 +270,54 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
             const uint32_t u = uni_u32(sv[0]);
             const double du = -uni_f64(sk[0]);  // mindist = -data[0]
             const uint32_t lastp = size - 1u;
-            const double xk = uni_f64(H.key(lastp));
-            const uint32_t xv = uni_u32(H.vtx(lastp));
+            // one round trip: the sink's first subtree (lanes < kRpLaNodes), the last node (lane
+            // 63) and, independent of the heap, u's target bit, row bounds and first 64 records
+            double k1 = -INFINITY;
+            uint32_t v1 = 0;
+            {
+                const uint32_t p1 = rp_sub_pos(0, lane);
+                if (lane < kRpLaNodes && p1 < lastp) H.node(p1, k1, v1, RPL_SINK_LD);
+                else if (lane == 63) H.node(lastp, k1, v1, RPL_SINK_LD);
+            }
+            const uint32_t tb = g.tbits[u >> 5];
+            const uint32_t rb = uni_u32(g.rowptr[u]), re = uni_u32(g.rowptr[u + 1]);
+            uint4 r0 = make_uint4(0u, 0u, 0u, 0u);
+            if (rb + (uint32_t)lane < re) r0 = g.rec[rb + (uint32_t)lane];
+            const double xk = rl_f64(k1, 63);
+            const uint32_t xv = rl_u32(v1, 63);
             size = lastp;
-            if (size > 0) rp_sink(H, 0, size, xk, xv, lane);
+            if (size > 0) rp_sink(H, 0, size, xk, xv, lane, k1, v1);
             n_pop++;
-            if ((g.tbits[u >> 5] >> (u & 31u)) & 1u) {
+            if ((tb >> (u & 31u)) & 1u) {
                 to_reach--;
                 // every target is popped: its parent chain is final (relaxing u's edges, as
                 // igraph still does, cannot change a popped vertex)
                 if (to_reach == 0) break;
             }
-            const uint32_t rb = uni_u32(g.rowptr[u]), re = uni_u32(g.rowptr[u + 1]);
             for (uint32_t base = rb; base < re; base += 64) {
                 const uint32_t j = base + (uint32_t)lane;
                 const bool act = j < re;
                 uint32_t t = 0, mypos = 0;
                 double w = 0.0, cur = 0.0;
+                rp_lines(nl, RPL_RELAX_LD, act, g.rec + j);
+#if SHD_RP_LINES
+                rp_lines(nl, RPL_RELAX_LD, act, vr + 4 * (size_t)lane + (act ? g.rec[j].x : 0));
+#endif
                 if (act) {
-                    const uint4 r = g.rec[j];
+                    const uint4 r = base == rb ? r0 : g.rec[j];
                     t = r.x;
                     w = __hiloint2double((int)r.w, (int)r.z);
-                    cur = dist[t];
-                    mypos = H.hpos[t];
+                    const uint4 x = vr[t];  // {dist, parent slot, heap position}
+                    cur = __hiloint2double((int)x.y, (int)x.x);
+                    mypos = x.w;
                 }
                 const double alt = __dadd_rn(du, w);
                 const bool first = act && cur < 0.0;
                 const bool impr = act && !first && alt < cur;
-                if (first || impr) {
-                    dist[t] = alt;
-                    par[t] = j;
+                rp_lines(nl, RPL_RELAX_ST, first || impr, vr + 4 * (size_t)lane + t);
+                if (first || impr) {  // dist and parent in one 12-B store
+                    const unsigned long long b = d2bits(alt);
+                    *reinterpret_cast<uint3*>(vr + t) = make_uint3((uint32_t)b, (uint32_t)(b >> 32), j);
                 }
                 unsigned long long m = __ballot(first || impr);
                 const unsigned long long fm = __ballot(first);
@@ -261,7 +338,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                         pos = rl_u32(mypos, l);
                         n_mod++;
                     }
-                    uint32_t mv, mp;
+                    uint32_t mv = 0, mp = 0;
                     const int f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp);
                     // later lanes whose vertex was moved down by this shift-up
                     for (int i = 0; i < f; ++i) {
@@ -274,9 +351,10 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 
         if (dbg_dist) {  // test hook: the replay's dist / parent vertex in relabelled ids
             for (size_t i = (size_t)lane; i < V; i += 64) {
-                const double d = dist[i];
+                const uint4 x = vr[i];
+                const double d = __hiloint2double((int)x.y, (int)x.x);
                 dbg_dist[i] = d;
-                dbg_par[i] = (d >= 0.0 && i != src) ? (int32_t)g.rec[par[i]].y : -1;
+                dbg_par[i] = (d >= 0.0 && i != src) ? (int32_t)g.rec[x.z].y : -1;
             }
         }
 
@@ -302,10 +380,10 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                     h = 1;
                 }
             } else {
-                bool bad = !(dist[t] >= 0.0);
+                bool bad = !(*reinterpret_cast<const double*>(vr + t) >= 0.0);
                 uint32_t v = t;
                 while (!bad && v != src) {
-                    const uint32_t j = par[v];
+                    const uint32_t j = vr_par(vr, v);
                     if ((int64_t)j >= g.nadj) {
                         bad = true;
                         break;
@@ -331,8 +409,8 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                             j = pbuf[(size_t)x * 64 + lane];
                         } else {
                             uint32_t y = t;  // the chain was validated by the walk above
-                            for (int z = 0; z < x; ++z) y = g.rec[par[y]].y;
-                            j = par[y];
+                            for (int z = 0; z < x; ++z) y = g.rec[vr_par(vr, y)].y;
+                            j = vr_par(vr, y);
                         }
                         const double2 hp = g.hop[j];
                         lat = __dadd_rn(lat, hp.x);
@@ -356,6 +434,9 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
         atomicAdd(&stats[ST_RP_PUSH], n_push);
         atomicAdd(&stats[ST_RP_MOD], n_mod);
         atomicAdd(&stats[ST_RP_ROWS], n_rows);
+#if SHD_RP_LINES
+        for (int i = 0; i < 6; ++i) atomicAdd(&stats[ST_RP_L0 + i], nl[i]);
+#endif
     }
 }
 

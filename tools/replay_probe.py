@@ -1,5 +1,5 @@
 """Probe: heap-replay cost on C4-int (integer latencies) for a row range, per row and per heap op.
-usage: python tools/replay_probe.py ROWS [SLOTS]"""
+usage: python tools/replay_probe.py ROWS [SLOTS] [all]  (all: only the replay_all mode)"""
 import sys
 import time
 
@@ -19,7 +19,8 @@ if slots:
     top.set_option("replay_slots", slots)
 lr = torch.empty((rows, A, 2), dtype=torch.float64, device="cuda")
 hp = torch.empty((rows, A), dtype=torch.int16, device="cuda")
-for mode in ("batch+replay", "replay_all"):
+modes = ("replay_all",) if len(sys.argv) > 3 and sys.argv[3] == "all" else ("batch+replay", "replay_all")
+for mode in modes:
     top.set_option("replay_all", 1 if mode == "replay_all" else 0)
     t0 = time.time()
     top.build_rows_into(0, rows, lr, hp)
@@ -31,3 +32,8 @@ for mode in ("batch+replay", "replay_all"):
               mode, time.time() - t0, st["sssp_kernel_ms"], st["replay_ms"], st["replay_rows"],
               st["replay_slots"], st["ambiguous_pairs"], st["replay_pops"] / r,
               st["replay_pushes"] / r, st["replay_modifies"] / r), flush=True)
+    if any(st["replay_lines"]):
+        pops = max(1, st["replay_pops"])
+        print("  64-B lines per pop: " + " ".join("%s %.1f" % (n, x / pops) for n, x in zip(
+            ("sink_ld", "sink_st", "shift_ld", "shift_st", "relax_ld", "relax_st"),
+            st["replay_lines"])) + " | total %.1f" % (sum(st["replay_lines"]) / pops), flush=True)
