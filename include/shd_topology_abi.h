@@ -108,7 +108,10 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * through the replay), "replay_slots" (concurrent replay wavefronts, 0 = auto), "devices" (N:
  * the table is built by N GPUs of this process -- rows sharded, RCCL all-gather of the rows and
  * all-reduce(MIN) of the minimum; devices device..device+N-1), "rccl" (1: use that exchange even
- * with one device).  Returns 0 or -1 for an unknown key / bad value. */
+ * with one device), "batch" (sources per SSSP workgroup: 8; 2 / 4 / 16; 1 = single-source
+ * kernel), "batch_fill" (sources per batch, <= batch; 0 = auto: the fewest that finish the rows
+ * in the same rounds of the slots), "source_order" / "batch_order" (row grouping and batch
+ * dequeue order).  Returns 0 or -1 for an unknown key / bad value. */
 int shdtopo_set_option(Topology* top, const char* key, double value);
 
 /* attach by raw IP and a rand_r state (same algorithm and RNG use as topology_attach) */
@@ -197,6 +200,7 @@ typedef struct {
     int64_t replay_lines[6];  /* profiling builds (-DSHD_RP_LINES=1) only, else 0: 64-B lines the
                                  replay touched in HBM -- sink loads, sink stores, shift-up loads,
                                  shift-up stores, relaxation loads, relaxation stores */
+    int64_t batch_fill;       /* sources per batch of the last batched build (<= batch) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -179,6 +179,8 @@ struct _Topology {
     int sourceOrder = 2;      // option "source_order": batch kernel source grouping (0 = row
                               // order, 1 = by the hub their h0-tree path enters the core, then
                               // pi, 2 = preorder of the h0 shortest-path tree)
+    int batchFill = 0;        // option "batch_fill": sources per batch (0 = auto: the fewest per
+                              // batch that finish the rows in the same rounds of the slots)
     int batchOrder = 2;       // option "batch_order": 0 grouped order, 1 shuffled, 2 / 3 by mean
                               // pi descending / ascending
     DevBuf<uint32_t> d_rowmap;
@@ -1087,10 +1089,22 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     std::stable_sort(perm.begin(), perm.end(),
                                      [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
                 }
-                // order of the batches (groups of K consecutive positions) in the dequeue: the
+                // sources per batch: a shard that leaves slots idle at K (8-GPU builds: 1250
+                // rows = 157 batches for 256 slots) spreads over every slot with fewer sources
+                // per batch (C4, 1250 rows: 89.7 -> 83.2 ms).  With more than one round it does
+                // not pay (2500 rows at 5 per batch: 146 -> 158 ms).
+                int kf = K;
+                if (top->batchFill > 0) {
+                    kf = std::min(K, top->batchFill);
+                } else {
+                    const int64_t S = std::max(1, ws.slots);
+                    if (rows <= (int64_t)K * S) kf = (int)std::min<int64_t>(K, (rows + S - 1) / S);
+                }
+                top->stats.batch_fill = kf;
+                // order of the batches (groups of kf consecutive positions) in the dequeue: the
                 // kernel ends with the slowest slot, so the last batches decide its tail
-                if (top->batchOrder != 0 && rows > K) {
-                    const int64_t nb = (rows + K - 1) / K;
+                if (top->batchOrder != 0 && rows > kf) {
+                    const int64_t nb = (rows + kf - 1) / kf;
                     std::vector<uint32_t> bo((size_t)nb);
                     std::iota(bo.begin(), bo.end(), 0u);
                     if (top->batchOrder == 1) {
@@ -1100,7 +1114,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                         std::vector<double> mp((size_t)nb, 0.0);
                         for (int64_t b = 0; b < nb; b++) {
                             int64_t c = 0;
-                            for (int64_t i = b * K; i < std::min(rows, (b + 1) * K); i++, c++) {
+                            for (int64_t i = b * kf; i < std::min(rows, (b + 1) * kf); i++, c++) {
                                 const double p = top->pot[(size_t)src[(size_t)perm[(size_t)i]]];
                                 mp[(size_t)b] += std::isfinite(p) ? p : 0.0;
                             }
@@ -1113,7 +1127,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     }
                     // the ragged batch (if any) stays last
                     const int64_t last = nb - 1;
-                    if (rows % K) {
+                    if (rows % kf) {
                         auto it = std::find(bo.begin(), bo.end(), (uint32_t)last);
                         bo.erase(it);
                         bo.push_back((uint32_t)last);
@@ -1121,7 +1135,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     std::vector<uint32_t> p2;
                     p2.reserve((size_t)rows);
                     for (uint32_t b : bo)
-                        for (int64_t i = (int64_t)b * K; i < std::min(rows, ((int64_t)b + 1) * K); i++)
+                        for (int64_t i = (int64_t)b * kf; i < std::min(rows, ((int64_t)b + 1) * kf); i++)
                             p2.push_back(perm[(size_t)i]);
                     perm.swap(p2);
                 }
@@ -1148,7 +1162,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     top->g.V);
                 top->stats.lds_hubs = bp.H;
                 HIPCHK(launch_sssp_batch(K, dev_csr(top), ws, top->d_sources.p,
-                                         top->d_srcsh.p, (int)rows, top->d_targets.p, (int)A,
+                                         top->d_srcsh.p, (int)rows, kf, top->d_targets.p, (int)A,
                                          delta, bp, (uint32_t)top->farCap, out_lr, out_hops,
                                          out_rowmin, top->d_stats.p, st));
                 HIPCHK(hipEventRecord(top->ev1, st));
@@ -1365,6 +1379,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->replaySlotsOpt = top->replaySlotsOpt;
     p->sourceOrder = top->sourceOrder;
     p->batchOrder = top->batchOrder;
+    p->batchFill = top->batchFill;
     p->attached = top->attached;
     p->colOf = top->colOf;
     p->A = top->A;
@@ -1926,6 +1941,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "replay_slots") top->replaySlotsOpt = (int)value;
     else if (k == "source_order") top->sourceOrder = (int)value;
     else if (k == "batch_order") top->batchOrder = (int)value;
+    else if (k == "batch_fill") top->batchFill = (int)value;
     else if (k == "devices") {
         const int n = (int)value;
         if (n < 1 || n > 64) return -1;

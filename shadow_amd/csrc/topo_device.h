@@ -179,9 +179,10 @@ hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d
 
 // Batched multi-source SSSP (topo_sssp_batch.hip): K in {2, 4, 8, 16} sources per workgroup in
 // lock-step over buckets of d + srcsh[row] (srcsh >= 2 delta).  plan from sssp_batch_lds_plan.
+// kf (1..K): sources per batch (batch b = positions [b kf, b kf + kf)).
 SsspLdsPlan sssp_batch_lds_plan(int K, int64_t hub_limit, uint32_t par_hubs, int64_t V);
 hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
-                             const double* d_srcsh, int nsrc, const uint32_t* d_targets, int A,
+                             const double* d_srcsh, int nsrc, int kf, const uint32_t* d_targets, int A,
                              double delta, const SsspLdsPlan& plan, uint32_t far_cap,
                              double2* out_lr, uint16_t* out_hops, double* out_rowmin,
                              unsigned long long* d_stats, hipStream_t stream);

@@ -66,6 +66,18 @@ constexpr uint32_t kRpT = (1u << SHD_RP_LDS_LEVELS) - 1u;  // heap positions hel
 constexpr int kRpLA = SHD_RP_LA;
 constexpr int kRpLaNodes = (2 << kRpLA) - 2;               // subtree nodes below the hole
 static_assert(kRpLA >= 1 && kRpLaNodes <= 64, "one node per lane");
+#ifndef SHD_RP_LA_HBM
+#define SHD_RP_LA_HBM SHD_RP_LA  // lookahead of a round whose subtree reaches the HBM levels
+#endif
+constexpr int kRpLaH = SHD_RP_LA_HBM;
+static_assert(kRpLaH >= 1 && kRpLaH <= kRpLA, "HBM lookahead");
+
+// levels loaded by a sink round from `head`: kRpLA while the subtree is in LDS (cheap), kRpLaH
+// once it reaches HBM (a level d below the hole costs 2^d x 16 B of lines; one more round trip
+// against fewer lines)
+__device__ __forceinline__ int rp_la(uint32_t head) {
+    return (((head + 2u) << kRpLA) - 2u) < kRpT ? kRpLA : kRpLaH;
+}
 
 __device__ __forceinline__ uint32_t rl_u32(uint32_t x, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
@@ -142,9 +154,10 @@ __device__ __forceinline__ uint32_t rp_sub_pos(uint32_t head, int lane) {
 // igraph_2wheap_sink of element (xk, xv) from position `head` (a hole) in a heap of `size`.
 // The path of larger children does not depend on x, so the subtree kRpLA levels below the hole
 // is loaded in one round trip; x stops where it is not smaller than the chosen child.  (k, v):
-// the first round's subtree, loaded by the caller together with its other loads.
+// the first round's subtree (rp_la(head) levels), loaded by the caller with its other loads.
 __device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t size, double xk,
                                         uint32_t xv, int lane, double k, uint32_t v) {
+    int la = rp_la(head);  // the caller loaded that many levels
     for (;;) {
         const uint32_t p = rp_sub_pos(head, lane);
         uint32_t cur = head, q = 0;
@@ -152,6 +165,7 @@ __device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t
         unsigned long long path = 0;
 #pragma unroll
         for (int s = 0; s < kRpLA; ++s) {
+            if (s >= la) break;
             const uint32_t L = 2u * cur + 1u;
             if (L >= size) {
                 stop = true;
@@ -186,7 +200,8 @@ __device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t
         const uint32_t pn = rp_sub_pos(head, lane);  // below the last moved node: not written above
         k = -INFINITY;
         v = 0;
-        if (lane < kRpLaNodes && pn < size) H.node(pn, k, v, RPL_SINK_LD);
+        la = rp_la(head);
+        if (lane < (2 << la) - 2 && pn < size) H.node(pn, k, v, RPL_SINK_LD);
     }
     if (lane == 0) H.put(head, xk, xv, RPL_SINK_ST);
 }

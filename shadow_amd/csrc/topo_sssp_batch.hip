@@ -702,8 +702,9 @@ __device__ __forceinline__ void expand_pairs(const uint32_t* Q, uint32_t nq, con
 template <int K>
 __global__ void __launch_bounds__(kSsspBlock, kBatchWgPerCu)
 sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
-                  const double* __restrict__ srcsh, int nsrc, const uint32_t* __restrict__ targets,
-                  int A, double delta, uint32_t H, uint32_t P, uint32_t far_cap,
+                  const double* __restrict__ srcsh, int nsrc, int kf,
+                  const uint32_t* __restrict__ targets, int A, double delta, uint32_t H,
+                  uint32_t P, uint32_t far_cap,
                   double2* __restrict__ out_lr, uint16_t* __restrict__ out_hops,
                   double* __restrict__ out_rowmin, unsigned long long* __restrict__ stats) {
     using MO = MaskOps<K>;
@@ -768,9 +769,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         __syncthreads();
         const uint32_t bidx = L.idx;
         __syncthreads();
-        if ((int64_t)bidx * K >= nsrc) break;
-        const int r0 = (int)bidx * K;
-        const int nk = min(K, nsrc - r0);
+        // batch bidx: sources [bidx kf, bidx kf + kf) in lanes 0..nk-1 (kf <= K: the host fills
+        // batches below K when that finishes the sources in fewer rounds of the slots)
+        if ((int64_t)bidx * kf >= nsrc) break;
+        const int r0 = (int)bidx * kf;
+        const int nk = min(kf, nsrc - r0);
         tk = wall_clock64();
 
         // ---------------- init: hubs in LDS, the tail's K-wide rows in HBM --------------------
@@ -1431,11 +1434,12 @@ SsspLdsPlan sssp_batch_lds_plan(int K, int64_t hub_limit, uint32_t par_hubs, int
 
 template <int K>
 static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
-                                 const double* d_srcsh, int nsrc, const uint32_t* d_targets, int A,
-                                 double delta, const SsspLdsPlan& plan, uint32_t far_cap,
+                                 const double* d_srcsh, int nsrc, int kf, const uint32_t* d_targets,
+                                 int A, double delta, const SsspLdsPlan& plan, uint32_t far_cap,
                                  double2* out_lr, uint16_t* out_hops, double* out_rowmin,
                                  unsigned long long* d_stats, hipStream_t stream) {
-    const int nb = (nsrc + K - 1) / K;
+    if (kf < 1 || kf > K) return hipErrorInvalidValue;
+    const int nb = (nsrc + kf - 1) / kf;
     const int grid = ws.slots < nb ? ws.slots : nb;
     if (grid < 1) return hipSuccess;
     if ((int64_t)plan.H > g.V || plan.P > plan.H || plan.bytes > kBMaxLds ||
@@ -1448,21 +1452,21 @@ static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(sssp_batch_kernel<K>, dim3(grid), dim3(kSsspBlock), plan.bytes, stream, g,
-                       ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan.H, plan.P, far_cap,
+                       ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan.H, plan.P, far_cap,
                        out_lr, out_hops, out_rowmin, d_stats);
     return hipGetLastError();
 }
 
 hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
-                             const double* d_srcsh, int nsrc, const uint32_t* d_targets, int A,
-                             double delta, const SsspLdsPlan& plan, uint32_t far_cap,
+                             const double* d_srcsh, int nsrc, int kf, const uint32_t* d_targets,
+                             int A, double delta, const SsspLdsPlan& plan, uint32_t far_cap,
                              double2* out_lr, uint16_t* out_hops, double* out_rowmin,
                              unsigned long long* d_stats, hipStream_t stream) {
     switch (K) {
-        case 2: return launch_batch_k<2>(g, ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
-        case 4: return launch_batch_k<4>(g, ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
-        case 8: return launch_batch_k<8>(g, ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
-        case 16: return launch_batch_k<16>(g, ws, d_sources, d_srcsh, nsrc, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 2: return launch_batch_k<2>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 4: return launch_batch_k<4>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 8: return launch_batch_k<8>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 16: return launch_batch_k<16>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
     }
     return hipErrorInvalidValue;
 }

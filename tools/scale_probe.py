@@ -18,8 +18,9 @@ A = len(top.attached_vertices())
 print("gen %.1fs A=%d" % (time.time() - t0, A), flush=True)
 lr = torch.empty((A, A, 2), dtype=torch.float64, device="cuda")
 hp = torch.empty((A, A), dtype=torch.int16, device="cuda")
-for K in (8, 4):
+for K, fill in ((8, 8), (8, 0)):
     top.set_option("batch", K)
+    top.set_option("batch_fill", fill)
     top.build_rows_into(0, 64, lr[:64], hp[:64])  # workspace + warm
     for n in (1, 2, 4, 8):
         rows = -(-A // n)
@@ -28,6 +29,6 @@ for K in (8, 4):
         top.build_rows_into(0, rows, lr[:rows], hp[:rows])
         torch.cuda.synchronize()
         st = top.stats()
-        print("K=%d N=%d rows=%d wall %.1f ms kernel %.1f ms (x N = %.1f ms of one-GPU work)" % (
-            K, n, rows, (time.time() - t0) * 1e3, st["sssp_kernel_ms"], st["sssp_kernel_ms"] * n),
+        print("K=%d fill=%d N=%d rows=%d wall %.1f ms kernel %.1f ms (x N = %.1f ms of one-GPU work)" % (
+            K, st["batch_fill"], n, rows, (time.time() - t0) * 1e3, st["sssp_kernel_ms"], st["sssp_kernel_ms"] * n),
             flush=True)
