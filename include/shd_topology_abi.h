@@ -201,6 +201,11 @@ typedef struct {
                                  replay touched in HBM -- sink loads, sink stores, shift-up loads,
                                  shift-up stores, relaxation loads, relaxation stores */
     int64_t batch_fill;       /* sources per batch of the last batched build (<= batch) */
+    double replay_phase_ms[4]; /* profiling builds (-DSHD_RP_TIME=1) only, else 0: replay wall
+                                  time summed over wavefronts -- sink, row + record loads, heap
+                                  operations of the relaxation, init + epilogue */
+    int64_t replay_sink_rounds; /* same builds: sink round trips and heap size, summed over pops */
+    int64_t replay_heap_sum;
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -38,7 +38,8 @@ class ShdStats(ctypes.Structure):
                 ("batch", i64), ("lds_hubs", i64), ("replay_rows", i64), ("replay_ms", dbl),
                 ("replay_pops", i64), ("replay_pushes", i64), ("replay_modifies", i64),
                 ("replay_slots", i64), ("route_bad_packets", i64), ("devices", i64),
-                ("exchange_ms", dbl), ("parent_phase_ms", dbl * 4), ("replay_lines", i64 * 6), ("batch_fill", i64)]
+                ("exchange_ms", dbl), ("parent_phase_ms", dbl * 4), ("replay_lines", i64 * 6), ("batch_fill", i64), ("replay_phase_ms", dbl * 4),
+                ("replay_sink_rounds", i64), ("replay_heap_sum", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):

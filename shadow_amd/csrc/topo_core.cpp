@@ -1265,6 +1265,14 @@ int collect_row_stats(Topology* top) {
     top->stats.replay_pushes = (int64_t)h[ST_RP_PUSH];
     top->stats.replay_modifies = (int64_t)h[ST_RP_MOD];
     for (int i = 0; i < 6; i++) top->stats.replay_lines[i] = (int64_t)h[ST_RP_L0 + i];
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->device) != hipSuccess || khz <= 0)
+            khz = 100000;
+        for (int i = 0; i < 4; i++) top->stats.replay_phase_ms[i] = (double)h[ST_RP_T0 + i] / (double)khz;
+        top->stats.replay_sink_rounds = (int64_t)h[ST_RP_T0 + 4];
+        top->stats.replay_heap_sum = (int64_t)h[ST_RP_T0 + 5];
+    }
     top->stats.replay_slots = top->stats.replay_rows ? std::min(top->rslots, top->rslotsUse) : 0;
     {
         int khz = 0;

@@ -71,7 +71,9 @@ enum StatIdx {
                         //   merged row scans, recount + finalize, next level (4 slots)
     ST_RP_L0 = 34,      // replay 64-B lines (SHD_RP_LINES builds): sink ld/st, shift-up ld/st,
                         // relaxation ld/st
-    ST_COUNT = 40
+    ST_RP_T0 = 40,      // replay wall ticks (SHD_RP_TIME builds): sink, loads, heap ops, rest
+                        // + sink rounds, heap size summed over pops
+    ST_COUNT = 46
 };
 
 struct DevCSR {

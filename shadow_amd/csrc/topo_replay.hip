@@ -59,6 +59,18 @@ using namespace dev;
 #ifndef SHD_RP_LINES
 #define SHD_RP_LINES 0  // profiling build: count the 64-B lines each part of the replay touches
 #endif
+#ifndef SHD_RP_TIME
+#define SHD_RP_TIME 0  // profiling build: wall time per part of a pop (sink, row + record loads,
+                       // heap operations of the relaxation, init + epilogue)
+#endif
+#if SHD_RP_TIME
+#define RP_TICK(i) do { const unsigned long long t_ = wall_clock64(); tph[i] += t_ - tlast; tlast = t_; } while (0)
+#else
+#define RP_TICK(i) do { } while (0)
+#endif
+#ifndef SHD_RP_SINK2
+#define SHD_RP_SINK2 1  // sink: path of larger children first (LDS levels while x is loaded)
+#endif
 #ifndef SHD_RP_LA
 #define SHD_RP_LA 5  // sink lookahead: heap levels loaded per round trip (<= 5: 62 nodes)
 #endif
@@ -159,6 +171,9 @@ __device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t
                                         uint32_t xv, int lane, double k, uint32_t v) {
     int la = rp_la(head);  // the caller loaded that many levels
     for (;;) {
+#if SHD_RP_TIME
+        H.nl[6]++;  // sink rounds
+#endif
         const uint32_t p = rp_sub_pos(head, lane);
         uint32_t cur = head, q = 0;
         bool stop = false;
@@ -206,13 +221,124 @@ __device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t
     if (lane == 0) H.put(head, xk, xv, RPL_SINK_ST);
 }
 
+// igraph_2wheap_delete_max's sink of x = the last element from the root (a hole) in a heap of
+// `size` (after the removal).  The path of larger children does not depend on x, so it is found
+// first: the LDS levels by uniform LDS reads while x's load is in flight, then the HBM levels
+// kRpLA per round trip (the first round is issued before x is waited for).  x stops at the first
+// path node it is not smaller than; the path nodes above the stop move up one level, in parallel
+// (lane i holds path node i).  (kx, vx): x in lane 63, loaded by the caller.
+__device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int lane, double kx,
+                                            uint32_t vx) {
+    uint32_t pp = 0, pv = 0;  // this lane's path node: position, vertex, key
+    double pk = INFINITY;
+    int np = 0;
+    uint32_t cur = 0;
+    bool bottom = false;
+    for (;;) {  // LDS levels (the children of an LDS level < 8 are in LDS: kRpT = 2^n - 1)
+        const uint32_t L = 2u * cur + 1u;
+        if (L >= size) {
+            bottom = true;
+            break;
+        }
+        if (L >= kRpT) break;
+        const double kL = uni_f64(H.sk[L]);
+        uint32_t c = L;
+        double kc = kL;
+        if (L + 1u < size) {
+            const double kR = uni_f64(H.sk[L + 1u]);
+            if (!(kL >= kR)) {
+                c = L + 1u;
+                kc = kR;
+            }
+        }
+        if (lane == np) {
+            pp = c;
+            pk = kc;
+            pv = H.sv[c];
+        }
+        cur = c;
+        np++;
+    }
+    double xk = 0.0;
+    uint32_t xv = 0;
+    bool havex = false;
+    int stop = -1;  // first path index x is not smaller than
+    while (!bottom) {
+#if SHD_RP_TIME
+        H.nl[6]++;  // HBM sink rounds
+#endif
+        const uint32_t p = rp_sub_pos(cur, lane);
+        double k = -INFINITY;
+        uint32_t v = 0;
+        if (lane < kRpLaNodes && p < size) H.node(p, k, v, RPL_SINK_LD);
+        if (!havex) {
+            xk = rl_f64(kx, 63);
+            xv = rl_u32(vx, 63);
+            havex = true;
+            const unsigned long long sm = __ballot(lane < np && !(xk < pk));
+            if (sm) {
+                stop = __ffsll((long long)sm) - 1;
+                break;
+            }
+        }
+        uint32_t q = 0;
+#pragma unroll
+        for (int s = 0; s < kRpLA; ++s) {
+            const uint32_t L = 2u * cur + 1u;
+            if (L >= size) {
+                bottom = true;
+                break;
+            }
+            const int li = (int)(2u * q);  // lane of the left child (BFS 2q+1)
+            const double kL = rl_f64(k, li);
+            int ci = li;
+            uint32_t c = L;
+            double kc = kL;
+            if (L + 1u < size) {
+                const double kR = rl_f64(k, li + 1);
+                if (!(kL >= kR)) {
+                    ci = li + 1;
+                    c = L + 1u;
+                    kc = kR;
+                }
+            }
+            if (!(xk < kc)) {
+                stop = np;
+                break;
+            }
+            const uint32_t vc = rl_u32(v, ci);
+            if (lane == np) {
+                pp = c;
+                pk = kc;
+                pv = vc;
+            }
+            cur = c;
+            np++;
+            q = (uint32_t)ci + 1u;
+        }
+        if (stop >= 0) break;
+    }
+    if (!havex) {
+        xk = rl_f64(kx, 63);
+        xv = rl_u32(vx, 63);
+        const unsigned long long sm = __ballot(lane < np && !(xk < pk));
+        stop = sm ? __ffsll((long long)sm) - 1 : np;
+    } else if (stop < 0) {
+        stop = np;
+    }
+    const uint32_t up = __shfl_up(pp, 1);  // the parent's position (path node lane - 1)
+    if (lane < stop) H.put(lane == 0 ? 0u : up, pk, pv, RPL_SINK_ST);
+    if (lane == 0) H.put(stop == 0 ? 0u : rl_u32(pp, stop - 1), xk, xv, RPL_SINK_ST);
+}
+
 // igraph_2wheap_shift_up of element (xk, xv) from position `pos` (a hole).  Returns the number f
 // of ancestors moved down one level; lane i < f holds the moved vertex (mv) and its new position.
 // Most shift-ups stop below the parent: it is read first (one node), the whole chain only when x
-// rises past it.
+// rises past it.  check = false: the caller knows x rises past the parent.
 __device__ __forceinline__ int rp_shift_up(const RpHeap& H, uint32_t pos, double xk, uint32_t xv,
-                                           int lane, uint32_t& mv, uint32_t& mp) {
-    if (SHD_RP_PROG && pos > 0) {
+                                           int lane, uint32_t& mv, uint32_t& mp,
+                                           bool check = true) {
+    if (SHD_RP_PROG && check && pos > 0) {
         double k0;
         uint32_t v0;
         H.node((pos - 1u) >> 1, k0, v0, RPL_SHIFT_LD);
@@ -254,7 +380,10 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
     const size_t V = (size_t)g.V;
     const size_t slot = blockIdx.x;
     uint4* vr = ws.vrec + slot * V;
-    unsigned long long nl[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long nl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#if SHD_RP_TIME
+    unsigned long long tph[4] = {0, 0, 0, 0}, tlast = wall_clock64();
+#endif
     RpHeap H{ws.node + slot * V, vr, sk, sv, nl};
     uint32_t* pbuf = ws.pathbuf + slot * (size_t)kMaxHops * 64;
     unsigned long long n_pop = 0, n_push = 0, n_mod = 0, n_rows = 0;
@@ -282,6 +411,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
         int64_t to_reach = full ? (int64_t)V + 1 : (int64_t)g.ntargets;
         while (size > 0 && to_reach > 0) {
             // igraph_2wheap_delete_max
+            RP_TICK(3);
             const uint32_t u = uni_u32(sv[0]);
             const double du = -uni_f64(sk[0]);  // mindist = -data[0]
             const uint32_t lastp = size - 1u;
@@ -289,20 +419,30 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
             // 63) and, independent of the heap, u's target bit, row bounds and first 64 records
             double k1 = -INFINITY;
             uint32_t v1 = 0;
+#if SHD_RP_SINK2
+            if (lane == 63) H.node(lastp, k1, v1, RPL_SINK_LD);
+#else
             {
                 const uint32_t p1 = rp_sub_pos(0, lane);
                 if (lane < kRpLaNodes && p1 < lastp) H.node(p1, k1, v1, RPL_SINK_LD);
                 else if (lane == 63) H.node(lastp, k1, v1, RPL_SINK_LD);
             }
+#endif
             const uint32_t tb = g.tbits[u >> 5];
             const uint32_t rb = uni_u32(g.rowptr[u]), re = uni_u32(g.rowptr[u + 1]);
             uint4 r0 = make_uint4(0u, 0u, 0u, 0u);
             if (rb + (uint32_t)lane < re) r0 = g.rec[rb + (uint32_t)lane];
-            const double xk = rl_f64(k1, 63);
-            const uint32_t xv = rl_u32(v1, 63);
             size = lastp;
-            if (size > 0) rp_sink(H, 0, size, xk, xv, lane, k1, v1);
+#if SHD_RP_TIME
+            nl[7] += size;  // heap size at the pop
+#endif
+#if SHD_RP_SINK2
+            if (size > 0) rp_pop_sink(H, size, lane, k1, v1);
+#else
+            if (size > 0) rp_sink(H, 0, size, rl_f64(k1, 63), rl_u32(v1, 63), lane, k1, v1);
+#endif
             n_pop++;
+            RP_TICK(0);
             if ((tb >> (u & 31u)) & 1u) {
                 to_reach--;
                 // every target is popped: its parent chain is final (relaxing u's edges, as
@@ -336,6 +476,20 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                 }
                 unsigned long long m = __ballot(first || impr);
                 const unsigned long long fm = __ballot(first);
+                RP_TICK(1);
+                // The step's heap operations run in lane order, but the parent of each one's
+                // position is read for all of them in one round trip: a push lands at size + the
+                // pushes before it, a modify at its vertex's position.  A read stays valid until
+                // an earlier operation moves nodes (dirty) or places its element at that parent.
+                uint32_t ppos = 0;
+                double pk = INFINITY;
+                if (first) ppos = size + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+                else if (impr) ppos = mypos;
+                if ((first || impr) && ppos > 0) {
+                    uint32_t pv;
+                    H.node((ppos - 1u) >> 1, pk, pv, RPL_SHIFT_LD);
+                }
+                bool stale = false, dirty = false;
                 while (m) {
                     const int l = __ffsll((long long)m) - 1;
                     m &= m - 1ull;
@@ -345,6 +499,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                     if ((fm >> l) & 1ull) {  // igraph_2wheap_push_with_index
                         if (size >= (uint32_t)V) {  // cannot happen (each vertex queued once)
                             if (lane == 0) atomicAdd(&stats[ST_OVERFLOW], 1ull);
+                            dirty = true;
                             continue;
                         }
                         pos = size++;
@@ -354,7 +509,20 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                         n_mod++;
                     }
                     uint32_t mv = 0, mp = 0;
-                    const int f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp);
+                    int f;
+                    if (SHD_RP_PROG && !dirty && pos > 0 && !__shfl(stale, l)) {
+                        if (xkey < rl_f64(pk, l)) {  // stays: data[x] < data[parent]
+                            if (lane == 0) H.put(pos, xkey, tv, RPL_SHIFT_ST);
+                            f = 0;
+                        } else {
+                            f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp, false);
+                        }
+                    } else {
+                        f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp);
+                    }
+                    if (f > 0) dirty = true;
+                    else if (ppos > 0 && ((ppos - 1u) >> 1) == pos) stale = true;
+                    RP_TICK(2);
                     // later lanes whose vertex was moved down by this shift-up
                     for (int i = 0; i < f; ++i) {
                         const uint32_t vi = rl_u32(mv, i), pi = rl_u32(mp, i);
@@ -451,6 +619,12 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
         atomicAdd(&stats[ST_RP_ROWS], n_rows);
 #if SHD_RP_LINES
         for (int i = 0; i < 6; ++i) atomicAdd(&stats[ST_RP_L0 + i], nl[i]);
+#endif
+#if SHD_RP_TIME
+        RP_TICK(3);
+        for (int i = 0; i < 4; ++i) atomicAdd(&stats[ST_RP_T0 + i], tph[i]);
+        atomicAdd(&stats[ST_RP_T0 + 4], nl[6]);
+        atomicAdd(&stats[ST_RP_T0 + 5], nl[7]);
 #endif
     }
 }

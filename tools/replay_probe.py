@@ -37,3 +37,9 @@ for mode in modes:
         print("  64-B lines per pop: " + " ".join("%s %.1f" % (n, x / pops) for n, x in zip(
             ("sink_ld", "sink_st", "shift_ld", "shift_st", "relax_ld", "relax_st"),
             st["replay_lines"])) + " | total %.1f" % (sum(st["replay_lines"]) / pops), flush=True)
+    if any(st["replay_phase_ms"]):
+        pops = max(1, st["replay_pops"])
+        print("  ns per pop (per wavefront): " + " ".join("%s %.0f" % (n, x * 1e6 / pops) for n, x in zip(
+            ("sink", "loads", "heap_ops", "rest"), st["replay_phase_ms"])) +
+            " | sink rounds %.2f, mean heap size %.0f" % (st["replay_sink_rounds"] / pops,
+                                                         st["replay_heap_sum"] / pops), flush=True)
