@@ -204,8 +204,10 @@ typedef struct {
     double replay_phase_ms[4]; /* profiling builds (-DSHD_RP_TIME=1) only, else 0: replay wall
                                   time summed over wavefronts -- sink, row + record loads, heap
                                   operations of the relaxation, init + epilogue */
-    int64_t replay_sink_rounds; /* same builds: sink round trips and heap size, summed over pops */
+    int64_t replay_sink_rounds; /* same builds: sink round trips and heap size, summed over pops, */
     int64_t replay_heap_sum;
+    double replay_sink_ms[3];   /*   the sink's LDS walk, HBM rounds and moves, */
+    int64_t replay_pf_hits;     /*   pops whose row bounds were prefetched */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -886,7 +886,10 @@ int ensure_replay_ws(Topology* top, int nrows) {
     const size_t per_slot = 32 * V + (size_t)kMaxHops * 64 * 4 + 64;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, top->device));
-    int want = top->replaySlotsOpt > 0 ? top->replaySlotsOpt : prop.multiProcessorCount * 20;
+    // wavefronts per CU: 20, or as many as the CU's LDS holds (each its heap's top levels)
+    const int lds = (replay_lds_bytes() + 255) & ~255;
+    const int per_cu = std::max(1, std::min(20, (int)(prop.sharedMemPerMultiprocessor > 0 ? prop.sharedMemPerMultiprocessor : 163840) / lds));
+    int want = top->replaySlotsOpt > 0 ? top->replaySlotsOpt : prop.multiProcessorCount * per_cu;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     const size_t held = (size_t)top->rslots * per_slot;
@@ -1272,6 +1275,8 @@ int collect_row_stats(Topology* top) {
         for (int i = 0; i < 4; i++) top->stats.replay_phase_ms[i] = (double)h[ST_RP_T0 + i] / (double)khz;
         top->stats.replay_sink_rounds = (int64_t)h[ST_RP_T0 + 4];
         top->stats.replay_heap_sum = (int64_t)h[ST_RP_T0 + 5];
+        for (int i = 0; i < 3; i++) top->stats.replay_sink_ms[i] = (double)h[ST_RP_T0 + 6 + i] / (double)khz;
+        top->stats.replay_pf_hits = (int64_t)h[ST_RP_T0 + 9];
     }
     top->stats.replay_slots = top->stats.replay_rows ? std::min(top->rslots, top->rslotsUse) : 0;
     {

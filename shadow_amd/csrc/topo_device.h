@@ -72,8 +72,9 @@ enum StatIdx {
     ST_RP_L0 = 34,      // replay 64-B lines (SHD_RP_LINES builds): sink ld/st, shift-up ld/st,
                         // relaxation ld/st
     ST_RP_T0 = 40,      // replay wall ticks (SHD_RP_TIME builds): sink, loads, heap ops, rest
-                        // + sink rounds, heap size summed over pops
-    ST_COUNT = 46
+                        // + sink rounds, heap size summed over pops, sink sub-phases
+                        // (LDS walk, HBM rounds, moves), root-prefetch hits
+    ST_COUNT = 50
 };
 
 struct DevCSR {
@@ -198,6 +199,7 @@ hipError_t launch_heap_replay(const ReplayCSR& g, const ReplayWs& ws, const uint
                               unsigned long long* d_stats, double* dbg_dist, int32_t* dbg_par,
                               hipStream_t stream);
 int replay_lds_levels();
+int replay_lds_bytes();  // LDS of one replay wavefront (its heap's top levels)
 
 hipError_t launch_pair_table_complete(int A, int64_t row0, int64_t rows, const double* elatAA,
                                       const double* elossAA, const double* vlossA, double2* out_lr,

@@ -68,8 +68,16 @@ using namespace dev;
 #else
 #define RP_TICK(i) do { } while (0)
 #endif
+#if SHD_RP_TIME  // sink sub-phases: LDS walk, HBM rounds, moves (nl[8..10], clock in nl[12])
+#define RP_STICK(i) do { const unsigned long long t_ = wall_clock64(); H.nl[8 + (i)] += t_ - H.nl[12]; H.nl[12] = t_; } while (0)
+#else
+#define RP_STICK(i) do { } while (0)
+#endif
 #ifndef SHD_RP_SINK2
 #define SHD_RP_SINK2 1  // sink: path of larger children first (LDS levels while x is loaded)
+#endif
+#ifndef SHD_RP_PREF
+#define SHD_RP_PREF 1  // the next root's row bounds and target bit loaded right after the sink
 #endif
 #ifndef SHD_RP_LA
 #define SHD_RP_LA 5  // sink lookahead: heap levels loaded per round trip (<= 5: 62 nodes)
@@ -78,6 +86,12 @@ constexpr uint32_t kRpT = (1u << SHD_RP_LDS_LEVELS) - 1u;  // heap positions hel
 constexpr int kRpLA = SHD_RP_LA;
 constexpr int kRpLaNodes = (2 << kRpLA) - 2;               // subtree nodes below the hole
 static_assert(kRpLA >= 1 && kRpLaNodes <= 64, "one node per lane");
+#ifndef SHD_RP_HL
+#define SHD_RP_HL 5  // levels per HBM round of the path-first sink (6: two nodes per lane)
+#endif
+constexpr int kHL = SHD_RP_HL;
+constexpr int kHNodes = (2 << kHL) - 2;
+static_assert(kHL >= 1 && kHNodes <= 128, "at most two nodes per lane");
 #ifndef SHD_RP_LA_HBM
 #define SHD_RP_LA_HBM SHD_RP_LA  // lookahead of a round whose subtree reaches the HBM levels
 #endif
@@ -121,6 +135,13 @@ __device__ __forceinline__ void rp_lines(unsigned long long* nl, int cat, bool a
 #endif
 }
 
+// The heap's top levels (positions < kRpT) of this workgroup's (= wavefront's) source, in LDS.
+// File-scope __shared__: every access is a ds_read/ds_write (a generic pointer let the compiler
+// merge the LDS and HBM branches of a node access into flat loads, which wait on both counters
+// and serialised the sink behind outstanding HBM loads: -4 to -7 %).
+__shared__ double rp_sk[kRpT];
+__shared__ uint32_t rp_sv[kRpT];
+
 // The heap of one source: keys (igraph's data = -dist) and vertices, positions < kRpT in LDS,
 // the rest as 16-B nodes {f64 key, u32 vertex, pad} in this slot's HBM (one line per node
 // access); the position of a queued vertex lives in its 16-B vertex record
@@ -128,14 +149,12 @@ __device__ __forceinline__ void rp_lines(unsigned long long* nl, int cat, bool a
 struct RpHeap {
     uint4* gn;
     uint4* vr;
-    double* sk;
-    uint32_t* sv;
     unsigned long long* nl;
     __device__ __forceinline__ void node(uint32_t p, double& k, uint32_t& v, int cat) const {
         rp_lines(nl, cat, p >= kRpT, gn + p);
         if (p < kRpT) {
-            k = sk[p];
-            v = sv[p];
+            k = rp_sk[p];
+            v = rp_sv[p];
         } else {
             const uint4 q = gn[p];
             k = __hiloint2double((int)q.y, (int)q.x);
@@ -146,8 +165,8 @@ struct RpHeap {
         rp_lines(nl, cat, p >= kRpT, gn + p);
         rp_lines(nl, cat, true, vr + 4 * (size_t)__lane_id() + v);  // random: one line each
         if (p < kRpT) {
-            sk[p] = k;
-            sv[p] = v;
+            rp_sk[p] = k;
+            rp_sv[p] = v;
         } else {
             const unsigned long long b = d2bits(k);
             gn[p] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), v, 0u);
@@ -229,67 +248,36 @@ __device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t
 // (lane i holds path node i).  (kx, vx): x in lane 63, loaded by the caller.
 __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int lane, double kx,
                                             uint32_t vx) {
+#if SHD_RP_TIME
+    H.nl[12] = wall_clock64();
+#endif
     uint32_t pp = 0, pv = 0;  // this lane's path node: position, vertex, key
     double pk = INFINITY;
     int np = 0;
     uint32_t cur = 0;
     bool bottom = false;
-    for (;;) {  // LDS levels (the children of an LDS level < 8 are in LDS: kRpT = 2^n - 1)
-        const uint32_t L = 2u * cur + 1u;
-        if (L >= size) {
-            bottom = true;
-            break;
-        }
-        if (L >= kRpT) break;
-        const double kL = uni_f64(H.sk[L]);
-        uint32_t c = L;
-        double kc = kL;
-        if (L + 1u < size) {
-            const double kR = uni_f64(H.sk[L + 1u]);
-            if (!(kL >= kR)) {
-                c = L + 1u;
-                kc = kR;
-            }
-        }
-        if (lane == np) {
-            pp = c;
-            pk = kc;
-            pv = H.sv[c];
-        }
-        cur = c;
-        np++;
-    }
-    double xk = 0.0;
-    uint32_t xv = 0;
-    bool havex = false;
-    int stop = -1;  // first path index x is not smaller than
-    while (!bottom) {
-#if SHD_RP_TIME
-        H.nl[6]++;  // HBM sink rounds
-#endif
+    // LDS levels, kRpLA per round: every lane reads its subtree node (one LDS round trip), the
+    // path is walked with readlanes
+    for (;;) {
+        const int dcur = 31 - __clz(cur + 1u);          // level of cur
+        const int nlds = SHD_RP_LDS_LEVELS - 1 - dcur;  // LDS levels below it
+        if (nlds <= 0) break;
+        const int la = nlds < kRpLA ? nlds : kRpLA;
         const uint32_t p = rp_sub_pos(cur, lane);
         double k = -INFINITY;
         uint32_t v = 0;
-        if (lane < kRpLaNodes && p < size) H.node(p, k, v, RPL_SINK_LD);
-        if (!havex) {
-            xk = rl_f64(kx, 63);
-            xv = rl_u32(vx, 63);
-            havex = true;
-            const unsigned long long sm = __ballot(lane < np && !(xk < pk));
-            if (sm) {
-                stop = __ffsll((long long)sm) - 1;
-                break;
-            }
+        if (lane < (2 << la) - 2 && p < size) {
+            k = rp_sk[p];
+            v = rp_sv[p];
         }
         uint32_t q = 0;
-#pragma unroll
-        for (int s = 0; s < kRpLA; ++s) {
+        for (int s = 0; s < la; ++s) {
             const uint32_t L = 2u * cur + 1u;
             if (L >= size) {
                 bottom = true;
                 break;
             }
-            const int li = (int)(2u * q);  // lane of the left child (BFS 2q+1)
+            const int li = (int)(2u * q);  // BFS index of the left child
             const double kL = rl_f64(k, li);
             int ci = li;
             uint32_t c = L;
@@ -302,11 +290,71 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
                     kc = kR;
                 }
             }
+            const uint32_t vc = rl_u32(v, ci);
+            if (lane == np) {
+                pp = c;
+                pk = kc;
+                pv = vc;
+            }
+            cur = c;
+            np++;
+            q = (uint32_t)ci + 1u;
+        }
+        if (bottom) break;
+    }
+    RP_STICK(0);
+    double xk = 0.0;
+    uint32_t xv = 0;
+    bool havex = false;
+    int stop = -1;  // first path index x is not smaller than
+    while (!bottom) {
+#if SHD_RP_TIME
+        H.nl[6]++;  // HBM sink rounds
+#endif
+        const uint32_t p = rp_sub_pos(cur, lane);
+        double k = -INFINITY, k2 = -INFINITY;
+        uint32_t v = 0, v2 = 0;
+        if (lane < kHNodes && p < size) H.node(p, k, v, RPL_SINK_LD);
+        if (kHNodes > 64) {  // BFS nodes 64.. in a second register
+            const uint32_t p2 = rp_sub_pos(cur, lane + 64);
+            if (lane + 64 < kHNodes && p2 < size) H.node(p2, k2, v2, RPL_SINK_LD);
+        }
+        if (!havex) {
+            xk = rl_f64(kx, 63);
+            xv = rl_u32(vx, 63);
+            havex = true;
+            const unsigned long long sm = __ballot(lane < np && !(xk < pk));
+            if (sm) {
+                stop = __ffsll((long long)sm) - 1;
+                break;
+            }
+        }
+        uint32_t q = 0;
+#pragma unroll
+        for (int s = 0; s < kHL; ++s) {
+            const uint32_t L = 2u * cur + 1u;
+            if (L >= size) {
+                bottom = true;
+                break;
+            }
+            const int li = (int)(2u * q);  // BFS index of the left child (2q+1 - 1)
+            const double kL = li < 64 ? rl_f64(k, li) : rl_f64(k2, li - 64);
+            int ci = li;
+            uint32_t c = L;
+            double kc = kL;
+            if (L + 1u < size) {
+                const double kR = li + 1 < 64 ? rl_f64(k, li + 1) : rl_f64(k2, li + 1 - 64);
+                if (!(kL >= kR)) {
+                    ci = li + 1;
+                    c = L + 1u;
+                    kc = kR;
+                }
+            }
             if (!(xk < kc)) {
                 stop = np;
                 break;
             }
-            const uint32_t vc = rl_u32(v, ci);
+            const uint32_t vc = ci < 64 ? rl_u32(v, ci) : rl_u32(v2, ci - 64);
             if (lane == np) {
                 pp = c;
                 pk = kc;
@@ -326,9 +374,11 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
     } else if (stop < 0) {
         stop = np;
     }
+    RP_STICK(1);
     const uint32_t up = __shfl_up(pp, 1);  // the parent's position (path node lane - 1)
     if (lane < stop) H.put(lane == 0 ? 0u : up, pk, pv, RPL_SINK_ST);
     if (lane == 0) H.put(stop == 0 ? 0u : rl_u32(pp, stop - 1), xk, xv, RPL_SINK_ST);
+    RP_STICK(2);
 }
 
 // igraph_2wheap_shift_up of element (xk, xv) from position `pos` (a hole).  Returns the number f
@@ -374,17 +424,15 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                    const uint32_t* __restrict__ targets, int A, int full, double2* out_lr,
                    uint16_t* out_hops, double* out_rowmin, unsigned long long* stats,
                    double* dbg_dist, int32_t* dbg_par) {
-    __shared__ double sk[kRpT];
-    __shared__ uint32_t sv[kRpT];
     const int lane = (int)threadIdx.x;
     const size_t V = (size_t)g.V;
     const size_t slot = blockIdx.x;
     uint4* vr = ws.vrec + slot * V;
-    unsigned long long nl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long nl[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #if SHD_RP_TIME
     unsigned long long tph[4] = {0, 0, 0, 0}, tlast = wall_clock64();
 #endif
-    RpHeap H{ws.node + slot * V, vr, sk, sv, nl};
+    RpHeap H{ws.node + slot * V, vr, nl};
     uint32_t* pbuf = ws.pathbuf + slot * (size_t)kMaxHops * 64;
     unsigned long long n_pop = 0, n_push = 0, n_mod = 0, n_rows = 0;
 
@@ -409,11 +457,15 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
             H.put(0, 0.0, src, RPL_SINK_ST);
         }
         int64_t to_reach = full ? (int64_t)V + 1 : (int64_t)g.ntargets;
+        // The root after a sink is the next pop's u unless a shift-up of the relaxation reaches
+        // the root: its row bounds (lanes 0, 1) and target word (lane 0) are loaded by vector
+        // loads right after the sink and used if it still is (C4-int: every pop).
+        uint32_t pf_u = 0xFFFFFFFFu, pf_r = 0, pf_t = 0;
         while (size > 0 && to_reach > 0) {
             // igraph_2wheap_delete_max
             RP_TICK(3);
-            const uint32_t u = uni_u32(sv[0]);
-            const double du = -uni_f64(sk[0]);  // mindist = -data[0]
+            const uint32_t u = uni_u32(rp_sv[0]);
+            const double du = -uni_f64(rp_sk[0]);  // mindist = -data[0]
             const uint32_t lastp = size - 1u;
             // one round trip: the sink's first subtree (lanes < kRpLaNodes), the last node (lane
             // 63) and, independent of the heap, u's target bit, row bounds and first 64 records
@@ -428,8 +480,19 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                 else if (lane == 63) H.node(lastp, k1, v1, RPL_SINK_LD);
             }
 #endif
-            const uint32_t tb = g.tbits[u >> 5];
-            const uint32_t rb = uni_u32(g.rowptr[u]), re = uni_u32(g.rowptr[u + 1]);
+            uint32_t tb, rb, re;
+            if (SHD_RP_PREF && u == pf_u) {
+#if SHD_RP_TIME
+                nl[13]++;
+#endif
+                rb = rl_u32(pf_r, 0);
+                re = rl_u32(pf_r, 1);
+                tb = rl_u32(pf_t, 0);
+            } else {
+                tb = g.tbits[u >> 5];
+                rb = uni_u32(g.rowptr[u]);
+                re = uni_u32(g.rowptr[u + 1]);
+            }
             uint4 r0 = make_uint4(0u, 0u, 0u, 0u);
             if (rb + (uint32_t)lane < re) r0 = g.rec[rb + (uint32_t)lane];
             size = lastp;
@@ -443,6 +506,11 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 #endif
             n_pop++;
             RP_TICK(0);
+            if (SHD_RP_PREF && size > 0) {
+                pf_u = uni_u32(rp_sv[0]);
+                if (lane < 2) pf_r = g.rowptr[pf_u + (uint32_t)lane];
+                if (lane == 0) pf_t = g.tbits[pf_u >> 5];
+            }
             if ((tb >> (u & 31u)) & 1u) {
                 to_reach--;
                 // every target is popped: its parent chain is final (relaxing u's edges, as
@@ -625,6 +693,8 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
         for (int i = 0; i < 4; ++i) atomicAdd(&stats[ST_RP_T0 + i], tph[i]);
         atomicAdd(&stats[ST_RP_T0 + 4], nl[6]);
         atomicAdd(&stats[ST_RP_T0 + 5], nl[7]);
+        for (int i = 0; i < 3; ++i) atomicAdd(&stats[ST_RP_T0 + 6 + i], nl[8 + i]);
+        atomicAdd(&stats[ST_RP_T0 + 9], nl[13]);
 #endif
     }
 }
@@ -632,6 +702,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 }  // namespace
 
 int replay_lds_levels() { return SHD_RP_LDS_LEVELS; }
+int replay_lds_bytes() { return (int)kRpT * 12; }
 
 hipError_t launch_heap_replay(const ReplayCSR& g, const ReplayWs& ws, const uint32_t* d_sources,
                               const uint32_t* d_rows, int nrows, const uint32_t* d_targets, int A,

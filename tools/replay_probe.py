@@ -43,3 +43,6 @@ for mode in modes:
             ("sink", "loads", "heap_ops", "rest"), st["replay_phase_ms"])) +
             " | sink rounds %.2f, mean heap size %.0f" % (st["replay_sink_rounds"] / pops,
                                                          st["replay_heap_sum"] / pops), flush=True)
+        print("  sink ns per pop: lds_walk %.0f hbm_rounds %.0f moves %.0f | prefetch hits %.3f" % (
+            tuple(x * 1e6 / pops for x in st["replay_sink_ms"]) + (st["replay_pf_hits"] / pops,)),
+            flush=True)
