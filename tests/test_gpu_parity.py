@@ -100,6 +100,24 @@ def test_sssp_batch_widths(batch):
     assert np.array_equal(hops, ohops.astype(np.uint16))
 
 
+@pytest.mark.parametrize("fill", [0, 1, 3, 5, 8])
+@pytest.mark.parametrize("integer", [False, True])
+def test_sssp_batch_fill(fill, integer):
+    """Batches filled below K (option batch_fill; 0 = auto, which fills ceil(A / slots) here)
+    settle the same table: idle lanes, the ragged last batch and the batch order by mean pi."""
+    top, g = synthetic_pair(seed=19, n_routers=2000, n_poi=101, n_edges=20000, integer=integer)
+    top.set_option("batch_fill", fill)
+    otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay", "server"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    assert st["errors"] == 0
+    assert st["batch_fill"] == (fill if fill else min(8, -(-len(a) // st["slots"])))
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+
+
 def test_sssp_rows_shard_equals_full():
     """build_rows on a row range == the same rows of the full table (sharding correctness)."""
     import torch
