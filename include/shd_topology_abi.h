@@ -105,7 +105,10 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * queue, 0 = sized from V; small values force the scanning fallback), "events" (1 = diagnostic
  * kernel with event counters), "tie_replay" (1: rows whose target chains cross a d-tied parent
  * are recomputed by the exact heap replay; 0: reported only), "replay_all" (test hook: every row
- * through the replay), "replay_slots" (concurrent replay wavefronts, 0 = auto), "devices" (N:
+ * through the replay), "replay_slots" (concurrent replay wavefronts, 0 = auto), "replay_landmark"
+ * (1: the replay skips relaxations into vertices a landmark bound proves popped), "tie_dense"
+ * (-1 auto / 0 / 1: every row through the replay, no batch kernel, once a build replayed >= 90 %
+ * of its rows), "devices" (N:
  * the table is built by N GPUs of this process -- rows sharded, RCCL all-gather of the rows and
  * all-reduce(MIN) of the minimum; devices device..device+N-1), "rccl" (1: use that exchange even
  * with one device), "batch" (sources per SSSP workgroup: 8; 2 / 4 / 16; 1 = single-source
@@ -208,6 +211,10 @@ typedef struct {
     int64_t replay_heap_sum;
     double replay_sink_ms[3];   /*   the sink's LDS walk, HBM rounds and moves, */
     int64_t replay_pf_hits;     /*   pops whose row bounds were prefetched */
+    int64_t replay_skips;       /* replay relaxations into vertices the landmark bound proves
+                                   popped (their vertex record is not read) */
+    int64_t tie_dense;          /* 1: the last build ran every row through the replay because the
+                                   topology is tie-dense (option "tie_dense") */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -175,7 +175,14 @@ struct _Topology {
     // a d-tied parent, and every row of a directed topology
     bool tieReplay = true;    // option "tie_replay" (0: report ambiguous pairs only)
     bool replayAll = false;   // option "replay_all" (test hook: every row through the replay)
+    // option "tie_dense": -1 auto, 0 never, 1 always.  A tie-dense topology (integer latencies:
+    // C4-int replays every row) skips the batch kernel, whose rows the replay would recompute
+    // anyway; auto turns it on after a build of >= 64 rows that replayed >= 90 % of them.
+    int tieDenseOpt = -1;
+    bool tieDense = false;
     int replaySlotsOpt = 0;   // option "replay_slots" (0 = sized from the CUs and free HBM)
+    bool replayLandmark = true;  // option "replay_landmark": skip edges into vertices the
+                                 // landmark bound proves popped (topo_replay.hip)
     int sourceOrder = 2;      // option "source_order": batch kernel source grouping (0 = row
                               // order, 1 = by the hub their h0-tree path enters the core, then
                               // pi, 2 = preorder of the h0 shortest-path tree)
@@ -187,6 +194,7 @@ struct _Topology {
     bool replayUploaded = false;
     DevBuf<uint32_t> d_rrow;
     DevBuf<uint4> d_rrec;
+    DevBuf<uint32_t> d_rown;
     DevBuf<double2> d_rhop;
     DevBuf<uint32_t> d_tbits;
     DevBuf<uint4> d_rvrec, d_rnode;
@@ -835,6 +843,7 @@ int upload_replay(Topology* top) {
     for (int32_t k = 0; k < V; k++) rowptr[(size_t)k + 1] += rowptr[(size_t)k];
     const size_t nr = gstart.size();
     std::vector<uint4> rec(nr);
+    std::vector<uint32_t> own(nr);
     std::vector<double2> hop(nr);
     std::vector<uint32_t> fill(rowptr.begin(), rowptr.end() - 1);
     for (size_t gi = 0; gi < nr; gi++) {
@@ -846,16 +855,27 @@ int upload_replay(Topology* top) {
         const uint32_t k = fill[x]++;
         uint64_t wb;
         memcpy(&wb, &w, 8);
-        rec[k] = make_uint4((uint32_t)top->inv[(size_t)ey[id0]], x, (uint32_t)wb,
-                            (uint32_t)(wb >> 32));
+        // pi(y) = d(h0, y) rounded up to f32: the replay's landmark skip (topo_replay.hip)
+        const uint32_t y = (uint32_t)top->inv[(size_t)ey[id0]];
+        float pf = INFINITY;
+        if (!dir && y < top->pot.size() && std::isfinite(top->pot[y])) {
+            pf = (float)top->pot[y];
+            if ((double)pf < top->pot[y]) pf = std::nextafter(pf, INFINITY);
+        }
+        uint32_t pb;
+        memcpy(&pb, &pf, 4);
+        rec[k] = make_uint4(y, pb, (uint32_t)wb, (uint32_t)(wb >> 32));
+        own[k] = x;
         hop[k] = make_double2(g.elat[(size_t)ee[id0]], g.eloss[(size_t)ee[id0]]);
     }
     HIPCHK(top->d_rrow.ensure((size_t)V + 1));
     HIPCHK(top->d_rrec.ensure(std::max<size_t>(1, nr)));
+    HIPCHK(top->d_rown.ensure(std::max<size_t>(1, nr)));
     HIPCHK(top->d_rhop.ensure(std::max<size_t>(1, nr)));
     HIPCHK(hipMemcpy(top->d_rrow.p, rowptr.data(), sizeof(uint32_t) * ((size_t)V + 1), hipMemcpyHostToDevice));
     if (nr) {
         HIPCHK(hipMemcpy(top->d_rrec.p, rec.data(), sizeof(uint4) * nr, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_rown.p, own.data(), sizeof(uint32_t) * nr, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_rhop.p, hop.data(), sizeof(double2) * nr, hipMemcpyHostToDevice));
     }
     top->replayUploaded = true;
@@ -868,6 +888,9 @@ ReplayCSR replay_csr(Topology* top) {
     c.nadj = (int64_t)top->d_rrec.n;
     c.rowptr = top->d_rrow.p;
     c.rec = top->d_rrec.p;
+    c.own = top->d_rown.p;
+    // pi values exist for undirected topologies (upload_csr: d(h0, .) from relabelled vertex 0)
+    c.landmark = (!top->isDirected && top->replayLandmark && !top->pot.empty()) ? 0 : -1;
     c.hop = top->d_rhop.p;
     c.vloss = top->d_vloss.p;
     c.selfLat = top->d_selfLat.p;
@@ -1024,7 +1047,10 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         // heap replay; otherwise the batch kernel runs and flags the rows that need it
         // multigraphs too: the reference sums the igraph_get_eid edge of each hop, which the batch
         // epilogue (latency = distance) does not reproduce when parallel edges differ
-        const bool allReplay = top->isDirected || top->replayAll || top->hasMultiEdges;
+        const bool dense = top->tieReplay && (top->tieDenseOpt == 1 ||
+                                              (top->tieDenseOpt < 0 && top->tieDense));
+        const bool allReplay = top->isDirected || top->replayAll || top->hasMultiEdges || dense;
+        top->stats.tie_dense = dense ? 1 : 0;
         std::vector<uint32_t> src((size_t)rows), tgt((size_t)A);
         for (int64_t i = 0; i < rows; i++) src[(size_t)i] = (uint32_t)top->inv[(size_t)top->attached[(size_t)(row0 + i)]];
         for (int64_t i = 0; i < A; i++) tgt[(size_t)i] = (uint32_t)top->inv[(size_t)top->attached[(size_t)i]];
@@ -1192,6 +1218,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             HIPCHK(hipMemcpy(fl.data(), top->d_rowflag.p, (size_t)rows, hipMemcpyDeviceToHost));
             for (int64_t i = 0; i < rows; i++)
                 if (fl[(size_t)i]) rlist.push_back((uint32_t)i);
+            if (rows >= 64 && (int64_t)rlist.size() * 10 >= rows * 9) top->tieDense = true;
         }
         top->replayPending = false;
         if (!rlist.empty()) {
@@ -1277,6 +1304,7 @@ int collect_row_stats(Topology* top) {
         top->stats.replay_heap_sum = (int64_t)h[ST_RP_T0 + 5];
         for (int i = 0; i < 3; i++) top->stats.replay_sink_ms[i] = (double)h[ST_RP_T0 + 6 + i] / (double)khz;
         top->stats.replay_pf_hits = (int64_t)h[ST_RP_T0 + 9];
+        top->stats.replay_skips = (int64_t)h[ST_RP_SKIP];
     }
     top->stats.replay_slots = top->stats.replay_rows ? std::min(top->rslots, top->rslotsUse) : 0;
     {
@@ -1389,6 +1417,8 @@ void sync_peer(Topology* top, Topology* p) {
     p->farCap = top->farCap;
     p->tieReplay = top->tieReplay;
     p->replayAll = top->replayAll;
+    p->tieDenseOpt = top->tieDenseOpt;
+    p->tieDense = p->tieDense || top->tieDense;
     p->replaySlotsOpt = top->replaySlotsOpt;
     p->sourceOrder = top->sourceOrder;
     p->batchOrder = top->batchOrder;
@@ -1525,6 +1555,8 @@ int build_multi(Topology* top) {
         top->stats.build_ms = std::max(top->stats.build_ms, o.build_ms);
         top->stats.ambiguous_pairs += o.ambiguous_pairs;
         top->stats.replay_rows += o.replay_rows;
+        top->stats.replay_skips += o.replay_skips;
+        top->tieDense = top->tieDense || slot_engine(top, d)->tieDense;
         top->stats.errors += o.errors;
         top->stats.relaxations += o.relaxations;
     }
@@ -1952,6 +1984,8 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "tie_replay") top->tieReplay = value != 0;
     else if (k == "replay_all") top->replayAll = value != 0;
     else if (k == "replay_slots") top->replaySlotsOpt = (int)value;
+    else if (k == "replay_landmark") top->replayLandmark = value != 0;
+    else if (k == "tie_dense") top->tieDenseOpt = value < 0 ? -1 : (value != 0 ? 1 : 0);
     else if (k == "source_order") top->sourceOrder = (int)value;
     else if (k == "batch_order") top->batchOrder = (int)value;
     else if (k == "batch_fill") top->batchFill = (int)value;

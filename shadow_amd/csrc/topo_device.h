@@ -74,7 +74,8 @@ enum StatIdx {
     ST_RP_T0 = 40,      // replay wall ticks (SHD_RP_TIME builds): sink, loads, heap ops, rest
                         // + sink rounds, heap size summed over pops, sink sub-phases
                         // (LDS walk, HBM rounds, moves), root-prefetch hits
-    ST_COUNT = 50
+    ST_RP_SKIP = 50,    // replay relaxations whose vertex record the landmark skip did not read
+    ST_COUNT = 51
 };
 
 struct DevCSR {
@@ -141,13 +142,16 @@ struct ReplayCSR {
     int32_t V = 0;
     int64_t nadj = 0;
     const uint32_t* rowptr = nullptr;
+    // {u32 neighbour, f32 pi(neighbour) rounded up (+inf: no landmark), f64 w} per entry
     const uint4* rec = nullptr;
+    const uint32_t* own = nullptr;  // row (vertex) of each entry: the epilogue's parent walk
     const double2* hop = nullptr;
     const double* vloss = nullptr;
     const double* selfLat = nullptr;
     const double* selfLoss = nullptr;
     const uint32_t* tbits = nullptr;  // target (attached vertex) bitmap over V
     int64_t ntargets = 0;             // distinct targets (igraph's to_reach)
+    int32_t landmark = -1;            // vertex the rec pi values are measured from (-1: none)
 };
 
 // per-slot workspace of the heap replay (one wavefront = one slot), slot-major [slot][V]:

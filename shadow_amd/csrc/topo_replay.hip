@@ -37,6 +37,12 @@
 // registers; a shift-up loads the whole ancestor chain (<= 20 lanes) in one round trip and
 // finds its stop by a ballot; the relaxation of a row takes 64 edges per step.  The top
 // kRpLdsLevels levels of the heap live in LDS (the positions every sink starts from).
+//
+// Landmark skip.  Half the relaxations go to vertices already popped (each undirected edge is
+// relaxed from both ends) and change nothing, yet each reads a random 16-B vertex record.  The
+// row entry carries pi(t) = d(h0, t) (f32 rounded up; h0 = the top hub, relabelled vertex 0);
+// once h0 is popped, d(h0) + pi(t) < du (with a 1e-6 relative margin for the rounding of the
+// sums) proves t popped, and its record is not read: on C4-int 31-46 % of the relaxations.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -78,6 +84,9 @@ using namespace dev;
 #endif
 #ifndef SHD_RP_PREF
 #define SHD_RP_PREF 1  // the next root's row bounds and target bit loaded right after the sink
+#endif
+#ifndef SHD_RP_EARLY
+#define SHD_RP_EARLY 1  // the first 64 relaxation records are read during the pop's sink
 #endif
 #ifndef SHD_RP_LA
 #define SHD_RP_LA 5  // sink lookahead: heap levels loaded per round trip (<= 5: 62 nodes)
@@ -246,8 +255,12 @@ __device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t
 // kRpLA per round trip (the first round is issued before x is waited for).  x stops at the first
 // path node it is not smaller than; the path nodes above the stop move up one level, in parallel
 // (lane i holds path node i).  (kx, vx): x in lane 63, loaded by the caller.
+// pre / tq / xr: the vertex record of this lane's first relaxation target tq (pre: it is read)
+// is loaded with the first HBM round, its latency hidden behind the sink's; the heap positions
+// the sink moves are patched into it.
 __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int lane, double kx,
-                                            uint32_t vx) {
+                                            uint32_t vx, bool pre, uint32_t tq, uint4& xr) {
+    bool xl = !pre;  // record issued
 #if SHD_RP_TIME
     H.nl[12] = wall_clock64();
 #endif
@@ -319,6 +332,10 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
             const uint32_t p2 = rp_sub_pos(cur, lane + 64);
             if (lane + 64 < kHNodes && p2 < size) H.node(p2, k2, v2, RPL_SINK_LD);
         }
+        if (!xl) {
+            xr = H.vr[tq];
+            xl = true;
+        }
         if (!havex) {
             xk = rl_f64(kx, 63);
             xv = rl_u32(vx, 63);
@@ -375,9 +392,16 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
         stop = np;
     }
     RP_STICK(1);
+    if (!xl) xr = H.vr[tq];
     const uint32_t up = __shfl_up(pp, 1);  // the parent's position (path node lane - 1)
+    const uint32_t xp = stop == 0 ? 0u : rl_u32(pp, stop - 1);
     if (lane < stop) H.put(lane == 0 ? 0u : up, pk, pv, RPL_SINK_ST);
-    if (lane == 0) H.put(stop == 0 ? 0u : rl_u32(pp, stop - 1), xk, xv, RPL_SINK_ST);
+    if (lane == 0) H.put(xp, xk, xv, RPL_SINK_ST);
+    if (pre) {  // positions of the moved vertices in the early record
+        for (int i = 0; i < stop; ++i)
+            if (tq == rl_u32(pv, i)) xr.w = i == 0 ? 0u : rl_u32(pp, i - 1);
+        if (tq == xv) xr.w = xp;
+    }
     RP_STICK(2);
 }
 
@@ -434,7 +458,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 #endif
     RpHeap H{ws.node + slot * V, vr, nl};
     uint32_t* pbuf = ws.pathbuf + slot * (size_t)kMaxHops * 64;
-    unsigned long long n_pop = 0, n_push = 0, n_mod = 0, n_rows = 0;
+    unsigned long long n_pop = 0, n_push = 0, n_mod = 0, n_rows = 0, n_skip = 0;
 
     for (;;) {
         uint32_t item = 0;
@@ -461,6 +485,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
         // the root: its row bounds (lanes 0, 1) and target word (lane 0) are loaded by vector
         // loads right after the sink and used if it still is (C4-int: every pop).
         uint32_t pf_u = 0xFFFFFFFFu, pf_r = 0, pf_t = 0;
+        double dh0 = INFINITY;  // d(landmark) once it is popped (no skip before)
         while (size > 0 && to_reach > 0) {
             // igraph_2wheap_delete_max
             RP_TICK(3);
@@ -499,10 +524,17 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 #if SHD_RP_TIME
             nl[7] += size;  // heap size at the pop
 #endif
+            if (u == (uint32_t)g.landmark) dh0 = du;
+            // this lane's first relaxation target, read during the sink unless skipped
+            const bool live0 = SHD_RP_EARLY && rb + (uint32_t)lane < re &&
+                               !(__dmul_rn(__dadd_rn(dh0, (double)__uint_as_float(r0.y)), 1.000001) < du);
+            uint4 xr0 = make_uint4(0u, 0u, 0u, 0u);
 #if SHD_RP_SINK2
-            if (size > 0) rp_pop_sink(H, size, lane, k1, v1);
+            if (size > 0) rp_pop_sink(H, size, lane, k1, v1, live0, r0.x, xr0);
+            else if (live0) xr0 = vr[r0.x];
 #else
             if (size > 0) rp_sink(H, 0, size, rl_f64(k1, 63), rl_u32(v1, 63), lane, k1, v1);
+            if (live0) xr0 = vr[r0.x];
 #endif
             n_pop++;
             RP_TICK(0);
@@ -524,19 +556,29 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                 double w = 0.0, cur = 0.0;
                 rp_lines(nl, RPL_RELAX_LD, act, g.rec + j);
 #if SHD_RP_LINES
-                rp_lines(nl, RPL_RELAX_LD, act, vr + 4 * (size_t)lane + (act ? g.rec[j].x : 0));
+                rp_lines(nl, RPL_RELAX_LD, act && !(__dmul_rn(__dadd_rn(dh0, (double)__uint_as_float(g.rec[act ? j : 0].y)), 1.000001) < du),
+                         vr + 4 * (size_t)lane + (act ? g.rec[j].x : 0));
 #endif
+                bool live = act;
                 if (act) {
                     const uint4 r = base == rb ? r0 : g.rec[j];
                     t = r.x;
                     w = __hiloint2double((int)r.w, (int)r.z);
-                    const uint4 x = vr[t];  // {dist, parent slot, heap position}
+                    // landmark skip: d(t) <= d(h0) + pi(t) (the walk s -> h0 -> t; pi rounded
+                    // up, rounding of the sums far inside the 1e-6 margin) below du proves t
+                    // popped, and relaxing a popped vertex changes nothing: its record is not read
+                    live = !(__dmul_rn(__dadd_rn(dh0, (double)__uint_as_float(r.y)), 1.000001) < du);
+                }
+                if (live) {
+                    // {dist, parent slot, heap position}
+                    const uint4 x = SHD_RP_EARLY && base == rb ? xr0 : vr[t];
                     cur = __hiloint2double((int)x.y, (int)x.x);
                     mypos = x.w;
                 }
+                n_skip += (unsigned long long)__popcll(__ballot(act && !live));
                 const double alt = __dadd_rn(du, w);
-                const bool first = act && cur < 0.0;
-                const bool impr = act && !first && alt < cur;
+                const bool first = live && cur < 0.0;
+                const bool impr = live && !first && alt < cur;
                 rp_lines(nl, RPL_RELAX_ST, first || impr, vr + 4 * (size_t)lane + t);
                 if (first || impr) {  // dist and parent in one 12-B store
                     const unsigned long long b = d2bits(alt);
@@ -605,7 +647,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                 const uint4 x = vr[i];
                 const double d = __hiloint2double((int)x.y, (int)x.x);
                 dbg_dist[i] = d;
-                dbg_par[i] = (d >= 0.0 && i != src) ? (int32_t)g.rec[x.z].y : -1;
+                dbg_par[i] = (d >= 0.0 && i != src) ? (int32_t)g.own[x.z] : -1;
             }
         }
 
@@ -641,7 +683,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                     }
                     if (h < (uint32_t)kMaxHops) pbuf[(size_t)h * 64 + lane] = j;
                     h++;
-                    v = g.rec[j].y;
+                    v = g.own[j];
                     if (h > (uint32_t)V) bad = true;
                 }
                 lat = 0.0;
@@ -660,7 +702,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                             j = pbuf[(size_t)x * 64 + lane];
                         } else {
                             uint32_t y = t;  // the chain was validated by the walk above
-                            for (int z = 0; z < x; ++z) y = g.rec[vr_par(vr, y)].y;
+                            for (int z = 0; z < x; ++z) y = g.own[vr_par(vr, y)];
                             j = vr_par(vr, y);
                         }
                         const double2 hp = g.hop[j];
@@ -685,6 +727,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
         atomicAdd(&stats[ST_RP_PUSH], n_push);
         atomicAdd(&stats[ST_RP_MOD], n_mod);
         atomicAdd(&stats[ST_RP_ROWS], n_rows);
+        atomicAdd(&stats[ST_RP_SKIP], n_skip);
 #if SHD_RP_LINES
         for (int i = 0; i < 6; ++i) atomicAdd(&stats[ST_RP_L0 + i], nl[i]);
 #endif

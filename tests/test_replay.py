@@ -140,3 +140,58 @@ def test_multigraph_table(directed):
     assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(hops, ohops.astype(np.uint16))
     assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+
+
+def _table_bit_exact(top, g, verts):
+    a, lat, rel, hops = top.table()
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(a, oa)
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    return top.stats()
+
+
+@pytest.mark.parametrize("landmark", [1, 0])
+def test_tie_dense_replay_landmark_skip(landmark):
+    """tie_dense = 1: no batch kernel, every row through the replay; the replay's landmark skip
+    (relaxations into vertices d(h0) + pi(t) < du proves popped: their record is not read) on or
+    off -- every pair bit-exact against the oracle either way."""
+    top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=True)
+    top.set_option("tie_dense", 1)
+    top.set_option("replay_landmark", landmark)
+    otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
+    st = _table_bit_exact(top, g, verts)
+    assert st["tie_dense"] == 1 and st["errors"] == 0
+    assert st["replay_rows"] == len(top.attached_vertices())
+    assert st["ambiguous_pairs"] == 0  # the batch kernel did not run
+    if landmark:
+        assert st["replay_skips"] > st["replay_pops"]  # several per pop on this graph
+    else:
+        assert st["replay_skips"] == 0
+
+
+def test_tie_dense_auto_switch():
+    """tie_dense auto (-1): a build that replays >= 90 % of >= 64 rows switches the topology to
+    replay-only builds; the rebuilt rows are bit-identical."""
+    import torch
+    top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=True)
+    otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
+    A = len(top.attached_vertices())
+    outs, sts = [], []
+    for _ in range(2):
+        lr = torch.empty((A, A, 2), dtype=torch.float64, device="cuda")
+        hp = torch.empty((A, A), dtype=torch.int16, device="cuda")
+        top.build_rows_into(0, A, lr, hp)
+        torch.cuda.synchronize()
+        outs.append((lr.cpu().numpy(), hp.cpu().numpy()))
+        sts.append(top.stats())
+    dense = A >= 64 and sts[0]["replay_rows"] * 10 >= A * 9
+    assert sts[0]["tie_dense"] == 0
+    assert sts[1]["tie_dense"] == (1 if dense else 0)
+    if dense:
+        assert sts[1]["replay_rows"] == A and sts[1]["ambiguous_pairs"] == 0
+    assert np.array_equal(outs[0][0].view(np.uint64), outs[1][0].view(np.uint64))
+    assert np.array_equal(outs[0][1], outs[1][1])
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(outs[1][0][..., 0].view(np.uint64), olat.view(np.uint64))

@@ -1,5 +1,6 @@
 """Probe: heap-replay cost on C4-int (integer latencies) for a row range, per row and per heap op.
-usage: python tools/replay_probe.py ROWS [SLOTS] [all]  (all: only the replay_all mode)"""
+usage: python tools/replay_probe.py ROWS [SLOTS] [all] [LANDMARK]  (all: only the replay_all mode;
+LANDMARK 0: no landmark skip)"""
 import sys
 import time
 
@@ -17,6 +18,8 @@ A = len(top.attached_vertices())
 print("gen %.1fs A=%d" % (time.time() - t0, A), flush=True)
 if slots:
     top.set_option("replay_slots", slots)
+if len(sys.argv) > 4:
+    top.set_option("replay_landmark", int(sys.argv[4]))
 lr = torch.empty((rows, A, 2), dtype=torch.float64, device="cuda")
 hp = torch.empty((rows, A), dtype=torch.int16, device="cuda")
 modes = ("replay_all",) if len(sys.argv) > 3 and sys.argv[3] == "all" else ("batch+replay", "replay_all")
@@ -28,10 +31,10 @@ for mode in modes:
     st = top.stats()
     r = max(1, st["replay_rows"])
     print("%s: wall %.2fs sssp %.1f ms replay %.1f ms rows %d slots %d ambiguous %d | per row: "
-          "pops %.0f pushes %.0f mods %.0f" % (
+          "pops %.0f pushes %.0f mods %.0f skips %.0f" % (
               mode, time.time() - t0, st["sssp_kernel_ms"], st["replay_ms"], st["replay_rows"],
               st["replay_slots"], st["ambiguous_pairs"], st["replay_pops"] / r,
-              st["replay_pushes"] / r, st["replay_modifies"] / r), flush=True)
+              st["replay_pushes"] / r, st["replay_modifies"] / r, st["replay_skips"] / r), flush=True)
     if any(st["replay_lines"]):
         pops = max(1, st["replay_pops"])
         print("  64-B lines per pop: " + " ".join("%s %.1f" % (n, x / pops) for n, x in zip(
