@@ -85,9 +85,6 @@ using namespace dev;
 #ifndef SHD_RP_PREF
 #define SHD_RP_PREF 1  // the next root's row bounds and target bit loaded right after the sink
 #endif
-#ifndef SHD_RP_EARLY
-#define SHD_RP_EARLY 1  // the first 64 relaxation records are read during the pop's sink
-#endif
 #ifndef SHD_RP_LA
 #define SHD_RP_LA 5  // sink lookahead: heap levels loaded per round trip (<= 5: 62 nodes)
 #endif
@@ -255,12 +252,8 @@ __device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t
 // kRpLA per round trip (the first round is issued before x is waited for).  x stops at the first
 // path node it is not smaller than; the path nodes above the stop move up one level, in parallel
 // (lane i holds path node i).  (kx, vx): x in lane 63, loaded by the caller.
-// pre / tq / xr: the vertex record of this lane's first relaxation target tq (pre: it is read)
-// is loaded with the first HBM round, its latency hidden behind the sink's; the heap positions
-// the sink moves are patched into it.
 __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int lane, double kx,
-                                            uint32_t vx, bool pre, uint32_t tq, uint4& xr) {
-    bool xl = !pre;  // record issued
+                                            uint32_t vx) {
 #if SHD_RP_TIME
     H.nl[12] = wall_clock64();
 #endif
@@ -332,10 +325,6 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
             const uint32_t p2 = rp_sub_pos(cur, lane + 64);
             if (lane + 64 < kHNodes && p2 < size) H.node(p2, k2, v2, RPL_SINK_LD);
         }
-        if (!xl) {
-            xr = H.vr[tq];
-            xl = true;
-        }
         if (!havex) {
             xk = rl_f64(kx, 63);
             xv = rl_u32(vx, 63);
@@ -392,16 +381,9 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
         stop = np;
     }
     RP_STICK(1);
-    if (!xl) xr = H.vr[tq];
     const uint32_t up = __shfl_up(pp, 1);  // the parent's position (path node lane - 1)
-    const uint32_t xp = stop == 0 ? 0u : rl_u32(pp, stop - 1);
     if (lane < stop) H.put(lane == 0 ? 0u : up, pk, pv, RPL_SINK_ST);
-    if (lane == 0) H.put(xp, xk, xv, RPL_SINK_ST);
-    if (pre) {  // positions of the moved vertices in the early record
-        for (int i = 0; i < stop; ++i)
-            if (tq == rl_u32(pv, i)) xr.w = i == 0 ? 0u : rl_u32(pp, i - 1);
-        if (tq == xv) xr.w = xp;
-    }
+    if (lane == 0) H.put(stop == 0 ? 0u : rl_u32(pp, stop - 1), xk, xv, RPL_SINK_ST);
     RP_STICK(2);
 }
 
@@ -525,16 +507,10 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
             nl[7] += size;  // heap size at the pop
 #endif
             if (u == (uint32_t)g.landmark) dh0 = du;
-            // this lane's first relaxation target, read during the sink unless skipped
-            const bool live0 = SHD_RP_EARLY && rb + (uint32_t)lane < re &&
-                               !(__dmul_rn(__dadd_rn(dh0, (double)__uint_as_float(r0.y)), 1.000001) < du);
-            uint4 xr0 = make_uint4(0u, 0u, 0u, 0u);
 #if SHD_RP_SINK2
-            if (size > 0) rp_pop_sink(H, size, lane, k1, v1, live0, r0.x, xr0);
-            else if (live0) xr0 = vr[r0.x];
+            if (size > 0) rp_pop_sink(H, size, lane, k1, v1);
 #else
             if (size > 0) rp_sink(H, 0, size, rl_f64(k1, 63), rl_u32(v1, 63), lane, k1, v1);
-            if (live0) xr0 = vr[r0.x];
 #endif
             n_pop++;
             RP_TICK(0);
@@ -570,8 +546,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                     live = !(__dmul_rn(__dadd_rn(dh0, (double)__uint_as_float(r.y)), 1.000001) < du);
                 }
                 if (live) {
-                    // {dist, parent slot, heap position}
-                    const uint4 x = SHD_RP_EARLY && base == rb ? xr0 : vr[t];
+                    const uint4 x = vr[t];  // {dist, parent slot, heap position}
                     cur = __hiloint2double((int)x.y, (int)x.x);
                     mypos = x.w;
                 }
