@@ -215,6 +215,11 @@ typedef struct {
                                    popped (their vertex record is not read) */
     int64_t tie_dense;          /* 1: the last build ran every row through the replay because the
                                    topology is tie-dense (option "tie_dense") */
+    double batch_wave_ms[6];    /* profiling builds (-DSHD_BATCH_TIME=1) only, else 0: batch
+                                   kernel wave time summed over waves -- tail iterations' chunk
+                                   loads, phase A, phase B, then the same for hub iterations */
+    int64_t batch_rounds;       /*   phase-B rounds and the (edge, source) pairs that reached phase B */
+    int64_t batch_edges_b;
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -41,7 +41,8 @@ class ShdStats(ctypes.Structure):
                 ("exchange_ms", dbl), ("parent_phase_ms", dbl * 4), ("replay_lines", i64 * 6), ("batch_fill", i64), ("replay_phase_ms", dbl * 4),
                 ("replay_sink_rounds", i64), ("replay_heap_sum", i64),
                 ("replay_sink_ms", dbl * 3), ("replay_pf_hits", i64),
-                ("replay_skips", i64), ("tie_dense", i64)]
+                ("replay_skips", i64), ("tie_dense", i64),
+                ("batch_wave_ms", dbl * 6), ("batch_rounds", i64), ("batch_edges_b", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):

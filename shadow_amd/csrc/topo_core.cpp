@@ -1305,6 +1305,9 @@ int collect_row_stats(Topology* top) {
         for (int i = 0; i < 3; i++) top->stats.replay_sink_ms[i] = (double)h[ST_RP_T0 + 6 + i] / (double)khz;
         top->stats.replay_pf_hits = (int64_t)h[ST_RP_T0 + 9];
         top->stats.replay_skips = (int64_t)h[ST_RP_SKIP];
+        for (int i = 0; i < 6; i++) top->stats.batch_wave_ms[i] = (double)h[ST_BT0 + i] / (double)khz;
+        top->stats.batch_rounds = (int64_t)h[ST_BT0 + 6];
+        top->stats.batch_edges_b = (int64_t)h[ST_BT0 + 7];
     }
     top->stats.replay_slots = top->stats.replay_rows ? std::min(top->rslots, top->rslotsUse) : 0;
     {

@@ -75,7 +75,10 @@ enum StatIdx {
                         // + sink rounds, heap size summed over pops, sink sub-phases
                         // (LDS walk, HBM rounds, moves), root-prefetch hits
     ST_RP_SKIP = 50,    // replay relaxations whose vertex record the landmark skip did not read
-    ST_COUNT = 51
+    ST_BT0 = 51,        // batch kernel (SHD_BATCH_TIME builds): wave ticks of tail iterations in
+                        // chunk loads / phase A / phase B, the same for hub iterations, phase-B
+                        // rounds, surviving edges (8 slots)
+    ST_COUNT = 59
 };
 
 struct DevCSR {

@@ -14,7 +14,7 @@
 // C4: 8 random sources, delta = 3 ms, 1.84 distinct buckets per vertex).  Lock-step buckets over
 // the shifted keys therefore expand a vertex ONCE for all sources that reach it in the current
 // bucket: the adjacency row is read once, and each relaxation reads the target's K distances as
-// one line.  K lanes work on one edge (lane j = source j).
+// one line.  The (edge, source) pairs of an edge sit in adjacent lanes.
 //
 // Per-source correctness is untouched by the shift: source j's bucket of a distance d is
 // floor((d + sh_j) / delta) with sh_j = C - pi(s_j) >= 0, a monotone function of d, and source j's
@@ -57,6 +57,15 @@ using namespace dev;
 #endif
 #ifndef SHD_TAIL_HINT
 #define SHD_TAIL_HINT 1  // record each tail pair's improver during the SSSP (parent-pass guess)
+#endif
+#ifndef SHD_BATCH_TIME
+#define SHD_BATCH_TIME 0  // profiling build: per-wave time of the near iterations' parts
+#endif
+#if SHD_BATCH_TIME
+#define BT_TICK(i) do { const unsigned long long t_ = wall_clock64(); \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&L.bt[(WAVE ? 0 : 3) + (i)], t_ - bt_last); bt_last = t_; } while (0)
+#else
+#define BT_TICK(i) do { } while (0)
 #endif
 #ifndef SHD_BATCH_CHUNK
 #define SHD_BATCH_CHUNK 512
@@ -114,6 +123,8 @@ struct LdsB {
     unsigned long long pt[5];   // parent-pass phase ticks (diagnostic)
     unsigned long long dg[4];   // diagnostic: hub edges, hub source-relaxations, first-iteration
                                 // edges, first-iteration source-relaxations
+    unsigned long long bt[8];   // SHD_BATCH_TIME builds: wave ticks of tail / hub iterations in
+                                // chunk loads, phase A, phase B; phase-B rounds, active lanes
 };
 
 // Dynamic LDS after the control block: the hubs' (deferred) source masks, parent-tie bits of the
@@ -403,11 +414,14 @@ __device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t
     return total;
 }
 
-// Transposed near iteration (default): phase A takes one edge per lane (UA per lane in flight:
-// row search + 12-B record load done once per edge, not once per source); phase B shuffles the
-// edges of a wave so that K consecutive lanes hold one edge, lane j = source j, for UA * K rounds.
-// The K lanes' pre-check loads and atomics then hit ONE 64-B line per edge in one instruction
-// (coalesced: one DRAM request instead of up to K), and every lane keeps UA * K loads in flight.
+// Transposed near iteration: phase A takes one edge per lane (UA per lane in flight: row search
+// + 16-B record load done once per edge, not once per source) and applies the landmark filter
+// per (edge, source); phase B spreads the surviving (edge, source) pairs over the lanes, 64 per
+// round, the pairs of one edge in adjacent lanes: their pre-check loads and atomics hit ONE 64-B
+// line per edge in one instruction (coalesced: one DRAM request instead of up to K), and the
+// edge's queue bookkeeping is done once by its first lane.  (Edge rounds -- K lanes per edge,
+// lane j = source j -- left 39 % of the lanes idle: 38.7 k rounds per source against 25.0 k;
+// full C4 table 401 -> 398 ms, 1,250 rows 88.5 -> 84.4 ms.)
 // Hubs are deferred: a hub improved into bucket cb sets its bit in hdef (one mask per hub, no
 // parity) and joins the hub list hq once; the kernel expands the list only when the tail queue
 // is empty, so one hub expansion serves every source that reached it meanwhile (hub rows are
@@ -421,16 +435,10 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                                               uint32_t qcap, uint32_t* hq, const BBuckets& B) {
     using MO = MaskOps<K>;
     static_assert(64 % K == 0, "a wave holds whole edge groups");
-    constexpr int EPW = 64 / K;          // edges per wave per round
-    constexpr int R = UA * K;            // rounds: the wave's 64 * UA edges, EPW at a time
-    constexpr int RB = R < SHD_BATCH_RB ? R : SHD_BATCH_RB;
-    static_assert(R % RB == 0, "rounds per load batch");
+    constexpr int RB = SHD_BATCH_RB;     // phase-B rounds whose loads are in flight together
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
-    const uint32_t j = lane % K;         // phase B: this lane's source
-    const uint32_t ge = lane / K;        // phase B: this lane's edge within the round
     const uint32_t wv = tid >> 6;
-    const double shj = L.sh[j];
     // WAVE (tail iterations): each wave takes kBSub-vertex sub-chunks of the queue from an LDS
     // counter into its own slice of the chunk arrays; no barrier until the iteration ends.
     // Otherwise (hub iterations: long rows) block-wide 512-vertex chunks.
@@ -438,6 +446,9 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
     // WAVE: the next sub-chunk is taken and its queue entries loaded before this one is
     // expanded (one global round trip less on each sub-chunk's dependent chain)
     uint32_t nb0 = 0, nqv = 0;
+#if SHD_BATCH_TIME
+    unsigned long long bt_last = wall_clock64();
+#endif
     if (WAVE) {
         if (lane == 0) nb0 = atomicAdd(&L.qhead, kBSub);
         nb0 = __shfl(nb0, 0, 64);
@@ -459,6 +470,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             total = load_chunk<K, true>(Q + base, cnt, g, L, D, mcur, hdef, true,
                                         B.cb + (uint32_t)SHD_BATCH_SPEC);
         }
+        BT_TICK(0);
         constexpr uint32_t kStep = WAVE ? 64u : (uint32_t)kSsspBlock;  // lanes per phase-A slot
         for (uint32_t eb = 0; eb < total; eb += kStep * UA) {
             // phase A: edge e = eb + a * kStep (+ wv * 64 block-wide) + lane
@@ -499,90 +511,84 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     if (ad > bnd) amk[a] &= ~(1u << jj);
                 }
             }
-            // Compaction: the wave's surviving edges (any source left) move to the front, so
-            // phase B runs only ceil(survivors / EPW) rounds.  Lane l pulls survivor
-            // a' * 64 + l (the q-th set bit of the slots' ballots, found by popcount bisection).
-            unsigned long long sb[UA];
-            uint32_t nsv = 0;
+            // Pair compaction: the wave's surviving (edge, source) pairs, in edge order (edge
+            // E = a * 64 + lane), 64 per phase-B round; lane l of round r takes pair r * 64 + l:
+            // its edge is the last E whose exclusive pair offset is <= the pair's index (binary
+            // search over the offsets by shuffles), its source the matching set bit of the
+            // edge's mask.  The pairs of one edge sit in adjacent lanes: their loads and atomics
+            // on the target's 64-B line of K distances still go out as one request.
+            uint32_t po[UA];  // exclusive pair offset of edge (a, lane)
+            uint32_t npair = 0;
 #pragma unroll
             for (int a = 0; a < UA; a++) {
-                sb[a] = __ballot(amk[a] != 0u);
-                nsv += (uint32_t)__popcll(sb[a]);
+                uint32_t t_;
+                po[a] = npair + wave_excl_scan((uint32_t)__popc(amk[a]), &t_);
+                npair += t_;
             }
-            {
-                uint32_t cn[UA], cmk[UA], clo[UA], cwl[UA], cwh[UA], cpb[UA];
+            // the edge's data for the shuffles: (col | tree bit), (chunk slot | mask << 16)
+            uint32_t alm[UA];
 #pragma unroll
-                for (int a2 = 0; a2 < UA; a2++) {
-                    uint32_t q = (uint32_t)a2 * 64u + lane;
-                    const bool ok = q < nsv;
-                    int sa = 0;
-#pragma unroll
-                    for (int a = 0; a + 1 < UA; a++) {
-                        const uint32_t c = (uint32_t)__popcll(sb[a]);
-                        if (sa == a && q >= c) { q -= c; sa = a + 1; }
-                    }
-                    unsigned long long m = sb[0];
-#pragma unroll
-                    for (int a = 1; a < UA; a++) if (sa == a) m = sb[a];
-                    uint32_t pos = 0;
-#pragma unroll
-                    for (uint32_t wdt = 32; wdt >= 1; wdt >>= 1) {
-                        const uint32_t c = (uint32_t)__popcll(m & ((1ull << wdt) - 1ull));
-                        if (q >= c) { q -= c; pos += wdt; m >>= wdt; }
-                    }
-                    const int sl = ok ? (int)pos : (int)lane;
-                    cn[a2] = 0u; cmk[a2] = 0u; clo[a2] = 0u; cwl[a2] = 0u; cwh[a2] = 0u;
-                    cpb[a2] = 0u;
-#pragma unroll
-                    for (int a = 0; a < UA; a++) {
-                        const uint32_t xn = __shfl(an[a], sl, 64);
-                        const uint32_t xm = __shfl(amk[a], sl, 64);
-                        const uint32_t xl = __shfl(alo[a], sl, 64);
-                        const uint32_t xwl = __shfl(awl[a], sl, 64);
-                        const uint32_t xwh = __shfl(awh[a], sl, 64);
-                        const uint32_t xpb = kKapInRec ? __shfl(apb[a], sl, 64) : 0u;
-                        if (ok && sa == a) {
-                            cn[a2] = xn; cmk[a2] = xm; clo[a2] = xl; cwl[a2] = xwl; cwh[a2] = xwh;
-                            cpb[a2] = xpb;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int a = 0; a < UA; a++) {
-                    an[a] = cn[a]; amk[a] = cmk[a]; alo[a] = clo[a]; awl[a] = cwl[a];
-                    awh[a] = cwh[a]; apb[a] = cpb[a];
-                }
+            for (int a = 0; a < UA; a++) alm[a] = alo[a] | (amk[a] << 16);
+            BT_TICK(1);
+#if SHD_BATCH_TIME
+            if (lane == 0) {
+                atomicAdd(&L.bt[6], (unsigned long long)((npair + 63) / 64));
+                atomicAdd(&L.bt[7], (unsigned long long)npair);
             }
-            // phase B: round r holds edges r * EPW .. r * EPW + EPW - 1 of the wave's compacted
-            // 64 * UA; RB rounds at a time have their loads in flight, rounds past the
-            // survivors are skipped (uniform per wave)
+#endif
             uint32_t fm = kNoBucket;
-#pragma unroll
-            for (int r0 = 0; r0 < R; r0 += RB) {
-            if ((uint32_t)(r0 * EPW) >= nsv) break;
-            uint32_t n[RB], lo[RB];
-            unsigned long long ab[RB], cur[RB];  // ab = ~0: source inactive on this edge
+            for (uint32_t p0 = 0; p0 < npair; p0 += 64u * RB) {
+            uint32_t n[RB], lo[RB], jr[RB], er[RB];
+            unsigned long long ab[RB], cur[RB];  // ab = ~0: no pair in this lane
             float kz[RB];                         // kappa0 of the edge's target
             uint32_t tree[RB];
 #pragma unroll
             for (int rr = 0; rr < RB; rr++) {
-                const int r = r0 + rr;
-                const int a = (r * EPW) / 64;              // phase-A slot of this round's edges
-                const int src = (r * EPW) % 64 + (int)ge;  // lane holding the edge
-                // (shuffles only in uniform control flow: inactive source lanes read as 0)
-                const uint32_t nt = __shfl(an[a], src, 64);
-                n[rr] = nt & 0x7FFFFFFFu;
-                tree[rr] = nt >> 31;  // the h0-tree edge into n
-                const uint32_t mk = __shfl(amk[a], src, 64);
-                lo[rr] = __shfl(alo[a], src, 64);
-                const double w = __hiloint2double((int)__shfl(awh[a], src, 64),
-                                                  (int)__shfl(awl[a], src, 64));
-                const bool on = (mk >> j) & 1u;
-                ab[rr] = on ? d2bits(__dadd_rn(L.val[lo[rr] * K + j], w)) : ~0ull;
-                // pre-check: the K lanes of the edge read its target's line in one request
+                const uint32_t q = p0 + (uint32_t)rr * 64u + lane;
+                // last edge E (of UA * 64) with offset <= q (uniform shuffles, per-lane index)
+                uint32_t e = 0;
+#pragma unroll
+                for (uint32_t st = (uint32_t)UA * 32u; st >= 1u; st >>= 1) {
+                    const uint32_t c = e + st;
+                    uint32_t oc = 0;
+#pragma unroll
+                    for (int a = 0; a < UA; a++) {
+                        const uint32_t x = __shfl(po[a], (int)(c & 63u), 64);
+                        if ((c >> 6) == (uint32_t)a) oc = x;
+                    }
+                    if (oc <= q) e = c;
+                }
+                const int el = (int)(e & 63u);
+                uint32_t xn = 0, xlm = 0, xwl = 0, xwh = 0, xpb = 0, xo = 0;
+#pragma unroll
+                for (int a = 0; a < UA; a++) {
+                    const uint32_t t0 = __shfl(an[a], el, 64), t1 = __shfl(alm[a], el, 64);
+                    const uint32_t t2 = __shfl(awl[a], el, 64), t3 = __shfl(awh[a], el, 64);
+                    const uint32_t t4 = kKapInRec ? __shfl(apb[a], el, 64) : 0u;
+                    const uint32_t t5 = __shfl(po[a], el, 64);
+                    if ((e >> 6) == (uint32_t)a) {
+                        xn = t0; xlm = t1; xwl = t2; xwh = t3; xpb = t4; xo = t5;
+                    }
+                }
+                const bool on = q < npair;
+                er[rr] = on ? e : 0x10000u + lane;  // segment key (no segment across empty lanes)
+                // source: the (q - offset)-th set bit of the edge's mask
+                uint32_t mk = xlm >> 16, k = q - xo, jj = 0;
+#pragma unroll
+                for (uint32_t wdt = (uint32_t)K / 2u; wdt >= 1u; wdt >>= 1) {
+                    const uint32_t c = (uint32_t)__popc(mk & ((1u << wdt) - 1u));
+                    if (k >= c) { k -= c; jj += wdt; mk >>= wdt; }
+                }
+                jr[rr] = jj;
+                n[rr] = xn & 0x7FFFFFFFu;
+                tree[rr] = xn >> 31;  // the h0-tree edge into n
+                lo[rr] = xlm & 0xFFFFu;
+                const double w = __hiloint2double((int)xwh, (int)xwl);
+                ab[rr] = on ? d2bits(__dadd_rn(L.val[lo[rr] * K + jj], w)) : ~0ull;
+                // pre-check: the edge's pairs read its target's line in one request
                 const bool t = on && n[rr] >= D.H;
-                const unsigned long long x = D.dist[(t ? (size_t)n[rr] : (size_t)0) * K + j];
-                if (kKapInRec) kz[rr] = rec_kap0(__shfl(apb[a], src, 64));
+                const unsigned long long x = D.dist[(t ? (size_t)n[rr] : (size_t)0) * K + jj];
+                if (kKapInRec) kz[rr] = rec_kap0(xpb);
                 else kz[rr] = g.kap0[t ? n[rr] : 0u];
                 cur[rr] = t ? x : 0ull;
             }
@@ -590,8 +596,9 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             for (int rr = 0; rr < RB; rr++) {
                 bool im = false;
                 const bool on = ab[rr] != ~0ull;
+                const uint32_t jj = jr[rr];
                 if (on && n[rr] < D.H) {
-                    const size_t wi = (size_t)n[rr] * K + j;
+                    const size_t wi = (size_t)n[rr] * K + jj;
                     const unsigned long long old = atomicMin(&D.hd[wi], ab[rr]);
                     im = ab[rr] < old;
                     if (im) atomicAnd(&D.xb[wi >> 5], ~(1u << (wi & 31)));
@@ -600,42 +607,45 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                         else if (ab[rr] == old) atomicOr(&D.tb[wi >> 5], 1u << (wi & 31));
                     }
                 } else if (on && ab[rr] <= cur[rr]) {
-                    // the edge's K lanes: one coalesced atomic request per line.  Returning, so
+                    // the edge's pairs: one coalesced atomic request per line.  Returning, so
                     // that exactly one relaxation per value counts as its improver and every
                     // other one producing the same value as a tie (tie bit): "no tie bit" then
-                    // certifies a unique parent candidate for the parent pass.
-                    const size_t wi = (size_t)n[rr] * K + j;
+                    // certifies a unique parent candidate for the parent pass.  The improver is
+                    // the parent pass' second guess (a later improver's hint may be overwritten
+                    // by an earlier one's store: the pass verifies tightness; the h0-tree edge
+                    // needs no record: it is the pass' first guess)
+                    const size_t wi = (size_t)n[rr] * K + jj;
                     const unsigned long long old = atomicMin(&D.dist[wi], ab[rr]);
                     im = ab[rr] < old;
                     if (ab[rr] == old) atomicOr(&D.tie[wi >> 5], 1u << (wi & 31));
-                    // the improver as the parent pass' second guess (a later improver's hint may
-                    // be overwritten by an earlier one's store: the pass verifies tightness)
-                    // (the h0-tree edge needs no record: it is the pass' first guess)
                     if (SHD_TAIL_HINT && im && !tree[rr]) D.tpar[wi] = L.vx[lo[rr]];
                     cur[rr] = old;
                 }
                 bool nr = false, nf = false;
                 if (im) {
-                    const uint32_t b = bkt(bits2d(ab[rr]), shj, B.inv_delta);
-                    // a tail whose kappa-prefix is empty for this distance would expand no
-                    // edge (every one fails the landmark filter): settled without a queue entry
-                    if (b <= B.cb) nr = n[rr] < D.H || kappa_useful(kz[rr], L.dh0[j],
+                    const uint32_t b = bkt(bits2d(ab[rr]), L.sh[jj], B.inv_delta);
+                    if (b <= B.cb) nr = n[rr] < D.H || kappa_useful(kz[rr], L.dh0[jj],
                                                                     bits2d(ab[rr]), g.piMax);
                     else {
                         fm = b < fm ? b : fm;
-                        // a tail pair reached for the first time past cb: its vertex joins the
-                        // next sweep (later far improvements of a pending pair need no mark)
                         nf = cur[rr] == kInfBits;
                     }
                 }
-                const unsigned long long balf = __ballot(nf);
-                if (j == 0 && ((balf >> (ge * K)) & MO::kFull))
-                    (void)atomicOr(&D.pend[n[rr] >> 5], 1u << (n[rr] & 31));
-                // the edge's near bits -> one mask OR by its first lane
-                const unsigned long long bal = __ballot(nr);
-                const uint32_t gm = (uint32_t)(bal >> (ge * K)) & MO::kFull;
+                // the edge's pairs sit in adjacent lanes (<= K of them): their near bits and
+                // first-reach flags are OR-ed into the segment's first lane, which does the
+                // edge's pend and mask atomics once
+                uint32_t gm = nr ? 1u << jj : 0u, gf = nf ? 1u : 0u;
+#pragma unroll
+                for (int o = 1; o < K; o <<= 1) {
+                    const uint32_t ym = __shfl_down(gm, o, 64), yf = __shfl_down(gf, o, 64);
+                    const uint32_t ye = __shfl_down(er[rr], o, 64);
+                    if (lane + (uint32_t)o < 64u && ye == er[rr]) { gm |= ym; gf |= yf; }
+                }
+                const uint32_t pe = __shfl_up(er[rr], 1, 64);
+                const bool head = on && (lane == 0 || pe != er[rr]);
+                if (head && gf) (void)atomicOr(&D.pend[n[rr] >> 5], 1u << (n[rr] & 31));
                 bool first = false, hfirst = false;
-                if (j == 0 && gm) {
+                if (head && gm) {
                     if (n[rr] < D.H) hfirst = MO::set(hdef, n[rr], gm) == 0u;
                     else first = MO::set(mnxt, n[rr], gm) == 0u;
                 }
@@ -647,6 +657,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 fm = wave_min_u32(fm);
                 if (lane == 0) atomicMin(&L.fminb, fm);
             }
+            BT_TICK(2);
         }
         if (WAVE) {
             // the next sub-chunk overwrites this wave's slice: its lanes' LDS reads are done
@@ -762,6 +773,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     if (tid < 4) L.cnt[tid] = 0;
     if (tid < 5) L.pt[tid] = 0;
     if (tid < 4) L.dg[tid] = 0;
+    if (tid < 8) L.bt[tid] = 0;
     unsigned long long tk = wall_clock64();
 
     for (;;) {
@@ -1402,6 +1414,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         atomicAdd(&stats[ST_EV0 + 5], 0ull);
         atomicAdd(&stats[ST_EV0 + 5], n_par);
         for (int i = 0; i < 4; i++) atomicAdd(&stats[ST_PT0 + i], L.pt[1 + i]);
+        if (SHD_BATCH_TIME)
+            for (int i = 0; i < 8; i++) atomicAdd(&stats[ST_BT0 + i], L.bt[i]);
     }
 }
 

@@ -59,6 +59,13 @@ for rep in range(args.reps):
           tuple(x / rows for x in st["parent_phase_ms"]), flush=True)
     print("   split ms/src %.2f  far-scan sources %d" % (st["split_ms"] / rows,
                                                       st["far_scan_sources"]), flush=True)
+    if any(st["batch_wave_ms"]):
+        w = st["batch_wave_ms"]
+        print("   wave ms/src (SHD_BATCH_TIME): tail chunk %.2f A %.2f B %.2f | hub chunk %.2f A %.2f "
+              "B %.2f | phase-B rounds/src %.0f pairs/src %.0f (%.2f per round)" % tuple(
+                  [x / rows for x in w] + [st["batch_rounds"] / rows, st["batch_edges_b"] / rows,
+                                           st["batch_edges_b"] / max(1, st["batch_rounds"])]),
+              flush=True)
     print("   per-source events:", {k: "%.3g" % (v / rows) for k, v in st["events"].items()},
           flush=True)
 x = lr[..., 0].cpu().numpy()
