@@ -47,7 +47,7 @@ namespace {
 using namespace dev;
 
 #ifndef SHD_BATCH_RB
-#define SHD_BATCH_RB 4  // transposed relaxation: rounds whose loads are in flight together
+#define SHD_BATCH_RB 2  // phase-B rounds whose loads are in flight together (pair rounds: 2 < 3 < 4 by 1-4 %, 8 spills)
 #endif
 #ifndef SHD_BATCH_SPEC
 #define SHD_BATCH_SPEC 1  // buckets past cb whose hub sources join a hub expansion speculatively
