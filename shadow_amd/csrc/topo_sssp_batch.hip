@@ -356,13 +356,13 @@ __device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t
     if (lane < K) L.dh0[lane] = bits2d(D.get(0u, lane));  // any value read is a valid bound
     if (lane < cnt) {
         const uint32_t v = qv;  // this lane's queue entry (loaded by the caller)
+        // every load of the vertex in one round trip: its mask (a queued vertex's is almost
+        // never empty), row bounds, kappa probes and K distances
         const uint32_t m = MO::get_l2(mcur, v);
-        mcur[v] = 0;
         const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
-        deg = m ? r1 - r0 : 0u;
-        if (deg) {
-            const float4 ks = g.ksum[v];
-            double dv[K];
+        const float4 ks = g.ksum[v];
+        double dv[K];
+        {
             typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
             const u64x2* p = reinterpret_cast<const u64x2*>(D.dist + (size_t)v * K);
 #pragma unroll
@@ -371,6 +371,10 @@ __device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t
                 dv[2 * h] = bits2d(x.x);
                 dv[2 * h + 1] = bits2d(x.y);
             }
+        }
+        mcur[v] = 0;
+        deg = m ? r1 - r0 : 0u;
+        if (deg) {
             double T = -INFINITY;
 #pragma unroll
             for (int jj = 0; jj < K; jj++) {
