@@ -43,6 +43,7 @@ def test_sssp_synthetic_table(integer, hubs, batch):
     top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
     top.set_option("lds_hubs", hubs)
     top.set_option("batch", batch)
+    top.set_option("batch_fill", batch)  # whole batches (auto would run 1 source per slot here)
     otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()
@@ -89,6 +90,7 @@ def test_sssp_batch_widths(batch):
     """Every batch width settles the same table (ragged last batch included: A % K != 0)."""
     top, g = synthetic_pair(seed=17, n_routers=2000, n_poi=101, n_edges=20000)
     top.set_option("batch", batch)
+    top.set_option("batch_fill", batch)
     otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()
@@ -103,8 +105,9 @@ def test_sssp_batch_widths(batch):
 @pytest.mark.parametrize("fill", [0, 1, 3, 5, 8])
 @pytest.mark.parametrize("integer", [False, True])
 def test_sssp_batch_fill(fill, integer):
-    """Batches filled below K (option batch_fill; 0 = auto, which fills ceil(A / slots) here)
-    settle the same table: idle lanes, the ragged last batch and the batch order by mean pi."""
+    """Batches filled below K (option batch_fill; 0 = auto, which fills ceil(A / slots) here:
+    a slot per source for this short table) settle the same table: idle lanes, the ragged last
+    batch and the batch order by mean pi."""
     top, g = synthetic_pair(seed=19, n_routers=2000, n_poi=101, n_edges=20000, integer=integer)
     top.set_option("batch_fill", fill)
     otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay", "server"])
@@ -112,6 +115,10 @@ def test_sssp_batch_fill(fill, integer):
     st = top.stats()
     assert st["errors"] == 0
     assert st["batch_fill"] == (fill if fill else min(8, -(-len(a) // st["slots"])))
+    if fill == 0:  # a fresh workspace gets a slot per source (up to the CUs), not per batch of K
+        import torch
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        assert st["slots"] == min(len(a), cus)
     oa, olat, orel, ohops = g.table(verts)
     assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
@@ -360,6 +367,7 @@ def test_sssp_batch_peripheral_landmark(hubs):
     assert not top.is_complete
     top.set_option("lds_hubs", hubs)
     top.set_option("batch", 8)
+    top.set_option("batch_fill", 8)
     otop, ips, verts = attach_hosts(top, g, 60, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()

@@ -55,6 +55,7 @@ def test_integer_ties_table_bit_exact(batch):
     bit-exact against the oracle; the tie rows went through the replay."""
     top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=True)
     top.set_option("batch", batch)
+    top.set_option("batch_fill", batch)
     otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()
