@@ -592,7 +592,7 @@ int upload_csr(Topology* top) {
         // finds from 4 per-vertex probes (kappa at row positions 0, 1, 3, 7) and, past those,
         // a binary search in d_kap.  kappa is stored rounded down, so a cut is never too early.
         std::vector<uint32_t> adjk(4 * nadj);
-        std::vector<float> kap(nadj), ksum(4 * (size_t)V);
+        std::vector<float> kap(nadj), ksum(kKProbes * (size_t)V);
         std::vector<uint32_t> ord;
         std::vector<double> kd;
         auto down = [](double x) {
@@ -621,15 +621,15 @@ int upload_csr(Topology* top) {
                 if (top->sptPar[col[k]] == (uint32_t)v) adjk[4 * (size_t)(b + i)] |= 0x80000000u;
                 kap[b + i] = down(kd[k - b]);
             }
-            static const uint32_t probe[4] = {0, 1, 3, 7};
-            for (int q = 0; q < 4; q++)
-                ksum[4 * (size_t)v + q] = probe[q] < e - b ? kap[b + probe[q]] : INFINITY;
+            static const uint32_t probe[8] = {0, 1, 3, 7, 15, 31, 63, 127};
+            for (int q = 0; q < kKProbes; q++)
+                ksum[kKProbes * (size_t)v + q] = probe[q] < e - b ? kap[b + probe[q]] : INFINITY;
         }
         top->piMax = 0.0;
         for (double p : top->pot) if (std::isfinite(p)) top->piMax = std::max(top->piMax, p);
         HIPCHK(top->d_adjk.ensure(4 * nadj));
         HIPCHK(top->d_kap.ensure(nadj));
-        HIPCHK(top->d_ksum.ensure(4 * (size_t)V));
+        HIPCHK(top->d_ksum.ensure(kKProbes * (size_t)V));
         HIPCHK(top->d_kap0.ensure((size_t)V));
         {
             std::vector<uint32_t> spt(4 * (size_t)V, 0xFFFFFFFFu);
@@ -648,11 +648,11 @@ int upload_csr(Topology* top) {
                              hipMemcpyHostToDevice));
         }
         std::vector<float> k0((size_t)V);
-        for (int32_t v = 0; v < V; v++) k0[(size_t)v] = ksum[4 * (size_t)v];
+        for (int32_t v = 0; v < V; v++) k0[(size_t)v] = ksum[kKProbes * (size_t)v];
         HIPCHK(hipMemcpy(top->d_kap0.p, k0.data(), sizeof(float) * (size_t)V, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_adjk.p, adjk.data(), sizeof(uint32_t) * 4 * nadj, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_kap.p, kap.data(), sizeof(float) * nadj, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_ksum.p, ksum.data(), sizeof(float) * 4 * (size_t)V, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_ksum.p, ksum.data(), sizeof(float) * kKProbes * (size_t)V, hipMemcpyHostToDevice));
     }
     HIPCHK(hipMemcpy(top->d_vloss.p, vloss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(top->d_selfLat.p, selfLat.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));

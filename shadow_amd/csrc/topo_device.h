@@ -38,6 +38,13 @@ constexpr int kNearPerVertex = 2; // near-queue capacity per slot, in entries pe
 // down} (high, low half), so the batch relaxation gets the target's kappa0 with the record
 // instead of a random 4-B load per surviving edge; 0: f32 pi(col) rounded up, kappa0 from g.kap0
 constexpr bool kKapInRec = SHD_KAP_IN_REC != 0;
+#ifndef SHD_KPROBES
+#define SHD_KPROBES 8
+#endif
+// kappa probes per vertex (4 or 8): the batch kernel's cut of a kappa-sorted row needs a
+// binary search (dependent loads) only past the last probe
+constexpr int kKProbes = SHD_KPROBES;
+static_assert(kKProbes == 4 || kKProbes == 8, "kappa probes");
 
 // indices into the device stats block (unsigned long long[16])
 enum StatIdx {
@@ -88,7 +95,8 @@ struct DevCSR {
     const uint32_t* adj = nullptr;  // 16-B AdjRec {u32 col, f32 pi(col) rounded up, f64 wt}
     const uint32_t* adjk = nullptr; // the same records, each row sorted by kappa = w - pi(col)
     const float* kap = nullptr;     // kappa of adjk (f32 rounded down; -inf: pi unknown)
-    const float4* ksum = nullptr;   // per vertex: kappa at row positions 0, 1, 3, 7 (+inf past it)
+    const float4* ksum = nullptr;   // per vertex: kappa at row positions 0, 1, 3, 7[, 15, 31, 63,
+                                    // 127] (kKProbes floats, +inf past the row)
     const float* kap0 = nullptr;    // per vertex: smallest kappa of its row (+inf: empty row)
     const uint32_t* spt = nullptr;  // per vertex {h0-tree parent, its slot of (parent, v), f64 w}
     double piMax = 0.0;             // largest finite pi

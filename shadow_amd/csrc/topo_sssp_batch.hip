@@ -176,6 +176,29 @@ struct BBuckets {
     uint32_t cb;  // the bucket being settled
 };
 
+// End of the kappa-sorted row prefix that can pass threshold T: the first probe position
+// (0, 1, 3, 7[, 15, 31, 63, 127]) whose kappa exceeds T (an upper bound: the edges before it are
+// filtered per source in phase A), else a binary search past the last probe (long rows only).
+__device__ __forceinline__ uint32_t kappa_cut(const DevCSR& g, float4 ks0, float4 ks1, double T,
+                                              uint32_t r0, uint32_t deg) {
+    if ((double)ks0.x > T) return 0;
+    if ((double)ks0.y > T) return 1;
+    if ((double)ks0.z > T) return 3;
+    if ((double)ks0.w > T) return 7;
+    if (kKProbes > 4) {
+        if ((double)ks1.x > T) return 15;
+        if ((double)ks1.y > T) return 31;
+        if ((double)ks1.z > T) return 63;
+        if ((double)ks1.w > T) return 127;
+    }
+    uint32_t lo = kKProbes > 4 ? 128u : 8u, hi = deg;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((double)g.kap[r0 + mid] > T) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
 // One chunk of a near queue: take each vertex's source mask (clearing it), its row bounds and
 // its K distances (K lanes per vertex read its line once) into LDS; a block scan of the degrees
 // flattens the chunk's edges.  Returns the chunk's edge count (uniform); ends with a barrier.
@@ -219,7 +242,8 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
         const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
         deg = m ? r1 - r0 : 0u;
         if (CUT && deg) {
-            const float4 ks = g.ksum[v];
+            const float4 ks0 = g.ksum[kKProbes / 4 * (size_t)v];
+            const float4 ks1 = kKProbes > 4 ? g.ksum[kKProbes / 4 * (size_t)v + 1] : ks0;
             double dv[K];
             if (v < D.H) {
 #pragma unroll
@@ -245,19 +269,7 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
                 const double t = (h - dv[jj]) + 1e-5 * (h + dv[jj] + g.piMax) + 1e-9;
                 T = t > T ? t : T;
             }
-            uint32_t c;
-            if ((double)ks.x > T) c = 0;
-            else if ((double)ks.y > T) c = 1;
-            else if ((double)ks.z > T) c = 3;
-            else if ((double)ks.w > T) c = 7;
-            else {
-                uint32_t lo = 8, hi = deg;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if ((double)g.kap[r0 + mid] > T) hi = mid; else lo = mid + 1;
-                }
-                c = lo;
-            }
+            const uint32_t c = kappa_cut(g, ks0, ks1, T, r0, deg);
             deg = c < deg ? c : deg;
         }
         act = (unsigned long long)deg * (unsigned long long)__popc(m);
@@ -360,7 +372,8 @@ __device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t
         // never empty), row bounds, kappa probes and K distances
         const uint32_t m = MO::get_l2(mcur, v);
         const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
-        const float4 ks = g.ksum[v];
+        const float4 ks0 = g.ksum[kKProbes / 4 * (size_t)v];
+        const float4 ks1 = kKProbes > 4 ? g.ksum[kKProbes / 4 * (size_t)v + 1] : ks0;
         double dv[K];
         {
             typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
@@ -384,19 +397,7 @@ __device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t
                 const double t = (h - dv[jj]) + 1e-5 * (h + dv[jj] + g.piMax) + 1e-9;
                 T = t > T ? t : T;
             }
-            uint32_t c;
-            if ((double)ks.x > T) c = 0;
-            else if ((double)ks.y > T) c = 1;
-            else if ((double)ks.z > T) c = 3;
-            else if ((double)ks.w > T) c = 7;
-            else {
-                uint32_t lo = 8, hi = deg;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if ((double)g.kap[r0 + mid] > T) hi = mid; else lo = mid + 1;
-                }
-                c = lo;
-            }
+            const uint32_t c = kappa_cut(g, ks0, ks1, T, r0, deg);
             deg = c < deg ? c : deg;
         }
         act = (unsigned long long)deg * (unsigned long long)__popc(m);
