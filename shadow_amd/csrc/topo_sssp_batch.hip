@@ -958,9 +958,13 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 uint32_t* cl = sv + kSsspBlock;                           // compacted vertices
                 constexpr uint32_t kCl = (uint32_t)(sizeof(L.val) / 4) - kSsspBlock;
                 static_assert(kCl >= 256, "sweep compaction buffer");
+                // the next round's bitmap word is loaded before this round's chain (a sweep does
+                // not race with relaxations: rounds only rewrite their own words)
+                uint32_t nword = H / 32 + tid < pw ? ld_l2_u32(&D.pend[H / 32 + tid]) : 0u;
                 for (uint32_t wb = H / 32; wb < pw; wb += kSsspBlock) {
                     const uint32_t wi = wb + tid;
-                    const uint32_t word = wi < pw ? ld_l2_u32(&D.pend[wi]) : 0u;
+                    const uint32_t word = nword;
+                    nword = wi + kSsspBlock < pw ? ld_l2_u32(&D.pend[wi + kSsspBlock]) : 0u;
                     sv[tid] = 0u;
                     uint32_t tot;
                     const uint32_t off = block_excl_scan<kSsspBlock>((uint32_t)__popc(word), L.wave,
