@@ -1194,12 +1194,36 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     K, top->hubLimit, (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 20)),
                     top->g.V);
                 top->stats.lds_hubs = bp.H;
+                // diagnostic: SHD_BATCH_TRACE=<file> appends per batch {start tick, end tick,
+                // slot, near iterations, sweeps, expansions, relaxations, sources}, then per
+                // batch position {source vertex, pi bits}
+                const char* btf = getenv("SHD_BATCH_TRACE");
+                const int64_t nbt = (rows + kf - 1) / kf;
+                if (btf && *btf) HIPCHK(hipMalloc((void**)&ws.btrace, 64 * (size_t)nbt));
                 HIPCHK(launch_sssp_batch(K, dev_csr(top), ws, top->d_sources.p,
                                          top->d_srcsh.p, (int)rows, kf, top->d_targets.p, (int)A,
                                          delta, bp, (uint32_t)top->farCap, out_lr, out_hops,
                                          out_rowmin, top->d_stats.p, st));
                 HIPCHK(hipEventRecord(top->ev1, st));
                 HIPCHK(hipStreamSynchronize(st));  // sh must outlive the async copy
+                if (ws.btrace) {
+                    std::vector<unsigned long long> bt((size_t)nbt * 8);
+                    HIPCHK(hipMemcpy(bt.data(), ws.btrace, 64 * (size_t)nbt, hipMemcpyDeviceToHost));
+                    HIPCHK(hipFree(ws.btrace));
+                    ws.btrace = nullptr;
+                    if (FILE* f = fopen(btf, "ab")) {
+                        const int64_t hdr[4] = {nbt, kf, (int64_t)ws.slots, rows};
+                        fwrite(hdr, 8, 4, f);
+                        fwrite(bt.data(), 8, bt.size(), f);
+                        for (int64_t i = 0; i < rows; i++) {
+                            const double p = top->pot[(size_t)psrc[(size_t)i]];
+                            const int64_t rec[2] = {(int64_t)psrc[(size_t)i], 0};
+                            fwrite(rec, 8, 1, f);
+                            fwrite(&p, 8, 1, f);
+                        }
+                        fclose(f);
+                    }
+                }
             } else {
                 top->stats.lds_hubs = lds_plan(top).H;
                 HIPCHK(launch_sssp_rows(dev_csr(top), ws, top->d_sources.p, (int)rows,

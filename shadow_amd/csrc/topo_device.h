@@ -142,6 +142,8 @@ struct SlotWs {
     // batch kernel: output row of batch position p (sources are taken in a locality order, the
     // table keeps row order); nullptr = identity
     const uint32_t* rowmap = nullptr;
+    // diagnostic (SHD_BATCH_TRACE): per batch {wall_clock64 at dequeue, at its end, slot}
+    unsigned long long* btrace = nullptr;
 };
 
 // Incidence-order CSR of the heap replay (topo_replay.hip), relabelled vertex ids: row x holds

@@ -792,6 +792,12 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         const int r0 = (int)bidx * kf;
         const int nk = min(kf, nsrc - r0);
         tk = wall_clock64();
+        const unsigned long long bt_near = n_near, bt_sweep = n_sweep, bt_exp = n_expand,
+                                 bt_rel = L.cnt[0];
+        if (ws.btrace && tid == 0) {
+            ws.btrace[8 * (size_t)bidx] = tk;
+            ws.btrace[8 * (size_t)bidx + 2] = (unsigned long long)slot;
+        }
 
         // ---------------- init: hubs in LDS, the tail's K-wide rows in HBM --------------------
         for (uint32_t i = tid; i < H * K; i += kSsspBlock) D.hd[i] = kInfBits;
@@ -1399,6 +1405,15 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         }
         __syncthreads();
         { unsigned long long t = wall_clock64(); t_tgt += t - tk; tk = t; }
+        if (ws.btrace && tid == 0) {
+            unsigned long long* b = ws.btrace + 8 * (size_t)bidx;
+            b[1] = tk;
+            b[3] = n_near - bt_near;
+            b[4] = n_sweep - bt_sweep;
+            b[5] = n_expand - bt_exp;
+            b[6] = L.cnt[0] - bt_rel;
+            b[7] = (unsigned long long)nk;
+        }
     }
     if (tid == 0) {
         ctr[0] = iter;
