@@ -190,6 +190,11 @@ struct _Topology {
                               // batch that finish the rows in the same rounds of the slots)
     int batchOrder = 2;       // option "batch_order": 0 grouped order, 1 shuffled, 2 / 3 by mean
                               // pi descending / ascending
+    bool targetSkip = true;   // option "target_skip": target bits in the relaxation copy; pairs
+                              // into non-target tail vertices that would expand nothing are
+                              // dropped (topo_sssp_batch.hip)
+    std::vector<uint32_t> adjkTargets;  // the target set whose bits d_adjk carries
+    bool adjkFlagged = false;
     DevBuf<uint32_t> d_rowmap;
     bool replayUploaded = false;
     DevBuf<uint32_t> d_rrow;
@@ -651,6 +656,8 @@ int upload_csr(Topology* top) {
         for (int32_t v = 0; v < V; v++) k0[(size_t)v] = ksum[kKProbes * (size_t)v];
         HIPCHK(hipMemcpy(top->d_kap0.p, k0.data(), sizeof(float) * (size_t)V, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_adjk.p, adjk.data(), sizeof(uint32_t) * 4 * nadj, hipMemcpyHostToDevice));
+        top->adjkFlagged = false;  // no target bits yet (set per target set before a batch launch)
+        top->adjkTargets.clear();
         HIPCHK(hipMemcpy(top->d_kap.p, kap.data(), sizeof(float) * nadj, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_ksum.p, ksum.data(), sizeof(float) * kKProbes * (size_t)V, hipMemcpyHostToDevice));
     }
@@ -684,6 +691,7 @@ DevCSR dev_csr(Topology* top) {
     c.selfLat = top->d_selfLat.p;
     c.selfLoss = top->d_selfLoss.p;
     c.rows_sorted = top->rowsSorted ? 1 : 0;
+    c.tflags = top->adjkFlagged && top->targetSkip ? 1 : 0;
     return c;
 }
 
@@ -1071,6 +1079,16 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             HIPCHK(hipMemsetAsync(top->d_rowflag.p, 0, (size_t)rows, st));
             SlotWs ws = slot_ws(top);
             ws.rowflag = top->d_rowflag.p;
+            if (K > 1 && top->targetSkip && top->g.V < (1 << 30) && top->adjkTargets != tgt) {
+                // bit 30 of the relaxation copy's columns: the current target set
+                r = upload_target_bits(top, tgt, st);
+                if (r) return r;
+                HIPCHK(launch_mark_targets(top->d_adjk.p, (int64_t)(top->d_adjk.n / 4),
+                                           top->d_tbits.p, st));
+                HIPCHK(hipStreamSynchronize(st));
+                top->adjkTargets = tgt;
+                top->adjkFlagged = true;
+            }
             if (K > 1) {
                 // Batches of K sources settle in lock-step and share an expansion when their
                 // shifted distances to a vertex fall in one bucket: sources whose shortest paths
@@ -1454,6 +1472,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->sourceOrder = top->sourceOrder;
     p->batchOrder = top->batchOrder;
     p->batchFill = top->batchFill;
+    p->targetSkip = top->targetSkip;
     p->attached = top->attached;
     p->colOf = top->colOf;
     p->A = top->A;
@@ -2020,6 +2039,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "source_order") top->sourceOrder = (int)value;
     else if (k == "batch_order") top->batchOrder = (int)value;
     else if (k == "batch_fill") top->batchFill = (int)value;
+    else if (k == "target_skip") top->targetSkip = value != 0;
     else if (k == "devices") {
         const int n = (int)value;
         if (n < 1 || n > 64) return -1;

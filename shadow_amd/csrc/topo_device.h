@@ -105,6 +105,9 @@ struct DevCSR {
     const double* selfLat = nullptr;
     const double* selfLoss = nullptr;
     int rows_sorted = 0;  // adjacency rows ascending by neighbour (enables binary row search)
+    // bit 30 of adjk's column word marks an attached vertex (a table target); the batch
+    // relaxation then skips pairs into non-target tail vertices that would expand nothing
+    int tflags = 0;
 };
 
 // per-slot workspace, slot-major: array + slot * V
@@ -201,6 +204,9 @@ hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d
 // lock-step over buckets of d + srcsh[row] (srcsh >= 2 delta).  plan from sssp_batch_lds_plan.
 // kf (1..K): sources per batch (batch b = positions [b kf, b kf + kf)).
 SsspLdsPlan sssp_batch_lds_plan(int K, int64_t hub_limit, uint32_t par_hubs, int64_t V);
+// bit 30 of every adjk column word := the column is set in tbits (the attached vertices)
+hipError_t launch_mark_targets(uint32_t* adjk, int64_t nadj, const uint32_t* tbits,
+                               hipStream_t stream);
 hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                              const double* d_srcsh, int nsrc, int kf, const uint32_t* d_targets, int A,
                              double delta, const SsspLdsPlan& plan, uint32_t far_cap,

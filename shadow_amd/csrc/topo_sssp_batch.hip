@@ -575,8 +575,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                         xn = t0; xlm = t1; xwl = t2; xwh = t3; xpb = t4; xo = t5;
                     }
                 }
-                const bool on = q < npair;
-                er[rr] = on ? e : 0x10000u + lane;  // segment key (no segment across empty lanes)
+                bool on = q < npair;
                 // source: the (q - offset)-th set bit of the edge's mask
                 uint32_t mk = xlm >> 16, k = q - xo, jj = 0;
 #pragma unroll
@@ -585,16 +584,28 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     if (k >= c) { k -= c; jj += wdt; mk >>= wdt; }
                 }
                 jr[rr] = jj;
-                n[rr] = xn & 0x7FFFFFFFu;
+                n[rr] = xn & (g.tflags ? 0x3FFFFFFFu : 0x7FFFFFFFu);
                 tree[rr] = xn >> 31;  // the h0-tree edge into n
                 lo[rr] = xlm & 0xFFFFu;
                 const double w = __hiloint2double((int)xwh, (int)xwl);
-                ab[rr] = on ? d2bits(__dadd_rn(L.val[lo[rr] * K + jj], w)) : ~0ull;
+                const double abd = __dadd_rn(L.val[lo[rr] * K + jj], w);
+                if (kKapInRec) kz[rr] = rec_kap0(xpb);
+                // A tail vertex that is no table target and would expand nothing at this
+                // candidate (kappa0 above the landmark threshold, the test that keeps it out of
+                // the near queue) needs no distance at all: only targets and the vertices of
+                // their parent chains are read after the SSSP, and a chain vertex is expanded at
+                // its final distance (its chain edge passes the filter), so every relaxation that
+                // sets or ties its final value passes this test (a larger, stale d_j(h0) only
+                // widens it).  The pair is dropped before its pre-check load and atomics.
+                if (kKapInRec && g.tflags && on && n[rr] >= D.H && !((xn >> 30) & 1u) &&
+                    !kappa_useful(kz[rr], L.dh0[jj], abd, g.piMax))
+                    on = false;
+                er[rr] = on ? e : 0x10000u + lane;  // segment key (no segment across empty lanes)
+                ab[rr] = on ? d2bits(abd) : ~0ull;
                 // pre-check: the edge's pairs read its target's line in one request
                 const bool t = on && n[rr] >= D.H;
                 const unsigned long long x = D.dist[(t ? (size_t)n[rr] : (size_t)0) * K + jj];
-                if (kKapInRec) kz[rr] = rec_kap0(xpb);
-                else kz[rr] = g.kap0[t ? n[rr] : 0u];
+                if (!kKapInRec) kz[rr] = g.kap0[t ? n[rr] : 0u];
                 cur[rr] = t ? x : 0ull;
             }
 #pragma unroll
@@ -1441,6 +1452,26 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         if (SHD_BATCH_TIME)
             for (int i = 0; i < 8; i++) atomicAdd(&stats[ST_BT0 + i], L.bt[i]);
     }
+}
+
+__global__ void mark_targets_kernel(uint32_t* __restrict__ adjk, int64_t nadj,
+                                    const uint32_t* __restrict__ tbits) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nadj;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = adjk[kAdjWords * k];
+        const uint32_t v = c & 0x3FFFFFFFu;
+        const uint32_t t = (tbits[v >> 5] >> (v & 31u)) & 1u;
+        adjk[kAdjWords * k] = (c & ~0x40000000u) | (t << 30);
+    }
+}
+
+hipError_t launch_mark_targets(uint32_t* adjk, int64_t nadj, const uint32_t* tbits,
+                               hipStream_t stream) {
+    if (nadj <= 0) return hipSuccess;
+    const int64_t g = std::min<int64_t>((nadj + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(mark_targets_kernel, dim3((unsigned)g), dim3(256), 0, stream, adjk, nadj,
+                       tbits);
+    return hipGetLastError();
 }
 
 SsspLdsPlan sssp_batch_lds_plan(int K, int64_t hub_limit, uint32_t par_hubs, int64_t V) {

@@ -9,7 +9,7 @@ import pytest
 
 import oracle
 import shadow_amd as sa
-from helpers import attach_hosts, bundled_pair, rel_close, synthetic_pair
+from helpers import attach_hosts, bundled_pair, host_ip, rel_close, synthetic_pair
 
 pytestmark = pytest.mark.gpu
 
@@ -61,6 +61,37 @@ def test_sssp_synthetic_table(integer, hubs, batch):
     assert np.array_equal(hops, ohops.astype(np.uint16))
     assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
     assert top.getMinimumLatency() == olat.min()
+
+
+@pytest.mark.parametrize("integer", [False, True])
+def test_target_skip_exact_across_target_sets(integer):
+    """The batch relaxation drops pairs into non-target tail vertices that would expand nothing
+    (target bits in the relaxation copy).  Tables with the skip on equal the oracle and the
+    skip-off tables bit for bit, before and after a late attach changes the target set (the
+    bits are re-marked)."""
+    tops = []
+    for skip in (1, 0):
+        top, g = synthetic_pair(seed=17, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
+        top.set_option("target_skip", skip)
+        top.set_option("batch_fill", 8)
+        tops.append(top)
+    verts = []
+    st = 1
+    for lo, hi in ((0, 120), (120, 300)):  # second round: a late attach of new hosts
+        for k in range(lo, hi):
+            st = (st * 1103515245 + 12345) & 0xFFFFFFFF
+            th = ("client", "relay")[k % 2]
+            got = {top.attach_ip(host_ip(k + 1), st, typeHint=th) for top in tops}
+            assert len(got) == 1
+            verts.append(got.pop()[0])
+        oa, olat, orel, ohops = g.table(verts)
+        for top in tops:
+            a, lat, rel, hops = top.table()
+            assert np.array_equal(a, oa)
+            assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+            assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+            assert np.array_equal(hops, ohops.astype(np.uint16))
+        assert len(oa) > 0
 
 
 @pytest.mark.parametrize("which", ["far", "near"])
