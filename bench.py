@@ -164,8 +164,8 @@ def main():
                     help="C4-int variant (integer latencies U{1..100}: heavy parent ties)")
     ap.add_argument("--batch", type=int, default=8,
                     help="sources per SSSP workgroup (1 = single-source sssp_rows_kernel)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02i_sssp_pmc.json"))
-    ap.add_argument("--route-pmc-json", default=os.path.join(ROOT, "profiles", "r02i_route_pmc.json"))
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02k_sssp_pmc.json"))
+    ap.add_argument("--route-pmc-json", default=os.path.join(ROOT, "profiles", "r02k_route_pmc.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -331,7 +331,12 @@ def main():
                         units_per_launch=rows, bytes_per_unit=b_src, pmc=pmc_note)
         sssp = dict(kernel=kname, batch=K, lds_hubs=int(st["lds_hubs"]), sweeps=sweeps,
                     sweep_bytes=sweep_bytes, slots=st["slots"],
-                    phase_ms_per_source=[round(x / max(1, rows), 3) for x in st["phase_ms"]])
+                    phase_ms_per_source=[round(x / max(1, rows), 3) for x in st["phase_ms"]],
+                    # once per (graph, target set), in the warmup build: target bits and the
+                    # target-aware kappa fixpoint in the relaxation copy (outside the timed steps,
+                    # like the CSR upload and the h0 distances)
+                    target_prep_ms=round(float(st["target_prep_ms"]), 2),
+                    target_kappa_iters=int(st["target_kappa_iters"]))
         r_ms = float(np.mean(route_ms))
         route_roof = dict(bound="hbm", kernel="packet_route_kernel", kernel_ms=round(r_ms, 4),
                           achieved=round(n * 53 / (r_ms / 1e3) / 1e9, 1), peak=HBM_PEAK_GBS,

@@ -114,7 +114,10 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * with one device), "batch" (sources per SSSP workgroup: 8; 2 / 4 / 16; 1 = single-source
  * kernel), "batch_fill" (sources per batch, <= batch; 0 = auto: the fewest that finish the rows
  * in the same rounds of the slots), "source_order" / "batch_order" (row grouping and batch
- * dequeue order).  Returns 0 or -1 for an unknown key / bad value. */
+ * dequeue order), "target_skip" (1: the batch relaxation drops pairs into
+ * non-target vertices that would relax nothing reaching a target), "target_kappa" (iterations of
+ * the target-aware kappa fixpoint behind that test, 0 = the row's smallest kappa; default 12).
+ * Returns 0 or -1 for an unknown key / bad value. */
 int shdtopo_set_option(Topology* top, const char* key, double value);
 
 /* attach by raw IP and a rand_r state (same algorithm and RNG use as topology_attach) */
@@ -220,6 +223,10 @@ typedef struct {
                                    loads, phase A, phase B, then the same for hub iterations */
     int64_t batch_rounds;       /*   phase-B rounds and the (edge, source) pairs that reached phase B */
     int64_t batch_edges_b;
+    int64_t target_kappa_iters; /* iterations of the target-aware kappa fixpoint of the last target
+                                   set (option "target_kappa") */
+    double target_prep_ms;      /* wall time of that target-set preparation (target bits + kappa
+                                   fixpoint in the relaxation copy; once per target set) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -42,7 +42,8 @@ class ShdStats(ctypes.Structure):
                 ("replay_sink_rounds", i64), ("replay_heap_sum", i64),
                 ("replay_sink_ms", dbl * 3), ("replay_pf_hits", i64),
                 ("replay_skips", i64), ("tie_dense", i64),
-                ("batch_wave_ms", dbl * 6), ("batch_rounds", i64), ("batch_edges_b", i64)]
+                ("batch_wave_ms", dbl * 6), ("batch_rounds", i64), ("batch_edges_b", i64),
+                ("target_kappa_iters", i64), ("target_prep_ms", dbl)]
 
 
 class ShdSynthParams(ctypes.Structure):

@@ -207,6 +207,12 @@ SsspLdsPlan sssp_batch_lds_plan(int K, int64_t hub_limit, uint32_t par_hubs, int
 // bit 30 of every adjk column word := the column is set in tbits (the attached vertices)
 hipError_t launch_mark_targets(uint32_t* adjk, int64_t nadj, const uint32_t* tbits,
                                hipStream_t stream);
+// target-aware kappa fixpoint (topo_sssp_batch.hip): one step K_out = F(K_in) (K_in nullptr:
+// kappa0), then the f16 kappa field of the relaxation copy's records := K(column)
+hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const double* pot,
+                            const uint32_t* tbits, const double* Kin, double* Kout, int64_t V,
+                            unsigned int* changed, hipStream_t stream);
+hipError_t launch_kfix_store(uint32_t* adjk, int64_t nadj, const double* K, hipStream_t stream);
 hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                              const double* d_srcsh, int nsrc, int kf, const uint32_t* d_targets, int A,
                              double delta, const SsspLdsPlan& plan, uint32_t far_cap,

@@ -1474,6 +1474,92 @@ hipError_t launch_mark_targets(uint32_t* adjk, int64_t nadj, const uint32_t* tbi
     return hipGetLastError();
 }
 
+// Target-aware kappa bound of every vertex (the relaxation's skip test, see phase B).  A pair
+// into a non-target tail vertex y is dropped when y's kappa field exceeds the landmark threshold at
+// the candidate; kappa0 (the row's smallest w - pi) says "y would relax nothing".  The fixpoint
+//   K(x) = min over edges (x, y) of  target(y) ? kap(x, y)
+//                                   : max(kap(x, y), K(y) + w (1 - 2e-5) - 1e-9)
+// (kap = w - pi(y); K_0 = kappa0) says "y would relax nothing that reaches a target": along a
+// parent chain x -> y -> ... -> t the threshold at y is the one at x minus w (plus 1e-5 w of
+// margin), so K(x) stays under the threshold of every chain vertex at its final distance (every
+// iterate K_k is such a bound; they rise monotonically towards the fixpoint).  One wavefront per
+// vertex; Kin == nullptr computes K_0.
+__global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
+                                 const uint32_t* __restrict__ adj, const double* __restrict__ pot,
+                                 const uint32_t* __restrict__ tbits,
+                                 const double* __restrict__ Kin, double* __restrict__ Kout,
+                                 int64_t V, unsigned int* __restrict__ changed) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t x = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; x < V; x += nw) {
+        const uint32_t r0 = rowptr[x], r1 = rowptr[x + 1];
+        double m = INFINITY;
+        for (uint32_t k = r0 + lane; k < r1; k += 64u) {
+            const uint32_t y = adj[kAdjWords * k];
+            const double w = __hiloint2double((int)adj[kAdjWords * k + 3], (int)adj[kAdjWords * k + 2]);
+            const double p = pot[y];
+            const double kap = isfinite(p) ? w - p : -INFINITY;
+            double t = kap;
+            if (Kin && !((tbits[y >> 5] >> (y & 31u)) & 1u)) {
+                const double ky = Kin[y] + w * (1.0 - 2e-5) - 1e-9;
+                t = ky > kap ? ky : kap;
+            }
+            m = t < m ? t : m;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double y = __shfl_xor(m, o, 64);
+            m = y < m ? y : m;
+        }
+        if (lane == 0) {
+            if (Kin && !(m == Kin[x])) atomicOr(changed, 1u);
+            Kout[x] = m;
+        }
+    }
+}
+
+// largest half <= x (NaN: -inf)
+__device__ __forceinline__ uint32_t f16_down(double x) {
+    if (isnan(x)) return 0xFC00u;
+    const _Float16 h = (_Float16)(float)x;
+    uint32_t b = (uint32_t)__builtin_bit_cast(unsigned short, h);
+    if ((double)(float)h > x) {
+        if ((b & 0x7FFFu) == 0u) b = 0x8001u;  // +-0 -> the negative subnormal
+        else if (b & 0x8000u) b++;             // negative: larger magnitude
+        else b--;                              // positive (or +inf): smaller magnitude
+        if ((double)(float)__builtin_bit_cast(_Float16, (unsigned short)b) > x) b = 0xFC00u;
+    }
+    return b & 0xFFFFu;
+}
+
+// the kappa field of every relaxation-copy record := f16 of K(column), rounded down
+__global__ void kfix_store_kernel(uint32_t* __restrict__ adjk, int64_t nadj,
+                                  const double* __restrict__ K) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nadj;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t y = adjk[kAdjWords * k] & 0x3FFFFFFFu;
+        const uint32_t pb = adjk[kAdjWords * k + 1];
+        adjk[kAdjWords * k + 1] = (pb & 0xFFFF0000u) | f16_down(K[y]);
+    }
+}
+
+hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const double* pot,
+                            const uint32_t* tbits, const double* Kin, double* Kout, int64_t V,
+                            unsigned int* changed, hipStream_t stream) {
+    if (V <= 0) return hipSuccess;
+    const int64_t g = std::min<int64_t>((V + 3) / 4, 256 * 32);
+    hipLaunchKernelGGL(kfix_step_kernel, dim3((unsigned)g), dim3(256), 0, stream, rowptr, adj,
+                       pot, tbits, Kin, Kout, V, changed);
+    return hipGetLastError();
+}
+
+hipError_t launch_kfix_store(uint32_t* adjk, int64_t nadj, const double* K, hipStream_t stream) {
+    if (nadj <= 0) return hipSuccess;
+    const int64_t g = std::min<int64_t>((nadj + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(kfix_store_kernel, dim3((unsigned)g), dim3(256), 0, stream, adjk, nadj, K);
+    return hipGetLastError();
+}
+
 SsspLdsPlan sssp_batch_lds_plan(int K, int64_t hub_limit, uint32_t par_hubs, int64_t V) {
     auto bytes = [&](uint32_t H, uint32_t P) -> size_t {
         switch (K) {
