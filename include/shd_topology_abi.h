@@ -116,7 +116,7 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * in the same rounds of the slots), "source_order" / "batch_order" (row grouping and batch
  * dequeue order), "target_skip" (1: the batch relaxation drops pairs into
  * non-target vertices that would relax nothing reaching a target), "target_kappa" (iterations of
- * the target-aware kappa fixpoint behind that test, 0 = the row's smallest kappa; default 12).
+ * the target-aware kappa fixpoint behind that test, 0 = the row's smallest kappa; default 6).
  * Returns 0 or -1 for an unknown key / bad value. */
 int shdtopo_set_option(Topology* top, const char* key, double value);
 

@@ -195,10 +195,11 @@ struct _Topology {
                               // dropped (topo_sssp_batch.hip)
     std::vector<uint32_t> adjkTargets;  // the target set whose bits d_adjk carries
     bool adjkFlagged = false;
-    int targetKappa = 12;     // option "target_kappa": iterations of the target-aware kappa
-                              // fixpoint written into the relaxation copy (0: kappa0).  C4: 2
-                              // iterations 226 ms, 8: 197 ms, 32: 196 ms (no fixpoint is reached:
-                              // cycles without targets rise forever; every iterate is exact)
+    int targetKappa = 6;      // option "target_kappa": iterations of the target-aware kappa
+                              // fixpoint written into the relaxation copy (0: kappa0).  C4 kernel:
+                              // 2 iterations 226 ms, 4: 199, 6: 194, 12: 194, 32: 196 (no
+                              // fixpoint is reached: cycles without targets rise forever; every
+                              // iterate is exact)
     DevBuf<double> d_pot, d_kfA, d_kfB;
     DevBuf<unsigned int> d_kfChanged;
     DevBuf<uint32_t> d_rowmap;

@@ -1484,21 +1484,6 @@ hipError_t launch_mark_targets(uint32_t* adjk, int64_t nadj, const uint32_t* tbi
 // margin), so K(x) stays under the threshold of every chain vertex at its final distance (every
 // iterate K_k is such a bound; they rise monotonically towards the fixpoint).  One wavefront per
 // vertex; Kin == nullptr computes K_0.
-__device__ __forceinline__ double kfix_term(const uint32_t* __restrict__ adj,
-                                           const double* __restrict__ pot,
-                                           const uint32_t* __restrict__ tbits,
-                                           const double* __restrict__ Kin, uint32_t k) {
-    const uint32_t y = adj[kAdjWords * k];
-    const double w = __hiloint2double((int)adj[kAdjWords * k + 3], (int)adj[kAdjWords * k + 2]);
-    const double p = pot[y];
-    const double kap = isfinite(p) ? w - p : -INFINITY;
-    if (!Kin || ((tbits[y >> 5] >> (y & 31u)) & 1u)) return kap;
-    const double ky = Kin[y] + w * (1.0 - 2e-5) - 1e-9;
-    return ky > kap ? ky : kap;
-}
-
-// A wavefront takes 64 consecutive vertices: a lane walks its own row when it is short (<= 64
-// edges), then the wave walks each long row (hubs) with all lanes.
 __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
                                  const uint32_t* __restrict__ adj, const double* __restrict__ pot,
                                  const uint32_t* __restrict__ tbits,
@@ -1506,44 +1491,30 @@ __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
                                  int64_t V, unsigned int* __restrict__ changed) {
     const uint32_t lane = threadIdx.x & 63u;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t xb = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; xb < V;
-         xb += nw * 64) {
-        const int64_t x = xb + lane;
-        uint32_t r0 = 0, r1 = 0;
-        if (x < V) {
-            r0 = rowptr[x];
-            r1 = rowptr[x + 1];
-        }
-        const bool longrow = r1 - r0 > 64u;
+    for (int64_t x = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; x < V; x += nw) {
+        const uint32_t r0 = rowptr[x], r1 = rowptr[x + 1];
         double m = INFINITY;
-        if (!longrow)
-            for (uint32_t k = r0; k < r1; k++) {
-                const double t = kfix_term(adj, pot, tbits, Kin, k);
-                m = t < m ? t : m;
+        for (uint32_t k = r0 + lane; k < r1; k += 64u) {
+            const uint32_t y = adj[kAdjWords * k];
+            const double w = __hiloint2double((int)adj[kAdjWords * k + 3], (int)adj[kAdjWords * k + 2]);
+            const double p = pot[y];
+            const double kap = isfinite(p) ? w - p : -INFINITY;
+            double t = kap;
+            if (Kin && !((tbits[y >> 5] >> (y & 31u)) & 1u)) {
+                const double ky = Kin[y] + w * (1.0 - 2e-5) - 1e-9;
+                t = ky > kap ? ky : kap;
             }
-        unsigned long long lm = __ballot(longrow);
-        while (lm) {
-            const int l = __ffsll((long long)lm) - 1;
-            lm &= lm - 1ull;
-            const uint32_t a = (uint32_t)__shfl((int)r0, l, 64), b = (uint32_t)__shfl((int)r1, l, 64);
-            double mm = INFINITY;
-            for (uint32_t k = a + lane; k < b; k += 64u) {
-                const double t = kfix_term(adj, pot, tbits, Kin, k);
-                mm = t < mm ? t : mm;
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const double y = __shfl_xor(mm, o, 64);
-                mm = y < mm ? y : mm;
-            }
-            if ((int)lane == l) m = mm;
+            m = t < m ? t : m;
         }
-        bool ch = false;
-        if (x < V) {
-            ch = Kin && !(m == Kin[x]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double y = __shfl_xor(m, o, 64);
+            m = y < m ? y : m;
+        }
+        if (lane == 0) {
+            if (Kin && !(m == Kin[x])) atomicOr(changed, 1u);  // one lane per wave
             Kout[x] = m;
         }
-        if (__ballot(ch) && lane == 0) atomicOr(changed, 1u);
     }
 }
 
@@ -1576,7 +1547,7 @@ hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const d
                             const uint32_t* tbits, const double* Kin, double* Kout, int64_t V,
                             unsigned int* changed, hipStream_t stream) {
     if (V <= 0) return hipSuccess;
-    const int64_t g = std::min<int64_t>((V + 255) / 256, 256 * 32);
+    const int64_t g = std::min<int64_t>((V + 3) / 4, 256 * 32);
     hipLaunchKernelGGL(kfix_step_kernel, dim3((unsigned)g), dim3(256), 0, stream, rowptr, adj,
                        pot, tbits, Kin, Kout, V, changed);
     return hipGetLastError();
