@@ -195,6 +195,9 @@ struct _Topology {
                               // dropped (topo_sssp_batch.hip)
     std::vector<uint32_t> adjkTargets;  // the target set whose bits d_adjk carries
     bool adjkFlagged = false;
+    bool targetResort = true;  // option "target_resort": rows of the relaxation copy re-sorted
+                               // by the target-aware key per target set (kappa-prefix cuts stop
+                               // before heads that relax nothing reaching a target)
     int targetKappa = 6;      // option "target_kappa": iterations of the target-aware kappa
                               // fixpoint written into the relaxation copy (0: kappa0).  C4 kernel:
                               // 2 iterations 226 ms, 4: 199, 6: 194, 12: 194, 32: 196 (no
@@ -1117,6 +1120,10 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     std::swap(kin, kout);
                     if (!ch) break;
                 }
+                if (top->targetResort)
+                    HIPCHK(launch_kprime_resort(top->d_adjk.p, top->d_kap.p, top->d_ksum.p,
+                                                top->d_kap0.p, top->d_rowptr.p, V, nadj,
+                                                top->d_pot.p, top->d_tbits.p, kin, st));
                 HIPCHK(launch_kfix_store(top->d_adjk.p, nadj, kin, st));
                 HIPCHK(hipStreamSynchronize(st));
                 top->stats.target_kappa_iters = it;
@@ -1510,6 +1517,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->batchFill = top->batchFill;
     p->targetSkip = top->targetSkip;
     p->targetKappa = top->targetKappa;
+    p->targetResort = top->targetResort;
     p->attached = top->attached;
     p->colOf = top->colOf;
     p->A = top->A;
@@ -2078,6 +2086,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "batch_fill") top->batchFill = (int)value;
     else if (k == "target_skip") top->targetSkip = value != 0;
     else if (k == "target_kappa") top->targetKappa = (int)value;
+    else if (k == "target_resort") top->targetResort = value != 0;
     else if (k == "devices") {
         const int n = (int)value;
         if (n < 1 || n > 64) return -1;

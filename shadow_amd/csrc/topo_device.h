@@ -213,6 +213,11 @@ hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const d
                             const uint32_t* tbits, const double* Kin, double* Kout, int64_t V,
                             unsigned int* changed, hipStream_t stream);
 hipError_t launch_kfix_store(uint32_t* adjk, int64_t nadj, const double* K, hipStream_t stream);
+// re-sort every row of the relaxation copy (records, kappa array, probes, kappa0) by the
+// target-aware key kap' of the current target set (tbits) and K
+hipError_t launch_kprime_resort(uint32_t* adjk, float* kap, float* ksum, float* kap0,
+                                const uint32_t* rowptr, int64_t V, int64_t nadj, const double* pot,
+                                const uint32_t* tbits, const double* K, hipStream_t stream);
 hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                              const double* d_srcsh, int nsrc, int kf, const uint32_t* d_targets, int A,
                              double delta, const SsspLdsPlan& plan, uint32_t far_cap,

@@ -32,6 +32,7 @@
 // batch on C4) the sweeps are cheaper than per-(vertex, source) queue entries, which cost random
 // reads and atomics to merge (measured: DESIGN.md 4).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -1551,6 +1552,111 @@ hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const d
     hipLaunchKernelGGL(kfix_step_kernel, dim3((unsigned)g), dim3(256), 0, stream, rowptr, adj,
                        pot, tbits, Kin, Kout, V, changed);
     return hipGetLastError();
+}
+
+// Row order of the relaxation copy for a target set: each row sorted by
+// kap'(x, y) = target(y) ? kap(x, y) : max(kap(x, y), K(y) + w (1 - 2e-5) - 1e-9), the same bound
+// the pair skip applies per source (a head that relaxes nothing reaching a target sorts past the
+// landmark threshold), so the kappa-prefix cut of an expansion stops before such heads.  Keys
+// are f32 rounded down: a cut is never too early.
+__device__ __forceinline__ float f32_down(double x) {
+    if (isnan(x)) return -INFINITY;
+    float f = (float)x;
+    if ((double)f > x) f = nextafterf(f, -INFINITY);
+    return f;
+}
+
+__global__ void kprime_key_kernel(const uint32_t* __restrict__ adjk, int64_t nadj,
+                                  const double* __restrict__ pot,
+                                  const uint32_t* __restrict__ tbits, const double* __restrict__ K,
+                                  float* __restrict__ key, uint32_t* __restrict__ idx) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nadj;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t y = adjk[kAdjWords * k] & 0x3FFFFFFFu;
+        const double w = __hiloint2double((int)adjk[kAdjWords * k + 3], (int)adjk[kAdjWords * k + 2]);
+        const double p = pot[y];
+        double t = isfinite(p) ? w - p : -INFINITY;
+        if (!((tbits[y >> 5] >> (y & 31u)) & 1u)) {
+            const double ky = K[y] + w * (1.0 - 2e-5) - 1e-9;
+            t = ky > t ? ky : t;
+        }
+        key[k] = f32_down(t);
+        idx[k] = (uint32_t)k;
+    }
+}
+
+__global__ void kprime_gather_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                     const uint32_t* __restrict__ idx, int64_t nadj) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nadj;
+         k += (int64_t)gridDim.x * blockDim.x)
+        dst[k] = src[idx[k]];
+}
+
+__global__ void kprime_probe_kernel(const uint32_t* __restrict__ rowptr,
+                                    const float* __restrict__ kap, float* __restrict__ ksum,
+                                    float* __restrict__ kap0, int64_t V) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V;
+         v += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t b = rowptr[v], n = rowptr[v + 1] - b;
+#pragma unroll
+        for (int q = 0; q < kKProbes; q++) {
+            const uint32_t pq = (1u << q) - 1u;  // 0, 1, 3, 7, 15, 31, 63, 127
+            ksum[(size_t)kKProbes * v + q] = pq < n ? kap[b + pq] : INFINITY;
+        }
+        kap0[v] = n ? kap[b] : INFINITY;
+    }
+}
+
+hipError_t launch_kprime_resort(uint32_t* adjk, float* kap, float* ksum, float* kap0,
+                                const uint32_t* rowptr, int64_t V, int64_t nadj, const double* pot,
+                                const uint32_t* tbits, const double* K, hipStream_t stream) {
+    if (nadj <= 0 || V <= 0) return hipSuccess;
+    if (nadj > 0x7FFFFFFF) return hipErrorInvalidValue;
+    float* key_in = nullptr;
+    uint32_t *idx_in = nullptr, *idx_out = nullptr;
+    uint4* rec = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    hipError_t e = hipMalloc((void**)&key_in, sizeof(float) * (size_t)nadj);
+    if (e == hipSuccess) e = hipMalloc((void**)&idx_in, sizeof(uint32_t) * (size_t)nadj);
+    if (e == hipSuccess) e = hipMalloc((void**)&idx_out, sizeof(uint32_t) * (size_t)nadj);
+    if (e == hipSuccess) e = hipMalloc((void**)&rec, sizeof(uint4) * (size_t)nadj);
+    const int64_t ge = std::min<int64_t>((nadj + 255) / 256, 256 * 16);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(kprime_key_kernel, dim3((unsigned)ge), dim3(256), 0, stream, adjk, nadj,
+                           pot, tbits, K, key_in, idx_in);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess)
+        e = hipcub::DeviceSegmentedRadixSort::SortPairs(
+            nullptr, tmp_bytes, key_in, kap, idx_in, idx_out, (int)nadj, (int)V, rowptr,
+            rowptr + 1, 0, 32, stream);
+    if (e == hipSuccess) e = hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 1);
+    if (e == hipSuccess)
+        e = hipcub::DeviceSegmentedRadixSort::SortPairs(
+            tmp, tmp_bytes, key_in, kap, idx_in, idx_out, (int)nadj, (int)V, rowptr, rowptr + 1,
+            0, 32, stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(rec, adjk, sizeof(uint4) * (size_t)nadj, hipMemcpyDeviceToDevice, stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(kprime_gather_kernel, dim3((unsigned)ge), dim3(256), 0, stream, rec,
+                           reinterpret_cast<uint4*>(adjk), idx_out, nadj);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        const int64_t gv = std::min<int64_t>((V + 255) / 256, 256 * 16);
+        hipLaunchKernelGGL(kprime_probe_kernel, dim3((unsigned)gv), dim3(256), 0, stream, rowptr,
+                           kap, ksum, kap0, V);
+        e = hipGetLastError();
+    }
+    const hipError_t es = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = es;
+    (void)hipFree(key_in);
+    (void)hipFree(idx_in);
+    (void)hipFree(idx_out);
+    (void)hipFree(rec);
+    (void)hipFree(tmp);
+    return e;
 }
 
 hipError_t launch_kfix_store(uint32_t* adjk, int64_t nadj, const double* K, hipStream_t stream) {
