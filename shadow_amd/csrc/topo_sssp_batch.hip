@@ -68,6 +68,9 @@ using namespace dev;
 #else
 #define BT_TICK(i) do { } while (0)
 #endif
+#ifndef SHD_INIT_NT
+#define SHD_INIT_NT 1  // the batch's [V][K] distance reset with nontemporal stores
+#endif
 #ifndef SHD_BATCH_CHUNK
 #define SHD_BATCH_CHUNK 512
 #endif
@@ -825,9 +828,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         if (tid < (uint32_t)K) L.dh0[tid] = INFINITY;
         if (tid == 0) L.invd = B.inv_delta;
         {
-            ulonglong2* d2 = reinterpret_cast<ulonglong2*>(D.dist);
+            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+            u64x2* d2 = reinterpret_cast<u64x2*>(D.dist);
+            const u64x2 inf2 = {kInfBits, kInfBits};
             const size_t lo = (size_t)H * K / 2, hi = (size_t)V * K / 2;
-            for (size_t i = lo + tid; i < hi; i += kSsspBlock) d2[i] = make_ulonglong2(kInfBits, kInfBits);
+            for (size_t i = lo + tid; i < hi; i += kSsspBlock) {
+                if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + i);  // streaming: no L2 fill
+                else d2[i] = inf2;
+            }
         }
         if (tid == 0) {
             L.fminb = kNoBucket;
