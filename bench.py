@@ -164,8 +164,8 @@ def main():
                     help="C4-int variant (integer latencies U{1..100}: heavy parent ties)")
     ap.add_argument("--batch", type=int, default=8,
                     help="sources per SSSP workgroup (1 = single-source sssp_rows_kernel)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02u_sssp_pmc.json"))
-    ap.add_argument("--route-pmc-json", default=os.path.join(ROOT, "profiles", "r02u_route_pmc.json"))
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02w_sssp_pmc.json"))
+    ap.add_argument("--route-pmc-json", default=os.path.join(ROOT, "profiles", "r02w_route_pmc.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -71,6 +71,9 @@ using namespace dev;
 #ifndef SHD_INIT_NT
 #define SHD_INIT_NT 1  // the batch's [V][K] distance reset with nontemporal stores
 #endif
+#ifndef SHD_OUT_NT
+#define SHD_OUT_NT 1  // table rows written with nontemporal stores
+#endif
 #ifndef SHD_BATCH_CHUNK
 #define SHD_BATCH_CHUNK 512
 #endif
@@ -1414,8 +1417,16 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 if (lat == 0.0) lat = 1.0;
             }
             const size_t o = (size_t)(ws.rowmap ? (int)ws.rowmap[r0 + (int)j] : r0 + (int)j) * (size_t)A + k;
-            out_lr[o] = make_double2(lat, rel);
-            out_hops[o] = (uint16_t)(h > 65535u ? 65535u : h);
+            const uint16_t hh = (uint16_t)(h > 65535u ? 65535u : h);
+            if (SHD_OUT_NT) {  // the table (1.8 GB per launch) is not re-read by the kernel
+                typedef double f64x2 __attribute__((ext_vector_type(2)));
+                const f64x2 r2 = {lat, rel};
+                __builtin_nontemporal_store(r2, reinterpret_cast<f64x2*>(out_lr) + o);
+                __builtin_nontemporal_store(hh, out_hops + o);
+            } else {
+                out_lr[o] = make_double2(lat, rel);
+                out_hops[o] = hh;
+            }
             if (lat >= 0.0) atomicMin(&L.rmin[j], d2bits(lat));  // row minimum (runahead)
         }
         __syncthreads();
