@@ -3,21 +3,30 @@
 
 Workload (BASELINE.json configs 4 + 5; synthetic, generated in memory):
   * C4: power-law Internet topology, 990,000 routers + 10,000 poi, exactly 10,000,000 undirected
-    edges (Chung-Lu, deduplicated, spanning path, poi uplinks + self loops), seed 20261015;
+    edges (Chung-Lu, deduplicated, spanning path, poi uplinks + self loops), seed 20261015,
+    written as GraphML and loaded back through topology_new;
   * C5: 100,000 Tor-like hosts attached by type hint (94/5/1 % client/relay/server) through
     Shadow's seed chain; one scheduler window of 10,000,000 packets.
-A step = one build of the whole attached-vertex routing table (all A ~ 10^4 sources x A targets:
-near-far SSSP + parent/epilogue kernel per source, rows sharded over the ranks, RCCL all-gather of
-the rows, all-reduce(MIN) of the runahead minimum, table installed in the library).
+A step = one build of the whole attached-vertex routing table (all A = 10^4 sources x A targets:
+batched SSSP + parents + epilogue per source, rows sharded over the GPUs, the row exchange and the
+runahead minimum, the table installed in the library).
 value = A * E / t_step / 1e9 (Graph500 SSSP convention, undirected E) = GTEPS, whole job.
+cold_build = the first build of the loaded topology -- graph preparation (CSR, relabel, h0
+distances, kappa copy), target preparation, kernels, exchange -- what a Shadow run pays once.
 Packet routes are timed separately over resident windows and reported as packet_routes_per_s.
 
-Launch: python bench.py [--gpus 1 --steps K --warmup W]   or, for N > 1,
+Multi-GPU.  Default --mode library: the process that owns the Topology drives N
+GPUs itself (option "devices", RCCL all-gather + all-reduce(MIN) inside the library), as one
+Shadow process would.  Under torchrun only rank 0 works in this mode; the other ranks wait.
+--mode torchrun: one process per GPU builds its row shard and torch.distributed (RCCL) exchanges.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]   (N GPUs from one process), or
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
+import glob
+import hashlib
 import json
-import math
 import os
 import sys
 import time
@@ -32,13 +41,23 @@ sys.path.insert(0, ROOT)
 import shadow_amd as sa  # noqa: E402
 from shadow_amd import sharding  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SEED = 20261015
+PROFILE_TAG = "r03"            # profiles/<tag>_*_pmc.json: the committed counter passes
 
 
 def log(rank, *a):
     if rank == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def source_hash():
+    """Hash of the engine's sources: a committed PMC file applies only to the code it measured."""
+    h = hashlib.sha256()
+    for p in sorted(glob.glob(os.path.join(ROOT, "shadow_amd", "csrc", "*"))):
+        if p.endswith((".hip", ".cpp", ".h")):
+            h.update(open(p, "rb").read())
+    return h.hexdigest()[:12]
 
 
 def cpu_share():
@@ -140,11 +159,49 @@ def cpu_route_baseline(lat, rel, payload, state, now, jump):
     return len(lat) / (time.time() - t0)
 
 
+def load_pmc(path, key):
+    """A committed counter summary (tools/summarize_prof.py) if it was measured on this exact
+    workload and code (key), else None."""
+    if not path or not os.path.exists(path):
+        return None
+    try:
+        pm = json.load(open(path))
+    except Exception:
+        return None
+    return pm if pm.get("config_key") == key else None
+
+
+def hbm_roofline(kernel, kernel_ms, traffic_pm, model_bytes_per_unit, units, model_note):
+    """Roofline of one kernel: achieved = measured HBM bytes per launch (PMC, FETCH_SIZE +
+    WRITE_SIZE in separate passes) / the launch time -- a rate the memory system actually
+    delivered, so frac <= 1.  The algorithmic model of SURVEY.md 8(d) is reported beside it."""
+    k_s = kernel_ms / 1e3
+    traffic = traffic_pm["hbm_bytes_per_launch"] if traffic_pm else None
+    achieved = traffic / k_s / 1e9 if (traffic and k_s > 0) else None
+    model_achieved = units * model_bytes_per_unit / k_s / 1e9 if k_s > 0 else None
+    out = dict(bound="hbm", kernel=kernel, kernel_ms=round(kernel_ms, 3),
+               achieved=round(achieved, 2) if achieved else None, peak=HBM_PEAK_GBS, unit="GB/s",
+               frac=round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
+               traffic=traffic, units_per_launch=units,
+               pmc=traffic_pm.get("source") if traffic_pm else "no counter pass for this code",
+               model=dict(bytes_per_unit=model_bytes_per_unit,
+                          achieved=round(model_achieved, 2) if model_achieved else None,
+                          frac=round(model_achieved / HBM_PEAK_GBS, 5) if model_achieved else None,
+                          note=model_note))
+    if traffic_pm and traffic_pm.get("dram_requests_per_launch"):
+        out["dram_requests_per_unit"] = round(traffic_pm["dram_requests_per_launch"] / max(1, units))
+        out["dram_requests_per_s"] = round(traffic_pm["dram_requests_per_launch"] / k_s)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mode", choices=("library", "torchrun"), default="library",
+                    help="library: one process drives the GPUs (option devices); torchrun: one "
+                         "process per GPU exchanging through torch.distributed")
     ap.add_argument("--routers", type=int, default=990_000)
     ap.add_argument("--poi", type=int, default=10_000)
     ap.add_argument("--edges", type=int, default=10_000_000)
@@ -162,34 +219,49 @@ def main():
     ap.add_argument("--delta", type=float, default=0.0)
     ap.add_argument("--integer", action="store_true",
                     help="C4-int variant (integer latencies U{1..100}: heavy parent ties)")
-    ap.add_argument("--batch", type=int, default=8,
-                    help="sources per SSSP workgroup (1 = single-source sssp_rows_kernel)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02w_sssp_pmc.json"))
-    ap.add_argument("--route-pmc-json", default=os.path.join(ROOT, "profiles", "r02w_route_pmc.json"))
+    ap.add_argument("--batch", type=int, default=8, help="sources per SSSP workgroup (2/4/8/16)")
+    ap.add_argument("--opt", action="append", default=[], help="key=value library option")
+    ap.add_argument("--pmc-tag", default=PROFILE_TAG)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    library = args.mode == "library"
+    ngpu = max(args.gpus, world) if library else world
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if library:
+            # rank 0 drives every GPU through the library; the others only wait for it (gloo:
+            # they never touch a GPU)
+            dist.init_process_group("gloo")
+            if rank != 0:
+                dist.barrier()
+                dist.destroy_process_group()
+                return
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if not (world > 1 and not library):
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if library and ngpu > torch.cuda.device_count():
+        raise SystemExit("--gpus %d > %d visible devices" % (ngpu, torch.cuda.device_count()))
 
-    # ---- workload (identical on every rank; generation and loading are outside the timed
-    # region).  The generated C4 topology is written as GraphML once and loaded back through
-    # topology_new (shd-topology.c:1237 -> _topology_loadGraph :95-123), as Shadow loads it;
-    # the round trip must reproduce the generator's graph bit for bit. ----
+    # ---- workload (generation and loading are outside the timed region).  The generated C4
+    # topology is written as GraphML once and loaded back through topology_new
+    # (shd-topology.c:1237 -> _topology_loadGraph :95-123), as Shadow loads it; the round trip
+    # must reproduce the generator's graph bit for bit. ----
     t0 = time.time()
     gen = sa.Topology.synthetic(seed=SEED, n_routers=args.routers, n_poi=args.poi,
                                 n_edges=args.edges, integer_latency=args.integer)
     graphml = dict(generate_s=round(time.time() - t0, 2))
     top = gen
+    torchrun = world > 1 and not library
     if not args.no_graphml:
         import tempfile
         path = os.path.join(tempfile.gettempdir(), "shdtopo_c4_%s_%d.graphml.xml" % (
-            "int" if args.integer else "real", os.getpid() if world == 1 else 0))
-        if world > 1:
+            "int" if args.integer else "real", os.getpid() if not torchrun else 0))
+        if torchrun:
             path = path.replace("_0.graphml", "_%s.graphml" % os.environ.get("MASTER_PORT", "0"))
         try:
             if rank == 0:
@@ -197,7 +269,7 @@ def main():
                 gen.write_graphml(path)
                 graphml["write_s"] = round(time.time() - t1, 2)
                 graphml["bytes"] = os.path.getsize(path)
-            if world > 1:
+            if torchrun:
                 dist.barrier()
             t1 = time.time()
             top = sa.Topology.new(path)
@@ -209,7 +281,7 @@ def main():
                                           for x, y in zip(a_[1:], b_[1:])), "GraphML round trip"
             graphml["round_trip_bit_exact"] = True
         finally:
-            if world > 1:
+            if torchrun:
                 dist.barrier()
             if rank == 0 and os.path.exists(path):
                 os.unlink(path)
@@ -218,33 +290,69 @@ def main():
     top.set_option("batch", args.batch)
     if args.delta:
         top.set_option("delta", args.delta)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        top.set_option(k, float(v))
+    if library and ngpu > 1:
+        top.set_option("devices", ngpu)
     window0 = 10_000_000  # Shadow's default 10 ms window until the runahead is known
     pk = top.synth_packets(SEED, args.hosts, args.packets, 10**9, window0)
     attached = top.attached_vertices()
     A, V, E = len(attached), top.num_vertices, top.num_edges
-    log(rank, "workload ready in %.1fs: V=%d E=%d A=%d packets=%d" %
-        (time.time() - t0, V, E, A, args.packets))
+    log(rank, "workload ready in %.1fs: V=%d E=%d A=%d packets=%d, %d GPU(s), mode %s" %
+        (time.time() - t0, V, E, A, args.packets, ngpu, args.mode))
 
-    table = sharding.ShardedTable(A, rank, world, dev)
-    builder = sharding.hip_builder(top)
-    kernel_ms = []
-    replay_ms = []
+    kernel_ms, replay_ms = [], []
+    if library:
+        gmin_box = [None]
 
-    def step():
-        table.build(builder)
-        st_ = top.stats()
-        kernel_ms.append(st_["sssp_kernel_ms"])
-        replay_ms.append(st_["replay_ms"])
-        table.exchange()
-        lr, hops = table.table()
-        top.bind_table(lr, hops, float(table.gmin.item()),
-                       stream=torch.cuda.current_stream().cuda_stream)
+        def step():
+            top.rebuild()  # rows on every device, exchange, table installed (shdtopo_rebuild)
+            st_ = top.stats()
+            kernel_ms.append(st_["sssp_kernel_ms"])
+            replay_ms.append(st_["replay_ms"])
+            gmin_box[0] = top.getMinimumLatency()
+
+        def current_gmin():
+            return gmin_box[0]
+    else:
+        table = sharding.ShardedTable(A, rank, world, dev)
+        builder = sharding.hip_builder(top)
+
+        def step():
+            table.build(builder)
+            st_ = top.stats()
+            kernel_ms.append(st_["sssp_kernel_ms"])
+            replay_ms.append(st_["replay_ms"])
+            table.exchange()
+            lr, hops = table.table()
+            top.bind_table_ref(lr, hops, float(table.gmin.item()),
+                               stream=torch.cuda.current_stream().cuda_stream)
+
+        def current_gmin():
+            return float(table.gmin.item())
 
     def barrier():
-        if world > 1:
+        if torchrun:
             dist.barrier()
-        torch.cuda.synchronize()
+        for d in range(ngpu if library else 1):
+            torch.cuda.synchronize(d if library else local)
 
+    def max_over_ranks(x):
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        if torchrun:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ---- cold build: the first table of the loaded topology ----
+    barrier()
+    t0 = time.perf_counter()
+    step()
+    barrier()
+    cold_s = max_over_ranks(time.perf_counter() - t0)
+    st_cold = top.stats()
+    kernel_ms.clear()
+    replay_ms.clear()
     for _ in range(args.warmup):
         step()
     kernel_ms.clear()
@@ -254,107 +362,119 @@ def main():
     for _ in range(args.steps):
         step()
     barrier()
-    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    t_step = float(elapsed.item()) / args.steps
+    t_step = max_over_ranks(time.perf_counter() - t0) / args.steps
     st = top.stats()
-    gmin = float(table.gmin.item())
+    gmin = current_gmin()
     jump = int(gmin) * 1_000_000 if gmin >= 1.0 else window0   # shd-master.c:113-124
     gteps = A * E / t_step / 1e9
 
-    # ---- packet routes: this rank's slice of the window, inputs resident in HBM ----
-    p0, p1 = sharding.packet_range(args.packets, rank, world)
-    cu = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
-    d_src = cu(pk["src_col"][p0:p1])
-    d_dst = cu(pk["dst_col"][p0:p1])
-    d_pay = cu(pk["payload"][p0:p1].view(np.int32))
-    d_sin = cu(pk["state_in"][p0:p1].view(np.int32))
-    d_now = cu(pk["now"][p0:p1].view(np.int64))
-    n = p1 - p0
-    t_out = torch.empty(n, dtype=torch.int64, device=dev)
-    s_out = torch.empty(n, dtype=torch.int32, device=dev)
-    d_out = torch.empty(n, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream().cuda_stream
+    # ---- packet routes: the window split over the GPUs, inputs resident in HBM ----
+    nslice = ngpu if library else 1
+    sl = []
+    for s in range(nslice):
+        p0, p1 = sharding.packet_range(args.packets, s if library else rank,
+                                       ngpu if library else world)
+        d = torch.device("cuda", s if library else local)
+        cu = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(d)
+        n = p1 - p0
+        sl.append(dict(n=n, src=cu(pk["src_col"][p0:p1]), dst=cu(pk["dst_col"][p0:p1]),
+                       pay=cu(pk["payload"][p0:p1].view(np.int32)),
+                       sin=cu(pk["state_in"][p0:p1].view(np.int32)),
+                       now=cu(pk["now"][p0:p1].view(np.int64)),
+                       t=torch.empty(n, dtype=torch.int64, device=d),
+                       s=torch.empty(n, dtype=torch.int32, device=d),
+                       dl=torch.empty(n, dtype=torch.uint8, device=d)))
+
+    def route_once():
+        for s, x in enumerate(sl):
+            if library:
+                top.route_batch_device_slot(s, x["src"], x["dst"], x["pay"], x["sin"], x["now"],
+                                            jump, 1, x["t"], x["s"], x["dl"])
+            else:
+                top.route_batch_device(x["src"], x["dst"], x["pay"], x["sin"], x["now"], jump, 1,
+                                       x["t"], x["s"], x["dl"],
+                                       stream=torch.cuda.current_stream().cuda_stream)
     route_ms = []
     for i in range(2 + args.route_steps):
         if i == 2:
             barrier()
             tr0 = time.perf_counter()
-        top.route_batch_device(d_src, d_dst, d_pay, d_sin, d_now, jump, 1, t_out, s_out, d_out,
-                               stream=stream)
+        route_once()
         if i >= 2:
-            route_ms.append(top.stats()["route_kernel_ms"])
+            route_ms.append(top.stats()["route_kernel_ms"])  # slot 0's launch
     barrier()
-    rel_t = torch.tensor([time.perf_counter() - tr0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(rel_t, op=dist.ReduceOp.MAX)
-    t_window = float(rel_t.item()) / args.route_steps
+    t_window = max_over_ranks(time.perf_counter() - tr0) / args.route_steps
     routes_per_s = args.packets / t_window
 
     if rank == 0:
-        # roofline of the dominant kernel (the SSSP launch), algorithmic bytes per source =
-        # 2E (4 B col + 8 B weight) + V (4 B rowptr + 8 B dist read + 8 B dist write)
-        rows = table.r1 - table.r0
-        b_src = 24 * E + 20 * V
-        k_s = float(np.mean(kernel_ms)) / 1e3
-        achieved = rows * b_src / k_s / 1e9
+        srch = source_hash()
+        rows = A if library else (table.r1 - table.r0)
         K = int(st["batch"])
-        kname = "sssp_batch_kernel<%d>" % K if K > 1 else "sssp_rows_kernel"
-        # the batch kernel's per-bucket sweeps read only the 64-B lines of vertices with a
-        # pending bit (random 64-B requests, which FETCH_SIZE counts at their size): no streaming
-        # correction (MI355X_MICROARCH.md: only wide coalesced 128-B reads are tallied at half)
-        sweeps = int(st["far_splits"]) if K > 1 else 0
-        sweep_bytes = 0
-        traffic = None
-        pmc_note = None
-        pmc_requests = None
-        if os.path.exists(args.pmc_json):
-            try:
-                pm = json.load(open(args.pmc_json))
-                if not args.integer and pm.get("config_key") == "C4-%d-%d-%d-rows%d-%s" % (
-                        V, E, A, rows, kname):
-                    traffic = pm["hbm_bytes_per_launch"]
-                    pmc_note = pm.get("source")
-                    pmc_requests = pm.get("dram_requests_per_launch")
-            except Exception:
-                traffic = None
-        roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS,
-                        unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic,
-                        # measured HBM bytes (PMC) per launch / the launch time: what the memory
-                        # system actually moved, beside the per-source model above
-                        frac_measured=(round(traffic / k_s / 1e9 / HBM_PEAK_GBS, 5)
-                                       if traffic else None),
-                        dram_requests_per_source=(round(pmc_requests / rows)
-                                                  if pmc_requests else None),
-                        kernel=kname, kernel_ms=round(k_s * 1e3, 3),
-                        units_per_launch=rows, bytes_per_unit=b_src, pmc=pmc_note)
-        sssp = dict(kernel=kname, batch=K, lds_hubs=int(st["lds_hubs"]), sweeps=sweeps,
-                    sweep_bytes=sweep_bytes, slots=st["slots"],
+        tie_dense = bool(st["tie_dense"])
+        k_ms = float(np.mean(kernel_ms))
+        r_ms = float(np.mean(replay_ms))
+        wl = "C4%s" % ("int" if args.integer else "")
+        key = "%s-%d-%d-%d-rows%d-gpus%d-%s" % (wl, V, E, A, rows, ngpu, srch)
+        if tie_dense:
+            # C4-int: every row through the exact heap replay, the batch kernel does not run
+            pm = load_pmc(os.path.join(ROOT, "profiles", "%s_replay_pmc.json" % args.pmc_tag),
+                          key + "-heap_replay_kernel")
+            roofline = hbm_roofline(
+                "heap_replay_kernel", r_ms, pm, 0, rows,
+                "latency-bound: one wavefront walks igraph's sequential two-way heap per row; no "
+                "algorithmic byte model applies (per row: %d pops, %d pushes, %d modifies)" % (
+                    st["replay_pops"] // max(1, rows), st["replay_pushes"] // max(1, rows),
+                    st["replay_modifies"] // max(1, rows)))
+            roofline["model"] = None
+            if pm and pm.get("lines_per_pop"):
+                roofline["lines_per_pop"] = pm["lines_per_pop"]
+        else:
+            pm = load_pmc(os.path.join(ROOT, "profiles", "%s_sssp_pmc.json" % args.pmc_tag),
+                          key + "-sssp_batch_kernel")
+            roofline = hbm_roofline(
+                "sssp_batch_kernel<%d>" % K, k_ms, pm, 24 * E + 20 * V, rows,
+                "SURVEY.md 8(d): a full Dijkstra scan per source (24E + 20V bytes); the pruned "
+                "batch kernel touches a fraction of it, so this equivalent rate exceeds the HBM "
+                "peak and is not a bandwidth -- achieved / frac above are the measured bytes")
+        roofline["pmc_key"] = key
+        sssp = dict(kernel=roofline["kernel"], batch=K, lds_hubs=int(st["lds_hubs"]),
+                    sweeps=int(st["far_splits"]), slots=st["slots"],
+                    batch_fill=int(st["batch_fill"]),
                     phase_ms_per_source=[round(x / max(1, rows), 3) for x in st["phase_ms"]],
-                    # once per (graph, target set), in the warmup build: target bits and the
-                    # target-aware kappa fixpoint in the relaxation copy (outside the timed steps,
-                    # like the CSR upload and the h0 distances)
-                    target_prep_ms=round(float(st["target_prep_ms"]), 2),
-                    target_kappa_iters=int(st["target_kappa_iters"]))
-        r_ms = float(np.mean(route_ms))
-        route_roof = dict(bound="hbm", kernel="packet_route_kernel", kernel_ms=round(r_ms, 4),
-                          achieved=round(n * 53 / (r_ms / 1e3) / 1e9, 1), peak=HBM_PEAK_GBS,
-                          unit="GB/s", bytes_per_unit=53, units_per_launch=n)
-        route_roof["frac"] = round(route_roof["achieved"] / HBM_PEAK_GBS, 4)
-        route_roof["traffic"] = None
-        if os.path.exists(args.route_pmc_json) and world == 1 and n == 10_000_000:
-            try:
-                rp = json.load(open(args.route_pmc_json))
-                route_roof["traffic"] = rp["hbm_bytes_per_launch"]
-                route_roof["frac_measured"] = round(
-                    rp["hbm_bytes_per_launch"] / (r_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
-                route_roof["traffic_over_algorithmic"] = round(
-                    rp["hbm_bytes_per_launch"] / (n * 53), 3)
-            except Exception:
-                pass
+                    parent_phase_ms_per_source=[round(x / max(1, rows), 3)
+                                                for x in st["parent_phase_ms"]],
+                    touched_lines_per_build=int(st["touched_lines"]),
+                    tie_dense=tie_dense)
+        # cold build: the first table of the loaded topology, split into its parts
+        cs = st_cold
+        host_ms = cs["csr_host_ms"] + cs["csr_copy_ms"] + cs["order_ms"] + cs["replay_prep_ms"]
+        cold = dict(
+            ms=round(cold_s * 1e3, 2), gteps=round(A * E / cold_s / 1e9, 3),
+            graph_prep_ms=round(cs["csr_ms"], 2), graph_prep_host_ms=round(cs["csr_host_ms"], 2),
+            graph_prep_copy_ms=round(cs["csr_copy_ms"], 2), h0_rounds=int(cs["csr_h0_rounds"]),
+            target_prep_ms=round(cs["target_prep_ms"], 2),
+            target_kappa_iters=int(cs["target_kappa_iters"]),
+            order_ms=round(cs["order_ms"], 2), kernel_ms=round(cs["sssp_kernel_ms"], 2),
+            replay_prep_ms=round(cs["replay_prep_ms"], 2), replay_ms=round(cs["replay_ms"], 2),
+            exchange_ms=round(cs["exchange_ms"], 2),
+            host_ms=round(host_ms, 2), host_frac=round(host_ms / (cold_s * 1e3), 4),
+            host_preparations=int(cs["csr_host_runs"]),
+            note="host_ms = host work of the cold build (graph preparation copies + host compute, "
+                 "source ordering, replay CSR); the rest runs on the GPU(s)")
+        route_roof = None
+        if sl:
+            rkey = "C5-%d-%d-%d-%s-packet_route_kernel" % (sl[0]["n"], A, ngpu, srch)
+            rpm = load_pmc(os.path.join(ROOT, "profiles", "%s_route_pmc.json" % args.pmc_tag), rkey)
+            rk = float(np.mean(route_ms))
+            route_roof = hbm_roofline("packet_route_kernel", rk, rpm, 53, sl[0]["n"],
+                                      "SURVEY.md 8(d): 53 B per packet (24 B in, one 16-B record "
+                                      "gather, 13 B out)")
+            route_roof["pmc_key"] = rkey
+            if rpm:
+                route_roof["traffic_over_model"] = round(rpm["hbm_bytes_per_launch"] /
+                                                         (53 * sl[0]["n"]), 3)
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if ngpu == 1 and not args.no_cpu_baseline:
             nt = cpu_share()
             log(rank, "cpu baseline: %d sources on 1 thread, %d on %d threads..." % (
                 args.cpu_sample, args.cpu_sample_mt, nt))
@@ -368,14 +488,14 @@ def main():
             cpu["host_nproc"] = os.cpu_count()
             cpu["job_cpu_share"] = nt
         complete = None
-        if world == 1 and not args.no_complete:
+        if ngpu == 1 and not args.no_complete:
             complete = complete_table_lines()
         out = {
             "metric": "routing-table build GTEPS + packet-routes/sec at 1/2/4/8 MI355X "
                       "(%HBM roofline)",
             "value": round(gteps, 3),
             "unit": "GTEPS",
-            "n_gpus": world,
+            "n_gpus": ngpu,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(t_step * 1e3, 2),
@@ -385,14 +505,18 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": "C4%s synthetic power-law topology (1M vertices / 10M undirected "
-                            "edges, seed 20261015): full attached-vertex table, all %d sources x "
-                            "%d targets; C5: %d hosts, %d packets per window" %
-                            ("-int" if args.integer else "", A, A, args.hosts, args.packets),
+                "workload": "%s synthetic power-law topology (1M vertices / 10M undirected edges, "
+                            "seed 20261015): full attached-vertex table, all %d sources x %d "
+                            "targets; C5: %d hosts, %d packets per window" %
+                            ("C4-int" if args.integer else "C4", A, A, args.hosts, args.packets),
                 "vertices": V, "edges": E, "sources": A, "targets": A,
                 "packets_per_window": args.packets, "hosts": args.hosts,
-                "parallelism": "sources sharded /%d, RCCL all-gather + all-reduce(min)" % world,
+                "parallelism": ("%d GPU(s) driven by one process (library option devices): rows "
+                                "sharded, RCCL all-gather + all-reduce(min)" % ngpu) if library
+                               else ("%d processes: rows sharded, torch.distributed RCCL "
+                                     "all-gather + all-reduce(min)" % world),
             },
+            "cold_build": cold,
             "packet_routes_per_s": round(routes_per_s, 1),
             "ms_per_window": round(t_window * 1e3, 4),
             "roofline": roofline,
@@ -403,9 +527,12 @@ def main():
             "graphml": graphml,
             "complete_tables": complete,
             "ambiguous_pairs": st["ambiguous_pairs"],
+            "exchange": dict(kind={0: "none", 1: "rccl", 2: "peer copies"}.get(
+                int(st["exchange_kind"]), "?") if library else "torch.distributed",
+                             ms=round(st["exchange_ms"], 2)),
             # rows whose target chains cross a d-tied parent, recomputed in igraph's heap pop order
             # by heap_replay_kernel (its time is inside ms_per_step and stated separately here)
-            "replay": dict(rows=st["replay_rows"], ms=round(float(np.mean(replay_ms)), 3),
+            "replay": dict(rows=st["replay_rows"], ms=round(r_ms, 3),
                            pops=st["replay_pops"], pushes=st["replay_pushes"],
                            modifies=st["replay_modifies"], slots=st["replay_slots"]),
             "slots": st["slots"],

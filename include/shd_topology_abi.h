@@ -88,7 +88,10 @@ typedef struct {
  * been in array (= emission) order: first-rooted-wins orientation and running-minimum pushes.
  * The caller captures in[i].rngState before the sender's draw and advances the sender's
  * Random by that one draw itself (tests/c/engine_window.c shows the engine-side adapter).
- * Returns 0, or a negative error (unattached address: -2). */
+ * A packet whose address is not attached is not routed (the reference's getters return -1.0
+ * for it, shd-topology.c:882-892): delivered 0, time 0, rngState after its draw; the others are
+ * routed.  Returns 0 when every packet was routed, else the number of packets that were not, or
+ * a negative error (the outputs are then undefined). */
 int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketOut* out, size_t n,
                               uint64_t jumpNs, int clampInterHost);
 
@@ -154,8 +157,24 @@ int shdtopo_build_rows(Topology* top, int64_t row0, int64_t row1, void* d_lr, vo
  * The library copies it into its own buffers (same device). */
 int shdtopo_bind_table(Topology* top, const void* d_lr, const void* d_hops, double globalMin,
                        void* stream);
+/* Install an assembled table in place: the library reads the caller's buffers (same device; they
+ * must stay valid and unchanged until the next build or bind) instead of copying 1.8 GB. */
+int shdtopo_bind_table_ref(Topology* top, const void* d_lr, const void* d_hops, double globalMin,
+                           void* stream);
+/* Rebuild the whole table now for the current attached set (topology_getLatency & co. build it
+ * lazily; this forces the build, e.g. to time it). */
+int shdtopo_rebuild(Topology* top);
 /* Copy the current table to host memory (lat, rel: f64[A*A]; hops: u16[A*A]; any may be NULL) */
 int shdtopo_table_to_host(Topology* top, double* lat, double* rel, uint16_t* hops);
+
+/* topology_routePacketBatch with the packets' vertices instead of their IPs (SoA host arrays;
+ * -1 = not attached): the window adapter resolves them at emit, so a host detached before the
+ * flush (the reference routed its packet at emit, shd-worker.c:345-369) is still routed while its
+ * vertex is a table column.  Same outputs and return value. */
+int shdtopo_route_batch_vertices(Topology* top, const int32_t* srcVertex, const int32_t* dstVertex,
+                                 const uint32_t* payloadLength, const uint32_t* rngState,
+                                 const uint64_t* now, size_t n, uint64_t jumpNs,
+                                 int clampInterHost, TopoPacketOut* out);
 
 /* Route n packets whose inputs are resident in HBM (SoA, attached-column indices). */
 int shdtopo_route_batch_device(Topology* top, const int32_t* d_srcCol, const int32_t* d_dstCol,
@@ -163,6 +182,15 @@ int shdtopo_route_batch_device(Topology* top, const int32_t* d_srcCol, const int
                                const uint64_t* d_now, int64_t n, uint64_t jumpNs, int clamp,
                                uint64_t* d_time, uint32_t* d_stateOut, uint8_t* d_delivered,
                                void* stream);
+
+/* The same on device slot `slot` of a multi-GPU Topology (option "devices": every slot holds the
+ * whole table after the exchange; inputs and outputs in that device's HBM, stream NULL = the
+ * slot's own).  Slot 0 = shdtopo_route_batch_device. */
+int shdtopo_route_batch_device_slot(Topology* top, int slot, const int32_t* d_srcCol,
+                                    const int32_t* d_dstCol, const uint32_t* d_payload,
+                                    const uint32_t* d_stateIn, const uint64_t* d_now, int64_t n,
+                                    uint64_t jumpNs, int clamp, uint64_t* d_time,
+                                    uint32_t* d_stateOut, uint8_t* d_delivered, void* stream);
 
 /* lazily tracked minimum (reference trajectory, shd-topology.c:500-511) */
 double shdtopo_get_lazy_minimum_latency(Topology* top);
@@ -227,6 +255,24 @@ typedef struct {
                                    set (option "target_kappa") */
     double target_prep_ms;      /* wall time of that target-set preparation (target bits + kappa
                                    fixpoint in the relaxation copy; once per target set) */
+    /* cold-build breakdown (the once-per-topology work a Shadow run pays before its first table,
+       shd-topology.c:757-794 times the reference's equivalent inside the run): */
+    double csr_ms;              /* wall time of the graph preparation (upload, relabel, CSR, h0
+                                   distances, kappa-sorted copy); 0 when it ran in an earlier build */
+    double csr_host_ms;         /*   of which CPU work on the host (not waiting for the GPU) */
+    double csr_copy_ms;         /*   of which host <-> device copies (the parsed edge arrays in,
+                                     perm / inv / pi / h0-tree parents out) */
+    int64_t csr_h0_rounds;      /*   frontier rounds of its h0 distances (pi = d(h0, .)) */
+    double order_ms;            /* host: source order, batch order and bucket shifts of the last
+                                   batched build */
+    double replay_prep_ms;      /* wall time of the heap replay's incidence CSR (once per topology) */
+    int64_t touched_lines;      /* tail distance lines the batches of the last build reset (only the
+                                   lines a batch lowered from +inf are reset for the next one) */
+    int64_t csr_host_runs;      /* host-side graph preparations in the last build (a multi-GPU
+                                   build prepares once and shares it with its peer engines) */
+    int64_t exchange_kind;      /* the last build's row exchange: 0 none (one device), 1 RCCL
+                                   all-gather + all-reduce(MIN), 2 device-to-device peer copies
+                                   (engines sharing a device, or RCCL unavailable) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 
@@ -235,6 +281,15 @@ int shdtopo_get_stats(Topology* top, ShdStats* out);
  * stopping when every attached vertex is popped.  dist f64[V] (-1 = unreached) and parent int32[V]
  * (-1 = none) receive the replay's result in original vertex ids.  Returns 0 or an error. */
 int shdtopo_replay_source(Topology* top, int32_t src, int full, double* dist, int32_t* parent);
+
+/* Test hook: the device graph preparation (topo_prep.hip) read back -- perm
+ * int32[V] (relabelled -> original vertex), rowptr u32[V+1], the adjacency columns u32[2E']
+ * (relabelled ids, rows ascending by neighbour), pi f64[V] (= d(h0, .), relabelled ids) and the
+ * h0-tree parents u32[V] (relabelled, ~0 = none).  Any pointer may be NULL (call with NULLs to
+ * size col).  Prepares the graph if needed.  Returns 2E', or a negative error (-2: complete or
+ * directed topology, which have no such CSR). */
+int64_t shdtopo_export_csr(Topology* top, int32_t* perm, uint32_t* rowptr, uint32_t* col,
+                           double* pot, uint32_t* treeParent);
 
 /* Copy the parsed graph into host arrays (document order; any pointer may be NULL):
  * eu, ev int32[E]; elat, eloss f64[E]; vloss f64[V].  Used by tools and oracle cross-checks. */

@@ -61,7 +61,10 @@ int64_t topowindow_pending(TopoWindow* w);
 
 /* route every recorded packet in one batch on the GPU, then deliver them in order and clear the
  * window.  jumpNs / multiThreaded: the inter-host clamp of shd-worker.c:310-324 (0 = serial).
- * Returns 0 or the error of topology_routePacketBatch. */
+ * Vertices are resolved at emit: a packet whose sender or receiver was detached since is still
+ * routed while its vertex keeps another host (the table's columns), else delivered 0 (dropped).
+ * Returns 0, or a negative error of the batch -- then nothing is delivered and the packets stay
+ * recorded (in order, before any emitted since) for the next flush. */
 int topowindow_flush(TopoWindow* w, uint64_t jumpNs, int multiThreaded, TopoWindowDeliver deliver,
                      void* ctx);
 

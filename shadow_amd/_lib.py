@@ -43,7 +43,11 @@ class ShdStats(ctypes.Structure):
                 ("replay_sink_ms", dbl * 3), ("replay_pf_hits", i64),
                 ("replay_skips", i64), ("tie_dense", i64),
                 ("batch_wave_ms", dbl * 6), ("batch_rounds", i64), ("batch_edges_b", i64),
-                ("target_kappa_iters", i64), ("target_prep_ms", dbl)]
+                ("target_kappa_iters", i64), ("target_prep_ms", dbl),
+                ("csr_ms", dbl), ("csr_host_ms", dbl), ("csr_copy_ms", dbl), ("csr_h0_rounds", i64),
+                ("order_ms", dbl),
+                ("replay_prep_ms", dbl), ("touched_lines", i64), ("csr_host_runs", i64),
+                ("exchange_kind", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):
@@ -81,14 +85,21 @@ SIGNATURES = {
     "shdtopo_shard_rows": (None, [i64, ctypes.c_int, ctypes.c_int, P, P]),
     "shdtopo_build_rows": (ctypes.c_int, [P, i64, i64, P, P, P, P]),
     "shdtopo_bind_table": (ctypes.c_int, [P, P, P, dbl, P]),
+    "shdtopo_bind_table_ref": (ctypes.c_int, [P, P, P, dbl, P]),
+    "shdtopo_rebuild": (ctypes.c_int, [P]),
     "shdtopo_table_to_host": (ctypes.c_int, [P, P, P, P]),
     "shdtopo_route_batch_device": (ctypes.c_int, [P, P, P, P, P, P, i64, u64, ctypes.c_int, P,
                                                   P, P, P]),
+    "shdtopo_route_batch_device_slot": (ctypes.c_int, [P, ctypes.c_int, P, P, P, P, P, i64, u64,
+                                                       ctypes.c_int, P, P, P, P]),
+    "shdtopo_route_batch_vertices": (ctypes.c_int, [P, P, P, P, P, P, ctypes.c_size_t, u64,
+                                                    ctypes.c_int, P]),
     "shdtopo_get_lazy_minimum_latency": (dbl, [P]),
     "shdtopo_get_stats": (ctypes.c_int, [P, P]),
     "shdtopo_write_graphml": (ctypes.c_int, [P, cstr]),
     "shdtopo_replay_source": (ctypes.c_int, [P, i32, ctypes.c_int, P, P]),
     "shdtopo_export_graph": (ctypes.c_int, [P, P, P, P, P, P]),
+    "shdtopo_export_csr": (i64, [P, P, P, P, P, P]),
     "shdtopo_new_synthetic": (P, [P]),
     "shdtopo_synth_packets": (ctypes.c_int, [P, u64, i64, i64, u64, u64, P, P, P, P, P, P, P]),
 }

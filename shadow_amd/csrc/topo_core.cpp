@@ -96,7 +96,12 @@ struct DevBuf {
 }  // namespace
 
 struct _Topology {
-    HostGraph g;
+    // the parsed graph; the peer engines of a multi-GPU build share the owner's (read-only)
+    std::shared_ptr<HostGraph> gp = std::make_shared<HostGraph>();
+    HostGraph& g = *gp;
+    _Topology() = default;
+    explicit _Topology(std::shared_ptr<HostGraph> shared) : gp(std::move(shared)), g(*gp) {}
+
     bool isComplete = false;
     bool isDirected = false;
     bool hasMultiEdges = false;
@@ -109,15 +114,9 @@ struct _Topology {
     int device = 0;
     int64_t hubLimit = -1;  // LDS-cached hub distances (-1 = fill the LDS)
     int64_t parHubs = 2048; // hubs whose parent is hinted during the SSSP (0 = always scan)
-    int wgPerCu = 1;        // SSSP workgroups per CU (each owns 1/wgPerCu of the LDS)
-    int batchK = 8;         // sources per SSSP workgroup (1 = sssp_rows_kernel, else
-                            // sssp_batch_kernel with K in {2, 4, 8, 16})
-    bool events = false;    // per-edge event counters (diagnostic kernel build)
-    int64_t nearCap = 0;    // near-queue entries per slot (0 = 2V; small values force the
-                            // bucket-rescan fallback, for tests)
-    int64_t farCap = 0;     // cap on the entries of one window bucket and of the overflow pile
-                            // (0 = sized from V; small values force the scanning fallback,
-                            // for tests)
+    int batchK = 8;         // sources per SSSP workgroup (sssp_batch_kernel<K>, K in {2,4,8,16})
+    uint32_t iterGuard = 4000000u;  // near iterations per batch before the kernel gives up
+                                    // (option "iter_guard": a test hook for the -4 error path)
 
     // attach state (shd-topology.c:20-24 virtualIP)
     std::shared_mutex ipMu;
@@ -137,27 +136,31 @@ struct _Topology {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     bool csrUploaded = false;
     bool rowsSorted = false;
-    std::vector<int32_t> perm;  // new -> old
-    std::vector<int32_t> inv;   // old -> new
-    std::vector<double> pot;    // batch mode: d(h0, v) from the top hub (new ids), the bucket shift
-    std::vector<uint32_t> sptPar, sptSlot;  // h0 shortest-path tree: parent, its adjacency slot
-    std::vector<uint32_t> sptPre;           // preorder number in that tree (source_order 2)
-    DevBuf<uint32_t> d_spt;     // per vertex {parent, slot of (parent -> v), f64 latency}
+    // host side of the graph preparation (upload_csr): shared with the peer engines of a
+    // multi-GPU build, which copy the device CSR from this engine instead of preparing it again
+    std::shared_ptr<HostPrep> hp;
+    int64_t csrHostRuns = 0;    // host-side preparations (peers that copied count none)
+    DevBuf<uint32_t> d_spt;     // per vertex {parent, slot of (v -> parent) in v's row, f64 latency}
+    DevBuf<uint32_t> d_sptPar;  // per vertex: h0-tree parent
     int wsK = 0;                // batch width the workspace was laid out for
-    int64_t wsRing = 0, wsOver = 0;
+    int64_t wsRing = 0;
     DevBuf<uint32_t> d_rowptr, d_adj;
     DevBuf<uint32_t> d_adjk;  // rows re-sorted by kappa = w - pi(col) (batch relaxation copy)
     DevBuf<float> d_kap, d_ksum, d_kap0;  // kappa of d_adjk (f32, rounded down), per-vertex probes
-    double piMax = 0.0;
     double meanLat = -1.0;
     uint64_t ipGen = 1, geomGen = 0;  // attach/detach generation; compute_geometry's copy  // mean non-loop edge latency (default delta), computed once
     DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
-    DevBuf<unsigned long long> d_dist, d_best, d_memo, d_ring, d_over, d_qa, d_qb;
+    DevBuf<unsigned long long> d_dist, d_best, d_memo, d_qa, d_qb;
+    DevBuf<uint32_t> d_ring;
     DevBuf<uint32_t> d_stamp, d_cnt, d_bslot, d_par, d_pathbuf,
         d_counters;
     int slots = 0;
     DevBuf<double2> d_lr;
     DevBuf<uint16_t> d_hops;
+    // a table installed in place (shdtopo_bind_table_ref): caller-owned HBM read instead of d_lr /
+    // d_hops until the next build or bind
+    const double2* extLr = nullptr;
+    const uint16_t* extHops = nullptr;
     DevBuf<double> d_rowmin;
     DevBuf<double> d_elatAA, d_elossAA, d_vlossA;
     DevBuf<uint32_t> d_sources, d_targets;
@@ -195,6 +198,8 @@ struct _Topology {
                               // dropped (topo_sssp_batch.hip)
     std::vector<uint32_t> adjkTargets;  // the target set whose bits d_adjk carries
     bool adjkFlagged = false;
+    bool adjkPlain = false;    // d_adjk / d_kap / d_ksum / d_kap0 are the plain kappa-sorted copy
+    bool adjkResorted = false; // ... re-sorted by the target-aware key of adjkTargets
     bool targetResort = true;  // option "target_resort": rows of the relaxation copy re-sorted
                                // by the target-aware key per target set (kappa-prefix cuts stop
                                // before heads that relax nothing reaching a target)
@@ -238,7 +243,7 @@ struct _Topology {
     // attached-set generations: setGen bumps whenever a vertex gains its first or loses its last
     // host (the table's columns change); tableGen = the setGen the device table was built for
     std::atomic<uint64_t> setGen{1};
-    uint64_t tableGen = 0;
+    std::atomic<uint64_t> tableGen{0};  // written under buildMu, read lock-free by table_current
     std::atomic<uint64_t> tableSerial{0};  // bumps on every device table build / bind
     bool geomInit = false;
 
@@ -403,44 +408,40 @@ int dev_init(Topology* top) {
     return 0;
 }
 
-// CSR without self loops, vertices relabelled by descending degree so that the hot (hub)
-// distance words cluster in a few cache lines (power-law graphs: most adjacency entries point
-// at hubs).  Self loops go to selfLat/selfLoss (first = lowest edge id, as orc_get_eid).
-SsspLdsPlan lds_plan(Topology* top);
-
-// IEEE half bits of x rounded up (up) or down (!up): directed rounding, so a stored bound never
-// tightens (+-inf for NaN).  Exact search over the finite halves, sorted once.
-uint16_t f16_directed(double x, bool up) {
-    static const std::vector<std::pair<double, uint16_t>> tab = [] {
-        std::vector<std::pair<double, uint16_t>> t;
-        for (uint32_t b = 0; b < 0x10000u; b++) {
-            const uint32_t e = (b >> 10) & 31u, m = b & 1023u;
-            if (e == 31u) continue;  // inf / NaN
-            const double mag = e == 0 ? std::ldexp((double)m, -24) : std::ldexp((double)(1024 + m), (int)e - 25);
-            t.push_back({(b & 0x8000u) ? -mag : mag, (uint16_t)b});
-        }
-        std::sort(t.begin(), t.end());
-        return t;
-    }();
-    if (std::isnan(x)) return up ? 0x7C00 : 0xFC00;
-    if (up) {
-        auto it = std::lower_bound(tab.begin(), tab.end(), std::make_pair(x, (uint16_t)0));
-        return it == tab.end() ? (uint16_t)0x7C00 : it->second;  // smallest half >= x
-    }
-    auto it = std::upper_bound(tab.begin(), tab.end(), std::make_pair(x, (uint16_t)0xFFFF));
-    return it == tab.begin() ? (uint16_t)0xFC00 : std::prev(it)->second;  // largest half <= x
-}
-
+int upload_csr_impl(Topology* top);
 int upload_csr(Topology* top) {
     if (top->csrUploaded) return 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int r = upload_csr_impl(top);
+    top->stats.csr_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return r;
+}
+
+// Hubs of the tail grouping: the tail is grouped by its highest-ranked neighbour
+// among the first kGroupHubs vertices of the degree order (the count the former single-source
+// kernel held in LDS, where the grouping was tuned).
+constexpr int64_t kGroupHubs = 16565;
+
+// Graph preparation.  Directed topologies only run the heap replay (its out-edge
+// rows, upload_replay) and keep their labels.  Undirected ones are prepared on the GPU
+// (topo_prep.hip): the parsed edge arrays are copied to HBM once, and the relabel, the CSR, the
+// h0 distances and tree and the kappa-sorted relaxation copy are built there; the host keeps only
+// perm / inv / pi / the h0-tree parents (source ordering of the batched builds, the replay CSR).
+int upload_csr_impl(Topology* top) {
     HostGraph& g = top->g;
     const int32_t V = g.V;
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t) {
+        return std::chrono::duration<double, std::milli>(clk::now() - t).count();
+    };
+    double host_ms = 0.0, copy_ms = 0.0;
+    top->hp = std::make_shared<HostPrep>();
+    top->csrHostRuns++;
     if (top->isDirected) {
-        // Directed topologies run only the heap replay (its out-edge rows: upload_replay); the
-        // batch kernel's undirected CSR, relabel and landmark are not built.  Identity labels.
-        top->perm.resize((size_t)V);
-        std::iota(top->perm.begin(), top->perm.end(), 0);
-        top->inv = top->perm;
+        const auto th = clk::now();
+        top->hp->perm.resize((size_t)V);
+        std::iota(top->hp->perm.begin(), top->hp->perm.end(), 0);
+        top->hp->inv = top->hp->perm;
         std::vector<double> selfLat((size_t)V, NAN), selfLoss((size_t)V, 0.0);
         for (int64_t e = 0; e < g.E; e++) {
             const int32_t a = g.eu[(size_t)e];
@@ -449,239 +450,107 @@ int upload_csr(Topology* top) {
                 selfLoss[(size_t)a] = g.eloss[(size_t)e];
             }
         }
+        host_ms += ms_since(th);
+        const auto tc = clk::now();
         HIPCHK(top->d_vloss.ensure((size_t)V));
         HIPCHK(top->d_selfLat.ensure((size_t)V));
         HIPCHK(top->d_selfLoss.ensure((size_t)V));
         HIPCHK(hipMemcpy(top->d_vloss.p, g.vloss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_selfLat.p, selfLat.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(top->d_selfLoss.p, selfLoss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
+        copy_ms += ms_since(tc);
+        top->stats.csr_host_ms = host_ms;
+        top->stats.csr_copy_ms = copy_ms;
         top->csrUploaded = true;
         return 0;
     }
-    std::vector<uint32_t> deg((size_t)V, 0);
-    for (int64_t e = 0; e < g.E; e++) {
-        int32_t a = g.eu[(size_t)e], b = g.ev[(size_t)e];
-        if (a == b) continue;
-        deg[(size_t)a]++;
-        deg[(size_t)b]++;
+    const int64_t E = g.E;
+    if (2 * E >= (int64_t)INT32_MAX || (int64_t)V >= (int64_t)1 << 30) {
+        CRITICAL("topology too large for the device CSR (%d vertices, %lld edges)", V, (long long)E);
+        return -7;
     }
-    // 1) hubs: the H highest-degree vertices take ids 0..H-1 (their distances live in LDS)
-    top->perm.resize((size_t)V);
-    std::iota(top->perm.begin(), top->perm.end(), 0);
-    std::stable_sort(top->perm.begin(), top->perm.end(),
-                     [&](int32_t x, int32_t y) { return deg[(size_t)x] > deg[(size_t)y]; });
-    // 2) tail: grouped by "primary hub" (its highest-degree hub neighbour), so that expanding a
-    //    hub relaxes a dense run of tail distance words (8 per 64-B line) instead of one random
-    //    line per neighbour -- the SSSP is bound by random DRAM requests (profiles/).
-    const int64_t H = (int64_t)lds_plan(top).H;
-    if (getenv("SHDTOPO_NO_TAILGROUP") == nullptr && H < V) {
-        std::vector<int32_t> hubrank((size_t)V, INT32_MAX);
-        for (int64_t i = 0; i < H; i++) hubrank[(size_t)top->perm[(size_t)i]] = (int32_t)i;
-        std::vector<int32_t> primary((size_t)V, INT32_MAX);
-        for (int64_t e = 0; e < g.E; e++) {
-            int32_t a = g.eu[(size_t)e], b = g.ev[(size_t)e];
-            if (a == b) continue;
-            primary[(size_t)a] = std::min(primary[(size_t)a], hubrank[(size_t)b]);
-            primary[(size_t)b] = std::min(primary[(size_t)b], hubrank[(size_t)a]);
-        }
-        std::stable_sort(top->perm.begin() + H, top->perm.end(), [&](int32_t x, int32_t y) {
-            return primary[(size_t)x] < primary[(size_t)y];
-        });
-    }
-    top->inv.resize((size_t)V);
-    for (int32_t i = 0; i < V; i++) top->inv[(size_t)top->perm[(size_t)i]] = i;
-    std::vector<uint32_t> rowptr((size_t)V + 1, 0);
-    for (int32_t i = 0; i < V; i++) rowptr[(size_t)i + 1] = rowptr[(size_t)i] + deg[(size_t)top->perm[(size_t)i]];
-    const size_t nadj = rowptr[(size_t)V];
-    std::vector<uint32_t> col(nadj);
-    std::vector<double> wt(nadj), aloss(nadj);
-    std::vector<uint32_t> fillp(rowptr.begin(), rowptr.end() - 1);
-    std::vector<double> selfLat((size_t)V, NAN), selfLoss((size_t)V, 0.0), vloss((size_t)V);
-    for (int64_t e = 0; e < g.E; e++) {
-        int32_t a = g.eu[(size_t)e], b = g.ev[(size_t)e];
-        int32_t na = top->inv[(size_t)a], nb = top->inv[(size_t)b];
-        if (a == b) {
-            if (std::isnan(selfLat[(size_t)na])) {
-                selfLat[(size_t)na] = g.elat[(size_t)e];
-                selfLoss[(size_t)na] = g.eloss[(size_t)e];
-            }
-            continue;
-        }
-        size_t pa = fillp[(size_t)na]++, pb = fillp[(size_t)nb]++;
-        col[pa] = (uint32_t)nb; wt[pa] = g.elat[(size_t)e]; aloss[pa] = g.eloss[(size_t)e];
-        col[pb] = (uint32_t)na; wt[pb] = g.elat[(size_t)e]; aloss[pb] = g.eloss[(size_t)e];
-    }
-    // each row sorted by neighbour: a hub's expansion then walks the distance array in address
-    // order (neighbours sharing a line coalesce, DRAM pages are reused)
-    top->rowsSorted = getenv("SHDTOPO_NO_ROWSORT") == nullptr;
-    if (top->rowsSorted) {
-        std::vector<uint32_t> idx;
-        std::vector<uint32_t> c2;
-        std::vector<double> w2, l2;
-        for (int32_t i = 0; i < V; i++) {
-            size_t b = rowptr[(size_t)i], e = rowptr[(size_t)i + 1];
-            if (e - b < 2) continue;
-            idx.resize(e - b);
-            std::iota(idx.begin(), idx.end(), 0u);
-            std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
-                return col[b + x] < col[b + y] || (col[b + x] == col[b + y] && x < y);
-            });
-            c2.resize(e - b); w2.resize(e - b); l2.resize(e - b);
-            for (size_t k = 0; k < e - b; k++) {
-                c2[k] = col[b + idx[k]]; w2[k] = wt[b + idx[k]]; l2[k] = aloss[b + idx[k]];
-            }
-            std::copy(c2.begin(), c2.end(), col.begin() + (long)b);
-            std::copy(w2.begin(), w2.end(), wt.begin() + (long)b);
-            std::copy(l2.begin(), l2.end(), aloss.begin() + (long)b);
-        }
-    }
-    for (int32_t i = 0; i < V; i++) vloss[(size_t)i] = g.vloss[(size_t)top->perm[(size_t)i]];
-    // batch mode: distances from the top hub (vertex 0 after the relabel).  pi(s) = d(h0, s)
-    // shifts source s's buckets so that the batch's sources reach a vertex in the same bucket
-    // (see topo_sssp_batch.hip); only an estimate: any shift keeps the SSSP exact.
+    hipStream_t st = top->stream;
+    // 1) the parsed graph to HBM (document order)
+    DevBuf<int32_t> eu, ev;
+    DevBuf<double> elat, eloss, vl0;
+    HIPCHK(eu.ensure((size_t)E));
+    HIPCHK(ev.ensure((size_t)E));
+    HIPCHK(elat.ensure((size_t)E));
+    HIPCHK(eloss.ensure((size_t)E));
+    HIPCHK(vl0.ensure((size_t)V));
     {
-        top->pot.assign((size_t)V, INFINITY);
-        top->sptPar.assign((size_t)V, 0xFFFFFFFFu);
-        top->sptSlot.assign((size_t)V, 0xFFFFFFFFu);
-        using QE = std::pair<double, int32_t>;
-        std::priority_queue<QE, std::vector<QE>, std::greater<QE>> pq;
-        top->pot[0] = 0.0;
-        pq.push({0.0, 0});
-        while (!pq.empty()) {
-            const QE t = pq.top();
-            pq.pop();
-            if (t.first > top->pot[(size_t)t.second]) continue;
-            for (uint32_t k = rowptr[(size_t)t.second]; k < rowptr[(size_t)t.second + 1]; k++) {
-                const double a = t.first + wt[k];
-                if (a < top->pot[col[k]]) {
-                    top->pot[col[k]] = a;
-                    top->sptPar[col[k]] = (uint32_t)t.second;  // h0-tree parent: the batch
-                    top->sptSlot[col[k]] = k;                  // parent pass' first guess
-                    pq.push({a, (int32_t)col[k]});
-                }
-            }
-        }
+        const auto tc = clk::now();
+        HIPCHK(hipMemcpyAsync(eu.p, g.eu.data(), 4 * (size_t)E, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(ev.p, g.ev.data(), 4 * (size_t)E, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(elat.p, g.elat.data(), 8 * (size_t)E, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(eloss.p, g.eloss.data(), 8 * (size_t)E, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(vl0.p, g.vloss.data(), 8 * (size_t)V, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+        copy_ms += ms_since(tc);
     }
+    // 2) degrees, relabel, rows
+    DevBuf<uint32_t> deg, selfE, dperm, dinv;
+    HIPCHK(deg.ensure((size_t)V));
+    HIPCHK(selfE.ensure((size_t)V));
+    int64_t nadj = 0;
+    HIPCHK(prep_degrees(V, E, eu.p, ev.p, deg.p, selfE.p, &nadj, st));
+    const uint32_t H = (uint32_t)std::min<int64_t>(kGroupHubs, V);
+    HIPCHK(dperm.ensure((size_t)V));
+    HIPCHK(dinv.ensure((size_t)V));
     HIPCHK(top->d_rowptr.ensure((size_t)V + 1));
-    HIPCHK(top->d_adj.ensure(4 * nadj));
-    HIPCHK(top->d_aloss.ensure(nadj));
     HIPCHK(top->d_vloss.ensure((size_t)V));
     HIPCHK(top->d_selfLat.ensure((size_t)V));
     HIPCHK(top->d_selfLoss.ensure((size_t)V));
-    HIPCHK(hipMemcpy(top->d_rowptr.p, rowptr.data(), sizeof(uint32_t) * ((size_t)V + 1), hipMemcpyHostToDevice));
-    if (nadj) {
-        // kappa0 of every vertex: the smallest kappa = w - pi(col) of its row (+inf: empty row,
-        // -inf: pi unknown), as the kappa-sorted copy below computes it
-        std::vector<double> kmin((size_t)V, INFINITY);
-        for (int32_t v = 0; v < V; v++)
-            for (uint32_t k = rowptr[(size_t)v]; k < rowptr[(size_t)v + 1]; k++) {
-                const double pv = top->pot[col[k]];
-                kmin[(size_t)v] = std::min(kmin[(size_t)v], std::isfinite(pv) ? wt[k] - pv : -INFINITY);
-            }
-        // 16-B records {col, pi(col) as f32 rounded up | {f16 pi up, f16 kappa0 down}, f64 w}
-        std::vector<uint32_t> adj(4 * nadj);
-        for (size_t k = 0; k < nadj; k++) {
-            uint64_t wb;
-            memcpy(&wb, &wt[k], 8);
-            const double pv = top->pot[col[k]];
-            uint32_t pb;
-            if (kKapInRec) {
-                pb = ((uint32_t)f16_directed(std::isfinite(pv) ? pv : INFINITY, true) << 16) |
-                     (uint32_t)f16_directed(kmin[col[k]], false);
-            } else {
-                float pf = (float)pv;
-                if (std::isfinite(pv) && (double)pf < pv) pf = std::nextafter(pf, INFINITY);
-                if (!std::isfinite(pv)) pf = INFINITY;
-                memcpy(&pb, &pf, 4);
-            }
-            adj[4 * k] = col[k];
-            adj[4 * k + 1] = pb;
-            adj[4 * k + 2] = (uint32_t)wb;
-            adj[4 * k + 3] = (uint32_t)(wb >> 32);
-        }
-        HIPCHK(hipMemcpy(top->d_adj.p, adj.data(), sizeof(uint32_t) * 4 * nadj, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_aloss.p, aloss.data(), sizeof(double) * nadj, hipMemcpyHostToDevice));
-        // Batch relaxation copy: each row re-sorted by kappa = w - pi(col).  The landmark filter
-        // keeps edge (u, v) for source j only if d_j(u) + w <= d_j(h0) + pi(v), i.e. kappa <=
-        // d_j(h0) - d_j(u) (+ margin): a prefix of the kappa-sorted row, whose end the kernel
-        // finds from 4 per-vertex probes (kappa at row positions 0, 1, 3, 7) and, past those,
-        // a binary search in d_kap.  kappa is stored rounded down, so a cut is never too early.
-        std::vector<uint32_t> adjk(4 * nadj);
-        std::vector<float> kap(nadj), ksum(kKProbes * (size_t)V);
-        std::vector<uint32_t> ord;
-        std::vector<double> kd;
-        auto down = [](double x) {
-            if (std::isnan(x)) return -INFINITY;
-            float f = (float)x;
-            if ((double)f > x) f = std::nextafter(f, -INFINITY);
-            return f;
-        };
-        for (int32_t v = 0; v < V; v++) {
-            const uint32_t b = rowptr[(size_t)v], e = rowptr[(size_t)v + 1];
-            ord.resize(e - b);
-            kd.resize(e - b);
-            for (uint32_t k = b; k < e; k++) {
-                const double pv = top->pot[col[k]];
-                kd[k - b] = std::isfinite(pv) ? wt[k] - pv : -INFINITY;
-                ord[k - b] = k;
-            }
-            std::stable_sort(ord.begin(), ord.end(),
-                             [&](uint32_t x, uint32_t y) { return kd[x - b] < kd[y - b]; });
-            for (uint32_t i = 0; i < e - b; i++) {
-                const uint32_t k = ord[i];
-                std::copy(adj.begin() + 4 * (size_t)k, adj.begin() + 4 * (size_t)k + 4,
-                          adjk.begin() + 4 * (size_t)(b + i));
-                // bit 31 of the relaxation copy's column: this edge is the h0-tree edge into
-                // the column (its parent pass finds it without a recorded hint)
-                if (top->sptPar[col[k]] == (uint32_t)v) adjk[4 * (size_t)(b + i)] |= 0x80000000u;
-                kap[b + i] = down(kd[k - b]);
-            }
-            static const uint32_t probe[8] = {0, 1, 3, 7, 15, 31, 63, 127};
-            for (int q = 0; q < kKProbes; q++)
-                ksum[kKProbes * (size_t)v + q] = probe[q] < e - b ? kap[b + probe[q]] : INFINITY;
-        }
-        top->piMax = 0.0;
-        for (double p : top->pot) if (std::isfinite(p)) top->piMax = std::max(top->piMax, p);
-        HIPCHK(top->d_adjk.ensure(4 * nadj));
-        HIPCHK(top->d_kap.ensure(nadj));
-        HIPCHK(top->d_ksum.ensure(kKProbes * (size_t)V));
-        HIPCHK(top->d_kap0.ensure((size_t)V));
-        {
-            std::vector<uint32_t> spt(4 * (size_t)V, 0xFFFFFFFFu);
-            for (int32_t v = 0; v < V; v++) {
-                const uint32_t k = top->sptSlot[(size_t)v];
-                if (k == 0xFFFFFFFFu) continue;
-                uint64_t wb;
-                memcpy(&wb, &wt[k], 8);
-                spt[4 * (size_t)v] = top->sptPar[(size_t)v];
-                spt[4 * (size_t)v + 1] = k;
-                spt[4 * (size_t)v + 2] = (uint32_t)wb;
-                spt[4 * (size_t)v + 3] = (uint32_t)(wb >> 32);
-            }
-            HIPCHK(top->d_spt.ensure(4 * (size_t)V));
-            HIPCHK(hipMemcpy(top->d_spt.p, spt.data(), sizeof(uint32_t) * 4 * (size_t)V,
-                             hipMemcpyHostToDevice));
-        }
-        std::vector<float> k0((size_t)V);
-        for (int32_t v = 0; v < V; v++) k0[(size_t)v] = ksum[kKProbes * (size_t)v];
-        HIPCHK(hipMemcpy(top->d_kap0.p, k0.data(), sizeof(float) * (size_t)V, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_adjk.p, adjk.data(), sizeof(uint32_t) * 4 * nadj, hipMemcpyHostToDevice));
-        top->adjkFlagged = false;  // no target bits yet (set per target set before a batch launch)
-        top->adjkTargets.clear();
-        HIPCHK(hipMemcpy(top->d_kap.p, kap.data(), sizeof(float) * nadj, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_ksum.p, ksum.data(), sizeof(float) * kKProbes * (size_t)V, hipMemcpyHostToDevice));
+    HIPCHK(prep_relabel(V, E, H, eu.p, ev.p, deg.p, selfE.p, elat.p, eloss.p, vl0.p, dperm.p,
+                        dinv.p, top->d_rowptr.p, top->d_vloss.p, top->d_selfLat.p,
+                        top->d_selfLoss.p, st));
+    deg.release();
+    selfE.release();
+    vl0.release();
+    HIPCHK(top->d_adj.ensure(4 * (size_t)nadj));
+    HIPCHK(top->d_aloss.ensure((size_t)nadj));
+    HIPCHK(prep_adjacency(V, E, nadj, eu.p, ev.p, dinv.p, elat.p, eloss.p, top->d_adj.p,
+                          top->d_aloss.p, st));
+    eu.release(); ev.release(); elat.release(); eloss.release();
+    // 3) pi = d(h0, .), the h0 tree, the records' landmark fields
+    HIPCHK(top->d_pot.ensure((size_t)V));
+    int iters = 0;
+    HIPCHK(prep_h0_distances(V, top->d_rowptr.p, top->d_adj.p, top->d_pot.p, &iters, st));
+    top->stats.csr_h0_rounds = iters;
+    HIPCHK(top->d_sptPar.ensure((size_t)V));
+    HIPCHK(top->d_spt.ensure(4 * (size_t)V));
+    HIPCHK(prep_tree(V, nadj, H, top->d_rowptr.p, top->d_adj.p, top->d_pot.p, top->d_sptPar.p,
+                     top->d_spt.p, &top->hp->piMax, st));
+    // 4) the kappa-sorted relaxation copy
+    HIPCHK(top->d_adjk.ensure(4 * (size_t)nadj));
+    HIPCHK(top->d_kap.ensure((size_t)nadj));
+    HIPCHK(top->d_ksum.ensure(kKProbes * (size_t)V));
+    HIPCHK(top->d_kap0.ensure((size_t)V));
+    HIPCHK(launch_kappa_copy(V, nadj, H, top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
+                             top->d_sptPar.p, top->d_adjk.p, top->d_kap.p, top->d_ksum.p,
+                             top->d_kap0.p, st));
+    top->adjkPlain = true;
+    top->adjkFlagged = false;
+    top->adjkTargets.clear();
+    top->rowsSorted = true;
+    // 5) what the host keeps
+    {
+        const auto tc = clk::now();
+        top->hp->perm.resize((size_t)V);
+        top->hp->inv.resize((size_t)V);
+        top->hp->pot.resize((size_t)V);
+        top->hp->sptPar.resize((size_t)V);
+        HIPCHK(hipMemcpyAsync(top->hp->perm.data(), dperm.p, 4 * (size_t)V, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(top->hp->inv.data(), dinv.p, 4 * (size_t)V, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(top->hp->pot.data(), top->d_pot.p, 8 * (size_t)V, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(top->hp->sptPar.data(), top->d_sptPar.p, 4 * (size_t)V, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        copy_ms += ms_since(tc);
     }
-    HIPCHK(hipMemcpy(top->d_vloss.p, vloss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(top->d_selfLat.p, selfLat.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(top->d_selfLoss.p, selfLoss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
+    top->stats.csr_host_ms = host_ms;
+    top->stats.csr_copy_ms = copy_ms;
     top->csrUploaded = true;
     return 0;
-}
-
-SsspLdsPlan lds_plan(Topology* top) {
-    return sssp_lds_plan(top->wgPerCu, top->hubLimit,
-                         (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 30)),
-                         top->g.V);
 }
 
 DevCSR dev_csr(Topology* top) {
@@ -695,94 +564,90 @@ DevCSR dev_csr(Topology* top) {
     c.ksum = reinterpret_cast<const float4*>(top->d_ksum.p);
     c.kap0 = top->d_kap0.p;
     c.spt = top->d_spt.p;
-    c.piMax = top->piMax;
+    c.piMax = top->hp->piMax;
     c.aloss = top->d_aloss.p;
     c.vloss = top->d_vloss.p;
     c.selfLat = top->d_selfLat.p;
     c.selfLoss = top->d_selfLoss.p;
     c.rows_sorted = top->rowsSorted ? 1 : 0;
-    c.tflags = top->adjkFlagged && top->targetSkip ? 1 : 0;
+    c.tflags = top->adjkFlagged && top->targetSkip ? 1 : 0;  // marks of the launch's target set
     return c;
 }
 
-int batch_k(Topology* top) {
-    const int k = top->batchK;
-    return (k == 2 || k == 4 || k == 8 || k == 16) ? k : 1;
-}
-int64_t ring_entries(Topology* top, int K) {  // batch kernel: the parent pass' pair list
-    // batch: V * K pair list + V vertex list (parent pass), then the sweep's pending bitmap
-    return K <= 1 ? (int64_t)kRingPerVertex * top->g.V
-                  : (int64_t)top->g.V * (K + 1) + (top->g.V + 31) / 32 + 64 +
-                        (top->g.V * K + 31) / 32 + 64;
-}
-int64_t queue_stride(Topology* top, int K) {  // u64 per slot of each near queue
+int batch_k(Topology* top) { return top->batchK; }  // 2, 4, 8 or 16 (shdtopo_set_option)
+
+// Per-slot u32 scratch after the parent pass' V * K pair list: the merged vertex list (V), the
+// sweep's pending bitmap, the (vertex, source) tie bitmap and the touched-line bitmap (a tail
+// vertex whose distance line the batch lowered from +inf: only those lines are reset for the
+// next batch).
+int64_t bitmap_words(int64_t n) { return (n + 31) / 32 + 64; }
+int64_t ring_entries(Topology* top, int K) {
     const int64_t V = top->g.V;
-    return K <= 1 ? (int64_t)kNearPerVertex * V : std::max<int64_t>(kNearPerVertex * V, V * K / 2);
+    return V * (K + 1) + bitmap_words(V) + bitmap_words(V * K) + bitmap_words(V);
 }
-int64_t over_entries(Topology* top, int K) {  // the batch kernel keeps no overflow pile
-    return K <= 1 ? (int64_t)kOverPerVertex * top->g.V : 0;
+int64_t queue_stride(Topology* top, int K) {  // u64 per slot of each near queue / pair list
+    const int64_t V = top->g.V;
+    return std::max<int64_t>(2 * V, V * K / 2);
 }
 
-// Per-slot workspace.  Single-source mode (K = 1): 264 B x V.  Batch mode:
-// dist [V][K], two K-bit masks per vertex, u32 near queues, the (vertex, source) window and pile,
-// plus the per-source parent-pass arrays (reused for each source of the batch).
+// Per-slot workspace of the batched SSSP: dist [V][K], two K-bit masks per
+// vertex, two queues, the per-(vertex, source) parent-pass arrays, the scratch bitmaps.
 int ensure_workspace(Topology* top, int nsrc) {
     const int64_t V = top->g.V;
     const int K = batch_k(top);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, top->device));
-    // batch mode: a short shard runs fewer sources per batch (auto batch_fill), so it can use a
-    // slot per source up to the CUs' slots -- sized by sources, not by batches of K (an 8-GPU
-    // shard of 1,250 rows got 157 slots for 250 batches of 5: 120 ms instead of 73)
-    const int units = (K > 1 && top->batchFill > 0) ? (nsrc + top->batchFill - 1) / top->batchFill
-                                                    : nsrc;
-    int want = top->slotsOpt > 0 ? top->slotsOpt
-                                 : prop.multiProcessorCount *
-                                       (K > 1 ? kBatchWgPerCu : sssp_max_blocks_per_cu(top->wgPerCu));
-    const size_t maskb = K > 1 ? 2 * (((size_t)V * (K <= 8 ? 1 : 2) + 255) / 256 * 256) : 0;
+    // a short shard runs fewer sources per batch (auto batch_fill), so it can use a slot per
+    // source up to the CUs' slots -- sized by sources, not by batches of K (an 8-GPU shard of
+    // 1,250 rows got 157 slots for 250 batches of 5: 120 ms instead of 73)
+    const int units = top->batchFill > 0 ? (nsrc + top->batchFill - 1) / top->batchFill : nsrc;
+    int want = top->slotsOpt > 0 ? top->slotsOpt : prop.multiProcessorCount * kBatchWgPerCu;
+    const size_t maskb = 2 * (((size_t)V * (K <= 8 ? 1 : 2) + 255) / 256 * 256);
     const int64_t ringE = ring_entries(top, K);
-    const int64_t overE = over_entries(top, K);
-    const size_t hparN = K > 1 ? (size_t)std::min<int64_t>(top->parHubs, 1 << 20) * K : 0;
-    // dist (K words/vertex), per-(vertex, source) best/memo 16 B + stamp/cnt/bslot/par 16 B, near
-    // queues, window (u64 entries single-source, u32 pair list batched), overflow piles
+    const size_t hparN = (size_t)std::min<int64_t>(top->parHubs, 1 << 20) * K;
+    // dist (K words/vertex), per-(vertex, source) best/memo 16 B + stamp/cnt/bslot/par 16 B, the
+    // queues, the u32 scratch, masks, hub hints, path buffer
     const int64_t qs = queue_stride(top, K);
-    size_t per_slot = (size_t)V * (8 * (size_t)K + 32 * (size_t)K) + 16 * (size_t)qs +
-                      (size_t)ringE * (K > 1 ? 4 : 8) + (size_t)overE * (K > 1 ? 16 : 32) + maskb + 4 * hparN +
-                      (size_t)kMaxHops * kSsspBlock * 4 + 16;
+    const size_t per_slot = (size_t)V * (8 * (size_t)K + 32 * (size_t)K) + 16 * (size_t)qs +
+                            (size_t)ringE * 4 + maskb + 4 * hparN +
+                            (size_t)kMaxHops * kSsspBlock * 4 + 16;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     // memory already held by this workspace counts as available
-    const size_t held = top->slots > 0 ? top->d_dist.n * 8 + top->d_ring.n * 8 + top->d_over.n * 8 : 0;
+    const size_t held = top->slots > 0 ? (size_t)top->slots * per_slot : 0;
     int memcap = (int)std::max<size_t>(1, ((freeb + held) * 3 / 5) / per_slot);
     want = std::min(want, memcap);
     want = std::max(1, std::min(want, std::max(1, units)));
-    if (top->slots >= want && top->wsK == K && top->wsRing == ringE && top->wsOver == overE) return 0;
+    if (top->slots >= want && top->wsK == K && top->wsRing == ringE) return 0;
     if (top->slots > 0) {
         // layout change: release before re-allocating
-        top->d_dist.release(); top->d_ring.release(); top->d_over.release();
+        top->d_dist.release(); top->d_ring.release(); top->d_best.release();
+        top->d_memo.release(); top->d_stamp.release(); top->d_cnt.release();
+        top->d_bslot.release(); top->d_par.release(); top->d_pathbuf.release();
         top->d_qa.release(); top->d_qb.release(); top->d_mask.release(); top->d_hpar.release();
         top->slots = 0;
     }
     const size_t n = (size_t)want * (size_t)V;
     const size_t pn = n * (size_t)K;  // per-(vertex, source) arrays
-    HIPCHK(top->d_dist.ensure(n * (size_t)K));
+    HIPCHK(top->d_dist.ensure(pn));
     HIPCHK(top->d_best.ensure(pn));
     HIPCHK(top->d_memo.ensure(pn));
     HIPCHK(top->d_stamp.ensure(pn));
     HIPCHK(top->d_qa.ensure((size_t)want * (size_t)qs));
     HIPCHK(top->d_qb.ensure((size_t)want * (size_t)qs));
-    HIPCHK(top->d_ring.ensure((size_t)want * (size_t)ringE * (K > 1 ? 4 : 8) / 8));
-    HIPCHK(top->d_over.ensure((size_t)want * (size_t)overE * (K > 1 ? 2 : 4)));
+    HIPCHK(top->d_ring.ensure((size_t)want * (size_t)ringE));
     HIPCHK(top->d_cnt.ensure(pn));
     HIPCHK(top->d_bslot.ensure(pn));
     HIPCHK(top->d_par.ensure(pn));
     HIPCHK(top->d_pathbuf.ensure((size_t)want * kMaxHops * kSsspBlock));
     HIPCHK(top->d_counters.ensure((size_t)want * 4));
-    if (K > 1) {
-        HIPCHK(top->d_mask.ensure((size_t)want * maskb));
-        HIPCHK(top->d_hpar.ensure(std::max<size_t>(1, (size_t)want * hparN)));
-        HIPCHK(hipMemsetAsync(top->d_mask.p, 0, (size_t)want * maskb, top->stream));
-    }
+    HIPCHK(top->d_mask.ensure((size_t)want * maskb));
+    HIPCHK(top->d_hpar.ensure(std::max<size_t>(1, (size_t)want * hparN)));
+    HIPCHK(hipMemsetAsync(top->d_mask.p, 0, (size_t)want * maskb, top->stream));
+    // every distance starts at +inf and no line is marked touched: a batch resets only the lines
+    // it touched (the kernel's init)
+    HIPCHK(launch_fill_u64(top->d_dist.p, 0x7FF0000000000000ull, (int64_t)pn, top->stream));
+    HIPCHK(hipMemsetAsync(top->d_ring.p, 0, sizeof(uint32_t) * (size_t)want * (size_t)ringE, top->stream));
     HIPCHK(hipMemsetAsync(top->d_stamp.p, 0, sizeof(uint32_t) * pn, top->stream));
     HIPCHK(hipMemsetAsync(top->d_memo.p, 0, sizeof(unsigned long long) * pn, top->stream));
     HIPCHK(hipMemsetAsync(top->d_counters.p, 0, sizeof(uint32_t) * (size_t)want * 4, top->stream));
@@ -790,7 +655,6 @@ int ensure_workspace(Topology* top, int nsrc) {
     top->slots = want;
     top->wsK = K;
     top->wsRing = ringE;
-    top->wsOver = overE;
     top->stats.slots = want;
     return 0;
 }
@@ -800,14 +664,13 @@ SlotWs slot_ws(Topology* top) {
     w.slots = top->slots;
     w.V = top->g.V;
     w.dist = top->d_dist.p; w.stamp = top->d_stamp.p;
-    w.qa = top->d_qa.p; w.qb = top->d_qb.p; w.ring = top->d_ring.p; w.over = top->d_over.p;
+    w.qa = top->d_qa.p; w.qb = top->d_qb.p; w.ring = top->d_ring.p;
     w.best = top->d_best.p; w.cnt = top->d_cnt.p; w.bslot = top->d_bslot.p;
     w.memo = top->d_memo.p; w.par = top->d_par.p; w.pathbuf = top->d_pathbuf.p;
     w.counters = top->d_counters.p;
-    w.K = top->wsK > 1 ? top->wsK : 1;
+    w.K = top->wsK;
     w.ring_entries = top->wsRing;
     w.q_stride = queue_stride(top, w.K);
-    w.over_entries = top->wsOver;
     w.mask = top->d_mask.p;
     w.hpar = top->d_hpar.p;
     return w;
@@ -820,8 +683,16 @@ SlotWs slot_ws(Topology* top) {
 // and are dropped; a parallel group becomes one entry with the group's minimum latency (same
 // heap history, topo_replay.hip) and the lowest edge id's latency/loss for the hop
 // (igraph_get_eid as orc_get_eid).  Needs perm/inv (upload_csr).
+int upload_replay_impl(Topology* top);
 int upload_replay(Topology* top) {
     if (top->replayUploaded) return 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int r = upload_replay_impl(top);
+    top->stats.replay_prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return r;
+}
+
+int upload_replay_impl(Topology* top) {
     const HostGraph& g = top->g;
     const int32_t V = g.V;
     const bool dir = top->isDirected;
@@ -859,7 +730,7 @@ int upload_replay(Topology* top) {
         const uint32_t id = o2[i];
         if (i == 0 || ex[id] != ex[o2[i - 1]] || ey[id] != ey[o2[i - 1]]) {
             gstart.push_back(i);
-            rowptr[(size_t)top->inv[(size_t)ex[id]] + 1]++;
+            rowptr[(size_t)top->hp->inv[(size_t)ex[id]] + 1]++;
         }
     }
     for (int32_t k = 0; k < V; k++) rowptr[(size_t)k + 1] += rowptr[(size_t)k];
@@ -873,16 +744,16 @@ int upload_replay(Topology* top) {
         const uint32_t id0 = o2[b];  // lowest edge id of the group: igraph_get_eid's edge
         double w = g.elat[(size_t)ee[id0]];
         for (size_t i = b + 1; i < e; i++) w = std::min(w, g.elat[(size_t)ee[o2[i]]]);
-        const uint32_t x = (uint32_t)top->inv[(size_t)ex[id0]];
+        const uint32_t x = (uint32_t)top->hp->inv[(size_t)ex[id0]];
         const uint32_t k = fill[x]++;
         uint64_t wb;
         memcpy(&wb, &w, 8);
         // pi(y) = d(h0, y) rounded up to f32: the replay's landmark skip (topo_replay.hip)
-        const uint32_t y = (uint32_t)top->inv[(size_t)ey[id0]];
+        const uint32_t y = (uint32_t)top->hp->inv[(size_t)ey[id0]];
         float pf = INFINITY;
-        if (!dir && y < top->pot.size() && std::isfinite(top->pot[y])) {
-            pf = (float)top->pot[y];
-            if ((double)pf < top->pot[y]) pf = std::nextafter(pf, INFINITY);
+        if (!dir && y < top->hp->pot.size() && std::isfinite(top->hp->pot[y])) {
+            pf = (float)top->hp->pot[y];
+            if ((double)pf < top->hp->pot[y]) pf = std::nextafter(pf, INFINITY);
         }
         uint32_t pb;
         memcpy(&pb, &pf, 4);
@@ -912,7 +783,7 @@ ReplayCSR replay_csr(Topology* top) {
     c.rec = top->d_rrec.p;
     c.own = top->d_rown.p;
     // pi values exist for undirected topologies (upload_csr: d(h0, .) from relabelled vertex 0)
-    c.landmark = (!top->isDirected && top->replayLandmark && !top->pot.empty()) ? 0 : -1;
+    c.landmark = (!top->isDirected && top->replayLandmark && top->hp && !top->hp->pot.empty()) ? 0 : -1;
     c.hop = top->d_rhop.p;
     c.vloss = top->d_vloss.p;
     c.selfLat = top->d_selfLat.p;
@@ -1026,6 +897,14 @@ double default_delta(Topology* top) {
     return std::max(1e-9, (batch_k(top) > 1 ? 0.2 : 0.06) * mean);
 }
 
+// per-build cold-path timings start at 0: a build that finds the graph (or the target set)
+// already prepared reports 0 for that step
+void reset_build_stats(Topology* top) {
+    top->stats.csr_ms = top->stats.csr_host_ms = top->stats.csr_copy_ms = 0.0;
+    top->stats.order_ms = top->stats.replay_prep_ms = top->stats.target_prep_ms = 0.0;
+    top->stats.csr_host_runs = 0;
+}
+
 // Enqueue rows [row0,row1) into out buffers (device pointers) on `st`.
 int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uint16_t* out_hops,
                  double* out_rowmin, hipStream_t st) {
@@ -1074,8 +953,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         const bool allReplay = top->isDirected || top->replayAll || top->hasMultiEdges || dense;
         top->stats.tie_dense = dense ? 1 : 0;
         std::vector<uint32_t> src((size_t)rows), tgt((size_t)A);
-        for (int64_t i = 0; i < rows; i++) src[(size_t)i] = (uint32_t)top->inv[(size_t)top->attached[(size_t)(row0 + i)]];
-        for (int64_t i = 0; i < A; i++) tgt[(size_t)i] = (uint32_t)top->inv[(size_t)top->attached[(size_t)i]];
+        for (int64_t i = 0; i < rows; i++) src[(size_t)i] = (uint32_t)top->hp->inv[(size_t)top->attached[(size_t)(row0 + i)]];
+        for (int64_t i = 0; i < A; i++) tgt[(size_t)i] = (uint32_t)top->hp->inv[(size_t)top->attached[(size_t)i]];
         HIPCHK(top->d_sources.ensure((size_t)rows));
         HIPCHK(top->d_targets.ensure((size_t)A));
         HIPCHK(hipMemcpyAsync(top->d_sources.p, src.data(), sizeof(uint32_t) * (size_t)rows, hipMemcpyHostToDevice, st));
@@ -1089,30 +968,44 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             HIPCHK(hipMemsetAsync(top->d_rowflag.p, 0, (size_t)rows, st));
             SlotWs ws = slot_ws(top);
             ws.rowflag = top->d_rowflag.p;
-            if (K > 1 && top->targetSkip && top->g.V < (1 << 30) && top->adjkTargets != tgt) {
+            // The relaxation copy's target-derived content (bit 30 target marks, the records'
+            // target-aware kappa field, the rows re-sorted by it) belongs to one target set: a new
+            // set first restores the plain copy from d_adj (stale keys of an older set
+            // would cut rows that lead to the new targets), then prepares the new set if the
+            // target skip is on.
+            const int64_t nadjk = (int64_t)(top->d_adjk.n / 4);
+            if (!top->adjkPlain && top->adjkTargets != tgt) {
+                HIPCHK(launch_kappa_copy(top->g.V, nadjk, (uint32_t)std::min<int64_t>(kGroupHubs, top->g.V),
+                                         top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
+                                         top->d_sptPar.p, top->d_adjk.p, top->d_kap.p,
+                                         top->d_ksum.p, top->d_kap0.p, st));
+                top->adjkPlain = true;
+                top->adjkFlagged = false;
+                top->adjkResorted = false;
+                top->adjkTargets.clear();
+            }
+            if (top->targetSkip && top->adjkPlain) {
                 // bit 30 of the relaxation copy's columns: the current target set
                 const auto tp0 = std::chrono::steady_clock::now();
                 r = upload_target_bits(top, tgt, st);
                 if (r) return r;
-                const int64_t nadj = (int64_t)(top->d_adjk.n / 4);
-                HIPCHK(launch_mark_targets(top->d_adjk.p, nadj, top->d_tbits.p, st));
+                HIPCHK(launch_mark_targets(top->d_adjk.p, nadjk, top->d_tbits.p, st));
                 // the records' kappa field: the target-aware fixpoint (kappa0 with 0 iterations)
                 const int64_t V = top->g.V;
-                HIPCHK(top->d_pot.ensure((size_t)V));
+                const uint32_t nwave = (uint32_t)std::min<int64_t>(kGroupHubs, V);
                 HIPCHK(top->d_kfA.ensure((size_t)V));
                 HIPCHK(top->d_kfB.ensure((size_t)V));
                 HIPCHK(top->d_kfChanged.ensure(1));
-                HIPCHK(hipMemcpyAsync(top->d_pot.p, top->pot.data(), sizeof(double) * (size_t)V,
-                                      hipMemcpyHostToDevice, st));
                 HIPCHK(launch_kfix_step(top->d_rowptr.p, top->d_adj.p, top->d_pot.p, top->d_tbits.p,
-                                        nullptr, top->d_kfA.p, V, top->d_kfChanged.p, st));
+                                        nullptr, top->d_kfA.p, V, nwave, top->d_kfChanged.p, st));
                 double* kin = top->d_kfA.p;
                 double* kout = top->d_kfB.p;
                 int it = 0;
                 for (; it < top->targetKappa; it++) {
                     HIPCHK(hipMemsetAsync(top->d_kfChanged.p, 0, sizeof(unsigned int), st));
                     HIPCHK(launch_kfix_step(top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
-                                            top->d_tbits.p, kin, kout, V, top->d_kfChanged.p, st));
+                                            top->d_tbits.p, kin, kout, V, nwave,
+                                            top->d_kfChanged.p, st));
                     unsigned int ch = 0;
                     HIPCHK(hipMemcpyAsync(&ch, top->d_kfChanged.p, sizeof(unsigned int),
                                           hipMemcpyDeviceToHost, st));
@@ -1122,17 +1015,20 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 }
                 if (top->targetResort)
                     HIPCHK(launch_kprime_resort(top->d_adjk.p, top->d_kap.p, top->d_ksum.p,
-                                                top->d_kap0.p, top->d_rowptr.p, V, nadj,
+                                                top->d_kap0.p, top->d_rowptr.p, V, nadjk,
                                                 top->d_pot.p, top->d_tbits.p, kin, st));
-                HIPCHK(launch_kfix_store(top->d_adjk.p, nadj, kin, st));
+                HIPCHK(launch_kfix_store(top->d_adjk.p, nadjk, kin, st));
                 HIPCHK(hipStreamSynchronize(st));
                 top->stats.target_kappa_iters = it;
                 top->stats.target_prep_ms = std::chrono::duration<double, std::milli>(
                     std::chrono::steady_clock::now() - tp0).count();
                 top->adjkTargets = tgt;
                 top->adjkFlagged = true;
+                top->adjkPlain = false;
+                top->adjkResorted = top->targetResort;
             }
-            if (K > 1) {
+            {
+                const auto to0 = std::chrono::steady_clock::now();
                 // Batches of K sources settle in lock-step and share an expansion when their
                 // shifted distances to a vertex fall in one bucket: sources whose shortest paths
                 // enter the hub core through the same hub share the most.  Batch position p takes
@@ -1140,41 +1036,39 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 std::vector<uint32_t> perm((size_t)rows);
                 std::iota(perm.begin(), perm.end(), 0u);
                 if (top->sourceOrder == 2) {
-                    // preorder of the h0 shortest-path tree: sources in one subtree (sharing the
-                    // longest path prefix from h0) are adjacent
-                    if (top->sptPre.empty()) {
-                        const size_t Vn = (size_t)top->g.V;
-                        std::vector<uint32_t> cnt(Vn + 1, 0), ch(Vn);
-                        for (size_t v = 0; v < Vn; v++)
-                            if (top->sptPar[v] != 0xFFFFFFFFu) cnt[top->sptPar[v] + 1]++;
-                        for (size_t v = 0; v < Vn; v++) cnt[v + 1] += cnt[v];
-                        std::vector<uint32_t> fillc(cnt.begin(), cnt.end() - 1);
-                        for (size_t v = 0; v < Vn; v++)
-                            if (top->sptPar[v] != 0xFFFFFFFFu) ch[fillc[top->sptPar[v]]++] = (uint32_t)v;
-                        top->sptPre.assign(Vn, 0xFFFFFFFFu);
-                        std::vector<uint32_t> stk{0u};
-                        uint32_t next = 0;
-                        while (!stk.empty()) {
-                            const uint32_t v = stk.back();
-                            stk.pop_back();
-                            top->sptPre[v] = next++;
-                            for (uint32_t k = cnt[v + 1]; k > cnt[v]; k--) stk.push_back(ch[k - 1]);
+                    // preorder of the h0 shortest-path tree (children by ascending vertex id):
+                    // sources in one subtree (sharing the longest path prefix from h0) are
+                    // adjacent.  Preorder = lexicographic order of the root-first parent paths,
+                    // so only the sources' paths are walked (O(rows x depth), not a DFS of V);
+                    // a vertex outside the tree sorts last.
+                    std::vector<std::vector<uint32_t>> path((size_t)rows);
+                    std::vector<uint8_t> inTree((size_t)rows, 0);
+                    for (int64_t i = 0; i < rows; i++) {
+                        auto& p = path[(size_t)i];
+                        uint32_t v = src[(size_t)i];
+                        while (v != 0xFFFFFFFFu && p.size() <= (size_t)top->g.V) {
+                            p.push_back(v);
+                            v = top->hp->sptPar[v];
                         }
+                        inTree[(size_t)i] = !p.empty() && p.back() == 0u;
+                        std::reverse(p.begin(), p.end());
                     }
                     std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
-                        return top->sptPre[src[a]] < top->sptPre[src[b]];
+                        if (inTree[a] != inTree[b]) return inTree[a] > inTree[b];
+                        return std::lexicographical_compare(path[a].begin(), path[a].end(),
+                                                            path[b].begin(), path[b].end());
                     });
                 } else if (top->sourceOrder == 1) {
-                    const uint32_t Hc = (uint32_t)lds_plan(top).H;
+                    const uint32_t Hc = (uint32_t)std::min<int64_t>(kGroupHubs, top->g.V);
                     std::vector<uint64_t> key((size_t)rows);
                     for (int64_t i = 0; i < rows; i++) {
                         uint32_t v = src[(size_t)i];
                         for (int hop = 0; v >= Hc && hop < 64; hop++) {  // up the h0 tree
-                            const uint32_t p = top->sptPar[(size_t)v];
+                            const uint32_t p = top->hp->sptPar[(size_t)v];
                             if (p == 0xFFFFFFFFu) break;
                             v = p;
                         }
-                        const double pi = top->pot[(size_t)src[(size_t)i]];
+                        const double pi = top->hp->pot[(size_t)src[(size_t)i]];
                         const float pf = std::isfinite(pi) ? (float)pi : INFINITY;
                         uint32_t pb;
                         memcpy(&pb, &pf, 4);
@@ -1209,7 +1103,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                         for (int64_t b = 0; b < nb; b++) {
                             int64_t c = 0;
                             for (int64_t i = b * kf; i < std::min(rows, (b + 1) * kf); i++, c++) {
-                                const double p = top->pot[(size_t)src[(size_t)perm[(size_t)i]]];
+                                const double p = top->hp->pot[(size_t)src[(size_t)perm[(size_t)i]]];
                                 mp[(size_t)b] += std::isfinite(p) ? p : 0.0;
                             }
                             mp[(size_t)b] /= (double)std::max<int64_t>(1, c);
@@ -1241,15 +1135,17 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 ws.rowmap = top->d_rowmap.p;
                 // bucket shift per row: sh = C - pi(src) >= 2 delta (topo_sssp_batch.hip)
                 const double delta = default_delta(top);
-                const double pmax = top->piMax;  // largest finite pi (upload_csr)
+                const double pmax = top->hp->piMax;  // largest finite pi (upload_csr)
                 std::vector<double> sh((size_t)rows);
                 for (int64_t i = 0; i < rows; i++) {
-                    const double p = top->pot[(size_t)psrc[(size_t)i]];
+                    const double p = top->hp->pot[(size_t)psrc[(size_t)i]];
                     sh[(size_t)i] = (pmax - (std::isfinite(p) ? p : pmax)) + 2.0 * delta;
                 }
                 HIPCHK(top->d_srcsh.ensure((size_t)rows));
                 HIPCHK(hipMemcpyAsync(top->d_srcsh.p, sh.data(), sizeof(double) * (size_t)rows,
                                       hipMemcpyHostToDevice, st));
+                top->stats.order_ms = std::chrono::duration<double, std::milli>(
+                    std::chrono::steady_clock::now() - to0).count();
                 HIPCHK(hipEventRecord(top->ev0, st));
                 const SsspLdsPlan bp = sssp_batch_lds_plan(
                     K, top->hubLimit, (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 20)),
@@ -1263,7 +1159,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 if (btf && *btf) HIPCHK(hipMalloc((void**)&ws.btrace, 64 * (size_t)nbt));
                 HIPCHK(launch_sssp_batch(K, dev_csr(top), ws, top->d_sources.p,
                                          top->d_srcsh.p, (int)rows, kf, top->d_targets.p, (int)A,
-                                         delta, bp, (uint32_t)top->farCap, out_lr, out_hops,
+                                         delta, bp, top->iterGuard, out_lr, out_hops,
                                          out_rowmin, top->d_stats.p, st));
                 HIPCHK(hipEventRecord(top->ev1, st));
                 HIPCHK(hipStreamSynchronize(st));  // sh must outlive the async copy
@@ -1277,7 +1173,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                         fwrite(hdr, 8, 4, f);
                         fwrite(bt.data(), 8, bt.size(), f);
                         for (int64_t i = 0; i < rows; i++) {
-                            const double p = top->pot[(size_t)psrc[(size_t)i]];
+                            const double p = top->hp->pot[(size_t)psrc[(size_t)i]];
                             const int64_t rec[2] = {(int64_t)psrc[(size_t)i], 0};
                             fwrite(rec, 8, 1, f);
                             fwrite(&p, 8, 1, f);
@@ -1285,14 +1181,6 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                         fclose(f);
                     }
                 }
-            } else {
-                top->stats.lds_hubs = lds_plan(top).H;
-                HIPCHK(launch_sssp_rows(dev_csr(top), ws, top->d_sources.p, (int)rows,
-                                        top->d_targets.p, (int)A, default_delta(top), lds_plan(top),
-                                        (uint32_t)top->farCap,
-                                        (uint32_t)top->nearCap, top->events,
-                                        out_lr, out_hops,
-                                        out_rowmin, top->d_stats.p, st));
             }
         }
         HIPCHK(hipEventRecord(top->ev1, st));
@@ -1380,6 +1268,7 @@ int collect_row_stats(Topology* top) {
                 h[ST_FARSCAN]);
     top->stats.far_scan_sources = (int64_t)h[ST_FARSCAN];
     top->stats.replay_rows = (int64_t)h[ST_RP_ROWS];
+    top->stats.touched_lines = (int64_t)h[ST_TOUCHED];
     top->stats.replay_pops = (int64_t)h[ST_RP_POPS];
     top->stats.replay_pushes = (int64_t)h[ST_RP_PUSH];
     top->stats.replay_modifies = (int64_t)h[ST_RP_MOD];
@@ -1418,8 +1307,12 @@ void push_min_to_engine(double m) {
     if (worker_updateMinTimeJump && m > 0) worker_updateMinTimeJump(m);
 }
 
+const double2* tab_lr(const Topology* top) { return top->extLr ? top->extLr : top->d_lr.p; }
+const uint16_t* tab_hops(const Topology* top) { return top->extHops ? top->extHops : top->d_hops.p; }
+
 bool table_current(Topology* top) {
-    return top->tableValid.load(std::memory_order_acquire) && top->tableGen == top->setGen.load();
+    return top->tableValid.load(std::memory_order_acquire) &&
+           top->tableGen.load(std::memory_order_acquire) == top->setGen.load();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1485,8 +1378,7 @@ int num_devices() {
 Topology* slot_engine(Topology* top, int d) { return d == 0 ? top : top->peers[(size_t)d - 1]; }
 
 Topology* make_peer(Topology* top, int phys) {
-    Topology* p = new Topology();
-    p->g = top->g;
+    Topology* p = new Topology(top->gp);
     p->isComplete = top->isComplete;
     p->isDirected = top->isDirected;
     p->hasMultiEdges = top->hasMultiEdges;
@@ -1502,16 +1394,14 @@ void sync_peer(Topology* top, Topology* p) {
     p->slotsOpt = top->slotsOpt;
     p->hubLimit = top->hubLimit;
     p->parHubs = top->parHubs;
-    p->wgPerCu = top->wgPerCu;
     p->batchK = top->batchK;
-    p->events = top->events;
-    p->nearCap = top->nearCap;
-    p->farCap = top->farCap;
+    p->iterGuard = top->iterGuard;
     p->tieReplay = top->tieReplay;
     p->replayAll = top->replayAll;
     p->tieDenseOpt = top->tieDenseOpt;
     p->tieDense = p->tieDense || top->tieDense;
     p->replaySlotsOpt = top->replaySlotsOpt;
+    p->replayLandmark = top->replayLandmark;
     p->sourceOrder = top->sourceOrder;
     p->batchOrder = top->batchOrder;
     p->batchFill = top->batchFill;
@@ -1522,6 +1412,48 @@ void sync_peer(Topology* top, Topology* p) {
     p->colOf = top->colOf;
     p->A = top->A;
     p->geomInit = true;
+}
+
+template <class T>
+hipError_t peer_copy(DevBuf<T>& dst, int ddev, const DevBuf<T>& src, int sdev, hipStream_t st) {
+    if (!src.p || src.n == 0) return hipSuccess;
+    const hipError_t e = dst.ensure(src.n);
+    if (e != hipSuccess) return e;
+    return hipMemcpyPeerAsync(dst.p, ddev, src.p, sdev, sizeof(T) * src.n, st);
+}
+
+// A peer engine takes the owner's prepared graph: the device CSR and landmark arrays are copied
+// device to device (xGMI peer copies; the same device for a test configuration) and the host side
+// is shared -- the graph is prepared once per multi-GPU build, not once per device.
+int copy_csr_from(Topology* p, int pdev, Topology* o, int odev) {
+    hipStream_t st = p->stream;
+    if (pdev != odev) {
+        const hipError_t e = hipDeviceEnablePeerAccess(odev, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+            (void)hipGetLastError();  // no direct access: the copies are staged by the runtime
+    }
+    HIPCHK(peer_copy(p->d_rowptr, pdev, o->d_rowptr, odev, st));
+    HIPCHK(peer_copy(p->d_adj, pdev, o->d_adj, odev, st));
+    HIPCHK(peer_copy(p->d_adjk, pdev, o->d_adjk, odev, st));
+    HIPCHK(peer_copy(p->d_kap, pdev, o->d_kap, odev, st));
+    HIPCHK(peer_copy(p->d_ksum, pdev, o->d_ksum, odev, st));
+    HIPCHK(peer_copy(p->d_kap0, pdev, o->d_kap0, odev, st));
+    HIPCHK(peer_copy(p->d_spt, pdev, o->d_spt, odev, st));
+    HIPCHK(peer_copy(p->d_sptPar, pdev, o->d_sptPar, odev, st));
+    HIPCHK(peer_copy(p->d_pot, pdev, o->d_pot, odev, st));
+    HIPCHK(peer_copy(p->d_aloss, pdev, o->d_aloss, odev, st));
+    HIPCHK(peer_copy(p->d_vloss, pdev, o->d_vloss, odev, st));
+    HIPCHK(peer_copy(p->d_selfLat, pdev, o->d_selfLat, odev, st));
+    HIPCHK(peer_copy(p->d_selfLoss, pdev, o->d_selfLoss, odev, st));
+    HIPCHK(hipStreamSynchronize(st));
+    p->hp = o->hp;
+    p->rowsSorted = o->rowsSorted;
+    p->adjkPlain = o->adjkPlain;
+    p->adjkFlagged = o->adjkFlagged;
+    p->adjkResorted = o->adjkResorted;
+    p->adjkTargets = o->adjkTargets;
+    p->csrUploaded = true;
+    return 0;
 }
 
 // N devices: slot d builds rows [d*R, min(A, (d+1)*R)) into its own full-size buffers (R*N rows,
@@ -1549,6 +1481,37 @@ int build_multi(Topology* top) {
     for (int d = 0; d < N; d++) {
         phys[(size_t)d] = slot_engine(top, d)->device % ndev;
         for (int e = 0; e < d; e++) distinct = distinct && phys[(size_t)e] != phys[(size_t)d];
+    }
+    // 0) the graph is prepared once, on this engine's device, and copied to the peers
+    {
+        const auto tp = std::chrono::steady_clock::now();
+        HIPCHK(hipSetDevice(phys[0]));
+        int r = dev_init(top);
+        if (r) return r;
+        bool did = false;
+        if (!top->isComplete) {
+            did = !top->csrUploaded;
+            r = upload_csr(top);
+            if (r) return r;
+            (void)default_delta(top);  // the mean latency, once (peers copy it)
+        }
+        for (int d = 1; d < N; d++) {
+            Topology* T = slot_engine(top, d);
+            reset_build_stats(T);
+            HIPCHK(hipSetDevice(phys[(size_t)d]));
+            r = dev_init(T);
+            if (r) return r;
+            T->meanLat = top->meanLat;
+            if (!top->isComplete && !T->csrUploaded) {
+                r = copy_csr_from(T, phys[(size_t)d], top, phys[0]);
+                if (r) return r;
+                did = true;
+            }
+        }
+        HIPCHK(hipSetDevice(phys[0]));
+        if (did)  // preparation + the peers' copies
+            top->stats.csr_ms = std::chrono::duration<double, std::milli>(
+                std::chrono::steady_clock::now() - tp).count();
     }
     // 1) rows, one host thread per device
     std::vector<int> rc(N, 0);
@@ -1586,18 +1549,30 @@ int build_multi(Topology* top) {
     HIPCHK(hipSetDevice(phys[0]));
     HIPCHK(hipEventRecord(top->ev2, top->stream));
     const auto tx0 = std::chrono::steady_clock::now();
-    if (distinct) {
+    bool useRccl = distinct;
+    if (useRccl) {
         RcclApi& api = rccl();
         if (!api.ok) {
-            CRITICAL("multi-GPU build needs RCCL: %s", api.why.c_str());
-            return -6;
-        }
-        if (top->commDevs != phys) {
+            WARNING("RCCL unavailable (%s): the rows are exchanged by peer copies", api.why.c_str());
+            useRccl = false;
+        } else if (top->commDevs != phys) {
             for (ncclComm_t c : top->comms) (void)api.commDestroy(c);
             top->comms.assign((size_t)N, nullptr);
-            NCCLCHK(api.commInitAll(top->comms.data(), N, phys.data()));
-            top->commDevs = phys;
+            top->commDevs.clear();
+            const ncclResult_t e = api.commInitAll(top->comms.data(), N, phys.data());
+            if (e != ncclSuccess) {
+                WARNING("ncclCommInitAll failed (%s): the rows are exchanged by peer copies",
+                        api.errStr(e));
+                top->comms.clear();
+                useRccl = false;
+            } else {
+                top->commDevs = phys;
+            }
         }
+    }
+    top->stats.exchange_kind = N > 1 || top->forceRccl ? (useRccl ? 1 : 2) : 0;
+    if (useRccl) {
+        RcclApi& api = rccl();
         NCCLCHK(api.groupStart());
         for (int d = 0; d < N; d++) {
             Topology* T = slot_engine(top, d);
@@ -1646,6 +1621,10 @@ int build_multi(Topology* top) {
     for (int d = 1; d < N; d++) {
         const ShdStats& o = slot_engine(top, d)->stats;
         top->stats.sssp_kernel_ms = std::max(top->stats.sssp_kernel_ms, o.sssp_kernel_ms);
+        top->stats.target_prep_ms = std::max(top->stats.target_prep_ms, o.target_prep_ms);
+        top->stats.order_ms = std::max(top->stats.order_ms, o.order_ms);
+        top->stats.replay_prep_ms = std::max(top->stats.replay_prep_ms, o.replay_prep_ms);
+        top->stats.touched_lines += o.touched_lines;
         top->stats.replay_ms = std::max(top->stats.replay_ms, o.replay_ms);
         top->stats.build_ms = std::max(top->stats.build_ms, o.build_ms);
         top->stats.ambiguous_pairs += o.ambiguous_pairs;
@@ -1667,6 +1646,9 @@ int ensure_table(Topology* top) {
     if (r) return r;
     const uint64_t sg = compute_geometry(top);
     const int64_t A = top->A;
+    reset_build_stats(top);
+    int64_t runs0 = top->csrHostRuns;
+    for (Topology* p : top->peers) runs0 += p->csrHostRuns;
     top->stats.devices = 1;
     top->stats.exchange_ms = 0.0;
     if (A > 0 && (top->devicesOpt > 1 || top->forceRccl)) {
@@ -1689,7 +1671,12 @@ int ensure_table(Topology* top) {
                      (long long)top->stats.errors);
         }
     }
-    top->tableGen = sg;
+    top->extLr = nullptr;  // the library's own buffers hold the new table
+    top->extHops = nullptr;
+    int64_t runs1 = top->csrHostRuns;
+    for (Topology* p : top->peers) runs1 += p->csrHostRuns;
+    top->stats.csr_host_runs = runs1 - runs0;
+    top->tableGen.store(sg, std::memory_order_release);
     top->tableSerial.fetch_add(1);
     top->tableValid.store(true, std::memory_order_release);
     if (!top->lazy && A > 0) push_min_to_engine(top->eagerMin);
@@ -1716,7 +1703,7 @@ int ensure_snapshot(Topology* top, bool full, std::shared_ptr<const HostTable>* 
             return 0;
         }
         auto h = std::make_shared<HostTable>();
-        h->gen = top->tableGen;
+        h->gen = top->tableGen.load(std::memory_order_acquire);
         h->serial = top->tableSerial.load();
         h->A = top->A;
         h->colOf = top->colOf;
@@ -1728,8 +1715,8 @@ int ensure_snapshot(Topology* top, bool full, std::shared_ptr<const HostTable>* 
             std::vector<double2> lr(n);
             h->hops.resize(n);
             if (n) {
-                HIPCHK(hipMemcpy(lr.data(), top->d_lr.p, sizeof(double2) * n, hipMemcpyDeviceToHost));
-                HIPCHK(hipMemcpy(h->hops.data(), top->d_hops.p, sizeof(uint16_t) * n, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(lr.data(), tab_lr(top), sizeof(double2) * n, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(h->hops.data(), tab_hops(top), sizeof(uint16_t) * n, hipMemcpyDeviceToHost));
             }
             h->lat.resize(n);
             h->rel.resize(n);
@@ -2071,11 +2058,12 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "device") top->device = (int)value;
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
     else if (k == "par_hubs") top->parHubs = (int64_t)value;
-    else if (k == "wg_per_cu") top->wgPerCu = std::max(1, std::min(8, (int)value));
-    else if (k == "far_cap") top->farCap = (int64_t)value;
-    else if (k == "near_cap") top->nearCap = (int64_t)value;
-    else if (k == "events") top->events = value != 0;
-    else if (k == "batch") top->batchK = (int)value;
+    else if (k == "batch") {
+        const int b = (int)value;
+        if (b != 2 && b != 4 && b != 8 && b != 16) return -1;
+        top->batchK = b;
+    }
+    else if (k == "iter_guard") top->iterGuard = (uint32_t)std::max(1.0, std::min(4e9, value));
     else if (k == "tie_replay") top->tieReplay = value != 0;
     else if (k == "replay_all") top->replayAll = value != 0;
     else if (k == "replay_slots") top->replaySlotsOpt = (int)value;
@@ -2225,9 +2213,12 @@ int shdtopo_build_rows(Topology* top, int64_t row0, int64_t row1, void* d_lr, vo
     if (r) return r;
     compute_geometry(top);
     if (row0 < 0 || row1 > top->A || row0 > row1) return -2;
+    reset_build_stats(top);
+    const int64_t runs0 = top->csrHostRuns;
     hipStream_t st = stream ? (hipStream_t)stream : top->stream;
     r = enqueue_rows(top, row0, row1, (double2*)d_lr, (uint16_t*)d_hops, (double*)d_rowmin, st);
     if (r) return r;
+    top->stats.csr_host_runs = top->csrHostRuns - runs0;
     return collect_row_stats(top);
 }
 
@@ -2247,11 +2238,42 @@ int shdtopo_bind_table(Topology* top, const void* d_lr, const void* d_hops, doub
     HIPCHK(hipMemcpyAsync(top->d_hops.p, d_hops, sizeof(uint16_t) * n, hipMemcpyDeviceToDevice, st));
     if (top->A) HIPCHK(launch_row_min(top->A, top->A, top->d_lr.p, top->d_rowmin.p, st));
     HIPCHK(hipStreamSynchronize(st));
+    top->extLr = nullptr;
+    top->extHops = nullptr;
     top->eagerMin = globalMin;
-    top->tableGen = sg;
+    top->tableGen.store(sg, std::memory_order_release);
     top->tableSerial.fetch_add(1);
     top->tableValid.store(true, std::memory_order_release);
     return 0;
+}
+
+int shdtopo_bind_table_ref(Topology* top, const void* d_lr, const void* d_hops, double globalMin,
+                           void* stream) {
+    if (!top || !d_lr || !d_hops) return -1;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    int r = dev_init(top);
+    if (r) return r;
+    const uint64_t sg = compute_geometry(top);
+    hipStream_t st = stream ? (hipStream_t)stream : top->stream;
+    HIPCHK(top->d_rowmin.ensure((size_t)top->A));
+    if (top->A) HIPCHK(launch_row_min(top->A, top->A, (const double2*)d_lr, top->d_rowmin.p, st));
+    HIPCHK(hipStreamSynchronize(st));
+    top->extLr = (const double2*)d_lr;
+    top->extHops = (const uint16_t*)d_hops;
+    top->eagerMin = globalMin;
+    top->tableGen.store(sg, std::memory_order_release);
+    top->tableSerial.fetch_add(1);
+    top->tableValid.store(true, std::memory_order_release);
+    return 0;
+}
+
+int shdtopo_rebuild(Topology* top) {
+    if (!top) return -1;
+    {
+        std::lock_guard<std::mutex> lk(top->buildMu);
+        top->tableValid.store(false);
+    }
+    return ensure_table(top);
 }
 
 int shdtopo_table_to_host(Topology* top, double* lat, double* rel, uint16_t* hops) {
@@ -2275,7 +2297,7 @@ int route_locked(Topology* top, const int32_t* d_srcCol, const int32_t* d_dstCol
                  int64_t n, uint64_t jumpNs, int clamp, uint64_t* d_time, uint32_t* d_stateOut,
                  uint8_t* d_delivered, hipStream_t st) {
     HIPCHK(hipEventRecord(top->ev2, st));
-    HIPCHK(launch_packet_route(n, d_srcCol, d_dstCol, d_payload, d_stateIn, d_now, top->d_lr.p,
+    HIPCHK(launch_packet_route(n, d_srcCol, d_dstCol, d_payload, d_stateIn, d_now, tab_lr(top),
                                top->A, jumpNs, clamp, d_time, d_stateOut, d_delivered,
                                top->d_stats.p + ST_ROUTE_BAD, st));
     HIPCHK(hipEventRecord(top->ev3, st));
@@ -2300,30 +2322,21 @@ int shdtopo_route_batch_device(Topology* top, const int32_t* d_srcCol, const int
                         d_time, d_stateOut, d_delivered, st);
 }
 
-int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketOut* out, size_t n,
-                              uint64_t jumpNs, int clampInterHost) {
-    if (!top || (!in && n) || (!out && n)) return -1;
-    if (n == 0) return ensure_table(top);
-    std::vector<int32_t> sv(n), dv(n), sc(n), dc(n);
-    std::vector<uint32_t> pay(n), sin(n), sout(n);
-    std::vector<uint64_t> now(n), tim(n);
+}  // extern "C"
+
+namespace {
+// worker_schedulePacket (shd-worker.c:332-370) for n packets given by their vertices (-1: the
+// address is not attached).  A packet whose vertex is not a column of the current table is not
+// routed: delivered 0, time 0, and rngState the sender's state after its draw (the draw was taken
+// at emit).  Returns the number of such packets, or a negative error.
+int64_t route_vertices(Topology* top, const int32_t* sv, const int32_t* dv, const uint32_t* pay,
+                       const uint32_t* sin, const uint64_t* now, size_t n, uint64_t jumpNs,
+                       int clampInterHost, TopoPacketOut* out) {
+    std::vector<int32_t> sc(n), dc(n);
+    std::vector<uint32_t> sout(n);
+    std::vector<uint64_t> tim(n);
     std::vector<uint8_t> dl(n);
-    {
-        std::shared_lock<std::shared_mutex> lk(top->ipMu);
-        for (size_t i = 0; i < n; i++) {
-            auto a = top->virtualIP.find(in[i].srcIP);
-            auto b = top->virtualIP.find(in[i].dstIP);
-            if (a == top->virtualIP.end() || b == top->virtualIP.end() || a->second < 0 || b->second < 0) {
-                CRITICAL("packet %zu: address is not connected to the topology", i);
-                return -2;
-            }
-            sv[i] = a->second;
-            dv[i] = b->second;
-            pay[i] = in[i].payloadLength;
-            sin[i] = in[i].rngState;
-            now[i] = in[i].now;
-        }
-    }
+    int64_t bad = 0;
     // the snapshot and the device table must be the same build: retry if a rebuild intervened
     for (int attempt = 0;; attempt++) {
         std::shared_ptr<const HostTable> h;
@@ -2338,12 +2351,14 @@ int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketO
         // Lazy mode answers every packet as the reference's getReliability/getLatency pair would
         // in emission order (cache orientation, running-minimum pushes): resolved here,
         // sequentially; the kernel reads the chosen row.
+        bad = 0;
         for (size_t i = 0; i < n; i++) {
-            sc[i] = h->colOf[(size_t)sv[i]];
-            dc[i] = h->colOf[(size_t)dv[i]];
+            sc[i] = sv[i] >= 0 && sv[i] < top->g.V ? h->colOf[(size_t)sv[i]] : -1;
+            dc[i] = dv[i] >= 0 && dv[i] < top->g.V ? h->colOf[(size_t)dv[i]] : -1;
             if (sc[i] < 0 || dc[i] < 0 || sc[i] >= h->A || dc[i] >= h->A) {
-                CRITICAL("packet %zu: address is not connected to the current routing table", i);
-                return -2;
+                sc[i] = dc[i] = -1;  // not routed (the kernel leaves it undelivered)
+                bad++;
+                continue;
             }
             if (top->lazy) {
                 if (top->isComplete) {
@@ -2359,9 +2374,9 @@ int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketO
         HIPCHK(top->b_time.ensure(n)); HIPCHK(top->b_dl.ensure(n));
         HIPCHK(hipMemcpyAsync(top->b_src.p, sc.data(), 4 * n, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(top->b_dst.p, dc.data(), 4 * n, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(top->b_pay.p, pay.data(), 4 * n, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(top->b_sin.p, sin.data(), 4 * n, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(top->b_now.p, now.data(), 8 * n, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(top->b_pay.p, pay, 4 * n, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(top->b_sin.p, sin, 4 * n, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(top->b_now.p, now, 8 * n, hipMemcpyHostToDevice, st));
         r = route_locked(top, top->b_src.p, top->b_dst.p, top->b_pay.p, top->b_sin.p,
                          top->b_now.p, (int64_t)n, jumpNs, clampInterHost, top->b_time.p,
                          top->b_sout.p, top->b_dl.p, st);
@@ -2375,10 +2390,77 @@ int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketO
     for (size_t i = 0; i < n; i++) {
         out[i].time = tim[i];
         out[i].rngState = sout[i];
+        if (sc[i] < 0) {  // not routed: the state after the sender's one draw
+            uint32_t s = sin[i];
+            (void)glibc_rand_r(&s);
+            out[i].rngState = s;
+        }
         out[i].delivered = dl[i];
         out[i]._pad[0] = out[i]._pad[1] = out[i]._pad[2] = 0;
     }
-    return 0;
+    if (bad) WARNING("%lld packets of a batch have an address that is not attached: not routed",
+                     (long long)bad);
+    return bad;
+}
+}  // namespace
+
+extern "C" {
+
+int shdtopo_route_batch_device_slot(Topology* top, int slot, const int32_t* d_srcCol,
+                                    const int32_t* d_dstCol, const uint32_t* d_payload,
+                                    const uint32_t* d_stateIn, const uint64_t* d_now, int64_t n,
+                                    uint64_t jumpNs, int clamp, uint64_t* d_time,
+                                    uint32_t* d_stateOut, uint8_t* d_delivered, void* stream) {
+    if (!top || slot < 0) return -1;
+    int r = ensure_table(top);
+    if (r) return r;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    if (slot > 0 && (top->stats.devices <= slot || slot > (int)top->peers.size())) return -2;
+    Topology* T = slot_engine(top, slot);
+    int prev = 0;
+    HIPCHK(hipGetDevice(&prev));
+    HIPCHK(hipSetDevice(T->device % std::max(1, num_devices())));
+    hipStream_t st = stream ? (hipStream_t)stream : T->stream;
+    r = route_locked(T, d_srcCol, d_dstCol, d_payload, d_stateIn, d_now, n, jumpNs, clamp, d_time,
+                     d_stateOut, d_delivered, st);
+    HIPCHK(hipSetDevice(prev));
+    return r;
+}
+
+int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketOut* out, size_t n,
+                              uint64_t jumpNs, int clampInterHost) {
+    if (!top || (!in && n) || (!out && n)) return -1;
+    if (n == 0) return ensure_table(top);
+    std::vector<int32_t> sv(n), dv(n);
+    std::vector<uint32_t> pay(n), sin(n);
+    std::vector<uint64_t> now(n);
+    {
+        std::shared_lock<std::shared_mutex> lk(top->ipMu);
+        for (size_t i = 0; i < n; i++) {
+            auto a = top->virtualIP.find(in[i].srcIP);
+            auto b = top->virtualIP.find(in[i].dstIP);
+            sv[i] = a == top->virtualIP.end() ? -1 : a->second;
+            dv[i] = b == top->virtualIP.end() ? -1 : b->second;
+            pay[i] = in[i].payloadLength;
+            sin[i] = in[i].rngState;
+            now[i] = in[i].now;
+        }
+    }
+    const int64_t r = route_vertices(top, sv.data(), dv.data(), pay.data(), sin.data(), now.data(),
+                                     n, jumpNs, clampInterHost, out);
+    return r < 0 ? (int)r : (int)std::min<int64_t>(r, INT32_MAX);
+}
+
+int shdtopo_route_batch_vertices(Topology* top, const int32_t* srcVertex, const int32_t* dstVertex,
+                                 const uint32_t* payloadLength, const uint32_t* rngState,
+                                 const uint64_t* now, size_t n, uint64_t jumpNs,
+                                 int clampInterHost, TopoPacketOut* out) {
+    if (!top || (n && (!srcVertex || !dstVertex || !payloadLength || !rngState || !now || !out)))
+        return -1;
+    if (n == 0) return ensure_table(top);
+    const int64_t r = route_vertices(top, srcVertex, dstVertex, payloadLength, rngState, now, n,
+                                     jumpNs, clampInterHost, out);
+    return r < 0 ? (int)r : (int)std::min<int64_t>(r, INT32_MAX);
 }
 
 int shdtopo_get_stats(Topology* top, ShdStats* out) {
@@ -2416,10 +2498,10 @@ int shdtopo_replay_source(Topology* top, int32_t srcv, int full, double* dist, i
     if (r) return r;
     hipStream_t st = top->stream;
     std::vector<uint32_t> tgt((size_t)A);
-    for (int64_t i = 0; i < A; i++) tgt[(size_t)i] = (uint32_t)top->inv[(size_t)top->attached[(size_t)i]];
+    for (int64_t i = 0; i < A; i++) tgt[(size_t)i] = (uint32_t)top->hp->inv[(size_t)top->attached[(size_t)i]];
     r = upload_target_bits(top, tgt, st);
     if (r) return r;
-    const uint32_t s = (uint32_t)top->inv[(size_t)srcv], row = 0;
+    const uint32_t s = (uint32_t)top->hp->inv[(size_t)srcv], row = 0;
     const size_t V = (size_t)top->g.V;
     DevBuf<uint32_t> d_s, d_row, d_tg;
     DevBuf<double2> d_lr;
@@ -2432,21 +2514,46 @@ int shdtopo_replay_source(Topology* top, int32_t srcv, int full, double* dist, i
     HIPCHK(hipMemcpy(d_s.p, &s, 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_row.p, &row, 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_tg.p, tgt.data(), 4 * (size_t)A, hipMemcpyHostToDevice));
-    HIPCHK(hipMemsetAsync(top->d_stats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
-    HIPCHK(launch_fill_u64(top->d_stats.p + ST_GLOBAL_MIN, 0x7FF0000000000000ull, 1, st));
+    // its own counters: the last real build's statistics (not read yet) stay intact
+    DevBuf<unsigned long long> d_st;
+    HIPCHK(d_st.ensure(ST_COUNT));
+    HIPCHK(hipMemsetAsync(d_st.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
+    HIPCHK(launch_fill_u64(d_st.p + ST_GLOBAL_MIN, 0x7FF0000000000000ull, 1, st));
     HIPCHK(launch_heap_replay(replay_csr(top), replay_ws(top), d_s.p, d_row.p, 1, d_tg.p, (int)A,
-                              full, d_lr.p, d_h.p, nullptr, top->d_stats.p, d_dist.p, d_par.p, st));
+                              full, d_lr.p, d_h.p, nullptr, d_st.p, d_dist.p, d_par.p, st));
     HIPCHK(hipStreamSynchronize(st));
     std::vector<double> hd(V);
     std::vector<int32_t> hp(V);
     HIPCHK(hipMemcpy(hd.data(), d_dist.p, 8 * V, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(hp.data(), d_par.p, 4 * V, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < V; i++) {  // relabelled -> original ids
-        const size_t o = (size_t)top->perm[i];
+        const size_t o = (size_t)top->hp->perm[i];
         dist[o] = hd[i];
-        parent[o] = hp[i] < 0 ? -1 : top->perm[(size_t)hp[i]];
+        parent[o] = hp[i] < 0 ? -1 : top->hp->perm[(size_t)hp[i]];
     }
     return 0;
+}
+
+int64_t shdtopo_export_csr(Topology* top, int32_t* perm, uint32_t* rowptr, uint32_t* col,
+                           double* pot, uint32_t* treeParent) {
+    if (!top) return -1;
+    std::lock_guard<std::mutex> lk(top->buildMu);
+    if (top->isComplete || top->isDirected) return -2;
+    int r = dev_init(top);
+    if (r) return r;
+    r = upload_csr(top);
+    if (r) return r;
+    const size_t V = (size_t)top->g.V, nadj = top->d_adj.n / 4;
+    if (perm) memcpy(perm, top->hp->perm.data(), 4 * V);
+    if (pot) memcpy(pot, top->hp->pot.data(), 8 * V);
+    if (treeParent) memcpy(treeParent, top->hp->sptPar.data(), 4 * V);
+    if (rowptr) HIPCHK(hipMemcpy(rowptr, top->d_rowptr.p, 4 * (V + 1), hipMemcpyDeviceToHost));
+    if (col && nadj) {
+        std::vector<uint32_t> rec(4 * nadj);
+        HIPCHK(hipMemcpy(rec.data(), top->d_adj.p, 16 * nadj, hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < nadj; k++) col[k] = rec[4 * k];
+    }
+    return (int64_t)nadj;
 }
 
 int shdtopo_export_graph(Topology* top, int32_t* eu, int32_t* ev, double* elat, double* eloss,

@@ -2,9 +2,10 @@
 //
 // HBM layout (all arrays in the degree-relabelled vertex order, see DESIGN.md "Data layout"):
 //   CSR of the undirected topology without self loops:
-//     rowptr u32[V+1], adj {u32 col, f64 latency}[2E'] (12-B AoS), aloss f64[2E'] (edge loss)
-//   per vertex: vloss f64[V], selfLat f64[V] (NaN = no self loop), selfLoss f64[V]
-//   per SSSP slot (one workgroup = one source at a time): 264 B x V of workspace
+//     rowptr u32[V+1], adj {u32 col, u32 pi / kappa0 field, f64 latency}[2E'] (16-B AoS), its
+//     kappa-sorted copy adjk, aloss f64[2E'] (edge loss)
+//   per vertex: vloss f64[V], selfLat f64[V] (NaN = no self loop), selfLoss f64[V], pi f64[V]
+//   per SSSP slot (one workgroup = K sources at a time): DESIGN.md 3.2
 //   routing table: {f64 lat, f64 rel}[A][A] (16-B records, one gather per packet) + u16 hops
 #pragma once
 
@@ -23,14 +24,6 @@ constexpr int kSsspBlock = SHD_SSSP_BLOCK;  // threads per SSSP workgroup
 #endif
 constexpr int kBatchWgPerCu = SHD_BATCH_WGPCU;  // batch-kernel workgroups per CU (share its LDS)
 constexpr int kMaxHops = 48;      // per-thread path buffer depth (longer paths: O(h^2) walk)
-#ifndef SHD_RING_PER_VERTEX
-#define SHD_RING_PER_VERTEX 16
-#endif
-constexpr int kRingPerVertex = SHD_RING_PER_VERTEX;  // bucket-window entries per slot, in entries
-                                                     // per vertex (split evenly over the buckets)
-constexpr int kOverPerVertex = 2;  // overflow-pile capacity per slot, in 16-B entries per vertex
-                                   // (double buffered: a refill streams the kept entries over)
-constexpr int kNearPerVertex = 2; // near-queue capacity per slot, in entries per vertex
 #ifndef SHD_KAP_IN_REC
 #define SHD_KAP_IN_REC 1
 #endif
@@ -85,7 +78,8 @@ enum StatIdx {
     ST_BT0 = 51,        // batch kernel (SHD_BATCH_TIME builds): wave ticks of tail iterations in
                         // chunk loads / phase A / phase B, the same for hub iterations, phase-B
                         // rounds, surviving edges (8 slots)
-    ST_COUNT = 59
+    ST_TOUCHED = 59,    // tail distance lines reset at batch starts (lines the batches touched)
+    ST_COUNT = 60
 };
 
 struct DevCSR {
@@ -110,40 +104,34 @@ struct DevCSR {
     int tflags = 0;
 };
 
-// per-slot workspace, slot-major: array + slot * V
+// per-slot workspace of the batched SSSP (sssp_batch_kernel, K sources per slot), slot-major:
+// array + slot * V [* K]
 struct SlotWs {
     int slots = 0;
     int64_t V = 0;
-    unsigned long long* dist = nullptr;  // f64 bits, +inf = unreached
-    uint32_t* stamp = nullptr;           // near-queue / chain-queue dedupe (iteration id)
-    unsigned long long* qa = nullptr;  // near queues: (hi32 of the pushed distance << 32) |
-    unsigned long long* qb = nullptr;  // vertex, kNearPerVertex * V entries (no dedupe)
-    unsigned long long* ring = nullptr;  // bucket window: kRingPerVertex * V entries, same format
-    unsigned long long* over = nullptr;  // overflow pile (buckets past the window), 2 buffers of
-                                         // kOverPerVertex * V {u64 key, u64 vertex} entries
+    unsigned long long* dist = nullptr;  // [V][K] f64 bits, +inf = unreached (rows < H unused)
+    uint32_t* stamp = nullptr;           // parent pass: walk claim tag per (vertex, source)
+    unsigned long long* qa = nullptr;    // near queues / parent pair lists (q_stride u64 per slot)
+    unsigned long long* qb = nullptr;
+    uint32_t* ring = nullptr;            // ring_entries u32 per slot: parent pair list, vertex
+                                         // list, pending bitmap, tie bitmap
     unsigned long long* best = nullptr;  // parent pass: min d[u] over candidates
     uint32_t* cnt = nullptr;             // parent pass: candidates at the min
     uint32_t* bslot = nullptr;           // parent pass: lowest adjacency slot at the min
-    unsigned long long* memo = nullptr;  // (source epoch << 32) | ambiguous << 31 | slot
-    uint32_t* par = nullptr;             // parent vertex
+    unsigned long long* memo = nullptr;  // (batch epoch << 32) | ambiguous << 31 | slot
+    uint32_t* par = nullptr;             // parent vertex (the SSSP's improver hint before)
     uint32_t* pathbuf = nullptr;         // [slot][kMaxHops][kSsspBlock]
-    uint32_t* counters = nullptr;        // [slot][4]: iteration id, (unused), source epoch
-    // batched kernel (sssp_batch_kernel, K sources per slot): dist is [V][K] per slot, ring holds
-    // ring_entries u32 entries per slot (the parent pass' pair list; no overflow pile:
-    // over_entries is 0); qa / qb hold q_stride u64 per slot (near queues, parent pair lists of
-    // V * K u32); stamp/best/cnt/bslot/memo/par are per (vertex, source) pair, V * K per slot;
-    // mask = 2 parities of a K-bit mask per vertex; hpar [P][K] parent hints
-    int K = 1;
+    uint32_t* counters = nullptr;        // [slot][4]: iteration id, (unused), batch epoch
+    int K = 8;
     int64_t q_stride = 0;
     int64_t ring_entries = 0;
-    int64_t over_entries = 0;
-    uint8_t* mask = nullptr;
-    uint32_t* hpar = nullptr;
+    uint8_t* mask = nullptr;             // 2 parities of a K-bit source mask per vertex
+    uint32_t* hpar = nullptr;            // [P][K] parent hints of the LDS hubs
     // per row of the launch: set to 1 when a pair of the row crosses a d-tied parent (its parent
     // chain needs igraph's heap pop order: the row is recomputed by heap_replay_kernel)
     uint8_t* rowflag = nullptr;
-    // batch kernel: output row of batch position p (sources are taken in a locality order, the
-    // table keeps row order); nullptr = identity
+    // output row of batch position p (sources are taken in a locality order, the table keeps
+    // row order); nullptr = identity
     const uint32_t* rowmap = nullptr;
     // diagnostic (SHD_BATCH_TRACE): per batch {wall_clock64 at dequeue, at its end, slot}
     unsigned long long* btrace = nullptr;
@@ -182,23 +170,13 @@ struct ReplayWs {
     uint32_t* pathbuf = nullptr;
 };
 
-// LDS plan of one SSSP workgroup: H hub distance words (+ their queue bitmaps) and P parent
-// hints, sized to the workgroup's share of the CU's 160 KiB (wg_per_cu workgroups per CU).
+// LDS plan of one batched SSSP workgroup: H hub distance rows (+ their queue masks) and P
+// parent hints, sized to the CU's 160 KiB.
 struct SsspLdsPlan {
     uint32_t H = 0;     // LDS-resident hub distances (vertex ids 0..H-1 after the relabel)
     uint32_t P = 0;     // hubs with parent hints (P <= H)
     size_t bytes = 0;   // dynamic LDS per workgroup
 };
-// hub_limit: cap on H (-1 = as many as fit); V: vertices of the graph (H <= V)
-SsspLdsPlan sssp_lds_plan(int wg_per_cu, int64_t hub_limit, uint32_t par_hubs, int64_t V);
-
-hipError_t launch_sssp_rows(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
-                            int nsrc, const uint32_t* d_targets, int A, double delta,
-                            const SsspLdsPlan& plan, uint32_t far_cap,
-                            uint32_t near_cap, bool events,
-                            double2* out_lr,
-                            uint16_t* out_hops, double* out_rowmin, unsigned long long* d_stats,
-                            hipStream_t stream);
 
 // Batched multi-source SSSP (topo_sssp_batch.hip): K in {2, 4, 8, 16} sources per workgroup in
 // lock-step over buckets of d + srcsh[row] (srcsh >= 2 delta).  plan from sssp_batch_lds_plan.
@@ -211,7 +189,7 @@ hipError_t launch_mark_targets(uint32_t* adjk, int64_t nadj, const uint32_t* tbi
 // kappa0), then the f16 kappa field of the relaxation copy's records := K(column)
 hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const double* pot,
                             const uint32_t* tbits, const double* Kin, double* Kout, int64_t V,
-                            unsigned int* changed, hipStream_t stream);
+                            uint32_t nwave, unsigned int* changed, hipStream_t stream);
 hipError_t launch_kfix_store(uint32_t* adjk, int64_t nadj, const double* K, hipStream_t stream);
 // re-sort every row of the relaxation copy (records, kappa array, probes, kappa0) by the
 // target-aware key kap' of the current target set (tbits) and K
@@ -220,7 +198,7 @@ hipError_t launch_kprime_resort(uint32_t* adjk, float* kap, float* ksum, float* 
                                 const uint32_t* tbits, const double* K, hipStream_t stream);
 hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                              const double* d_srcsh, int nsrc, int kf, const uint32_t* d_targets, int A,
-                             double delta, const SsspLdsPlan& plan, uint32_t far_cap,
+                             double delta, const SsspLdsPlan& plan, uint32_t iter_guard,
                              double2* out_lr, uint16_t* out_hops, double* out_rowmin,
                              unsigned long long* d_stats, hipStream_t stream);
 
@@ -252,7 +230,37 @@ hipError_t launch_row_min(int64_t rows, int64_t A, const double2* lr, double* ou
 hipError_t launch_fill_u64(unsigned long long* p, unsigned long long v, int64_t n,
                            hipStream_t stream);
 
-// SSSP workgroups one CU holds with the LDS plan of wg_per_cu (registers and LDS permitting)
-int sssp_max_blocks_per_cu(int wg_per_cu);
+// ---- graph preparation on the GPU (topo_prep.hip), once per topology: DESIGN.md 3.1 ----
+// Input arrays are the parsed graph in HBM (document order: eu / ev int32[E], elat / eloss f64[E],
+// vloss f64[V]); outputs are in the relabelled vertex order.  Each call synchronises `st`.
+// degrees of the non-loop graph (deg u32[V]), the lowest-id self loop (selfE, ~0 = none) and
+// the adjacency size *nadj = 2 x non-loop edges
+hipError_t prep_degrees(int64_t V, int64_t E, const int32_t* eu, const int32_t* ev, uint32_t* deg,
+                        uint32_t* selfE, int64_t* nadj, hipStream_t st);
+// relabel (degree descending, the tail grouped by its primary hub among the first H): perm
+// (new -> old), inv (old -> new), rowptr u32[V+1], per-vertex loss and self-loop arrays
+hipError_t prep_relabel(int64_t V, int64_t E, uint32_t H, const int32_t* eu, const int32_t* ev,
+                        const uint32_t* deg, const uint32_t* selfE, const double* elat,
+                        const double* eloss, const double* vloss_in, uint32_t* perm,
+                        uint32_t* inv, uint32_t* rowptr, double* vloss, double* selfLat,
+                        double* selfLoss, hipStream_t st);
+// 16-B adjacency records {col, 0, f64 w} rows ascending by (neighbour, edge id), and aloss
+hipError_t prep_adjacency(int64_t V, int64_t E, int64_t nadj, const int32_t* eu, const int32_t* ev,
+                          const uint32_t* inv, const double* elat, const double* eloss,
+                          uint32_t* adj, double* aloss, hipStream_t st);
+// pi = d(h0, .) from vertex 0 (f64[V], +inf = unreached); *iterations = frontier rounds
+hipError_t prep_h0_distances(int64_t V, const uint32_t* rowptr, const uint32_t* adj, double* pot,
+                             int* iterations, hipStream_t st);
+// h0 tree (sptPar u32[V], spt {parent, slot in v's row, f64 w}[V]), the records' pi / kappa0
+// field, *piMax = the largest finite pi; rows < nwave take a wavefront each
+hipError_t prep_tree(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* rowptr,
+                     uint32_t* adj, const double* pot, uint32_t* sptPar, uint32_t* spt,
+                     double* piMax, hipStream_t st);
+// the plain kappa-sorted relaxation copy (adjk, kap, ksum, kap0) of adj: also restores it after
+// a target-aware re-sort when the target-aware order no longer applies
+hipError_t launch_kappa_copy(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* rowptr,
+                             const uint32_t* adj, const double* pot, const uint32_t* sptPar,
+                             uint32_t* adjk, float* kap, float* ksum, float* kap0,
+                             hipStream_t st);
 
 }  // namespace shdtopo

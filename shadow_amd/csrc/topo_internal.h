@@ -69,7 +69,16 @@ inline int32_t glibc_rand_r(uint32_t* seed) {
 }
 inline double rand_r_double(uint32_t* seed) { return (double)glibc_rand_r(seed) / 2147483647.0; }
 
-uint32_t string_to_ip(const char* s);
+// Host side of the graph preparation (topo_core.cpp upload_csr), relabelled ids.
+struct HostPrep {
+    std::vector<int32_t> perm;      // new -> old
+    std::vector<int32_t> inv;       // old -> new
+    std::vector<double> pot;        // pi = d(h0, v) from the top hub: bucket shifts, batch order
+    std::vector<uint32_t> sptPar;   // h0 shortest-path tree parent (source ordering)
+    double piMax = 0.0;             // largest finite pi
+};
+
+uint32_t string_to_ip(const char* s);  // inet_pton(AF_INET) as shd-address.c:137-144
 
 // Immutable host mirror of one device routing table (the per-call getters' view): the column
 // map it was built for, row minima, and (full) the A x A latency / reliability / hop arrays.
@@ -82,7 +91,7 @@ struct HostTable {
     bool full = false;
     std::vector<double> lat, rel;
     std::vector<uint16_t> hops;
-};  // inet_pton(AF_INET) as shd-address.c:137-144
+};
 
 // Index of the attachment candidates (the "poi" vertices) so that attaching H hosts costs
 // O(H + V) instead of the reference's O(H * V) string scan (shd-topology.c:1087); candidate

@@ -130,6 +130,7 @@ struct LdsB {
     unsigned long long pt[5];   // parent-pass phase ticks (diagnostic)
     unsigned long long dg[4];   // diagnostic: hub edges, hub source-relaxations, first-iteration
                                 // edges, first-iteration source-relaxations
+    unsigned long long touched; // tail lines reset (touched by the slot's previous batches)
     unsigned long long bt[8];   // SHD_BATCH_TIME builds: wave ticks of tail / hub iterations in
                                 // chunk loads, phase A, phase B; phase-B rounds, active lanes
 };
@@ -170,6 +171,7 @@ struct BView {
     uint32_t* hpar;            // HBM [P][K]: vertex whose relaxation last lowered hub v for j
     uint32_t* pend;            // HBM, 1 bit per vertex: a tail vertex with a pair pending past cb
     uint32_t* tie;             // HBM, 1 bit per (tail vertex, source): a relaxation tied its value
+    uint32_t* touch;           // HBM, 1 bit per tail vertex: the batch lowered its line from +inf
     uint32_t* tpar;            // HBM [V][K]: vertex whose relaxation last lowered the tail pair
                                // (SHD_TAIL_HINT; the parent pass' par array, free during the SSSP)
     uint32_t H, P;
@@ -645,6 +647,9 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     cur[rr] = old;
                 }
                 bool nr = false, nf = false;
+                // first reach of a tail line (old value +inf): the line joins the batch's
+                // touched set, the only lines reset for the next batch
+                const bool ft = im && n[rr] >= D.H && cur[rr] == kInfBits;
                 if (im) {
                     const uint32_t b = bkt(bits2d(ab[rr]), L.sh[jj], B.inv_delta);
                     if (b <= B.cb) nr = n[rr] < D.H || kappa_useful(kz[rr], L.dh0[jj],
@@ -656,8 +661,8 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 }
                 // the edge's pairs sit in adjacent lanes (<= K of them): their near bits and
                 // first-reach flags are OR-ed into the segment's first lane, which does the
-                // edge's pend and mask atomics once
-                uint32_t gm = nr ? 1u << jj : 0u, gf = nf ? 1u : 0u;
+                // edge's pend, touch and mask atomics once
+                uint32_t gm = nr ? 1u << jj : 0u, gf = (nf ? 1u : 0u) | (ft ? 2u : 0u);
 #pragma unroll
                 for (int o = 1; o < K; o <<= 1) {
                     const uint32_t ym = __shfl_down(gm, o, 64), yf = __shfl_down(gf, o, 64);
@@ -666,7 +671,8 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 }
                 const uint32_t pe = __shfl_up(er[rr], 1, 64);
                 const bool head = on && (lane == 0 || pe != er[rr]);
-                if (head && gf) (void)atomicOr(&D.pend[n[rr] >> 5], 1u << (n[rr] & 31));
+                if (head && (gf & 1u)) (void)atomicOr(&D.pend[n[rr] >> 5], 1u << (n[rr] & 31));
+                if (head && (gf & 2u)) (void)atomicOr(&D.touch[n[rr] >> 5], 1u << (n[rr] & 31));
                 bool first = false, hfirst = false;
                 if (head && gm) {
                     if (n[rr] < D.H) hfirst = MO::set(hdef, n[rr], gm) == 0u;
@@ -738,7 +744,7 @@ __global__ void __launch_bounds__(kSsspBlock, kBatchWgPerCu)
 sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                   const double* __restrict__ srcsh, int nsrc, int kf,
                   const uint32_t* __restrict__ targets, int A, double delta, uint32_t H,
-                  uint32_t P, uint32_t far_cap,
+                  uint32_t P, uint32_t iter_guard,
                   double2* __restrict__ out_lr, uint16_t* __restrict__ out_hops,
                   double* __restrict__ out_rowmin, unsigned long long* __restrict__ stats) {
     using MO = MaskOps<K>;
@@ -779,7 +785,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     const uint32_t cap = (uint32_t)V;
     BBuckets B;
     B.inv_delta = 1.0 / delta;
-    (void)far_cap;  // no bounded far structure to overflow (single-source kernel test hook)
     // parent-pass pair lists: qa / qb (pcur / pnxt) and the ring memory (fscr), V * K entries each,
     // then the merged vertex list
     uint32_t* fscr = reinterpret_cast<uint32_t*>(ws.ring) + (size_t)slot * ws.ring_entries;
@@ -788,6 +793,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     D.pend = vscr + (size_t)V;
     const uint32_t tw = (uint32_t)((V * K + 31) / 32);  // words of the tie bitmap
     D.tie = D.pend + pw + 64;
+    D.touch = D.tie + tw + 64;  // touched-line bitmap (one bit per tail vertex)
     const uint32_t pcap = (uint32_t)(V * K);
 
     uint32_t iter = ctr[0], mep = ctr[2];
@@ -797,6 +803,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     if (tid < 5) L.pt[tid] = 0;
     if (tid < 4) L.dg[tid] = 0;
     if (tid < 8) L.bt[tid] = 0;
+    if (tid == 0) L.touched = 0;
     unsigned long long tk = wall_clock64();
 
     for (;;) {
@@ -831,14 +838,30 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         if (tid < (uint32_t)K) L.dh0[tid] = INFINITY;
         if (tid == 0) L.invd = B.inv_delta;
         {
+            // the distance lines the previous batch of this slot lowered from +inf back to +inf:
+            // only touched tail vertices (their bit in D.touch), not the whole [V][K] block
+            // (64 MB at K = 8 per batch)
             typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
             u64x2* d2 = reinterpret_cast<u64x2*>(D.dist);
             const u64x2 inf2 = {kInfBits, kInfBits};
-            const size_t lo = (size_t)H * K / 2, hi = (size_t)V * K / 2;
-            for (size_t i = lo + tid; i < hi; i += kSsspBlock) {
-                if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + i);  // streaming: no L2 fill
-                else d2[i] = inf2;
+            unsigned long long nt = 0;
+            for (uint32_t wi = H / 32 + tid; wi < pw; wi += kSsspBlock) {
+                uint32_t w = ld_l2_u32(&D.touch[wi]);
+                if (!w) continue;
+                D.touch[wi] = 0u;
+                nt += (unsigned long long)__popc(w);
+                while (w) {
+                    const uint32_t v = wi * 32u + (uint32_t)__ffs(w) - 1u;
+                    w &= w - 1u;
+#pragma unroll
+                    for (int h = 0; h < K / 2; h++) {
+                        if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + (size_t)v * (K / 2) + h);
+                        else d2[(size_t)v * (K / 2) + h] = inf2;
+                    }
+                }
             }
+            nt = wave_sum_u64(nt);
+            if ((tid & 63) == 0 && nt) atomicAdd(&L.touched, nt);
         }
         if (tid == 0) {
             L.fminb = kNoBucket;
@@ -853,6 +876,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             else {
                 D.dist[(size_t)s * K + tid] = 0ull;
                 atomicOr(&D.pend[s >> 5], 1u << (s & 31));
+                atomicOr(&D.touch[s >> 5], 1u << (s & 31));
             }
             atomicMin(&L.fminb, bkt(0.0, L.sh[tid], B.inv_delta));
         }
@@ -911,7 +935,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 { uint32_t* t = qin; qin = qout; qout = t; }
                 { M* t = mcur; mcur = mnxt; mnxt = t; }
                 n_near++;
-                if (++guard > 4000000u) {
+                if (++guard > iter_guard) {
                     aborted = true;
                     nq = 0;
                     break;
@@ -1464,6 +1488,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         atomicAdd(&stats[ST_EV0 + 2], L.dg[0]);
         atomicAdd(&stats[ST_EV0 + 4], L.dg[1]);
         atomicAdd(&stats[ST_EV0 + 7], L.dg[2]);
+        atomicAdd(&stats[ST_TOUCHED], L.touched);
         atomicAdd(&stats[ST_NEAR_IT + 0], 0ull);
         atomicAdd(&stats[ST_OVERSITE], 0ull);
         atomicAdd(&stats[ST_EV0 + 5], 0ull);
@@ -1504,26 +1529,35 @@ hipError_t launch_mark_targets(uint32_t* adjk, int64_t nadj, const uint32_t* tbi
 // margin), so K(x) stays under the threshold of every chain vertex at its final distance (every
 // iterate K_k is such a bound; they rise monotonically towards the fixpoint).  One wavefront per
 // vertex; Kin == nullptr computes K_0.
+__device__ __forceinline__ double kfix_term(const uint32_t* adj, const double* pot,
+                                            const uint32_t* tbits, const double* Kin, uint32_t k) {
+    const uint32_t y = adj[kAdjWords * k];
+    const double w = __hiloint2double((int)adj[kAdjWords * k + 3], (int)adj[kAdjWords * k + 2]);
+    const double p = pot[y];
+    const double kap = isfinite(p) ? w - p : -INFINITY;
+    double t = kap;
+    if (Kin && !((tbits[y >> 5] >> (y & 31u)) & 1u)) {
+        const double ky = Kin[y] + w * (1.0 - 2e-5) - 1e-9;
+        t = ky > kap ? ky : kap;
+    }
+    return t;
+}
+
+// A wavefront per hub row (ids < nwave: the long rows of the degree order), a thread per tail row
+// (a wavefront per row left 54 of 64 lanes idle on the C4 tail: 6.2 ms per step).
 __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
                                  const uint32_t* __restrict__ adj, const double* __restrict__ pot,
                                  const uint32_t* __restrict__ tbits,
                                  const double* __restrict__ Kin, double* __restrict__ Kout,
-                                 int64_t V, unsigned int* __restrict__ changed) {
+                                 int64_t V, uint32_t nwave, unsigned int* __restrict__ changed) {
     const uint32_t lane = threadIdx.x & 63u;
-    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t x = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; x < V; x += nw) {
-        const uint32_t r0 = rowptr[x], r1 = rowptr[x + 1];
+    const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    bool ch = false;
+    for (int64_t x = gt >> 6; x < (int64_t)nwave; x += gs >> 6) {
         double m = INFINITY;
-        for (uint32_t k = r0 + lane; k < r1; k += 64u) {
-            const uint32_t y = adj[kAdjWords * k];
-            const double w = __hiloint2double((int)adj[kAdjWords * k + 3], (int)adj[kAdjWords * k + 2]);
-            const double p = pot[y];
-            const double kap = isfinite(p) ? w - p : -INFINITY;
-            double t = kap;
-            if (Kin && !((tbits[y >> 5] >> (y & 31u)) & 1u)) {
-                const double ky = Kin[y] + w * (1.0 - 2e-5) - 1e-9;
-                t = ky > kap ? ky : kap;
-            }
+        for (uint32_t k = rowptr[x] + lane; k < rowptr[x + 1]; k += 64u) {
+            const double t = kfix_term(adj, pot, tbits, Kin, k);
             m = t < m ? t : m;
         }
 #pragma unroll
@@ -1532,10 +1566,20 @@ __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
             m = y < m ? y : m;
         }
         if (lane == 0) {
-            if (Kin && !(m == Kin[x])) atomicOr(changed, 1u);  // one lane per wave
+            ch |= Kin && !(m == Kin[x]);
             Kout[x] = m;
         }
     }
+    for (int64_t x = (int64_t)nwave + gt; x < V; x += gs) {
+        double m = INFINITY;
+        for (uint32_t k = rowptr[x]; k < rowptr[x + 1]; k++) {
+            const double t = kfix_term(adj, pot, tbits, Kin, k);
+            m = t < m ? t : m;
+        }
+        ch |= Kin && !(m == Kin[x]);
+        Kout[x] = m;
+    }
+    if (__ballot(ch) && lane == 0) atomicOr(changed, 1u);  // one atomic per wave
 }
 
 // largest half <= x (NaN: -inf)
@@ -1565,11 +1609,12 @@ __global__ void kfix_store_kernel(uint32_t* __restrict__ adjk, int64_t nadj,
 
 hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const double* pot,
                             const uint32_t* tbits, const double* Kin, double* Kout, int64_t V,
-                            unsigned int* changed, hipStream_t stream) {
+                            uint32_t nwave, unsigned int* changed, hipStream_t stream) {
     if (V <= 0) return hipSuccess;
-    const int64_t g = std::min<int64_t>((V + 3) / 4, 256 * 32);
+    nwave = (uint32_t)std::min<int64_t>(nwave, V);
+    const int64_t g = std::min<int64_t>(std::max<int64_t>((V + 255) / 256, (nwave + 3) / 4), 256 * 32);
     hipLaunchKernelGGL(kfix_step_kernel, dim3((unsigned)g), dim3(256), 0, stream, rowptr, adj,
-                       pot, tbits, Kin, Kout, V, changed);
+                       pot, tbits, Kin, Kout, V, nwave, changed);
     return hipGetLastError();
 }
 
@@ -1715,7 +1760,7 @@ SsspLdsPlan sssp_batch_lds_plan(int K, int64_t hub_limit, uint32_t par_hubs, int
 template <int K>
 static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                                  const double* d_srcsh, int nsrc, int kf, const uint32_t* d_targets,
-                                 int A, double delta, const SsspLdsPlan& plan, uint32_t far_cap,
+                                 int A, double delta, const SsspLdsPlan& plan, uint32_t iter_guard,
                                  double2* out_lr, uint16_t* out_hops, double* out_rowmin,
                                  unsigned long long* d_stats, hipStream_t stream) {
     if (kf < 1 || kf > K) return hipErrorInvalidValue;
@@ -1732,21 +1777,21 @@ static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(sssp_batch_kernel<K>, dim3(grid), dim3(kSsspBlock), plan.bytes, stream, g,
-                       ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan.H, plan.P, far_cap,
+                       ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan.H, plan.P, iter_guard,
                        out_lr, out_hops, out_rowmin, d_stats);
     return hipGetLastError();
 }
 
 hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                              const double* d_srcsh, int nsrc, int kf, const uint32_t* d_targets,
-                             int A, double delta, const SsspLdsPlan& plan, uint32_t far_cap,
+                             int A, double delta, const SsspLdsPlan& plan, uint32_t iter_guard,
                              double2* out_lr, uint16_t* out_hops, double* out_rowmin,
                              unsigned long long* d_stats, hipStream_t stream) {
     switch (K) {
-        case 2: return launch_batch_k<2>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
-        case 4: return launch_batch_k<4>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
-        case 8: return launch_batch_k<8>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
-        case 16: return launch_batch_k<16>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, far_cap, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 2: return launch_batch_k<2>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, iter_guard, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 4: return launch_batch_k<4>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, iter_guard, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 8: return launch_batch_k<8>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, iter_guard, out_lr, out_hops, out_rowmin, d_stats, stream);
+        case 16: return launch_batch_k<16>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, iter_guard, out_lr, out_hops, out_rowmin, d_stats, stream);
     }
     return hipErrorInvalidValue;
 }

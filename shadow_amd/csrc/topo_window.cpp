@@ -14,11 +14,19 @@ __attribute__((weak)) uint32_t address_toNetworkIP(Address* address);
 __attribute__((weak)) double random_nextDouble(Random* random);
 }
 
+// One recorded packet: its vertices are resolved at emit, when the reference routed it
+// (shd-worker.c:345-369), so a host detached before the flush does not lose its packets.
+struct WinPacket {
+    int32_t srcV, dstV;
+    uint32_t payloadLength, rngState;
+    uint64_t now;
+    void* packet;
+};
+
 struct _TopoWindow {
     Topology* top = nullptr;
     std::mutex mu;  // worker threads emit concurrently; the window keeps their real-time order
-    std::vector<TopoPacketIn> in;
-    std::vector<void*> packets;
+    std::vector<WinPacket> in;
     std::vector<TopoPacketOut> out;
 };
 
@@ -39,17 +47,10 @@ int64_t topowindow_emit_state(TopoWindow* w, uint32_t srcIP, uint32_t dstIP,
     if (!w) return -1;
     // the reference's getters return -1.0 for an address the topology does not know (the
     // packet is then dropped unless a control packet): not routed here, the caller drops it
-    if (shdtopo_vertex_of_ip(w->top, srcIP) < 0 || shdtopo_vertex_of_ip(w->top, dstIP) < 0)
-        return -1;
-    TopoPacketIn p;
-    p.srcIP = srcIP;
-    p.dstIP = dstIP;
-    p.payloadLength = payloadLength;
-    p.rngState = preDrawState;
-    p.now = now;
+    const int32_t sv = shdtopo_vertex_of_ip(w->top, srcIP), dv = shdtopo_vertex_of_ip(w->top, dstIP);
+    if (sv < 0 || dv < 0) return -1;
     std::lock_guard<std::mutex> lk(w->mu);
-    w->in.push_back(p);
-    w->packets.push_back(packet);
+    w->in.push_back(WinPacket{sv, dv, payloadLength, preDrawState, now, packet});
     return (int64_t)w->in.size() - 1;
 }
 
@@ -75,21 +76,38 @@ int64_t topowindow_pending(TopoWindow* w) {
 int topowindow_flush(TopoWindow* w, uint64_t jumpNs, int multiThreaded, TopoWindowDeliver deliver,
                      void* ctx) {
     if (!w) return -1;
-    std::vector<TopoPacketIn> in;
-    std::vector<void*> packets;
+    std::vector<WinPacket> in;
     {
         std::lock_guard<std::mutex> lk(w->mu);
         in.swap(w->in);
-        packets.swap(w->packets);
     }
     if (in.empty()) return 0;
-    w->out.resize(in.size());
-    const int r = topology_routePacketBatch(w->top, in.data(), w->out.data(), in.size(), jumpNs,
-                                            multiThreaded);
-    if (r) return r;
+    const size_t n = in.size();
+    std::vector<int32_t> sv(n), dv(n);
+    std::vector<uint32_t> pay(n), st(n);
+    std::vector<uint64_t> now(n);
+    for (size_t i = 0; i < n; i++) {
+        sv[i] = in[i].srcV;
+        dv[i] = in[i].dstV;
+        pay[i] = in[i].payloadLength;
+        st[i] = in[i].rngState;
+        now[i] = in[i].now;
+    }
+    w->out.resize(n);
+    // a packet whose vertex left the table (its last host detached) comes back undelivered
+    const int r = shdtopo_route_batch_vertices(w->top, sv.data(), dv.data(), pay.data(), st.data(),
+                                               now.data(), n, jumpNs, multiThreaded, w->out.data());
+    if (r < 0) {
+        // nothing was routed: the window is put back in front of what was emitted meanwhile, so
+        // a later flush routes every packet in emission order
+        std::lock_guard<std::mutex> lk(w->mu);
+        in.insert(in.end(), w->in.begin(), w->in.end());
+        w->in.swap(in);
+        return r;
+    }
     if (deliver)
-        for (size_t i = 0; i < in.size(); i++)
-            deliver(ctx, packets[i], w->out[i].delivered, w->out[i].time);
+        for (size_t i = 0; i < n; i++)
+            deliver(ctx, in[i].packet, w->out[i].delivered, w->out[i].time);
     return 0;
 }
 

@@ -164,8 +164,9 @@ class Topology:
             ins[i].now = int(now[i])
         outs = (L.TopoPacketOut * n)()
         r = self._lib.topology_routePacketBatch(self._h, ins, outs, n, int(jump_ns), int(clamp))
-        if r != 0:
+        if r < 0:
             raise RuntimeError("topology_routePacketBatch failed: %d" % r)
+        self.last_unrouted = r  # packets whose address is not attached (delivered 0)
         t = np.array([o.time for o in outs], dtype=np.uint64)
         st = np.array([o.rngState for o in outs], dtype=np.uint32)
         dl = np.array([o.delivered for o in outs], dtype=np.uint8)
@@ -261,6 +262,23 @@ class Topology:
             raise RuntimeError("export_graph failed")
         return V, eu, ev, el, lo, vl
 
+    def export_csr(self):
+        """Test hook (shdtopo_export_csr): the GPU-prepared CSR -- perm (new -> old), rowptr, the
+        adjacency columns, pi = d(h0, .) and the h0-tree parents, relabelled ids."""
+        n = int(self._lib.shdtopo_export_csr(self._h, None, None, None, None, None))
+        if n < 0:
+            raise RuntimeError("shdtopo_export_csr failed: %d" % n)
+        V = self.num_vertices
+        perm = np.empty(V, np.int32)
+        rowptr = np.empty(V + 1, np.uint32)
+        col = np.empty(max(n, 1), np.uint32)
+        pot = np.empty(V, np.float64)
+        par = np.empty(V, np.uint32)
+        r = self._lib.shdtopo_export_csr(self._h, _p(perm), _p(rowptr), _p(col), _p(pot), _p(par))
+        if r != n:
+            raise RuntimeError("shdtopo_export_csr failed: %d" % r)
+        return dict(perm=perm, rowptr=rowptr, col=col[:n], pot=pot, tree_parent=par)
+
     def replay_source(self, src, full=True):
         """Test hook (shdtopo_replay_source): the exact heap replay's (dist, parent vertex) from
         vertex `src`, original ids; full=False stops when every attached vertex is popped."""
@@ -285,11 +303,50 @@ class Topology:
         if r != 0:
             raise RuntimeError("shdtopo_build_rows failed: %d" % r)
 
+    def rebuild(self):
+        """shdtopo_rebuild: build the whole table now (the getters build it lazily)."""
+        r = self._lib.shdtopo_rebuild(self._h)
+        if r != 0:
+            raise RuntimeError("shdtopo_rebuild failed: %d" % r)
+
+    def bind_table_ref(self, lr, hops, global_min, stream=0):
+        """Install lr / hops in place (the tensors must outlive the binding)."""
+        r = self._lib.shdtopo_bind_table_ref(self._h, lr.data_ptr(), hops.data_ptr(),
+                                             float(global_min), stream or None)
+        if r != 0:
+            raise RuntimeError("shdtopo_bind_table_ref failed: %d" % r)
+        self._bound = (lr, hops)  # keep the buffers alive while bound
+
     def bind_table(self, lr, hops, global_min, stream=0):
         r = self._lib.shdtopo_bind_table(self._h, lr.data_ptr(), hops.data_ptr(),
                                          float(global_min), stream or None)
         if r != 0:
             raise RuntimeError("shdtopo_bind_table failed: %d" % r)
+
+    def route_batch_vertices(self, src_v, dst_v, payload, rng_state, now, jump_ns, clamp=True):
+        """shdtopo_route_batch_vertices: (time, delivered, state, not-routed count)."""
+        n = len(src_v)
+        c = lambda x, t: np.ascontiguousarray(x, dtype=t)
+        sv, dv = c(src_v, np.int32), c(dst_v, np.int32)
+        pay, st, nw = c(payload, np.uint32), c(rng_state, np.uint32), c(now, np.uint64)
+        outs = (L.TopoPacketOut * max(n, 1))()
+        r = self._lib.shdtopo_route_batch_vertices(self._h, _p(sv), _p(dv), _p(pay), _p(st),
+                                                   _p(nw), n, int(jump_ns), int(clamp), outs)
+        if r < 0:
+            raise RuntimeError("shdtopo_route_batch_vertices failed: %d" % r)
+        t = np.array([outs[i].time for i in range(n)], dtype=np.uint64)
+        s = np.array([outs[i].rngState for i in range(n)], dtype=np.uint32)
+        dl = np.array([outs[i].delivered for i in range(n)], dtype=np.uint8)
+        return t, dl, s, r
+
+    def route_batch_device_slot(self, slot, src_col, dst_col, payload, state_in, now, jump_ns,
+                                clamp, t_out, state_out, delivered, stream=0):
+        r = self._lib.shdtopo_route_batch_device_slot(
+            self._h, int(slot), src_col.data_ptr(), dst_col.data_ptr(), payload.data_ptr(),
+            state_in.data_ptr(), now.data_ptr(), int(src_col.numel()), int(jump_ns), int(clamp),
+            t_out.data_ptr(), state_out.data_ptr(), delivered.data_ptr(), stream or None)
+        if r != 0:
+            raise RuntimeError("shdtopo_route_batch_device_slot failed: %d" % r)
 
     def route_batch_device(self, src_col, dst_col, payload, state_in, now, jump_ns, clamp,
                            t_out, state_out, delivered, stream=0):

@@ -33,17 +33,16 @@ def test_complete_table_bundled(name):
     assert top.getMinimumLatency() == olat.min()
 
 
-@pytest.mark.parametrize("batch", [1, 8])
+@pytest.mark.parametrize("fill", [1, 8])
 @pytest.mark.parametrize("hubs", [-1, 0, 700])
 @pytest.mark.parametrize("integer", [False, True])
-def test_sssp_synthetic_table(integer, hubs, batch):
-    """SSSP branch: sssp_rows_kernel (batch 1) / sssp_batch_kernel (8 sources per workgroup), plus
-    the heap replay of tie rows, vs the igraph-0.7 Dijkstra + helper restatement.  `hubs` caps the LDS-resident distance rows:
-    all (-1: as many as fit), none, or mixed."""
+def test_sssp_synthetic_table(integer, hubs, fill):
+    """SSSP branch: sssp_batch_kernel (8 sources per workgroup; fill 1 = one source per batch),
+    plus the heap replay of tie rows, vs the igraph-0.7 Dijkstra + helper restatement.  `hubs`
+    caps the LDS-resident distance rows: all (-1: as many as fit), none, or mixed."""
     top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
     top.set_option("lds_hubs", hubs)
-    top.set_option("batch", batch)
-    top.set_option("batch_fill", batch)  # whole batches (auto would run 1 source per slot here)
+    top.set_option("batch_fill", fill)  # whole batches (auto would run 1 source per slot here)
     otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()
@@ -94,23 +93,68 @@ def test_target_skip_exact_across_target_sets(integer):
         assert len(oa) > 0
 
 
-@pytest.mark.parametrize("which", ["far", "near"])
-@pytest.mark.parametrize("hubs", [-1, 0])
-def test_sssp_queue_overflow_fallback(hubs, which):
-    """Single-source kernel (batch 1): a far pile / near queue too small for the source: entries
-    are lost, the source switches to splits that scan every distance (re-expanding the current
-    bucket after a near-queue loss) with deduplicated pushes, and the table is still bit-exact.
-    (The batch kernel has no bounded far structure -- every bucket starts with a sweep -- and its
-    near queue is deduplicated by the source masks, so it has nothing to overflow.)"""
-    top, g = synthetic_pair(seed=13, n_routers=2500, n_poi=120, n_edges=25000)
-    top.set_option("lds_hubs", hubs)
-    top.set_option("batch", 1)
-    top.set_option(which + "_cap", 48)
-    otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay"])
+@pytest.mark.parametrize("integer", [False, True])
+def test_single_slot_reuses_touched_lines(integer):
+    """One SSSP slot runs every batch: each batch resets only the distance lines the previous
+    batches of the slot lowered from +inf (the touched-line bitmap), never the whole [V][K]
+    block.  Two builds (the second after a late attach) equal the oracle bit for bit."""
+    top, g = synthetic_pair(seed=23, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
+    top.set_option("slots", 1)
+    top.set_option("batch_fill", 3)
+    verts = []
+    st = 7
+    for lo, hi in ((0, 90), (90, 260)):
+        for k in range(lo, hi):
+            st = (st * 1103515245 + 12345) & 0xFFFFFFFF
+            v, _ = top.attach_ip(host_ip(k + 1), st, typeHint=("client", "relay")[k % 2])
+            verts.append(v)
+        a, lat, rel, hops = top.table()
+        s_ = top.stats()
+        assert s_["slots"] == 1 and s_["errors"] == 0
+        assert 0 < s_["touched_lines"] < len(a) * top.num_vertices
+        oa, olat, orel, ohops = g.table(verts)
+        assert np.array_equal(a, oa)
+        assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+        assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+        assert np.array_equal(hops, ohops.astype(np.uint16))
+
+
+@pytest.mark.parametrize("toggle", ["target_skip", "target_resort"])
+def test_target_options_toggled_on_one_topology(toggle):
+    """the target-aware re-sort rewrites the relaxation copy for one target set.
+    Turning the skip (or the re-sort) off on the same Topology and then changing the target set
+    must not leave the old set's keys in the copy: it is restored from the plain adjacency."""
+    top, g = synthetic_pair(seed=29, n_routers=3000, n_poi=150, n_edges=30000)
+    top.set_option("batch_fill", 8)
+    verts = []
+    st = 3
+    for rnd, (lo, hi) in enumerate(((0, 100), (100, 240), (240, 330))):
+        for k in range(lo, hi):
+            st = (st * 1103515245 + 12345) & 0xFFFFFFFF
+            v, _ = top.attach_ip(host_ip(k + 1), st, typeHint=("client", "relay")[k % 2])
+            verts.append(v)
+        a, lat, rel, hops = top.table()
+        oa, olat, orel, ohops = g.table(verts)
+        assert np.array_equal(a, oa)
+        assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+        assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+        assert np.array_equal(hops, ohops.astype(np.uint16))
+        top.set_option(toggle, rnd % 2)  # off after round 0, on again after round 1
+
+
+def test_iteration_guard_error_then_clean_build():
+    """The batch kernel's iteration guard (a batch that never settles) is reported: the build
+    returns -4 (abort() under the default abort_on_error), and the next build with the guard
+    restored is bit-exact -- nothing of the aborted batches leaks into it."""
+    top, g = synthetic_pair(seed=31, n_routers=2000, n_poi=101, n_edges=20000)
+    top.set_option("abort_on_error", 0)
+    otop, ips, verts = attach_hosts(top, g, 250, type_hints=["client", "relay"])
+    top.set_option("iter_guard", 3)
+    with pytest.raises(RuntimeError, match="-4"):
+        top.build()
+    top.set_option("iter_guard", 4e6)
     a, lat, rel, hops = top.table()
-    st = top.stats()
     oa, olat, orel, ohops = g.table(verts)
-    assert st["far_scan_sources"] > 0 and st["errors"] == 0
     assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
     assert np.array_equal(hops, ohops.astype(np.uint16))

@@ -81,3 +81,60 @@ def test_getters_trigger_multi_device_build():
         assert top.reliability_ip(x, y) == otop.get_reliability(x, y)
     assert top.stats()["devices"] == 2
     assert top.lazyMinimumLatency() == otop.minimum_path_latency
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [2, 3])
+def test_multi_device_build_prepares_the_graph_once(devices):
+    """One multi-GPU build prepares the graph once (on the owner's device) and the peer engines
+    copy its device CSR and share its host arrays: one host preparation per build, none in the
+    next build, and the peers' tables equal the owner's (checked against the oracle above)."""
+    top, g = synthetic_pair(seed=37, n_routers=2500, n_poi=120, n_edges=25000)
+    top.set_option("devices", devices)
+    otop, ips, verts = attach_hosts(top, g, 200, type_hints=["client", "relay"])
+    top.build()
+    st = top.stats()
+    assert st["devices"] == devices and st["csr_host_runs"] == 1 and st["csr_ms"] > 0
+    assert st["exchange_kind"] == 2  # engines sharing the test box's one device: peer copies
+    top.rebuild()
+    st = top.stats()
+    assert st["csr_host_runs"] == 0 and st["csr_ms"] == 0
+    a, lat, rel, hops = top.table()
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+
+
+@pytest.mark.gpu
+def test_route_on_every_device_slot():
+    """shdtopo_route_batch_device_slot: every engine of a devices = 3 Topology holds the whole
+    table after the exchange and routes a window slice bit-exactly like slot 0."""
+    import torch
+    top, g = synthetic_pair(seed=39, n_routers=1500, n_poi=80, n_edges=15000)
+    top.set_option("devices", 3)
+    attach_hosts(top, g, 150, type_hints=["client", "relay"])
+    a, lat, rel, hops = top.table()
+    A, n = len(a), 5000
+    rng = np.random.default_rng(9)
+    s = rng.integers(0, A, n).astype(np.int32)
+    d = rng.integers(0, A, n).astype(np.int32)
+    pay = np.where(rng.random(n) < 0.8, 1448, 0).astype(np.int32)
+    sin = rng.integers(0, 2**31, n).astype(np.int32)
+    now = rng.integers(10**9, 2 * 10**9, n).astype(np.int64)
+    cu = lambda x: torch.from_numpy(x).cuda()
+    outs = []
+    for slot in range(3):
+        t_out = torch.empty(n, dtype=torch.int64, device="cuda")
+        s_out = torch.empty(n, dtype=torch.int32, device="cuda")
+        d_out = torch.empty(n, dtype=torch.uint8, device="cuda")
+        top.route_batch_device_slot(slot, cu(s), cu(d), cu(pay), cu(sin), cu(now), 4_000_000, 1,
+                                    t_out, s_out, d_out)
+        torch.cuda.synchronize()
+        outs.append((t_out.cpu().numpy(), s_out.cpu().numpy(), d_out.cpu().numpy()))
+    ot, od, os_ = oracle.route_packets(lat[s, d], rel[s, d], pay.view(np.uint32),
+                                       sin.view(np.uint32), now.view(np.uint64), 4_000_000, 1)
+    for t_, s_, d_ in outs:
+        assert np.array_equal(t_.view(np.uint64), ot)
+        assert np.array_equal(s_.view(np.uint32), os_)
+        assert np.array_equal(d_, od)

@@ -160,3 +160,64 @@ def test_master_min_jump():
     assert oracle.master_min_jump(0) == 10_000_000
     assert oracle.master_min_jump(7.9) == 7_000_000
     assert oracle.master_min_jump(7.9, runahead_ms=9) == 9_000_000
+
+
+def _scipy_rows(V, eu, ev, elat, eloss, vloss, sources, targets):
+    """Latency / reliability / hops of every (source, target) pair from scipy's shortest-path
+    TREE (dijkstra with return_predecessors) -- an implementation independent of the oracle's
+    igraph restatement.  On a tie-free graph the shortest paths are unique, so any correct
+    Dijkstra returns igraph's parents; reliability then follows shd-topology.c:561-671 (A.4)."""
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import dijkstra
+    m = eu != ev
+    A = sp.coo_matrix((elat[m], (eu[m], ev[m])), shape=(V, V)).tocsr()
+    eidx = {}
+    for e in np.nonzero(m)[0]:
+        eidx.setdefault((min(eu[e], ev[e]), max(eu[e], ev[e])), e)
+    dist, pred = dijkstra(A, directed=False, indices=np.asarray(sources), return_predecessors=True)
+    out_lat = np.zeros((len(sources), len(targets)))
+    out_rel = np.zeros_like(out_lat)
+    out_hops = np.zeros((len(sources), len(targets)), np.int64)
+    for i, s in enumerate(sources):
+        for j, t in enumerate(targets):
+            if t == s:
+                continue
+            path = [int(t)]
+            while path[-1] != s:
+                path.append(int(pred[i, path[-1]]))
+            path.reverse()
+            rel = 1.0
+            rel *= (1.0 - vloss[s])
+            rel *= (1.0 - vloss[t])
+            for a, b in zip(path[:-1], path[1:]):
+                rel *= (1.0 - eloss[eidx[(min(a, b), max(a, b))]])
+            out_lat[i, j] = dist[i, t]
+            out_rel[i, j] = rel
+            out_hops[i, j] = len(path) - 1
+    return out_lat, out_rel, out_hops
+
+
+def test_oracle_paths_pinned_by_scipy_on_tie_free_graph():
+    """with continuous latencies shortest paths are unique, so scipy's
+    predecessor tree must equal the oracle's igraph parents -- and the oracle's hops and
+    reliability (the golden rows) must equal the ones rebuilt from scipy's tree.  This pins the
+    SSSP branch independently of the oracle's own restatement where no ties exist; tie handling
+    (integer latencies) stays parity-unpinned."""
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import dijkstra
+    z = np.load(os.path.join(GOLDEN, "synth_real.npz"))
+    V = int(z["V"])
+    g = oracle.OGraph(V, z["eu"], z["ev"], z["elat"], z["eloss"], z["vloss"])
+    m = z["eu"] != z["ev"]
+    A = sp.coo_matrix((z["elat"][m], (z["eu"][m], z["ev"][m])), shape=(V, V)).tocsr()
+    for s in z["sources"]:
+        d, pv, pe, rank = g.dijkstra(int(s))
+        ds, pred = dijkstra(A, directed=False, indices=int(s), return_predecessors=True)
+        reached = (d >= 0) & (np.arange(V) != s)
+        assert np.array_equal(pv[reached], pred[reached])
+    lat, rel, hops = _scipy_rows(V, z["eu"], z["ev"], z["elat"], z["eloss"], z["vloss"],
+                                 z["sources"], z["targets"])
+    other = z["targets"][None, :] != z["sources"][:, None]
+    assert np.array_equal(lat[other], z["lat"][other])
+    assert np.array_equal(rel[other].view(np.uint64), z["rel"][other].view(np.uint64))
+    assert np.array_equal(hops[other], z["hops"][other])

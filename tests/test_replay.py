@@ -49,13 +49,12 @@ def test_replay_early_exit_matches_oracle():
         assert np.array_equal(p[popped], opv[popped])
 
 
-@pytest.mark.parametrize("batch", [8, 1])
-def test_integer_ties_table_bit_exact(batch):
+@pytest.mark.parametrize("fill", [8, 1])
+def test_integer_ties_table_bit_exact(fill):
     """Integer latencies U{1..100}: every pair of the table -- hops and reliability included --
     bit-exact against the oracle; the tie rows went through the replay."""
     top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=True)
-    top.set_option("batch", batch)
-    top.set_option("batch_fill", batch)
+    top.set_option("batch_fill", fill)
     otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()
