@@ -452,6 +452,10 @@ def main():
             ms=round(cold_s * 1e3, 2), gteps=round(A * E / cold_s / 1e9, 3),
             graph_prep_ms=round(cs["csr_ms"], 2), graph_prep_host_ms=round(cs["csr_host_ms"], 2),
             graph_prep_copy_ms=round(cs["csr_copy_ms"], 2), h0_rounds=int(cs["csr_h0_rounds"]),
+            graph_prep_steps_ms=dict(zip(("upload", "relabel", "rows", "h0_distances", "h0_tree",
+                                          "kappa_copy", "copies_out"),
+                                         [round(x, 2) for x in cs["csr_step_ms"][:7]])),
+            workspace_ms=round(cs["workspace_ms"], 2),
             target_prep_ms=round(cs["target_prep_ms"], 2),
             target_kappa_iters=int(cs["target_kappa_iters"]),
             order_ms=round(cs["order_ms"], 2), kernel_ms=round(cs["sssp_kernel_ms"], 2),

@@ -270,6 +270,11 @@ typedef struct {
                                    lines a batch lowered from +inf are reset for the next one) */
     int64_t csr_host_runs;      /* host-side graph preparations in the last build (a multi-GPU
                                    build prepares once and shares it with its peer engines) */
+    double workspace_ms;        /* wall time of allocating + initialising the SSSP workspace
+                                   (first build, or a layout change) */
+    double csr_step_ms[8];      /* graph preparation steps (wall): upload of the parsed edges,
+                                   degrees + relabel, adjacency rows, h0 distances, h0 tree +
+                                   record fields, kappa-sorted copy, host copies out, (unused) */
     int64_t exchange_kind;      /* the last build's row exchange: 0 none (one device), 1 RCCL
                                    all-gather + all-reduce(MIN), 2 device-to-device peer copies
                                    (engines sharing a device, or RCCL unavailable) */

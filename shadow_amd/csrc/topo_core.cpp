@@ -26,6 +26,7 @@
 #include <numeric>
 #include <queue>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/shd_topology_abi.h"
@@ -39,6 +40,39 @@ __attribute__((weak)) void worker_updateMinTimeJump(double minPathLatency);
 }
 
 using namespace shdtopo;
+
+namespace shdtopo {
+// Page-locked allocations of the parsed graph's edge arrays (topo_internal.h PinnedAlloc): the
+// registry tells hipHostFree from free when a buffer is released.
+namespace {
+std::mutex g_pinMu;
+std::unordered_set<void*> g_pinned;
+}  // namespace
+void* pinned_alloc(size_t bytes) {
+    if (bytes == 0) bytes = 1;
+    void* p = nullptr;
+    if (!getenv("SHDTOPO_NO_PINNED") && hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess && p) {
+        std::lock_guard<std::mutex> lk(g_pinMu);
+        g_pinned.insert(p);
+        return p;
+    }
+    (void)hipGetLastError();  // no device (CPU-only use): ordinary memory
+    return malloc(bytes);
+}
+void pinned_free(void* p) {
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_pinMu);
+        auto it = g_pinned.find(p);
+        if (it != g_pinned.end()) {
+            g_pinned.erase(it);
+            (void)hipHostFree(p);
+            return;
+        }
+    }
+    free(p);
+}
+}  // namespace shdtopo
 
 namespace {
 
@@ -142,6 +176,7 @@ struct _Topology {
     int64_t csrHostRuns = 0;    // host-side preparations (peers that copied count none)
     DevBuf<uint32_t> d_spt;     // per vertex {parent, slot of (v -> parent) in v's row, f64 latency}
     DevBuf<uint32_t> d_sptPar;  // per vertex: h0-tree parent
+    DevBuf<double> d_sptLoss;   // per vertex: loss of the h0-tree edge (the parent pass' record)
     int wsK = 0;                // batch width the workspace was laid out for
     int64_t wsRing = 0;
     DevBuf<uint32_t> d_rowptr, d_adj;
@@ -150,10 +185,11 @@ struct _Topology {
     double meanLat = -1.0;
     uint64_t ipGen = 1, geomGen = 0;  // attach/detach generation; compute_geometry's copy  // mean non-loop edge latency (default delta), computed once
     DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
-    DevBuf<unsigned long long> d_dist, d_best, d_memo, d_qa, d_qb;
+    DevBuf<unsigned long long> d_dist, d_best, d_qa, d_qb;
     DevBuf<uint32_t> d_ring;
-    DevBuf<uint32_t> d_stamp, d_cnt, d_bslot, d_par, d_pathbuf,
-        d_counters;
+    DevBuf<uint4> d_prec;  // per (vertex, source) pair records of the parent pass
+    DevBuf<double> d_pathbuf;
+    DevBuf<uint32_t> d_cnt, d_bslot, d_counters;
     int slots = 0;
     DevBuf<double2> d_lr;
     DevBuf<uint16_t> d_hops;
@@ -210,7 +246,12 @@ struct _Topology {
                               // iterate is exact)
     DevBuf<double> d_pot, d_kfA, d_kfB;
     DevBuf<unsigned int> d_kfChanged;
-    DevBuf<uint32_t> d_rowmap;
+    DevBuf<uint32_t> d_rowmap, d_bsrc;  // batch order: output row and source of each position
+    // cache of the last batch order (enqueue_rows): the rows' sources, batch fill and options
+    std::vector<uint32_t> ordSrc, ordPsrc;
+    const HostPrep* ordHp = nullptr;
+    int ordKf = -1, ordSO = -1, ordBO = -1;
+    double ordDelta = -1.0;
     bool replayUploaded = false;
     DevBuf<uint32_t> d_rrow;
     DevBuf<uint4> d_rrec;
@@ -465,6 +506,13 @@ int upload_csr_impl(Topology* top) {
         return 0;
     }
     const int64_t E = g.E;
+    auto tstep = clk::now();
+    for (double& x : top->stats.csr_step_ms) x = 0.0;
+    auto step_done = [&](int i) {
+        const auto t = clk::now();
+        top->stats.csr_step_ms[i] = std::chrono::duration<double, std::milli>(t - tstep).count();
+        tstep = t;
+    };
     if (2 * E >= (int64_t)INT32_MAX || (int64_t)V >= (int64_t)1 << 30) {
         CRITICAL("topology too large for the device CSR (%d vertices, %lld edges)", V, (long long)E);
         return -7;
@@ -488,6 +536,7 @@ int upload_csr_impl(Topology* top) {
         HIPCHK(hipStreamSynchronize(st));
         copy_ms += ms_since(tc);
     }
+    step_done(0);
     // 2) degrees, relabel, rows
     DevBuf<uint32_t> deg, selfE, dperm, dinv;
     HIPCHK(deg.ensure((size_t)V));
@@ -507,20 +556,25 @@ int upload_csr_impl(Topology* top) {
     deg.release();
     selfE.release();
     vl0.release();
+    step_done(1);
     HIPCHK(top->d_adj.ensure(4 * (size_t)nadj));
     HIPCHK(top->d_aloss.ensure((size_t)nadj));
     HIPCHK(prep_adjacency(V, E, nadj, eu.p, ev.p, dinv.p, elat.p, eloss.p, top->d_adj.p,
                           top->d_aloss.p, st));
     eu.release(); ev.release(); elat.release(); eloss.release();
+    step_done(2);
     // 3) pi = d(h0, .), the h0 tree, the records' landmark fields
     HIPCHK(top->d_pot.ensure((size_t)V));
     int iters = 0;
     HIPCHK(prep_h0_distances(V, top->d_rowptr.p, top->d_adj.p, top->d_pot.p, &iters, st));
     top->stats.csr_h0_rounds = iters;
+    step_done(3);
     HIPCHK(top->d_sptPar.ensure((size_t)V));
     HIPCHK(top->d_spt.ensure(4 * (size_t)V));
-    HIPCHK(prep_tree(V, nadj, H, top->d_rowptr.p, top->d_adj.p, top->d_pot.p, top->d_sptPar.p,
-                     top->d_spt.p, &top->hp->piMax, st));
+    HIPCHK(top->d_sptLoss.ensure((size_t)V));
+    HIPCHK(prep_tree(V, nadj, H, top->d_rowptr.p, top->d_adj.p, top->d_aloss.p, top->d_pot.p,
+                     top->d_sptPar.p, top->d_spt.p, top->d_sptLoss.p, &top->hp->piMax, st));
+    step_done(4);
     // 4) the kappa-sorted relaxation copy
     HIPCHK(top->d_adjk.ensure(4 * (size_t)nadj));
     HIPCHK(top->d_kap.ensure((size_t)nadj));
@@ -533,6 +587,7 @@ int upload_csr_impl(Topology* top) {
     top->adjkFlagged = false;
     top->adjkTargets.clear();
     top->rowsSorted = true;
+    step_done(5);
     // 5) what the host keeps
     {
         const auto tc = clk::now();
@@ -547,6 +602,12 @@ int upload_csr_impl(Topology* top) {
         HIPCHK(hipStreamSynchronize(st));
         copy_ms += ms_since(tc);
     }
+    step_done(6);
+    MESSAGE("graph preparation: upload %.1f, relabel %.1f, rows %.1f, h0 distances %.1f (%d "
+            "rounds), tree %.1f, kappa copy %.1f, host copies %.1f ms",
+            top->stats.csr_step_ms[0], top->stats.csr_step_ms[1], top->stats.csr_step_ms[2],
+            top->stats.csr_step_ms[3], iters, top->stats.csr_step_ms[4],
+            top->stats.csr_step_ms[5], top->stats.csr_step_ms[6]);
     top->stats.csr_host_ms = host_ms;
     top->stats.csr_copy_ms = copy_ms;
     top->csrUploaded = true;
@@ -564,6 +625,7 @@ DevCSR dev_csr(Topology* top) {
     c.ksum = reinterpret_cast<const float4*>(top->d_ksum.p);
     c.kap0 = top->d_kap0.p;
     c.spt = top->d_spt.p;
+    c.sptLoss = top->d_sptLoss.p;
     c.piMax = top->hp->piMax;
     c.aloss = top->d_aloss.p;
     c.vloss = top->d_vloss.p;
@@ -605,12 +667,12 @@ int ensure_workspace(Topology* top, int nsrc) {
     const size_t maskb = 2 * (((size_t)V * (K <= 8 ? 1 : 2) + 255) / 256 * 256);
     const int64_t ringE = ring_entries(top, K);
     const size_t hparN = (size_t)std::min<int64_t>(top->parHubs, 1 << 20) * K;
-    // dist (K words/vertex), per-(vertex, source) best/memo 16 B + stamp/cnt/bslot/par 16 B, the
+    // dist (K words/vertex), per-(vertex, source) pair record 16 B + best/cnt/bslot 16 B, the
     // queues, the u32 scratch, masks, hub hints, path buffer
     const int64_t qs = queue_stride(top, K);
     const size_t per_slot = (size_t)V * (8 * (size_t)K + 32 * (size_t)K) + 16 * (size_t)qs +
                             (size_t)ringE * 4 + maskb + 4 * hparN +
-                            (size_t)kMaxHops * kSsspBlock * 4 + 16;
+                            (size_t)kMaxHops * kSsspBlock * 8 + 16;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     // memory already held by this workspace counts as available
@@ -619,11 +681,12 @@ int ensure_workspace(Topology* top, int nsrc) {
     want = std::min(want, memcap);
     want = std::max(1, std::min(want, std::max(1, units)));
     if (top->slots >= want && top->wsK == K && top->wsRing == ringE) return 0;
+    const auto tw0 = std::chrono::steady_clock::now();
     if (top->slots > 0) {
         // layout change: release before re-allocating
         top->d_dist.release(); top->d_ring.release(); top->d_best.release();
-        top->d_memo.release(); top->d_stamp.release(); top->d_cnt.release();
-        top->d_bslot.release(); top->d_par.release(); top->d_pathbuf.release();
+        top->d_prec.release(); top->d_cnt.release();
+        top->d_bslot.release(); top->d_pathbuf.release();
         top->d_qa.release(); top->d_qb.release(); top->d_mask.release(); top->d_hpar.release();
         top->slots = 0;
     }
@@ -631,14 +694,12 @@ int ensure_workspace(Topology* top, int nsrc) {
     const size_t pn = n * (size_t)K;  // per-(vertex, source) arrays
     HIPCHK(top->d_dist.ensure(pn));
     HIPCHK(top->d_best.ensure(pn));
-    HIPCHK(top->d_memo.ensure(pn));
-    HIPCHK(top->d_stamp.ensure(pn));
+    HIPCHK(top->d_prec.ensure(pn));
     HIPCHK(top->d_qa.ensure((size_t)want * (size_t)qs));
     HIPCHK(top->d_qb.ensure((size_t)want * (size_t)qs));
     HIPCHK(top->d_ring.ensure((size_t)want * (size_t)ringE));
     HIPCHK(top->d_cnt.ensure(pn));
     HIPCHK(top->d_bslot.ensure(pn));
-    HIPCHK(top->d_par.ensure(pn));
     HIPCHK(top->d_pathbuf.ensure((size_t)want * kMaxHops * kSsspBlock));
     HIPCHK(top->d_counters.ensure((size_t)want * 4));
     HIPCHK(top->d_mask.ensure((size_t)want * maskb));
@@ -648,14 +709,17 @@ int ensure_workspace(Topology* top, int nsrc) {
     // it touched (the kernel's init)
     HIPCHK(launch_fill_u64(top->d_dist.p, 0x7FF0000000000000ull, (int64_t)pn, top->stream));
     HIPCHK(hipMemsetAsync(top->d_ring.p, 0, sizeof(uint32_t) * (size_t)want * (size_t)ringE, top->stream));
-    HIPCHK(hipMemsetAsync(top->d_stamp.p, 0, sizeof(uint32_t) * pn, top->stream));
-    HIPCHK(hipMemsetAsync(top->d_memo.p, 0, sizeof(unsigned long long) * pn, top->stream));
+    // pair records: tag 0 matches no batch (batch tags start at 1); a parent hint of 0 is only
+    // a guess the parent pass verifies
+    HIPCHK(hipMemsetAsync(top->d_prec.p, 0, sizeof(uint4) * pn, top->stream));
     HIPCHK(hipMemsetAsync(top->d_counters.p, 0, sizeof(uint32_t) * (size_t)want * 4, top->stream));
     HIPCHK(hipStreamSynchronize(top->stream));
     top->slots = want;
     top->wsK = K;
     top->wsRing = ringE;
     top->stats.slots = want;
+    top->stats.workspace_ms = std::chrono::duration<double, std::milli>(
+        std::chrono::steady_clock::now() - tw0).count();
     return 0;
 }
 
@@ -663,10 +727,10 @@ SlotWs slot_ws(Topology* top) {
     SlotWs w;
     w.slots = top->slots;
     w.V = top->g.V;
-    w.dist = top->d_dist.p; w.stamp = top->d_stamp.p;
+    w.dist = top->d_dist.p; w.prec = top->d_prec.p;
     w.qa = top->d_qa.p; w.qb = top->d_qb.p; w.ring = top->d_ring.p;
     w.best = top->d_best.p; w.cnt = top->d_cnt.p; w.bslot = top->d_bslot.p;
-    w.memo = top->d_memo.p; w.par = top->d_par.p; w.pathbuf = top->d_pathbuf.p;
+    w.pathbuf = top->d_pathbuf.p;
     w.counters = top->d_counters.p;
     w.K = top->wsK;
     w.ring_entries = top->wsRing;
@@ -902,6 +966,7 @@ double default_delta(Topology* top) {
 void reset_build_stats(Topology* top) {
     top->stats.csr_ms = top->stats.csr_host_ms = top->stats.csr_copy_ms = 0.0;
     top->stats.order_ms = top->stats.replay_prep_ms = top->stats.target_prep_ms = 0.0;
+    top->stats.workspace_ms = 0.0;
     top->stats.csr_host_runs = 0;
 }
 
@@ -1029,6 +1094,25 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             }
             {
                 const auto to0 = std::chrono::steady_clock::now();
+                // sources per batch: a shard that leaves slots idle at K (8-GPU builds: 1250
+                // rows = 157 batches for 256 slots) spreads over every slot with fewer sources
+                // per batch (C4, 1250 rows: 89.7 -> 83.2 ms).  With more than one round it does
+                // not pay (2500 rows at 5 per batch: 146 -> 158 ms).
+                int kf = K;
+                if (top->batchFill > 0) {
+                    kf = std::min(K, top->batchFill);
+                } else {
+                    const int64_t S = std::max(1, ws.slots);
+                    if (rows <= (int64_t)K * S) kf = (int)std::min<int64_t>(K, (rows + S - 1) / S);
+                }
+                top->stats.batch_fill = kf;
+                const double delta = default_delta(top);
+                // the order, the row map and the bucket shifts depend only on the sources, the
+                // batch fill and the options: a rebuild of the same rows reuses them
+                const bool cached = top->ordHp == top->hp.get() && top->ordKf == kf &&
+                                    top->ordSO == top->sourceOrder && top->ordBO == top->batchOrder &&
+                                    top->ordDelta == delta && top->ordSrc == src;
+                if (!cached) {
                 // Batches of K sources settle in lock-step and share an expansion when their
                 // shifted distances to a vertex fall in one bucket: sources whose shortest paths
                 // enter the hub core through the same hub share the most.  Batch position p takes
@@ -1077,18 +1161,6 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     std::stable_sort(perm.begin(), perm.end(),
                                      [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
                 }
-                // sources per batch: a shard that leaves slots idle at K (8-GPU builds: 1250
-                // rows = 157 batches for 256 slots) spreads over every slot with fewer sources
-                // per batch (C4, 1250 rows: 89.7 -> 83.2 ms).  With more than one round it does
-                // not pay (2500 rows at 5 per batch: 146 -> 158 ms).
-                int kf = K;
-                if (top->batchFill > 0) {
-                    kf = std::min(K, top->batchFill);
-                } else {
-                    const int64_t S = std::max(1, ws.slots);
-                    if (rows <= (int64_t)K * S) kf = (int)std::min<int64_t>(K, (rows + S - 1) / S);
-                }
-                top->stats.batch_fill = kf;
                 // order of the batches (groups of kf consecutive positions) in the dequeue: the
                 // kernel ends with the slowest slot, so the last batches decide its tail
                 if (top->batchOrder != 0 && rows > kf) {
@@ -1130,11 +1202,10 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 std::vector<uint32_t> psrc((size_t)rows);
                 for (int64_t i = 0; i < rows; i++) psrc[(size_t)i] = src[(size_t)perm[(size_t)i]];
                 HIPCHK(top->d_rowmap.ensure((size_t)rows));
+                HIPCHK(top->d_bsrc.ensure((size_t)rows));
                 HIPCHK(hipMemcpyAsync(top->d_rowmap.p, perm.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
-                HIPCHK(hipMemcpyAsync(top->d_sources.p, psrc.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
-                ws.rowmap = top->d_rowmap.p;
+                HIPCHK(hipMemcpyAsync(top->d_bsrc.p, psrc.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
                 // bucket shift per row: sh = C - pi(src) >= 2 delta (topo_sssp_batch.hip)
-                const double delta = default_delta(top);
                 const double pmax = top->hp->piMax;  // largest finite pi (upload_csr)
                 std::vector<double> sh((size_t)rows);
                 for (int64_t i = 0; i < rows; i++) {
@@ -1144,6 +1215,17 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 HIPCHK(top->d_srcsh.ensure((size_t)rows));
                 HIPCHK(hipMemcpyAsync(top->d_srcsh.p, sh.data(), sizeof(double) * (size_t)rows,
                                       hipMemcpyHostToDevice, st));
+                HIPCHK(hipStreamSynchronize(st));  // perm / psrc / sh must outlive the copies
+                top->ordPsrc.swap(psrc);
+                top->ordSrc = src;
+                top->ordHp = top->hp.get();
+                top->ordKf = kf;
+                top->ordSO = top->sourceOrder;
+                top->ordBO = top->batchOrder;
+                top->ordDelta = delta;
+                }
+                ws.rowmap = top->d_rowmap.p;
+                const std::vector<uint32_t>& psrc = top->ordPsrc;
                 top->stats.order_ms = std::chrono::duration<double, std::milli>(
                     std::chrono::steady_clock::now() - to0).count();
                 HIPCHK(hipEventRecord(top->ev0, st));
@@ -1157,7 +1239,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 const char* btf = getenv("SHD_BATCH_TRACE");
                 const int64_t nbt = (rows + kf - 1) / kf;
                 if (btf && *btf) HIPCHK(hipMalloc((void**)&ws.btrace, 64 * (size_t)nbt));
-                HIPCHK(launch_sssp_batch(K, dev_csr(top), ws, top->d_sources.p,
+                HIPCHK(launch_sssp_batch(K, dev_csr(top), ws, top->d_bsrc.p,
                                          top->d_srcsh.p, (int)rows, kf, top->d_targets.p, (int)A,
                                          delta, bp, top->iterGuard, out_lr, out_hops,
                                          out_rowmin, top->d_stats.p, st));
@@ -1205,8 +1287,6 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             if (r) return r;
             r = upload_target_bits(top, tgt, st);
             if (r) return r;
-            // the batch kernel took its sources in locality order: the replay indexes by row
-            HIPCHK(hipMemcpy(top->d_sources.p, src.data(), sizeof(uint32_t) * (size_t)rows, hipMemcpyHostToDevice));
             HIPCHK(top->d_rrows.ensure(rlist.size()));
             HIPCHK(hipMemcpy(top->d_rrows.p, rlist.data(), 4 * rlist.size(), hipMemcpyHostToDevice));
             HIPCHK(hipEventRecord(top->evr0, st));
@@ -1440,6 +1520,7 @@ int copy_csr_from(Topology* p, int pdev, Topology* o, int odev) {
     HIPCHK(peer_copy(p->d_kap0, pdev, o->d_kap0, odev, st));
     HIPCHK(peer_copy(p->d_spt, pdev, o->d_spt, odev, st));
     HIPCHK(peer_copy(p->d_sptPar, pdev, o->d_sptPar, odev, st));
+    HIPCHK(peer_copy(p->d_sptLoss, pdev, o->d_sptLoss, odev, st));
     HIPCHK(peer_copy(p->d_pot, pdev, o->d_pot, odev, st));
     HIPCHK(peer_copy(p->d_aloss, pdev, o->d_aloss, odev, st));
     HIPCHK(peer_copy(p->d_vloss, pdev, o->d_vloss, odev, st));

@@ -92,7 +92,8 @@ struct DevCSR {
     const float4* ksum = nullptr;   // per vertex: kappa at row positions 0, 1, 3, 7[, 15, 31, 63,
                                     // 127] (kKProbes floats, +inf past the row)
     const float* kap0 = nullptr;    // per vertex: smallest kappa of its row (+inf: empty row)
-    const uint32_t* spt = nullptr;  // per vertex {h0-tree parent, its slot of (parent, v), f64 w}
+    const uint32_t* spt = nullptr;  // per vertex {h0-tree parent, its slot in v's row, f64 w}
+    const double* sptLoss = nullptr; // per vertex: packet loss of that h0-tree edge
     double piMax = 0.0;             // largest finite pi
     const double* aloss = nullptr;
     const double* vloss = nullptr;
@@ -110,7 +111,8 @@ struct SlotWs {
     int slots = 0;
     int64_t V = 0;
     unsigned long long* dist = nullptr;  // [V][K] f64 bits, +inf = unreached (rows < H unused)
-    uint32_t* stamp = nullptr;           // parent pass: walk claim tag per (vertex, source)
+    uint4* prec = nullptr;               // [V][K] pair records {parent | amb << 31 | bad << 30,
+                                         // batch tag, f64 loss of the parent edge}
     unsigned long long* qa = nullptr;    // near queues / parent pair lists (q_stride u64 per slot)
     unsigned long long* qb = nullptr;
     uint32_t* ring = nullptr;            // ring_entries u32 per slot: parent pair list, vertex
@@ -118,10 +120,8 @@ struct SlotWs {
     unsigned long long* best = nullptr;  // parent pass: min d[u] over candidates
     uint32_t* cnt = nullptr;             // parent pass: candidates at the min
     uint32_t* bslot = nullptr;           // parent pass: lowest adjacency slot at the min
-    unsigned long long* memo = nullptr;  // (batch epoch << 32) | ambiguous << 31 | slot
-    uint32_t* par = nullptr;             // parent vertex (the SSSP's improver hint before)
-    uint32_t* pathbuf = nullptr;         // [slot][kMaxHops][kSsspBlock]
-    uint32_t* counters = nullptr;        // [slot][4]: iteration id, (unused), batch epoch
+    double* pathbuf = nullptr;           // [slot][kMaxHops][kSsspBlock] edge losses of a path
+    uint32_t* counters = nullptr;        // [slot][4]: batch tag, (unused)
     int K = 8;
     int64_t q_stride = 0;
     int64_t ring_entries = 0;
@@ -254,8 +254,8 @@ hipError_t prep_h0_distances(int64_t V, const uint32_t* rowptr, const uint32_t* 
 // h0 tree (sptPar u32[V], spt {parent, slot in v's row, f64 w}[V]), the records' pi / kappa0
 // field, *piMax = the largest finite pi; rows < nwave take a wavefront each
 hipError_t prep_tree(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* rowptr,
-                     uint32_t* adj, const double* pot, uint32_t* sptPar, uint32_t* spt,
-                     double* piMax, hipStream_t st);
+                     uint32_t* adj, const double* aloss, const double* pot, uint32_t* sptPar,
+                     uint32_t* spt, double* sptLoss, double* piMax, hipStream_t st);
 // the plain kappa-sorted relaxation copy (adjk, kap, ksum, kap0) of adj: also restores it after
 // a target-aware re-sort when the target-aware order no longer applies
 hipError_t launch_kappa_copy(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* rowptr,

@@ -518,6 +518,7 @@ bool graphml_parse(const char* buf, size_t len, HostGraph& g, std::string& err) 
     const char* p = P.run(buf, end, true, &edge_at);
     if (P.failed) return false;
     bool done = edge_at == nullptr;
+    bool chunked = false;
     // 2) the edge section in parallel chunks split at <edge> tags (node ids are read-only now;
     //    anything unusual in a chunk makes the whole section fall back to the sequential pass)
     if (!done) {
@@ -555,17 +556,26 @@ bool graphml_parse(const char* buf, size_t len, HostGraph& g, std::string& err) 
             bool ok = true;
             for (size_t c = 0; c < nc; c++) ok = ok && !bad[c];
             if (ok) {
-                size_t ne = 0;
+                size_t ne = eo.eu.size();
                 for (auto& o : outs) ne += o.eu.size();
-                eo.eu.reserve(ne); eo.ev.reserve(ne); eo.lat.reserve(ne); eo.jit.reserve(ne); eo.loss.reserve(ne);
+                // straight into the graph's (page-locked) arrays, after any edges parsed
+                // sequentially before the chunked part
+                g.eu.reserve(ne); g.ev.reserve(ne); g.elat.reserve(ne); g.ejitter.reserve(ne); g.eloss.reserve(ne);
+                g.eu.assign(eo.eu.begin(), eo.eu.end());
+                g.ev.assign(eo.ev.begin(), eo.ev.end());
+                g.elat.assign(eo.lat.begin(), eo.lat.end());
+                g.ejitter.assign(eo.jit.begin(), eo.jit.end());
+                g.eloss.assign(eo.loss.begin(), eo.loss.end());
                 for (auto& o : outs) {
-                    eo.eu.insert(eo.eu.end(), o.eu.begin(), o.eu.end());
-                    eo.ev.insert(eo.ev.end(), o.ev.begin(), o.ev.end());
-                    eo.lat.insert(eo.lat.end(), o.lat.begin(), o.lat.end());
-                    eo.jit.insert(eo.jit.end(), o.jit.begin(), o.jit.end());
-                    eo.loss.insert(eo.loss.end(), o.loss.begin(), o.loss.end());
+                    g.eu.insert(g.eu.end(), o.eu.begin(), o.eu.end());
+                    g.ev.insert(g.ev.end(), o.ev.begin(), o.ev.end());
+                    g.elat.insert(g.elat.end(), o.lat.begin(), o.lat.end());
+                    g.ejitter.insert(g.ejitter.end(), o.jit.begin(), o.jit.end());
+                    g.eloss.insert(g.eloss.end(), o.loss.begin(), o.loss.end());
                 }
+                eo = EdgeOut();
                 done = true;
+                chunked = true;
             }
         }
         if (!done) {
@@ -574,11 +584,13 @@ bool graphml_parse(const char* buf, size_t len, HostGraph& g, std::string& err) 
         }
     }
     if (!P.graph_seen) { err = "no <graph> element"; return false; }
-    g.eu = std::move(eo.eu);
-    g.ev = std::move(eo.ev);
-    g.elat = std::move(eo.lat);
-    g.ejitter = std::move(eo.jit);
-    g.eloss = std::move(eo.loss);
+    if (!chunked) {
+        g.eu.assign(eo.eu.begin(), eo.eu.end());
+        g.ev.assign(eo.ev.begin(), eo.ev.end());
+        g.elat.assign(eo.lat.begin(), eo.lat.end());
+        g.ejitter = std::move(eo.jit);
+        g.eloss.assign(eo.loss.begin(), eo.loss.end());
+    }
     g.E = (int64_t)g.eu.size();
     g.vid.resize((size_t)g.V);
     for (int32_t v = 0; v < g.V; v++) g.vid[(size_t)v] = ids.keys[(size_t)v].str();

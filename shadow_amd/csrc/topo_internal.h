@@ -4,6 +4,7 @@
 #include <atomic>
 #include <cstdint>
 #include <mutex>
+#include <new>
 #include <shared_mutex>
 #include <string>
 #include <unordered_map>
@@ -13,6 +14,31 @@
 
 namespace shdtopo {
 
+// Page-locked host memory for the arrays the graph preparation uploads (topo_core.cpp
+// upload_csr): the copy is then a DMA at PCIe speed instead of the runtime's staged pageable
+// copy.  Ordinary memory when no GPU is present (the CPU-only parser and tests).
+void* pinned_alloc(size_t bytes);
+void pinned_free(void* p);
+template <class T>
+struct PinnedAlloc {
+    using value_type = T;
+    PinnedAlloc() = default;
+    template <class U>
+    PinnedAlloc(const PinnedAlloc<U>&) {}
+    T* allocate(size_t n) {
+        void* p = pinned_alloc(n * sizeof(T));
+        if (!p) throw std::bad_alloc();
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t) { pinned_free(p); }
+    template <class U>
+    bool operator==(const PinnedAlloc<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const PinnedAlloc<U>&) const { return false; }
+};
+template <class T>
+using PinnedVec = std::vector<T, PinnedAlloc<T>>;
+
 // The parsed topology: what igraph_read_graph_graphml + the C attribute table hold for the
 // reference (shd-topology.c:95-123).  Vertex index = order of first appearance of the node id,
 // edge id = order of <edge> elements (igraph 0.7.1 GraphML reader).
@@ -20,8 +46,9 @@ struct HostGraph {
     int32_t V = 0;
     int64_t E = 0;
     bool directed = false;
-    std::vector<int32_t> eu, ev;           // endpoints in document order
-    std::vector<double> elat, ejitter, eloss;
+    PinnedVec<int32_t> eu, ev;             // endpoints in document order
+    PinnedVec<double> elat, eloss;
+    std::vector<double> ejitter;
     std::vector<std::string> vid, vtype, vip, vgeo;
     std::vector<double> vbwup, vbwdown, vloss;
 };

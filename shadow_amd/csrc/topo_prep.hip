@@ -336,10 +336,11 @@ __device__ __forceinline__ void tree_scan(const uint32_t* rowptr, const uint32_t
 }
 
 __device__ __forceinline__ void tree_store(uint32_t v, const TreeBest& best, const uint32_t* adj,
-                                           uint32_t* sptPar, uint32_t* spt, double kmin,
-                                           double* kap0d) {
+                                           const double* aloss, uint32_t* sptPar, uint32_t* spt,
+                                           double* sptLoss, double kmin, double* kap0d) {
     const bool ok = best.u != 0xFFFFFFFFu;
     sptPar[v] = ok ? best.u : 0xFFFFFFFFu;
+    sptLoss[v] = ok ? aloss[best.k] : 0.0;
     uint4 r = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     if (ok) r = make_uint4(best.u, best.k, adj[kAdjWords * best.k + 2], adj[kAdjWords * best.k + 3]);
     reinterpret_cast<uint4*>(spt)[v] = r;
@@ -348,8 +349,9 @@ __device__ __forceinline__ void tree_store(uint32_t v, const TreeBest& best, con
 
 __global__ void __launch_bounds__(kPB)
 prep_tree_kernel(int64_t V, uint32_t nwave, const uint32_t* __restrict__ rowptr,
-                 const uint32_t* __restrict__ adj, const double* __restrict__ pot,
-                 uint32_t* __restrict__ sptPar, uint32_t* __restrict__ spt,
+                 const uint32_t* __restrict__ adj, const double* __restrict__ aloss,
+                 const double* __restrict__ pot, uint32_t* __restrict__ sptPar,
+                 uint32_t* __restrict__ spt, double* __restrict__ sptLoss,
                  double* __restrict__ kap0d, unsigned long long* __restrict__ pimax) {
     const uint32_t lane = threadIdx.x & 63u;
     const int64_t nw = gstride() >> 6;
@@ -370,7 +372,7 @@ prep_tree_kernel(int64_t V, uint32_t nwave, const uint32_t* __restrict__ rowptr,
             const double km = __shfl_xor(kmin, o, 64);
             kmin = km < kmin ? km : kmin;
         }
-        if (lane == 0) tree_store((uint32_t)v, best, adj, sptPar, spt, kmin, kap0d);
+        if (lane == 0) tree_store((uint32_t)v, best, adj, aloss, sptPar, spt, sptLoss, kmin, kap0d);
     }
     // tail rows: a thread each
     unsigned long long pm = 0;
@@ -381,7 +383,7 @@ prep_tree_kernel(int64_t V, uint32_t nwave, const uint32_t* __restrict__ rowptr,
         TreeBest best = none;
         double kmin = INFINITY;
         tree_scan(rowptr, adj, pot, (uint32_t)v, dv, 0u, 1u, best, kmin);
-        tree_store((uint32_t)v, best, adj, sptPar, spt, kmin, kap0d);
+        tree_store((uint32_t)v, best, adj, aloss, sptPar, spt, sptLoss, kmin, kap0d);
     }
     pm = wave_min_u64(~pm);
     if (lane == 0 && pm != ~0ull) atomicMax(pimax, ~pm);
@@ -608,8 +610,8 @@ hipError_t prep_h0_distances(int64_t V, const uint32_t* rowptr, const uint32_t* 
 }
 
 hipError_t prep_tree(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* rowptr,
-                     uint32_t* adj, const double* pot, uint32_t* sptPar, uint32_t* spt,
-                     double* piMax, hipStream_t st) {
+                     uint32_t* adj, const double* aloss, const double* pot, uint32_t* sptPar,
+                     uint32_t* spt, double* sptLoss, double* piMax, hipStream_t st) {
     Tmp<double> kap0d;
     Tmp<unsigned long long> pm;
     PCHK(kap0d.alloc(V));
@@ -617,8 +619,8 @@ hipError_t prep_tree(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* ro
     PCHK(hipMemsetAsync(pm.p, 0, 8, st));
     nwave = (uint32_t)std::min<int64_t>(nwave, V);
     const unsigned g = std::max(grid_for(V), (unsigned)std::min<int64_t>((nwave + 3) / 4, 256 * 64));
-    hipLaunchKernelGGL(prep_tree_kernel, dim3(g), dim3(kPB), 0, st, V, nwave, rowptr, adj, pot,
-                       sptPar, spt, kap0d.p, pm.p);
+    hipLaunchKernelGGL(prep_tree_kernel, dim3(g), dim3(kPB), 0, st, V, nwave, rowptr, adj, aloss,
+                       pot, sptPar, spt, sptLoss, kap0d.p, pm.p);
     PCHK(hipGetLastError());
     if (nadj > 0)
         hipLaunchKernelGGL(prep_recfield_kernel, dim3(grid_for(nadj)), dim3(kPB), 0, st, nadj, adj,

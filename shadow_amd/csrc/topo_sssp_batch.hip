@@ -172,8 +172,9 @@ struct BView {
     uint32_t* pend;            // HBM, 1 bit per vertex: a tail vertex with a pair pending past cb
     uint32_t* tie;             // HBM, 1 bit per (tail vertex, source): a relaxation tied its value
     uint32_t* touch;           // HBM, 1 bit per tail vertex: the batch lowered its line from +inf
-    uint32_t* tpar;            // HBM [V][K]: vertex whose relaxation last lowered the tail pair
-                               // (SHD_TAIL_HINT; the parent pass' par array, free during the SSSP)
+    uint32_t* tpar;            // HBM [V][K] pair records (word 0): vertex whose relaxation last
+                               // lowered the tail pair (SHD_TAIL_HINT; the parent field before
+                               // the parent pass)
     uint32_t H, P;
     __device__ __forceinline__ unsigned long long get(uint32_t v, uint32_t j) const {
         return v < H ? hd[(size_t)v * K + j] : ld_l2_u64(&dist[(size_t)v * K + j]);
@@ -643,7 +644,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     const unsigned long long old = atomicMin(&D.dist[wi], ab[rr]);
                     im = ab[rr] < old;
                     if (ab[rr] == old) atomicOr(&D.tie[wi >> 5], 1u << (wi & 31));
-                    if (SHD_TAIL_HINT && im && !tree[rr]) D.tpar[wi] = L.vx[lo[rr]];
+                    if (SHD_TAIL_HINT && im && !tree[rr]) D.tpar[4 * wi] = L.vx[lo[rr]];
                     cur[rr] = old;
                 }
                 bool nr = false, nf = false;
@@ -772,15 +773,17 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     M* mB = reinterpret_cast<M*>(ws.mask + (size_t)slot * 2 * mbytes + mbytes);
     uint32_t* qa = reinterpret_cast<uint32_t*>(ws.qa + (size_t)slot * ws.q_stride);
     uint32_t* qb = reinterpret_cast<uint32_t*>(ws.qb + (size_t)slot * ws.q_stride);
-    // parent-pass state per (vertex, source) pair
-    uint32_t* stamp = ws.stamp + (size_t)slot * V * K;
+    // parent-pass state per (vertex, source) pair q = v * K + j: the pair record {parent vertex
+    // (| amb << 31 | bad << 30), claim tag (the batch that resolved it), f64 loss of the parent
+    // edge} -- one 16-B line access per hop of a walk or of the epilogue -- and the row-scan
+    // scratch best / cnt / bslot
+    uint4* prec = ws.prec + (size_t)slot * V * K;
+    uint32_t* precw = reinterpret_cast<uint32_t*>(prec);
     unsigned long long* best = ws.best + (size_t)slot * V * K;
     uint32_t* cntc = ws.cnt + (size_t)slot * V * K;
     uint32_t* bslot = ws.bslot + (size_t)slot * V * K;
-    unsigned long long* memo = ws.memo + (size_t)slot * V * K;
-    uint32_t* par = ws.par + (size_t)slot * V * K;
-    D.tpar = par;
-    uint32_t* pbuf = ws.pathbuf + (size_t)slot * kMaxHops * kSsspBlock;
+    D.tpar = precw;
+    double* pbuf = ws.pathbuf + (size_t)slot * kMaxHops * kSsspBlock;
     uint32_t* ctr = ws.counters + (size_t)slot * 4;
     const uint32_t cap = (uint32_t)V;
     BBuckets B;
@@ -796,7 +799,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     D.touch = D.tie + tw + 64;  // touched-line bitmap (one bit per tail vertex)
     const uint32_t pcap = (uint32_t)(V * K);
 
-    uint32_t iter = ctr[0], mep = ctr[2];
+    uint32_t iter = ctr[0];
     unsigned long long n_near = 0, n_sweep = 0, n_expand = 0, n_par = 0;
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, t_split = 0;
     if (tid < 4) L.cnt[tid] = 0;
@@ -1125,10 +1128,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // pairs with several candidates get a recount at the minimum.  All K sources' chains run
         // in the same levels, so the pass has K times the parallelism of one source's.
         if ((int)tid < nk) L.src[tid] = sources[r0 + tid];
-        mep++;
-        const unsigned long long mtag = (unsigned long long)mep << 32;
         iter++;
-        const uint32_t ep = iter;  // claim tag of this batch's pairs (stamp)
+        const uint32_t ep = iter;  // claim tag of this batch's pair records
         if (tid == 0) L.qtail = 0;
         __syncthreads();
         uint32_t* pcur = qa;
@@ -1148,28 +1149,34 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         __syncthreads();
         uint32_t nF = min(L.qtail, pcap);
         __syncthreads();
+        // A pair's record: its parent, the batch's tag, the loss of the parent edge (one store)
+        auto put = [&](uint32_t q, uint32_t u, double loss) {
+            const unsigned long long lb = d2bits(loss);
+            prec[q] = make_uint4(u, ep, (uint32_t)lb, (uint32_t)(lb >> 32));
+        };
         // A guess certified without scanning a row: the first P hubs' recorded improver (LDS
-        // hint, no tie bit) or a tail's h0-tree parent (no tie bit, the edge is tight).  Sets
-        // memo / par; false: the pair needs a row scan.
-        auto try_hint = [&](uint32_t q) -> bool {
+        // hint, no tie bit) or a tail's h0-tree parent (no tie bit, the edge is tight).  Writes
+        // the pair record and returns the parent in *pu; false: the pair needs a row scan.
+        auto try_hint = [&](uint32_t q, uint32_t* pout) -> bool {
             const uint32_t v = q / K, j = q % K;
             if (v >= H) {
                 if ((D.tie[q >> 5] >> (q & 31)) & 1u) return false;
-                const uint32_t pu = g.spt[4 * (size_t)v];
+                const uint4 sp = reinterpret_cast<const uint4*>(g.spt)[v];
+                const double sl = g.sptLoss[v];
                 const unsigned long long dv = D.get(v, j);
+                const uint32_t pu = sp.x;
                 if (pu < (uint32_t)V) {
-                    const double wt = __hiloint2double((int)g.spt[4 * (size_t)v + 3],
-                                                       (int)g.spt[4 * (size_t)v + 2]);
+                    const double wt = __hiloint2double((int)sp.w, (int)sp.z);
                     if (__dadd_rn(bits2d(D.get(pu, j)), wt) == bits2d(dv)) {
-                        memo[q] = mtag | (unsigned long long)g.spt[4 * (size_t)v + 1];
-                        par[q] = pu;
+                        put(q, pu, sl);
+                        *pout = pu;
                         return true;
                     }
                 }
                 if (!SHD_TAIL_HINT || !g.rows_sorted) return false;
                 // second guess: the recorded improver u; the edge is found in v's own row (a
                 // tail: short) -- the same undirected edge, same latency and loss as u's slot
-                const uint32_t u = par[q];
+                const uint32_t u = precw[4 * (size_t)q] & 0x3FFFFFFFu;
                 if (u >= (uint32_t)V || u == v) return false;
                 const unsigned long long du = D.get(u, j);
                 uint32_t lo = g.rowptr[v], hi = g.rowptr[v + 1];
@@ -1183,8 +1190,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 double wt;
                 adj_load(g, lo, c, wt);
                 if (__dadd_rn(bits2d(du), wt) != bits2d(dv)) return false;
-                memo[q] = mtag | (unsigned long long)lo;
-                par[q] = u;
+                put(q, u, g.aloss[lo]);
+                *pout = u;
                 return true;
             }
             if (!g.rows_sorted || v >= P || ((D.tb[q >> 5] >> (q & 31)) & 1u)) return false;
@@ -1200,8 +1207,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             double wt;
             adj_load(g, lo, c, wt);
             if (__dadd_rn(bits2d(D.get(u, j)), wt) != bits2d(D.get(v, j))) return false;
-            memo[q] = mtag | (unsigned long long)lo;
-            par[q] = u;
+            put(q, u, g.aloss[lo]);
+            *pout = u;
             return true;
         };
         while (nF > 0) {
@@ -1214,10 +1221,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             __syncthreads();
             for (uint32_t i = tid; i < nF; i += kSsspBlock) {
                 uint32_t q = pcur[i];
-                if (atomicExch(&stamp[q], ep) == ep) continue;
+                if (atomicExch(&precw[4 * (size_t)q + 1], ep) == ep) continue;
                 for (;;) {
                     const uint32_t j = q % K;
-                    if (!try_hint(q)) {
+                    uint32_t u = 0;
+                    if (!try_hint(q, &u)) {
                         best[q] = kInfBits;
                         cntc[q] = 0;
                         bslot[q] = 0xFFFFFFFFu;
@@ -1226,10 +1234,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         else atomicOr(&L.fover, 128u);
                         break;
                     }
-                    const uint32_t u = par[q];
                     if (u == L.src[j]) break;
                     q = u * K + j;
-                    if (atomicExch(&stamp[q], ep) == ep) break;
+                    if (atomicExch(&precw[4 * (size_t)q + 1], ep) == ep) break;
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1341,11 +1348,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 const uint32_t c = ld_l2_u32(&cntc[q]);
                 if (jr == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
                     atomicAdd(&stats[ST_ERRORS], 1ull);
-                    memo[q] = mtag | 0x7FFFFFFFull;
-                    par[q] = L.src[q % K];
+                    prec[q] = make_uint4(L.src[q % K] | 0x40000000u, ep, 0u, 0u);
                 } else {
-                    memo[q] = mtag | (c > 1 ? 0x80000000ull : 0ull) | (unsigned long long)jr;
-                    par[q] = adj_col(g, jr);
+                    const unsigned long long lb = d2bits(g.aloss[jr]);
+                    prec[q] = make_uint4(adj_col(g, jr) | (c > 1 ? 0x80000000u : 0u), ep,
+                                         (uint32_t)lb, (uint32_t)(lb >> 32));
                 }
             }
             __syncthreads();
@@ -1361,7 +1368,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 if (i < nS) {
                     const uint32_t qc = fscr[i];
                     const uint32_t j = qc % K;
-                    const uint32_t u = par[qc];
+                    const uint32_t u = precw[4 * (size_t)qc] & 0x3FFFFFFFu;
                     q = u * K + j;
                     p = u != L.src[j];
                 }
@@ -1405,15 +1412,19 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 bool amb = false, bad = false;
                 uint32_t v = t;
                 while (v != src) {
-                    const unsigned long long m = memo[v * K + j];
-                    if ((m & 0xFFFFFFFF00000000ull) != mtag || (m & 0x7FFFFFFFull) == 0x7FFFFFFFull) {
+                    // the pair record, L1-bypassing (written by other waves of the workgroup)
+                    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 rv = __builtin_nontemporal_load(
+                        reinterpret_cast<const u32x4*>(prec) + (size_t)v * K + j);
+                    const uint4 r = make_uint4(rv.x, rv.y, rv.z, rv.w);
+                    if (r.y != ep || (r.x & 0x40000000u)) {
                         bad = true;
                         break;
                     }
-                    amb |= (m >> 31) & 1ull;
-                    if (h < kMaxHops) pbuf[(size_t)h * kSsspBlock + tid] = (uint32_t)(m & 0x7FFFFFFFull);
+                    amb |= (r.x >> 31) != 0u;
+                    if (h < kMaxHops) pbuf[(size_t)h * kSsspBlock + tid] = __hiloint2double((int)r.w, (int)r.z);
                     h++;
-                    v = par[v * K + j];
+                    v = r.x & 0x3FFFFFFFu;
                     if (h > (uint32_t)V) { bad = true; break; }
                 }
                 rel = 1.0;
@@ -1425,13 +1436,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     rel = -1.0;
                 } else if (h <= (uint32_t)kMaxHops) {
                     for (int x = (int)h - 1; x >= 0; --x)
-                        rel *= (1.0 - g.aloss[pbuf[(size_t)x * kSsspBlock + tid]]);
+                        rel *= (1.0 - pbuf[(size_t)x * kSsspBlock + tid]);
                 } else {
                     atomicAdd(&stats[ST_LONGPATH], 1ull);
                     for (int x = (int)h - 1; x >= 0; --x) {  // edge at depth x from t
                         uint32_t y = t;
-                        for (int z = 0; z < x; ++z) y = par[y * K + j];
-                        rel *= (1.0 - g.aloss[(uint32_t)(memo[y * K + j] & 0x7FFFFFFFull)]);
+                        for (int z = 0; z < x; ++z) y = prec[(size_t)y * K + j].x & 0x3FFFFFFFu;
+                        const uint4 r = prec[(size_t)y * K + j];
+                        rel *= (1.0 - __hiloint2double((int)r.w, (int)r.z));
                     }
                 }
                 if (amb) {
@@ -1472,7 +1484,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     }
     if (tid == 0) {
         ctr[0] = iter;
-        ctr[2] = mep;
         atomicAdd(&stats[ST_RELAX], L.cnt[0]);
         atomicAdd(&stats[ST_T_INIT], t_init);
         atomicAdd(&stats[ST_T_SSSP], t_sssp);
