@@ -444,6 +444,7 @@ def main():
                     parent_phase_ms_per_source=[round(x / max(1, rows), 3)
                                                 for x in st["parent_phase_ms"]],
                     touched_lines_per_build=int(st["touched_lines"]),
+                    walk_steps_per_source=round(st["walk_steps"] / max(1, rows)),
                     tie_dense=tie_dense)
         # cold build: the first table of the loaded topology, split into its parts
         cs = st_cold
@@ -461,6 +462,11 @@ def main():
             order_ms=round(cs["order_ms"], 2), kernel_ms=round(cs["sssp_kernel_ms"], 2),
             replay_prep_ms=round(cs["replay_prep_ms"], 2), replay_ms=round(cs["replay_ms"], 2),
             exchange_ms=round(cs["exchange_ms"], 2),
+            build_wall_ms=round(cs["build_wall_ms"], 2),
+            build_steps_ms=dict(zip(("device_init", "geometry_table_alloc", "prep_to_launch",
+                                     "sssp_kernel", "replay_rest", "stats"),
+                                    [round(x, 2) for x in cs["build_step_ms"][:6]])),
+            module_load_ms=round(cs["module_load_ms"], 2),
             host_ms=round(host_ms, 2), host_frac=round(host_ms / (cold_s * 1e3), 4),
             host_preparations=int(cs["csr_host_runs"]),
             note="host_ms = host work of the cold build (graph preparation copies + host compute, "

@@ -275,6 +275,15 @@ typedef struct {
     double csr_step_ms[8];      /* graph preparation steps (wall): upload of the parsed edges,
                                    degrees + relabel, adjacency rows, h0 distances, h0 tree +
                                    record fields, kappa-sorted copy, host copies out, (unused) */
+    double module_load_ms;      /* device init: loading the kernels' code objects (once per
+                                   engine, before its first build) */
+    double build_wall_ms;       /* wall time of the last whole-table build (topology_getLatency's
+                                   lazy build, shdtopo_build / shdtopo_rebuild) */
+    int64_t walk_steps;         /* parent-pass walk steps (pairs resolved) of the last build */
+    double build_step_ms[8];    /* wall checkpoints of the last whole-table build: device init,
+                                   geometry + table buffers, preparation up to the SSSP launch
+                                   (graph, workspace, target set, order), the SSSP kernel, the tie
+                                   replay + rest of the rows, statistics, (unused) x 2 */
     int64_t exchange_kind;      /* the last build's row exchange: 0 none (one device), 1 RCCL
                                    all-gather + all-reduce(MIN), 2 device-to-device peer copies
                                    (engines sharing a device, or RCCL unavailable) */

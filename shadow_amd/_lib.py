@@ -47,7 +47,9 @@ class ShdStats(ctypes.Structure):
                 ("csr_ms", dbl), ("csr_host_ms", dbl), ("csr_copy_ms", dbl), ("csr_h0_rounds", i64),
                 ("order_ms", dbl),
                 ("replay_prep_ms", dbl), ("touched_lines", i64), ("csr_host_runs", i64),
-                ("workspace_ms", dbl), ("csr_step_ms", dbl * 8), ("exchange_kind", i64)]
+                ("workspace_ms", dbl), ("csr_step_ms", dbl * 8), ("module_load_ms", dbl),
+                ("build_wall_ms", dbl), ("walk_steps", i64), ("build_step_ms", dbl * 8),
+                ("exchange_kind", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):

@@ -177,6 +177,11 @@ struct _Topology {
     DevBuf<uint32_t> d_spt;     // per vertex {parent, slot of (v -> parent) in v's row, f64 latency}
     DevBuf<uint32_t> d_sptPar;  // per vertex: h0-tree parent
     DevBuf<double> d_sptLoss;   // per vertex: loss of the h0-tree edge (the parent pass' record)
+    // the parsed edge arrays (document order) and old -> new ids, kept in HBM after the graph
+    // preparation: the heap replay's CSR is built from them (prep_replay_csr)
+    DevBuf<int32_t> d_eu, d_ev;
+    DevBuf<double> d_elat, d_eloss;
+    DevBuf<uint32_t> d_inv;
     int wsK = 0;                // batch width the workspace was laid out for
     int64_t wsRing = 0;
     DevBuf<uint32_t> d_rowptr, d_adj;
@@ -253,6 +258,7 @@ struct _Topology {
     int ordKf = -1, ordSO = -1, ordBO = -1;
     double ordDelta = -1.0;
     bool replayUploaded = false;
+    int64_t rnadj = 0;  // entries of the replay CSR
     DevBuf<uint32_t> d_rrow;
     DevBuf<uint4> d_rrec;
     DevBuf<uint32_t> d_rown;
@@ -307,6 +313,7 @@ struct _Topology {
     bool rowsPending = false;  // a launch whose stats have not been read back yet
     bool routePending = false;
     ShdStats stats{};
+    std::chrono::steady_clock::time_point bstepT;
 };
 
 namespace {
@@ -445,6 +452,14 @@ int dev_init(Topology* top) {
     HIPCHK(hipEventCreate(&top->evr0));
     HIPCHK(hipEventCreate(&top->evr1));
     HIPCHK(top->d_stats.ensure(ST_COUNT));
+    // the kernels' code objects, loaded here rather than by the first build's launches
+    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(preload_prep_module());
+    HIPCHK(preload_batch_module());
+    HIPCHK(preload_kernels_module());
+    HIPCHK(preload_replay_module());
+    top->stats.module_load_ms = std::chrono::duration<double, std::milli>(
+        std::chrono::steady_clock::now() - t0).count();
     top->devInit = true;
     return 0;
 }
@@ -493,6 +508,17 @@ int upload_csr_impl(Topology* top) {
         }
         host_ms += ms_since(th);
         const auto tc = clk::now();
+        const size_t E = (size_t)g.E;
+        HIPCHK(top->d_eu.ensure(E));
+        HIPCHK(top->d_ev.ensure(E));
+        HIPCHK(top->d_elat.ensure(E));
+        HIPCHK(top->d_eloss.ensure(E));
+        HIPCHK(top->d_inv.ensure((size_t)V));
+        HIPCHK(hipMemcpy(top->d_eu.p, g.eu.data(), 4 * E, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_ev.p, g.ev.data(), 4 * E, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_elat.p, g.elat.data(), 8 * E, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_eloss.p, g.eloss.data(), 8 * E, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(top->d_inv.p, top->hp->inv.data(), 4 * (size_t)V, hipMemcpyHostToDevice));
         HIPCHK(top->d_vloss.ensure((size_t)V));
         HIPCHK(top->d_selfLat.ensure((size_t)V));
         HIPCHK(top->d_selfLoss.ensure((size_t)V));
@@ -519,8 +545,12 @@ int upload_csr_impl(Topology* top) {
     }
     hipStream_t st = top->stream;
     // 1) the parsed graph to HBM (document order)
-    DevBuf<int32_t> eu, ev;
-    DevBuf<double> elat, eloss, vl0;
+    // (kept in HBM: the heap replay's incidence CSR is built from them on the GPU too)
+    DevBuf<int32_t>& eu = top->d_eu;
+    DevBuf<int32_t>& ev = top->d_ev;
+    DevBuf<double>& elat = top->d_elat;
+    DevBuf<double>& eloss = top->d_eloss;
+    DevBuf<double> vl0;
     HIPCHK(eu.ensure((size_t)E));
     HIPCHK(ev.ensure((size_t)E));
     HIPCHK(elat.ensure((size_t)E));
@@ -538,7 +568,8 @@ int upload_csr_impl(Topology* top) {
     }
     step_done(0);
     // 2) degrees, relabel, rows
-    DevBuf<uint32_t> deg, selfE, dperm, dinv;
+    DevBuf<uint32_t> deg, selfE, dperm;
+    DevBuf<uint32_t>& dinv = top->d_inv;
     HIPCHK(deg.ensure((size_t)V));
     HIPCHK(selfE.ensure((size_t)V));
     int64_t nadj = 0;
@@ -561,7 +592,6 @@ int upload_csr_impl(Topology* top) {
     HIPCHK(top->d_aloss.ensure((size_t)nadj));
     HIPCHK(prep_adjacency(V, E, nadj, eu.p, ev.p, dinv.p, elat.p, eloss.p, top->d_adj.p,
                           top->d_aloss.p, st));
-    eu.release(); ev.release(); elat.release(); eloss.release();
     step_done(2);
     // 3) pi = d(h0, .), the h0 tree, the records' landmark fields
     HIPCHK(top->d_pot.ensure((size_t)V));
@@ -746,7 +776,8 @@ SlotWs slot_ws(Topology* top) {
 // original neighbour id; directed (mode OUT) = out-neighbours ascending.  Self loops never relax
 // and are dropped; a parallel group becomes one entry with the group's minimum latency (same
 // heap history, topo_replay.hip) and the lowest edge id's latency/loss for the hop
-// (igraph_get_eid as orc_get_eid).  Needs perm/inv (upload_csr).
+// (igraph_get_eid as orc_get_eid).  Built on the GPU (prep_replay_csr) from the parsed edges
+// upload_csr keeps in HBM.
 int upload_replay_impl(Topology* top);
 int upload_replay(Topology* top) {
     if (top->replayUploaded) return 0;
@@ -758,83 +789,19 @@ int upload_replay(Topology* top) {
 
 int upload_replay_impl(Topology* top) {
     const HostGraph& g = top->g;
-    const int32_t V = g.V;
+    const int64_t V = g.V, E = g.E;
     const bool dir = top->isDirected;
-    // entries (x, y, e) in edge-id order, then stable counting sorts by y and by x
-    std::vector<int32_t> ex, ey, ee;
-    ex.reserve((size_t)g.E * (dir ? 1 : 2));
-    ey.reserve(ex.capacity());
-    ee.reserve(ex.capacity());
-    for (int64_t e = 0; e < g.E; e++) {
-        const int32_t a = g.eu[(size_t)e], b = g.ev[(size_t)e];
-        if (a == b) continue;
-        ex.push_back(a); ey.push_back(b); ee.push_back((int32_t)e);
-        if (!dir) { ex.push_back(b); ey.push_back(a); ee.push_back((int32_t)e); }
-    }
-    const size_t n = ex.size();
-    std::vector<uint32_t> o1(n), o2(n);
-    std::vector<int64_t> cnt((size_t)V + 1);
-    auto csort = [&](const std::vector<int32_t>& key, const std::vector<uint32_t>* in,
-                     std::vector<uint32_t>& out) {
-        std::fill(cnt.begin(), cnt.end(), 0);
-        for (size_t i = 0; i < n; i++) cnt[(size_t)key[in ? (*in)[i] : i] + 1]++;
-        for (int32_t k = 0; k < V; k++) cnt[(size_t)k + 1] += cnt[(size_t)k];
-        for (size_t i = 0; i < n; i++) {
-            const uint32_t id = in ? (*in)[i] : (uint32_t)i;
-            out[(size_t)cnt[(size_t)key[id]]++] = id;
-        }
-    };
-    csort(ey, nullptr, o1);  // by neighbour (edge ids ascending within)
-    csort(ex, &o1, o2);      // by row, stable: (x, y, e)
-    // merge parallel groups; count entries per relabelled row
-    std::vector<uint32_t> rowptr((size_t)V + 1, 0);
-    std::vector<size_t> gstart;
-    gstart.reserve(n);
-    for (size_t i = 0; i < n; i++) {
-        const uint32_t id = o2[i];
-        if (i == 0 || ex[id] != ex[o2[i - 1]] || ey[id] != ey[o2[i - 1]]) {
-            gstart.push_back(i);
-            rowptr[(size_t)top->hp->inv[(size_t)ex[id]] + 1]++;
-        }
-    }
-    for (int32_t k = 0; k < V; k++) rowptr[(size_t)k + 1] += rowptr[(size_t)k];
-    const size_t nr = gstart.size();
-    std::vector<uint4> rec(nr);
-    std::vector<uint32_t> own(nr);
-    std::vector<double2> hop(nr);
-    std::vector<uint32_t> fill(rowptr.begin(), rowptr.end() - 1);
-    for (size_t gi = 0; gi < nr; gi++) {
-        const size_t b = gstart[gi], e = gi + 1 < nr ? gstart[gi + 1] : n;
-        const uint32_t id0 = o2[b];  // lowest edge id of the group: igraph_get_eid's edge
-        double w = g.elat[(size_t)ee[id0]];
-        for (size_t i = b + 1; i < e; i++) w = std::min(w, g.elat[(size_t)ee[o2[i]]]);
-        const uint32_t x = (uint32_t)top->hp->inv[(size_t)ex[id0]];
-        const uint32_t k = fill[x]++;
-        uint64_t wb;
-        memcpy(&wb, &w, 8);
-        // pi(y) = d(h0, y) rounded up to f32: the replay's landmark skip (topo_replay.hip)
-        const uint32_t y = (uint32_t)top->hp->inv[(size_t)ey[id0]];
-        float pf = INFINITY;
-        if (!dir && y < top->hp->pot.size() && std::isfinite(top->hp->pot[y])) {
-            pf = (float)top->hp->pot[y];
-            if ((double)pf < top->hp->pot[y]) pf = std::nextafter(pf, INFINITY);
-        }
-        uint32_t pb;
-        memcpy(&pb, &pf, 4);
-        rec[k] = make_uint4(y, pb, (uint32_t)wb, (uint32_t)(wb >> 32));
-        own[k] = x;
-        hop[k] = make_double2(g.elat[(size_t)ee[id0]], g.eloss[(size_t)ee[id0]]);
-    }
+    const size_t cap = std::max<size_t>(1, (size_t)(dir ? E : 2 * E));
     HIPCHK(top->d_rrow.ensure((size_t)V + 1));
-    HIPCHK(top->d_rrec.ensure(std::max<size_t>(1, nr)));
-    HIPCHK(top->d_rown.ensure(std::max<size_t>(1, nr)));
-    HIPCHK(top->d_rhop.ensure(std::max<size_t>(1, nr)));
-    HIPCHK(hipMemcpy(top->d_rrow.p, rowptr.data(), sizeof(uint32_t) * ((size_t)V + 1), hipMemcpyHostToDevice));
-    if (nr) {
-        HIPCHK(hipMemcpy(top->d_rrec.p, rec.data(), sizeof(uint4) * nr, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_rown.p, own.data(), sizeof(uint32_t) * nr, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_rhop.p, hop.data(), sizeof(double2) * nr, hipMemcpyHostToDevice));
-    }
+    HIPCHK(top->d_rrec.ensure(cap));
+    HIPCHK(top->d_rown.ensure(cap));
+    HIPCHK(top->d_rhop.ensure(cap));
+    int64_t nr = 0;
+    HIPCHK(prep_replay_csr(V, E, dir ? 1 : 0, top->d_eu.p, top->d_ev.p, top->d_elat.p,
+                           top->d_eloss.p, top->d_inv.p, dir ? nullptr : top->d_pot.p,
+                           top->d_rrow.p, top->d_rrec.p, top->d_rown.p, top->d_rhop.p, &nr,
+                           top->stream));
+    top->rnadj = nr;
     top->replayUploaded = true;
     return 0;
 }
@@ -842,7 +809,7 @@ int upload_replay_impl(Topology* top) {
 ReplayCSR replay_csr(Topology* top) {
     ReplayCSR c;
     c.V = top->g.V;
-    c.nadj = (int64_t)top->d_rrec.n;
+    c.nadj = top->rnadj;
     c.rowptr = top->d_rrow.p;
     c.rec = top->d_rrec.p;
     c.own = top->d_rown.p;
@@ -959,6 +926,14 @@ double default_delta(Topology* top) {
     // tuned on C4: single-source 0.06 x mean (~3 ms); the batch kernel gains from
     // wider buckets (sources of a batch share more expansions) up to 0.2 x mean (~10 ms)
     return std::max(1e-9, (batch_k(top) > 1 ? 0.2 : 0.06) * mean);
+}
+
+// wall checkpoints of a whole-table build (ShdStats.build_step_ms): the time since the previous
+// mark goes to step i
+void bstep_mark(Topology* top, int i) {
+    const auto t = std::chrono::steady_clock::now();
+    top->stats.build_step_ms[i] += std::chrono::duration<double, std::milli>(t - top->bstepT).count();
+    top->bstepT = t;
 }
 
 // per-build cold-path timings start at 0: a build that finds the graph (or the target set)
@@ -1239,11 +1214,13 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 const char* btf = getenv("SHD_BATCH_TRACE");
                 const int64_t nbt = (rows + kf - 1) / kf;
                 if (btf && *btf) HIPCHK(hipMalloc((void**)&ws.btrace, 64 * (size_t)nbt));
+                bstep_mark(top, 2);
                 HIPCHK(launch_sssp_batch(K, dev_csr(top), ws, top->d_bsrc.p,
                                          top->d_srcsh.p, (int)rows, kf, top->d_targets.p, (int)A,
                                          delta, bp, top->iterGuard, out_lr, out_hops,
                                          out_rowmin, top->d_stats.p, st));
                 HIPCHK(hipEventRecord(top->ev1, st));
+                bstep_mark(top, 3);
                 HIPCHK(hipStreamSynchronize(st));  // sh must outlive the async copy
                 if (ws.btrace) {
                     std::vector<unsigned long long> bt((size_t)nbt * 8);
@@ -1349,6 +1326,7 @@ int collect_row_stats(Topology* top) {
     top->stats.far_scan_sources = (int64_t)h[ST_FARSCAN];
     top->stats.replay_rows = (int64_t)h[ST_RP_ROWS];
     top->stats.touched_lines = (int64_t)h[ST_TOUCHED];
+    top->stats.walk_steps = (int64_t)h[ST_WALK];
     top->stats.replay_pops = (int64_t)h[ST_RP_POPS];
     top->stats.replay_pushes = (int64_t)h[ST_RP_PUSH];
     top->stats.replay_modifies = (int64_t)h[ST_RP_MOD];
@@ -1526,6 +1504,11 @@ int copy_csr_from(Topology* p, int pdev, Topology* o, int odev) {
     HIPCHK(peer_copy(p->d_vloss, pdev, o->d_vloss, odev, st));
     HIPCHK(peer_copy(p->d_selfLat, pdev, o->d_selfLat, odev, st));
     HIPCHK(peer_copy(p->d_selfLoss, pdev, o->d_selfLoss, odev, st));
+    HIPCHK(peer_copy(p->d_eu, pdev, o->d_eu, odev, st));
+    HIPCHK(peer_copy(p->d_ev, pdev, o->d_ev, odev, st));
+    HIPCHK(peer_copy(p->d_elat, pdev, o->d_elat, odev, st));
+    HIPCHK(peer_copy(p->d_eloss, pdev, o->d_eloss, odev, st));
+    HIPCHK(peer_copy(p->d_inv, pdev, o->d_inv, odev, st));
     HIPCHK(hipStreamSynchronize(st));
     p->hp = o->hp;
     p->rowsSorted = o->rowsSorted;
@@ -1723,9 +1706,14 @@ int ensure_table(Topology* top) {
     if (table_current(top)) return 0;
     std::lock_guard<std::mutex> lk(top->buildMu);
     if (table_current(top)) return 0;
+    const auto tb0 = std::chrono::steady_clock::now();
+    for (double& x : top->stats.build_step_ms) x = 0.0;
+    top->bstepT = tb0;
+    auto bstep = [&](int i) { bstep_mark(top, i); };
     int r = dev_init(top);
     if (r) return r;
     const uint64_t sg = compute_geometry(top);
+    bstep(0);
     const int64_t A = top->A;
     reset_build_stats(top);
     int64_t runs0 = top->csrHostRuns;
@@ -1741,11 +1729,14 @@ int ensure_table(Topology* top) {
         }
     } else if (A > 0) {
         HIPCHK(top->d_lr.ensure((size_t)(A * A)));
+        bstep(1);
         HIPCHK(top->d_hops.ensure((size_t)(A * A)));
         HIPCHK(top->d_rowmin.ensure((size_t)A));
         r = enqueue_rows(top, 0, A, top->d_lr.p, top->d_hops.p, top->d_rowmin.p, top->stream);
+        bstep(4);
         if (r) return r;
         r = collect_row_stats(top);
+        bstep(5);
         if (r) return r;
         if (top->stats.errors) {
             CRITICAL("%lld attached pairs have no path/edge (e.g. a vertex without self loop)",
@@ -1757,6 +1748,8 @@ int ensure_table(Topology* top) {
     int64_t runs1 = top->csrHostRuns;
     for (Topology* p : top->peers) runs1 += p->csrHostRuns;
     top->stats.csr_host_runs = runs1 - runs0;
+    top->stats.build_wall_ms = std::chrono::duration<double, std::milli>(
+        std::chrono::steady_clock::now() - tb0).count();
     top->tableGen.store(sg, std::memory_order_release);
     top->tableSerial.fetch_add(1);
     top->tableValid.store(true, std::memory_order_release);
@@ -2295,6 +2288,8 @@ int shdtopo_build_rows(Topology* top, int64_t row0, int64_t row1, void* d_lr, vo
     compute_geometry(top);
     if (row0 < 0 || row1 > top->A || row0 > row1) return -2;
     reset_build_stats(top);
+    for (double& x : top->stats.build_step_ms) x = 0.0;
+    top->bstepT = std::chrono::steady_clock::now();
     const int64_t runs0 = top->csrHostRuns;
     hipStream_t st = stream ? (hipStream_t)stream : top->stream;
     r = enqueue_rows(top, row0, row1, (double2*)d_lr, (uint16_t*)d_hops, (double*)d_rowmin, st);

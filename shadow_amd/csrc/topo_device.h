@@ -79,7 +79,8 @@ enum StatIdx {
                         // chunk loads / phase A / phase B, the same for hub iterations, phase-B
                         // rounds, surviving edges (8 slots)
     ST_TOUCHED = 59,    // tail distance lines reset at batch starts (lines the batches touched)
-    ST_COUNT = 60
+    ST_WALK = 60,       // batch kernel parent pass: walk steps (pairs claimed and resolved)
+    ST_COUNT = 61
 };
 
 struct DevCSR {
@@ -262,5 +263,21 @@ hipError_t launch_kappa_copy(int64_t V, int64_t nadj, uint32_t nwave, const uint
                              const uint32_t* adj, const double* pot, const uint32_t* sptPar,
                              uint32_t* adjk, float* kap, float* ksum, float* kap0,
                              hipStream_t st);
+
+// the heap replay's incidence CSR (ReplayCSR) from the parsed edges in HBM: rows in relabelled
+// ids, each in igraph_incident order (ascending original neighbour; parallel groups merged, the
+// lowest edge id's latency / loss for the hop, the group's minimum latency for the heap).
+// rec / own / hop hold up to 2E (E directed) entries; *nrec = the entries written.
+hipError_t prep_replay_csr(int64_t V, int64_t E, int directed, const int32_t* eu,
+                           const int32_t* ev, const double* elat, const double* eloss,
+                           const uint32_t* inv, const double* pot, uint32_t* rowptr, uint4* rec,
+                           uint32_t* own, double2* hop, int64_t* nrec, hipStream_t st);
+
+// Load each kernel module's code object now (dev_init) instead of at its first launch inside
+// the first build: the runtime loads code objects lazily.
+hipError_t preload_batch_module();
+hipError_t preload_prep_module();
+hipError_t preload_kernels_module();
+hipError_t preload_replay_module();
 
 }  // namespace shdtopo

@@ -225,4 +225,9 @@ hipError_t launch_fill_u64(unsigned long long* p, unsigned long long v, int64_t 
     return hipGetLastError();
 }
 
+hipError_t preload_kernels_module() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void*)packet_route_kernel);
+}
+
 }  // namespace shdtopo

@@ -455,6 +455,74 @@ __global__ void kap_probe_kernel(int64_t V, const uint32_t* __restrict__ rowptr,
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// the heap replay's incidence CSR (ReplayCSR, topo_device.h): igraph_incident order
+// ---------------------------------------------------------------------------------------------
+// entries (x, y, e) of every non-loop edge (both directions when undirected), keyed by
+// (relabelled x, ORIGINAL y): a stable sort gives igraph's order in each row -- ascending original
+// neighbour, a parallel group by ascending edge id
+__global__ void rp_entry_kernel(int64_t E, int directed, const int32_t* __restrict__ eu,
+                                const int32_t* __restrict__ ev, const uint32_t* __restrict__ inv,
+                                unsigned long long* __restrict__ key, uint32_t* __restrict__ val,
+                                unsigned long long sentinel) {
+    for (int64_t e = gtid(); e < E; e += gstride()) {
+        const int32_t a = eu[e], b = ev[e];
+        unsigned long long k0 = sentinel, k1 = sentinel;
+        if (a != b) {
+            k0 = ((unsigned long long)inv[a] << 32) | (uint32_t)b;
+            if (!directed) k1 = ((unsigned long long)inv[b] << 32) | (uint32_t)a;
+        }
+        if (directed) {
+            key[e] = k0;
+            val[e] = (uint32_t)e;
+        } else {
+            key[2 * e] = k0;
+            key[2 * e + 1] = k1;
+            val[2 * e] = val[2 * e + 1] = (uint32_t)e;
+        }
+    }
+}
+
+// group starts (a parallel group merges into one entry) and the entries per row
+__global__ void rp_group_kernel(int64_t n, const unsigned long long* __restrict__ key,
+                                unsigned long long sentinel, uint32_t* __restrict__ start,
+                                uint32_t* __restrict__ rowcnt) {
+    for (int64_t i = gtid(); i < n; i += gstride()) {
+        const unsigned long long k = key[i];
+        const bool s = k != sentinel && (i == 0 || key[i - 1] != k);
+        start[i] = s ? 1u : 0u;
+        if (s) atomicAdd(&rowcnt[k >> 32], 1u);
+    }
+}
+
+__global__ void rp_fill_kernel(int64_t n, const unsigned long long* __restrict__ key,
+                               const uint32_t* __restrict__ eid, const uint32_t* __restrict__ start,
+                               const uint32_t* __restrict__ gpos, int directed,
+                               const uint32_t* __restrict__ inv, const double* __restrict__ pot,
+                               const double* __restrict__ elat, const double* __restrict__ eloss,
+                               uint4* __restrict__ rec, uint32_t* __restrict__ own,
+                               double2* __restrict__ hop) {
+    for (int64_t i = gtid(); i < n; i += gstride()) {
+        if (!start[i]) continue;
+        const unsigned long long k = key[i];
+        const uint32_t e0 = eid[i];  // the group's lowest edge id: igraph_get_eid's edge
+        double w = elat[e0];
+        for (int64_t j = i + 1; j < n && key[j] == k; j++) w = fmin(w, elat[eid[j]]);
+        const uint32_t g = gpos[i];
+        const uint32_t y = inv[(uint32_t)k];
+        // pi(y) = d(h0, y) rounded up to f32: the replay's landmark skip (topo_replay.hip)
+        float pf = INFINITY;
+        if (!directed && pot) {
+            const double p = pot[y];
+            if (isfinite(p)) pf = f32_up(p);
+        }
+        const unsigned long long wb = d2bits(w);
+        rec[g] = make_uint4(y, __float_as_uint(pf), (uint32_t)wb, (uint32_t)(wb >> 32));
+        own[g] = (uint32_t)(k >> 32);
+        hop[g] = make_double2(elat[e0], eloss[e0]);
+    }
+}
+
 __global__ void prep_fill_u64_kernel(unsigned long long* __restrict__ p, unsigned long long v,
                                      int64_t n) {
     for (int64_t i = gtid(); i < n; i += gstride()) p[i] = v;
@@ -666,6 +734,55 @@ hipError_t launch_kappa_copy(int64_t V, int64_t nadj, uint32_t nwave, const uint
                        kap0);
     PCHK(hipGetLastError());
     return hipStreamSynchronize(st);
+}
+
+hipError_t prep_replay_csr(int64_t V, int64_t E, int directed, const int32_t* eu,
+                           const int32_t* ev, const double* elat, const double* eloss,
+                           const uint32_t* inv, const double* pot, uint32_t* rowptr, uint4* rec,
+                           uint32_t* own, double2* hop, int64_t* nrec, hipStream_t st) {
+    const int64_t n = directed ? E : 2 * E;
+    Tmp<unsigned long long> k0, k1;
+    Tmp<uint32_t> v0, v1, start, gpos, cnt;
+    Tmp<unsigned char> tmp;
+    PCHK(k0.alloc(n));
+    PCHK(k1.alloc(n));
+    PCHK(v0.alloc(n));
+    PCHK(v1.alloc(n));
+    PCHK(start.alloc(n));
+    PCHK(gpos.alloc(n));
+    PCHK(cnt.alloc(V + 1));
+    const unsigned long long sentinel = (unsigned long long)V << 32;
+    hipLaunchKernelGGL(rp_entry_kernel, dim3(grid_for(E)), dim3(kPB), 0, st, E, directed, eu, ev,
+                       inv, k0.p, v0.p, sentinel);
+    PCHK(hipGetLastError());
+    const int endbit = 32 + bitlen((uint64_t)V);
+    size_t tb = 0, tb2 = 0, tb3 = 0;
+    PCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0.p, k1.p, v0.p, v1.p, (int)n, 0, endbit,
+                                            st));
+    PCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, start.p, gpos.p, (int)n, st));
+    PCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, cnt.p, rowptr, (int)(V + 1), st));
+    PCHK(tmp.alloc(std::max(tb, std::max(tb2, tb3))));
+    PCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k0.p, k1.p, v0.p, v1.p, (int)n, 0, endbit,
+                                            st));
+    PCHK(hipMemsetAsync(cnt.p, 0, sizeof(uint32_t) * (size_t)(V + 1), st));
+    hipLaunchKernelGGL(rp_group_kernel, dim3(grid_for(n)), dim3(kPB), 0, st, n, k1.p, sentinel,
+                       start.p, cnt.p);
+    PCHK(hipGetLastError());
+    PCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb2, start.p, gpos.p, (int)n, st));
+    PCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb3, cnt.p, rowptr, (int)(V + 1), st));
+    hipLaunchKernelGGL(rp_fill_kernel, dim3(grid_for(n)), dim3(kPB), 0, st, n, k1.p, v1.p, start.p,
+                       gpos.p, directed, inv, pot, elat, eloss, rec, own, hop);
+    PCHK(hipGetLastError());
+    uint32_t nr = 0;
+    PCHK(hipMemcpyAsync(&nr, rowptr + V, 4, hipMemcpyDeviceToHost, st));
+    PCHK(hipStreamSynchronize(st));
+    *nrec = nr;
+    return hipSuccess;
+}
+
+hipError_t preload_prep_module() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void*)prep_degree_kernel);
 }
 
 }  // namespace shdtopo

@@ -736,4 +736,9 @@ hipError_t launch_heap_replay(const ReplayCSR& g, const ReplayWs& ws, const uint
     return hipGetLastError();
 }
 
+hipError_t preload_replay_module() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void*)heap_replay_kernel);
+}
+
 }  // namespace shdtopo

@@ -800,7 +800,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     const uint32_t pcap = (uint32_t)(V * K);
 
     uint32_t iter = ctr[0];
-    unsigned long long n_near = 0, n_sweep = 0, n_expand = 0, n_par = 0;
+    unsigned long long n_near = 0, n_sweep = 0, n_expand = 0, n_par = 0, n_walk = 0;
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, t_split = 0;
     if (tid < 4) L.cnt[tid] = 0;
     if (tid < 5) L.pt[tid] = 0;
@@ -835,7 +835,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         for (uint32_t i = tid; i < tbw; i += kSsspBlock) D.tb[i] = 0u;
         for (uint32_t i = tid; i < xbw; i += kSsspBlock) D.xb[i] = 0u;
         for (uint32_t i = tid; i < pw; i += kSsspBlock) D.pend[i] = 0u;
-        for (uint32_t i = tid; i < tw; i += kSsspBlock) D.tie[i] = 0u;
+        // tie bits: set only on touched tail lines, so K >= 8 clears them with those lines below
+        if (K < 8)
+            for (uint32_t i = tid; i < tw; i += kSsspBlock) D.tie[i] = 0u;
         if (tid < (uint32_t)K) L.sh[tid] = (int)tid < nk ? srcsh[r0 + tid] : 0.0;
         // no landmark bound until h0 is reached (the sweeps test kappa0 against L.dh0)
         if (tid < (uint32_t)K) L.dh0[tid] = INFINITY;
@@ -861,6 +863,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + (size_t)v * (K / 2) + h);
                         else d2[(size_t)v * (K / 2) + h] = inf2;
                     }
+                    // the vertex's K tie bits (whole bytes for K >= 8)
+                    if (K == 8) reinterpret_cast<uint8_t*>(D.tie)[v] = 0u;
+                    else if (K == 16) reinterpret_cast<uint16_t*>(D.tie)[v] = 0u;
                 }
             }
             nt = wave_sum_u64(nt);
@@ -1223,6 +1228,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 uint32_t q = pcur[i];
                 if (atomicExch(&precw[4 * (size_t)q + 1], ep) == ep) continue;
                 for (;;) {
+                    n_walk++;
                     const uint32_t j = q % K;
                     uint32_t u = 0;
                     if (!try_hint(q, &u)) {
@@ -1482,6 +1488,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             b[7] = (unsigned long long)nk;
         }
     }
+    n_walk = wave_sum_u64(n_walk);
+    if ((tid & 63) == 0 && n_walk) atomicAdd(&stats[ST_WALK], n_walk);
     if (tid == 0) {
         ctr[0] = iter;
         atomicAdd(&stats[ST_RELAX], L.cnt[0]);
@@ -1805,6 +1813,11 @@ hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uin
         case 16: return launch_batch_k<16>(g, ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan, iter_guard, out_lr, out_hops, out_rowmin, d_stats, stream);
     }
     return hipErrorInvalidValue;
+}
+
+hipError_t preload_batch_module() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void*)sssp_batch_kernel<8>);
 }
 
 }  // namespace shdtopo
