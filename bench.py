@@ -445,6 +445,9 @@ def main():
                                                 for x in st["parent_phase_ms"]],
                     touched_lines_per_build=int(st["touched_lines"]),
                     walk_steps_per_source=round(st["walk_steps"] / max(1, rows)),
+                    walk_kinds_per_source=dict(zip(("tree", "tail_improver", "hub_improver",
+                                                    "row_scan"),
+                                                   [round(x / max(1, rows)) for x in st["walk_kinds"]])),
                     tie_dense=tie_dense)
         # cold build: the first table of the loaded topology, split into its parts
         cs = st_cold

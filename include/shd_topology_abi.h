@@ -287,6 +287,9 @@ typedef struct {
     int64_t exchange_kind;      /* the last build's row exchange: 0 none (one device), 1 RCCL
                                    all-gather + all-reduce(MIN), 2 device-to-device peer copies
                                    (engines sharing a device, or RCCL unavailable) */
+    int64_t walk_kinds[4];      /* of the walk steps: parents certified by the h0-tree guess, by a
+                                   tail's recorded improver, by a hub's recorded improver, and pairs
+                                   sent to the merged row scans */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

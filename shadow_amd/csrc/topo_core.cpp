@@ -702,7 +702,7 @@ int ensure_workspace(Topology* top, int nsrc) {
     const int64_t qs = queue_stride(top, K);
     const size_t per_slot = (size_t)V * (8 * (size_t)K + 32 * (size_t)K) + 16 * (size_t)qs +
                             (size_t)ringE * 4 + maskb + 4 * hparN +
-                            (size_t)kMaxHops * kSsspBlock * 8 + 16;
+                            kPathBufPerSlot * 8 + 16;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     // memory already held by this workspace counts as available
@@ -730,7 +730,7 @@ int ensure_workspace(Topology* top, int nsrc) {
     HIPCHK(top->d_ring.ensure((size_t)want * (size_t)ringE));
     HIPCHK(top->d_cnt.ensure(pn));
     HIPCHK(top->d_bslot.ensure(pn));
-    HIPCHK(top->d_pathbuf.ensure((size_t)want * kMaxHops * kSsspBlock));
+    HIPCHK(top->d_pathbuf.ensure((size_t)want * kPathBufPerSlot));
     HIPCHK(top->d_counters.ensure((size_t)want * 4));
     HIPCHK(top->d_mask.ensure((size_t)want * maskb));
     HIPCHK(top->d_hpar.ensure(std::max<size_t>(1, (size_t)want * hparN)));
@@ -1327,6 +1327,7 @@ int collect_row_stats(Topology* top) {
     top->stats.replay_rows = (int64_t)h[ST_RP_ROWS];
     top->stats.touched_lines = (int64_t)h[ST_TOUCHED];
     top->stats.walk_steps = (int64_t)h[ST_WALK];
+    for (int i = 0; i < 4; i++) top->stats.walk_kinds[i] = (int64_t)h[ST_WK0 + i];
     top->stats.replay_pops = (int64_t)h[ST_RP_POPS];
     top->stats.replay_pushes = (int64_t)h[ST_RP_PUSH];
     top->stats.replay_modifies = (int64_t)h[ST_RP_MOD];

@@ -24,6 +24,12 @@ constexpr int kSsspBlock = SHD_SSSP_BLOCK;  // threads per SSSP workgroup
 #endif
 constexpr int kBatchWgPerCu = SHD_BATCH_WGPCU;  // batch-kernel workgroups per CU (share its LDS)
 constexpr int kMaxHops = 48;      // per-thread path buffer depth (longer paths: O(h^2) walk)
+constexpr int kEpiR = 4;          // batch epilogue: rounds of results a lane may run ahead of the
+                                  // slowest lane of its wave (staged, then written coalesced)
+// doubles of the batch kernel's path buffer per slot: the chain losses [kMaxHops][kSsspBlock],
+// then the epilogue's staged {lat, rel} [kEpiR][kSsspBlock] and hops u16 [kEpiR][kSsspBlock]
+constexpr size_t kPathBufPerSlot = (size_t)kMaxHops * kSsspBlock + 2 * (size_t)kEpiR * kSsspBlock +
+                                   (size_t)kEpiR * kSsspBlock / 4;
 #ifndef SHD_KAP_IN_REC
 #define SHD_KAP_IN_REC 1
 #endif
@@ -80,7 +86,9 @@ enum StatIdx {
                         // rounds, surviving edges (8 slots)
     ST_TOUCHED = 59,    // tail distance lines reset at batch starts (lines the batches touched)
     ST_WALK = 60,       // batch kernel parent pass: walk steps (pairs claimed and resolved)
-    ST_COUNT = 61
+    ST_WK0 = 61,        //   of which resolved by the h0-tree guess, by a tail's improver, by a
+                        //   hub's improver, and pairs sent to row scans (4 slots)
+    ST_COUNT = 65
 };
 
 struct DevCSR {
@@ -121,7 +129,8 @@ struct SlotWs {
     unsigned long long* best = nullptr;  // parent pass: min d[u] over candidates
     uint32_t* cnt = nullptr;             // parent pass: candidates at the min
     uint32_t* bslot = nullptr;           // parent pass: lowest adjacency slot at the min
-    double* pathbuf = nullptr;           // [slot][kMaxHops][kSsspBlock] edge losses of a path
+    double* pathbuf = nullptr;           // [slot][kPathBufPerSlot]: edge losses of a path, staged
+                                         // epilogue results
     uint32_t* counters = nullptr;        // [slot][4]: batch tag, (unused)
     int K = 8;
     int64_t q_stride = 0;

@@ -783,7 +783,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     uint32_t* cntc = ws.cnt + (size_t)slot * V * K;
     uint32_t* bslot = ws.bslot + (size_t)slot * V * K;
     D.tpar = precw;
-    double* pbuf = ws.pathbuf + (size_t)slot * kMaxHops * kSsspBlock;
+    double* pbuf = ws.pathbuf + (size_t)slot * kPathBufPerSlot;
     uint32_t* ctr = ws.counters + (size_t)slot * 4;
     const uint32_t cap = (uint32_t)V;
     BBuckets B;
@@ -801,6 +801,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
 
     uint32_t iter = ctr[0];
     unsigned long long n_near = 0, n_sweep = 0, n_expand = 0, n_par = 0, n_walk = 0;
+    unsigned long long n_wk[4] = {0, 0, 0, 0};  // walk steps by kind (ST_WK0)
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, t_split = 0;
     if (tid < 4) L.cnt[tid] = 0;
     if (tid < 5) L.pt[tid] = 0;
@@ -1159,25 +1160,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             const unsigned long long lb = d2bits(loss);
             prec[q] = make_uint4(u, ep, (uint32_t)lb, (uint32_t)(lb >> 32));
         };
-        // A guess certified without scanning a row: the first P hubs' recorded improver (LDS
-        // hint, no tie bit) or a tail's h0-tree parent (no tie bit, the edge is tight).  Writes
-        // the pair record and returns the parent in *pu; false: the pair needs a row scan.
-        auto try_hint = [&](uint32_t q, uint32_t* pout) -> bool {
+        // A guess certified without scanning a row, past the h0-tree guess of a tail (tried by
+        // the walk itself): a tail's recorded improver (no tie bit, the edge is tight) or the
+        // first P hubs' recorded improver (LDS hint, no tie bit).  Writes the pair record and
+        // returns the parent in *pout; false: the pair needs a row scan.  dv = d_j(v).
+        auto try_hint = [&](uint32_t q, unsigned long long dv, uint32_t* pout) -> bool {
             const uint32_t v = q / K, j = q % K;
             if (v >= H) {
                 if ((D.tie[q >> 5] >> (q & 31)) & 1u) return false;
-                const uint4 sp = reinterpret_cast<const uint4*>(g.spt)[v];
-                const double sl = g.sptLoss[v];
-                const unsigned long long dv = D.get(v, j);
-                const uint32_t pu = sp.x;
-                if (pu < (uint32_t)V) {
-                    const double wt = __hiloint2double((int)sp.w, (int)sp.z);
-                    if (__dadd_rn(bits2d(D.get(pu, j)), wt) == bits2d(dv)) {
-                        put(q, pu, sl);
-                        *pout = pu;
-                        return true;
-                    }
-                }
                 if (!SHD_TAIL_HINT || !g.rows_sorted) return false;
                 // second guess: the recorded improver u; the edge is found in v's own row (a
                 // tail: short) -- the same undirected edge, same latency and loss as u's slot
@@ -1211,38 +1201,98 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             uint32_t c;
             double wt;
             adj_load(g, lo, c, wt);
-            if (__dadd_rn(bits2d(D.get(u, j)), wt) != bits2d(D.get(v, j))) return false;
+            if (__dadd_rn(bits2d(D.get(u, j)), wt) != bits2d(dv)) return false;
             put(q, u, g.aloss[lo]);
             *pout = u;
             return true;
         };
+        // A walk hop's inputs at tail vertex v for source j: its h0-tree record {parent, slot,
+        // f64 w}, that edge's loss, the tie word of (v, j) and d_j(v) -- independent loads, all
+        // in one round trip.  Hubs: d_j(v) only (LDS).
+        struct Hop {
+            uint4 sp;
+            double sl;
+            uint32_t tw;
+            unsigned long long d;
+        };
+        auto load_hop = [&](uint32_t v, uint32_t j) -> Hop {
+            Hop h;
+            const uint32_t q = v * K + j;
+            if (v >= H) {
+                h.sp = reinterpret_cast<const uint4*>(g.spt)[v];
+                h.sl = g.sptLoss[v];
+                h.tw = D.tie[q >> 5];
+                h.d = ld_l2_u64(&D.dist[(size_t)q]);
+            } else {
+                h.sp = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+                h.sl = 0.0;
+                h.tw = 0u;
+                h.d = D.hd[(size_t)q];
+            }
+            return h;
+        };
         while (nF > 0) {
             n_par += nF;
             unsigned long long tp0 = wall_clock64();
-            // Walks: each thread follows its pairs' chains towards the source while the guesses
-            // certify parents (no level barriers); a chain stops at the source, at a pair another
-            // walk claimed first (stamp), or at a pair that needs a row scan (-> fscr).
+            // Walks: chains are followed towards the source while the h0-tree guess certifies
+            // parents (no level barriers); a chain stops at the source, at a pair another walk
+            // claimed first (tag), or at a pair whose guess fails (-> S = fscr, claimed: the hint
+            // pass below resolves it).  One round trip per hop: the claim of q goes out with the
+            // loads of q's tree parent pu (d_j(pu) certifies the guess, pu's own hop inputs serve
+            // the next hop).  Flattened: a lane takes its next start pair as soon as its chain
+            // ends, so a wave runs for its busiest lane's total of hops, not for the sum over
+            // start pairs of the longest chain among its 64 lanes; the slower guesses (binary
+            // searches) are deferred so they do not stall the wave's other chains.
             if (tid == 0) L.qtail = 0;
             __syncthreads();
-            for (uint32_t i = tid; i < nF; i += kSsspBlock) {
-                uint32_t q = pcur[i];
-                if (atomicExch(&precw[4 * (size_t)q + 1], ep) == ep) continue;
+            {
+                uint32_t i = tid, q = 0, j = 0;
+                bool act = false, fresh = false;
+                Hop h;
+                h.sp = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+                h.sl = 0.0;
+                h.tw = 0u;
+                h.d = 0ull;
                 for (;;) {
-                    n_walk++;
-                    const uint32_t j = q % K;
-                    uint32_t u = 0;
-                    if (!try_hint(q, &u)) {
-                        best[q] = kInfBits;
-                        cntc[q] = 0;
-                        bslot[q] = 0xFFFFFFFFu;
-                        const uint32_t pos = atomicAdd(&L.qtail, 1u);
-                        if (pos < pcap) fscr[pos] = q;
-                        else atomicOr(&L.fover, 128u);
-                        break;
+                    if (!act && i < nF) {
+                        q = pcur[i];
+                        i += kSsspBlock;
+                        j = q % K;
+                        act = true;
+                        fresh = true;
                     }
-                    if (u == L.src[j]) break;
-                    q = u * K + j;
-                    if (atomicExch(&precw[4 * (size_t)q + 1], ep) == ep) break;
+                    if (!__any(act)) break;
+                    if (act && fresh) {
+                        h = load_hop(q / K, j);
+                        fresh = false;
+                    } else if (act) {
+                        const uint32_t v = q / K;
+                        const uint32_t pu = h.sp.x;
+                        const bool tree = v >= H && !((h.tw >> (q & 31)) & 1u) && pu < (uint32_t)V;
+                        Hop hn = h;
+                        if (tree) hn = load_hop(pu, j);
+                        if (atomicExch(&precw[4 * (size_t)q + 1], ep) == ep) {  // another walk's
+                            act = false;
+                        } else {
+                            n_walk++;
+                            if (tree && __dadd_rn(bits2d(hn.d), __hiloint2double((int)h.sp.w, (int)h.sp.z)) ==
+                                            bits2d(h.d)) {
+                                put(q, pu, h.sl);
+                                n_wk[0]++;
+                                if (pu == L.src[j]) {
+                                    act = false;
+                                } else {
+                                    q = pu * K + j;
+                                    h = hn;
+                                }
+                            } else {
+                                const uint32_t pos = atomicAdd(&L.qtail, 1u);
+                                if (pos < pcap) fscr[pos] = q;
+                                else atomicOr(&L.fover, 128u);
+                                act = false;
+                            }
+                        }
+                    }
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1252,114 +1302,145 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             if (tid == 0) L.pt[1] += wall_clock64() - tp0;  // walks
             if (nS == 0) break;
             tp0 = wall_clock64();
-            // merge the unresolved pairs by vertex (masks in mA / hdef, zero after the SSSP): a
-            // vertex's row is scanned once for every source whose chain needs it
+            // hint pass over S (pt[2] with the row scans): the recorded improvers (a tail's, the
+            // first P hubs'), in lockstep; the pairs left need a row scan: R, compacted into pcur
+            // (consumed by the walks)
             if (tid == 0) L.qtail = 0;
             __syncthreads();
             for (uint32_t ib = 0; ib < nS; ib += kSsspBlock) {
                 const uint32_t i = ib + tid;
-                bool first = false;
-                uint32_t v = 0;
-                if (i < nS) {
-                    const uint32_t q = fscr[i];
-                    v = q / K;
-                    first = (v < H ? MO::set(hdef, v, 1u << (q % K)) : MO::set(mA, v, 1u << (q % K))) == 0u;
-                }
-                wave_push_t<uint32_t>(first, v, vscr, &L.qtail, cap, &L.fover, 128u);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            const uint32_t nVs = min(L.qtail, cap);
-            __syncthreads();
-            // one pass over the merged rows: a lane per edge reads the neighbour's K distances
-            // (one line) and tests every source of the row's mask
-            for (uint32_t base = 0; base < nVs; base += kBChunk) {
-                const uint32_t cnt = min((uint32_t)kBChunk, nVs - base);
-                const uint32_t total = load_chunk<K>(vscr + base, cnt, g, L, D, mA, hdef, false);
-                for (uint32_t e = tid; e < total; e += kSsspBlock) {
-                    const int lo = chunk_slot<K>(L, cnt, e);
-                    const uint32_t jr = L.rs[lo] + (e - L.off[lo]);
-                    const uint32_t m = L.msk[lo];
-                    uint32_t u;
-                    double wt;
-                    adj_load(g, jr, u, wt);
-                    unsigned long long du[K];
-                    if (u < H) {
-#pragma unroll
-                        for (int q = 0; q < K; q++) du[q] = D.hd[(size_t)u * K + q];
-                    } else {
-                        // L1-bypassing 16-B loads of the line (lowered by atomics of other waves)
-                        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-                        const u64x2* p = reinterpret_cast<const u64x2*>(D.dist + (size_t)u * K);
-#pragma unroll
-                        for (int q = 0; q < K / 2; q++) {
-                            const u64x2 x = __builtin_nontemporal_load(p + q);
-                            du[2 * q] = x.x;
-                            du[2 * q + 1] = x.y;
-                        }
-                    }
-#pragma unroll
-                    for (int q = 0; q < K; q++) {
-                        if (((m >> q) & 1u) && __dadd_rn(bits2d(du[q]), wt) == L.val[lo * K + q]) {
-                            const uint32_t pq = L.vx[lo] * K + (uint32_t)q;
-                            atomicMin(&best[pq], du[q]);
-                            atomicAdd(&cntc[pq], 1u);
-                            atomicMin(&bslot[pq], jr);
-                        }
-                    }
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-            }
-            if (tid == 0) L.pt[2] += wall_clock64() - tp0;  // merged row scans
-            tp0 = wall_clock64();
-            // pairs with several candidates: recount at the minimum
-            if (tid == 0) L.qtail = 0;
-            __syncthreads();
-            for (uint32_t ib = 0; ib < nS; ib += kSsspBlock) {
-                const uint32_t i = ib + tid;
-                bool multi = false;
+                bool scan = false;
                 uint32_t q = 0;
                 if (i < nS) {
                     q = fscr[i];
-                    multi = ld_l2_u32(&cntc[q]) > 1u;
-                    if (multi) {
-                        atomicExch(&cntc[q], 0u);
-                        atomicExch(&bslot[q], 0xFFFFFFFFu);
+                    uint32_t u = 0;
+                    const bool ok = try_hint(q, D.get(q / K, q % K), &u);
+                    n_wk[ok ? (q / K >= H ? 1 : 2) : 3]++;
+                    if (!ok) {
+                        best[q] = kInfBits;
+                        cntc[q] = 0;
+                        bslot[q] = 0xFFFFFFFFu;
+                        scan = true;
                     }
                 }
-                wave_push_t<uint32_t>(multi, q, pnxt, &L.qtail, pcap, &L.fover, 128u);
+                wave_push_t<uint32_t>(scan, q, pcur, &L.qtail, pcap, &L.fover, 128u);
             }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            const uint32_t nM = min(L.qtail, pcap);
+            const uint32_t nR = min(L.qtail, pcap);
+            const uint32_t* rl = pcur;
             __syncthreads();
-            if (nM > 0) {
-                expand_pairs<K>(
-                    pnxt, nM, g, L,
-                    [&](uint32_t q, double& val) { val = bits2d(D.get(q / K, q % K)); },
-                    [&](uint32_t q, double dv, uint32_t jr) {
+            if (nR > 0) {
+                // merge the unresolved pairs by vertex (masks in mA / hdef, zero after the SSSP): a
+                // vertex's row is scanned once for every source whose chain needs it
+                if (tid == 0) L.qtail = 0;
+                __syncthreads();
+                for (uint32_t ib = 0; ib < nR; ib += kSsspBlock) {
+                    const uint32_t i = ib + tid;
+                    bool first = false;
+                    uint32_t v = 0;
+                    if (i < nR) {
+                        const uint32_t q = rl[i];
+                        v = q / K;
+                        first = (v < H ? MO::set(hdef, v, 1u << (q % K)) : MO::set(mA, v, 1u << (q % K))) == 0u;
+                    }
+                    wave_push_t<uint32_t>(first, v, vscr, &L.qtail, cap, &L.fover, 128u);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                const uint32_t nVs = min(L.qtail, cap);
+                __syncthreads();
+                // one pass over the merged rows: a lane per edge reads the neighbour's K distances
+                // (one line) and tests every source of the row's mask
+                for (uint32_t base = 0; base < nVs; base += kBChunk) {
+                    const uint32_t cnt = min((uint32_t)kBChunk, nVs - base);
+                    const uint32_t total = load_chunk<K>(vscr + base, cnt, g, L, D, mA, hdef, false);
+                    for (uint32_t e = tid; e < total; e += kSsspBlock) {
+                        const int lo = chunk_slot<K>(L, cnt, e);
+                        const uint32_t jr = L.rs[lo] + (e - L.off[lo]);
+                        const uint32_t m = L.msk[lo];
                         uint32_t u;
                         double wt;
                         adj_load(g, jr, u, wt);
-                        const unsigned long long du = D.get(u, q % K);
-                        if (__dadd_rn(bits2d(du), wt) == dv && du == ld_l2_u64(&best[q])) {
-                            atomicAdd(&cntc[q], 1u);
-                            atomicMin(&bslot[q], jr);
+                        unsigned long long du[K];
+                        if (u < H) {
+#pragma unroll
+                            for (int q = 0; q < K; q++) du[q] = D.hd[(size_t)u * K + q];
+                        } else {
+                            // L1-bypassing 16-B loads of the line (lowered by atomics of other waves)
+                            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+                            const u64x2* p = reinterpret_cast<const u64x2*>(D.dist + (size_t)u * K);
+#pragma unroll
+                            for (int q = 0; q < K / 2; q++) {
+                                const u64x2 x = __builtin_nontemporal_load(p + q);
+                                du[2 * q] = x.x;
+                                du[2 * q + 1] = x.y;
+                            }
                         }
-                    });
-            }
-            for (uint32_t i = tid; i < nS; i += kSsspBlock) {
-                const uint32_t q = fscr[i];
-                const uint32_t jr = ld_l2_u32(&bslot[q]);
-                const uint32_t c = ld_l2_u32(&cntc[q]);
-                if (jr == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
-                    atomicAdd(&stats[ST_ERRORS], 1ull);
-                    prec[q] = make_uint4(L.src[q % K] | 0x40000000u, ep, 0u, 0u);
-                } else {
-                    const unsigned long long lb = d2bits(g.aloss[jr]);
-                    prec[q] = make_uint4(adj_col(g, jr) | (c > 1 ? 0x80000000u : 0u), ep,
-                                         (uint32_t)lb, (uint32_t)(lb >> 32));
+#pragma unroll
+                        for (int q = 0; q < K; q++) {
+                            if (((m >> q) & 1u) && __dadd_rn(bits2d(du[q]), wt) == L.val[lo * K + q]) {
+                                const uint32_t pq = L.vx[lo] * K + (uint32_t)q;
+                                atomicMin(&best[pq], du[q]);
+                                atomicAdd(&cntc[pq], 1u);
+                                atomicMin(&bslot[pq], jr);
+                            }
+                        }
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
                 }
+                if (tid == 0) L.pt[2] += wall_clock64() - tp0;  // merged row scans
+                tp0 = wall_clock64();
+                // pairs with several candidates: recount at the minimum
+                if (tid == 0) L.qtail = 0;
+                __syncthreads();
+                for (uint32_t ib = 0; ib < nR; ib += kSsspBlock) {
+                    const uint32_t i = ib + tid;
+                    bool multi = false;
+                    uint32_t q = 0;
+                    if (i < nR) {
+                        q = rl[i];
+                        multi = ld_l2_u32(&cntc[q]) > 1u;
+                        if (multi) {
+                            atomicExch(&cntc[q], 0u);
+                            atomicExch(&bslot[q], 0xFFFFFFFFu);
+                        }
+                    }
+                    wave_push_t<uint32_t>(multi, q, pnxt, &L.qtail, pcap, &L.fover, 128u);
+                }
+                __syncthreads();
+                const uint32_t nM = min(L.qtail, pcap);
+                __syncthreads();
+                if (nM > 0) {
+                    expand_pairs<K>(
+                        pnxt, nM, g, L,
+                        [&](uint32_t q, double& val) { val = bits2d(D.get(q / K, q % K)); },
+                        [&](uint32_t q, double dv, uint32_t jr) {
+                            uint32_t u;
+                            double wt;
+                            adj_load(g, jr, u, wt);
+                            const unsigned long long du = D.get(u, q % K);
+                            if (__dadd_rn(bits2d(du), wt) == dv && du == ld_l2_u64(&best[q])) {
+                                atomicAdd(&cntc[q], 1u);
+                                atomicMin(&bslot[q], jr);
+                            }
+                        });
+                }
+                for (uint32_t i = tid; i < nR; i += kSsspBlock) {
+                    const uint32_t q = rl[i];
+                    const uint32_t jr = ld_l2_u32(&bslot[q]);
+                    const uint32_t c = ld_l2_u32(&cntc[q]);
+                    if (jr == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
+                        atomicAdd(&stats[ST_ERRORS], 1ull);
+                        prec[q] = make_uint4(L.src[q % K] | 0x40000000u, ep, 0u, 0u);
+                    } else {
+                        const unsigned long long lb = d2bits(g.aloss[jr]);
+                        prec[q] = make_uint4(adj_col(g, jr) | (c > 1 ? 0x80000000u : 0u), ep,
+                                             (uint32_t)lb, (uint32_t)(lb >> 32));
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             __syncthreads();
             if (tid == 0) L.pt[3] += wall_clock64() - tp0;  // recount + finalize
@@ -1374,7 +1455,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 if (i < nS) {
                     const uint32_t qc = fscr[i];
                     const uint32_t j = qc % K;
-                    const uint32_t u = precw[4 * (size_t)qc] & 0x3FFFFFFFu;
+                    // the parent (hint pass or row scan: R's records come from other threads)
+                    const uint32_t u = ld_l2_u32(&precw[4 * (size_t)qc]) & 0x3FFFFFFFu;
                     q = u * K + j;
                     p = u != L.src[j];
                 }
@@ -1490,6 +1572,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     }
     n_walk = wave_sum_u64(n_walk);
     if ((tid & 63) == 0 && n_walk) atomicAdd(&stats[ST_WALK], n_walk);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const unsigned long long x = wave_sum_u64(n_wk[i]);
+        if ((tid & 63) == 0 && x) atomicAdd(&stats[ST_WK0 + i], x);
+    }
     if (tid == 0) {
         ctr[0] = iter;
         atomicAdd(&stats[ST_RELAX], L.cnt[0]);

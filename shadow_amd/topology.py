@@ -246,6 +246,7 @@ class Topology:
         out["batch_wave_ms"] = list(out["batch_wave_ms"])
         out["csr_step_ms"] = list(out["csr_step_ms"])
         out["build_step_ms"] = list(out["build_step_ms"])
+        out["walk_kinds"] = list(out["walk_kinds"])
         out["events"] = dict(zip(("expanded", "tail_relax", "tail_improve", "window_taken",
                                   "overflow_refilled", "parent_vertices", "tail_settled_relax",
                                   "stale_skipped"),
