@@ -290,6 +290,12 @@ typedef struct {
     int64_t walk_kinds[4];      /* of the walk steps: parents certified by the h0-tree guess, by a
                                    tail's recorded improver, by a hub's recorded improver, and pairs
                                    sent to the merged row scans */
+    double build_wait_ms;       /* the last whole-table build's wait for the build lock (the
+                                   attach-time preparation thread, or another builder) */
+    double attach_prep_ms;      /* wall time of the attach-time preparation (option
+                                   "prepare_on_attach": device init + graph preparation in a
+                                   background thread from the first attach on, overlapping the
+                                   host's attach phase; 0 if it did not run) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -49,7 +49,8 @@ class ShdStats(ctypes.Structure):
                 ("replay_prep_ms", dbl), ("touched_lines", i64), ("csr_host_runs", i64),
                 ("workspace_ms", dbl), ("csr_step_ms", dbl * 8), ("module_load_ms", dbl),
                 ("build_wall_ms", dbl), ("walk_steps", i64), ("build_step_ms", dbl * 8),
-                ("exchange_kind", i64), ("walk_kinds", i64 * 4)]
+                ("exchange_kind", i64), ("walk_kinds", i64 * 4),
+                ("build_wait_ms", dbl), ("attach_prep_ms", dbl)]
 
 
 class ShdSynthParams(ctypes.Structure):

@@ -166,6 +166,16 @@ struct _Topology {
 
     // device state
     bool devInit = false;
+    int devId = 0;               // the device dev_init bound (every later entry re-binds it)
+    // Preparation at the first attach (option "prepare_on_attach", default on): a background
+    // thread initialises the device and prepares the graph (upload_csr) under buildMu while the
+    // host attaches its hosts, so the first table build -- whose lock waits for the thread --
+    // no longer pays them.  The device option must be set before the first attach.
+    bool prepOnAttach = true;
+    std::atomic<bool> prepStarted{false};
+    std::thread prepThread;
+    double prepBgMs = 0.0;       // the thread's wall time
+    int prepBgRc = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     bool csrUploaded = false;
@@ -249,7 +259,11 @@ struct _Topology {
                               // 2 iterations 226 ms, 4: 199, 6: 194, 12: 194, 32: 196 (no
                               // fixpoint is reached: cycles without targets rise forever; every
                               // iterate is exact)
-    DevBuf<double> d_pot, d_kfA, d_kfB;
+    DevBuf<double> d_pot, d_kfA, d_kfB, d_kfPart;
+    // hub rows cut into segments (HubSegs): {row, first entry} and the rows cut in several
+    DevBuf<uint2> d_hseg;
+    DevBuf<uint4> d_hmulti;
+    uint32_t hsegRows = 0, hsegN = 0, hmultiN = 0;
     DevBuf<unsigned int> d_kfChanged;
     DevBuf<uint32_t> d_rowmap, d_bsrc;  // batch order: output row and source of each position
     // cache of the last batch order (enqueue_rows): the rows' sources, batch fill and options
@@ -435,7 +449,20 @@ Topology* finish_new(Topology* top) {
 // device setup
 // ---------------------------------------------------------------------------------------------
 int dev_init(Topology* top) {
-    if (top->devInit) return 0;
+    if (top->devInit) {
+        // HIP's current device is per thread: bind this engine's device for the caller
+        HIPCHK(hipSetDevice(top->devId));
+        return 0;
+    }
+    const bool trace = getenv("SHDTOPO_TRACE_INIT") != nullptr;
+    auto ti = std::chrono::steady_clock::now();
+    auto tmark = [&](const char* what) {
+        if (!trace) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[shdtopo] dev_init %s: %.2f ms\n", what,
+                std::chrono::duration<double, std::milli>(t - ti).count());
+        ti = t;
+    };
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= 0) {
@@ -443,25 +470,45 @@ int dev_init(Topology* top) {
                  "(no CPU fallback)");
         return -1;
     }
-    HIPCHK(hipSetDevice(top->device % n));
+    tmark("device count");
+    top->devId = top->device % n;
+    HIPCHK(hipSetDevice(top->devId));
+    tmark("set device");
     HIPCHK(hipStreamCreateWithFlags(&top->stream, hipStreamNonBlocking));
+    tmark("stream");
     HIPCHK(hipEventCreate(&top->ev0));
     HIPCHK(hipEventCreate(&top->ev1));
     HIPCHK(hipEventCreate(&top->ev2));
     HIPCHK(hipEventCreate(&top->ev3));
     HIPCHK(hipEventCreate(&top->evr0));
     HIPCHK(hipEventCreate(&top->evr1));
+    tmark("events");
     HIPCHK(top->d_stats.ensure(ST_COUNT));
+    tmark("stats buffer");
     // the kernels' code objects, loaded here rather than by the first build's launches
     const auto t0 = std::chrono::steady_clock::now();
     HIPCHK(preload_prep_module());
+    tmark("prep module");
     HIPCHK(preload_batch_module());
+    tmark("batch module");
     HIPCHK(preload_kernels_module());
+    tmark("kernels module");
     HIPCHK(preload_replay_module());
+    tmark("replay module");
     top->stats.module_load_ms = std::chrono::duration<double, std::milli>(
         std::chrono::steady_clock::now() - t0).count();
     top->devInit = true;
     return 0;
+}
+
+HubSegs hub_segs(Topology* top) {
+    HubSegs h;
+    h.rows = top->hsegRows;
+    h.seg = top->d_hseg.p;
+    h.nseg = top->hsegN;
+    h.multi = top->d_hmulti.p;
+    h.nmulti = top->hmultiN;
+    return h;
 }
 
 int upload_csr_impl(Topology* top);
@@ -587,6 +634,27 @@ int upload_csr_impl(Topology* top) {
     deg.release();
     selfE.release();
     vl0.release();
+    {
+        // the hub rows' segment tables (HubSegs) from the head of the rowptr
+        std::vector<uint32_t> head((size_t)H + 1);
+        HIPCHK(hipMemcpyAsync(head.data(), top->d_rowptr.p, 4 * ((size_t)H + 1), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::vector<uint2> seg;
+        std::vector<uint4> multi;
+        hub_segments(head.data(), H, seg, multi);
+        top->d_hseg.release();
+        top->d_hmulti.release();
+        HIPCHK(top->d_hseg.ensure(seg.size()));
+        HIPCHK(hipMemcpyAsync(top->d_hseg.p, seg.data(), sizeof(uint2) * seg.size(), hipMemcpyHostToDevice, st));
+        if (!multi.empty()) {
+            HIPCHK(top->d_hmulti.ensure(multi.size()));
+            HIPCHK(hipMemcpyAsync(top->d_hmulti.p, multi.data(), sizeof(uint4) * multi.size(), hipMemcpyHostToDevice, st));
+        }
+        HIPCHK(hipStreamSynchronize(st));
+        top->hsegRows = H;
+        top->hsegN = (uint32_t)seg.size();
+        top->hmultiN = (uint32_t)multi.size();
+    }
     step_done(1);
     HIPCHK(top->d_adj.ensure(4 * (size_t)nadj));
     HIPCHK(top->d_aloss.ensure((size_t)nadj));
@@ -602,7 +670,7 @@ int upload_csr_impl(Topology* top) {
     HIPCHK(top->d_sptPar.ensure((size_t)V));
     HIPCHK(top->d_spt.ensure(4 * (size_t)V));
     HIPCHK(top->d_sptLoss.ensure((size_t)V));
-    HIPCHK(prep_tree(V, nadj, H, top->d_rowptr.p, top->d_adj.p, top->d_aloss.p, top->d_pot.p,
+    HIPCHK(prep_tree(V, nadj, hub_segs(top), top->d_rowptr.p, top->d_adj.p, top->d_aloss.p, top->d_pot.p,
                      top->d_sptPar.p, top->d_spt.p, top->d_sptLoss.p, &top->hp->piMax, st));
     step_done(4);
     // 4) the kappa-sorted relaxation copy
@@ -610,7 +678,7 @@ int upload_csr_impl(Topology* top) {
     HIPCHK(top->d_kap.ensure((size_t)nadj));
     HIPCHK(top->d_ksum.ensure(kKProbes * (size_t)V));
     HIPCHK(top->d_kap0.ensure((size_t)V));
-    HIPCHK(launch_kappa_copy(V, nadj, H, top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
+    HIPCHK(launch_kappa_copy(V, nadj, hub_segs(top), top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
                              top->d_sptPar.p, top->d_adjk.p, top->d_kap.p, top->d_ksum.p,
                              top->d_kap0.p, st));
     top->adjkPlain = true;
@@ -1015,8 +1083,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             // target skip is on.
             const int64_t nadjk = (int64_t)(top->d_adjk.n / 4);
             if (!top->adjkPlain && top->adjkTargets != tgt) {
-                HIPCHK(launch_kappa_copy(top->g.V, nadjk, (uint32_t)std::min<int64_t>(kGroupHubs, top->g.V),
-                                         top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
+                HIPCHK(launch_kappa_copy(top->g.V, nadjk, hub_segs(top), top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
                                          top->d_sptPar.p, top->d_adjk.p, top->d_kap.p,
                                          top->d_ksum.p, top->d_kap0.p, st));
                 top->adjkPlain = true;
@@ -1032,19 +1099,21 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 HIPCHK(launch_mark_targets(top->d_adjk.p, nadjk, top->d_tbits.p, st));
                 // the records' kappa field: the target-aware fixpoint (kappa0 with 0 iterations)
                 const int64_t V = top->g.V;
-                const uint32_t nwave = (uint32_t)std::min<int64_t>(kGroupHubs, V);
+                const HubSegs hs = hub_segs(top);
                 HIPCHK(top->d_kfA.ensure((size_t)V));
                 HIPCHK(top->d_kfB.ensure((size_t)V));
+                HIPCHK(top->d_kfPart.ensure(std::max<size_t>(1, hs.nseg)));
                 HIPCHK(top->d_kfChanged.ensure(1));
                 HIPCHK(launch_kfix_step(top->d_rowptr.p, top->d_adj.p, top->d_pot.p, top->d_tbits.p,
-                                        nullptr, top->d_kfA.p, V, nwave, top->d_kfChanged.p, st));
+                                        nullptr, top->d_kfA.p, V, hs, top->d_kfPart.p,
+                                        top->d_kfChanged.p, st));
                 double* kin = top->d_kfA.p;
                 double* kout = top->d_kfB.p;
                 int it = 0;
                 for (; it < top->targetKappa; it++) {
                     HIPCHK(hipMemsetAsync(top->d_kfChanged.p, 0, sizeof(unsigned int), st));
                     HIPCHK(launch_kfix_step(top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
-                                            top->d_tbits.p, kin, kout, V, nwave,
+                                            top->d_tbits.p, kin, kout, V, hs, top->d_kfPart.p,
                                             top->d_kfChanged.p, st));
                     unsigned int ch = 0;
                     HIPCHK(hipMemcpyAsync(&ch, top->d_kfChanged.p, sizeof(unsigned int),
@@ -1510,6 +1579,11 @@ int copy_csr_from(Topology* p, int pdev, Topology* o, int odev) {
     HIPCHK(peer_copy(p->d_elat, pdev, o->d_elat, odev, st));
     HIPCHK(peer_copy(p->d_eloss, pdev, o->d_eloss, odev, st));
     HIPCHK(peer_copy(p->d_inv, pdev, o->d_inv, odev, st));
+    HIPCHK(peer_copy(p->d_hseg, pdev, o->d_hseg, odev, st));
+    HIPCHK(peer_copy(p->d_hmulti, pdev, o->d_hmulti, odev, st));
+    p->hsegRows = o->hsegRows;
+    p->hsegN = o->hsegN;
+    p->hmultiN = o->hmultiN;
     HIPCHK(hipStreamSynchronize(st));
     p->hp = o->hp;
     p->rowsSorted = o->rowsSorted;
@@ -1705,14 +1779,21 @@ int build_multi(Topology* top) {
 // whole-table build on this GPU (for the current attached set)
 int ensure_table(Topology* top) {
     if (table_current(top)) return 0;
+    const auto tw0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lk(top->buildMu);
     if (table_current(top)) return 0;
     const auto tb0 = std::chrono::steady_clock::now();
+    // (waiting for the attach-time preparation thread, or another builder)
+    top->stats.build_wait_ms = std::chrono::duration<double, std::milli>(tb0 - tw0).count();
+    top->stats.attach_prep_ms = top->prepBgMs;
     for (double& x : top->stats.build_step_ms) x = 0.0;
     top->bstepT = tb0;
     auto bstep = [&](int i) { bstep_mark(top, i); };
     int r = dev_init(top);
     if (r) return r;
+    if (getenv("SHDTOPO_TRACE_INIT"))
+        fprintf(stderr, "[shdtopo] build: dev_init done at %.2f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
     const uint64_t sg = compute_geometry(top);
     bstep(0);
     const int64_t A = top->A;
@@ -2020,7 +2101,31 @@ void host_off(Topology* top, int32_t v) {
 }
 
 // shd-topology.c:1154-1166: g_hash_table_replace(virtualIP, ip, vertex)
+// The attach-time preparation (Topology::prepOnAttach): device init + graph preparation in a
+// background thread holding buildMu; a build (or any other buildMu holder) that comes first does
+// the work itself and the thread then finds nothing left to do.  Complete and directed topologies
+// have no batched-SSSP graph to prepare.
+void start_attach_prep(Topology* top) {
+    if (!top->prepOnAttach || top->isComplete || top->isDirected) return;
+    if (top->prepStarted.exchange(true)) return;
+    top->prepThread = std::thread([top]() {
+        std::lock_guard<std::mutex> lk(top->buildMu);
+        const auto t0 = std::chrono::steady_clock::now();
+        int n = 0;
+        if (!top->devInit && (hipGetDeviceCount(&n) != hipSuccess || n <= 0)) {
+            (void)hipGetLastError();
+            return;  // no GPU here: the first build reports it
+        }
+        int r = dev_init(top);
+        if (!r) r = upload_csr(top);
+        if (!r) r = hipStreamSynchronize(top->stream) == hipSuccess ? 0 : -1;
+        top->prepBgRc = r;
+        top->prepBgMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    });
+}
+
 void do_attach(Topology* top, uint32_t ip, int32_t v, uint64_t* bwDownOut, uint64_t* bwUpOut) {
+    start_attach_prep(top);
     {
         std::unique_lock<std::shared_mutex> lk(top->ipMu);
         auto it = top->virtualIP.find(ip);
@@ -2105,6 +2210,7 @@ Topology* shdtopo_new_synthetic(const ShdSynthParams* p) {
 
 void topology_free(Topology* top) {
     if (!top) return;
+    if (top->prepThread.joinable()) top->prepThread.join();
     for (Topology* p : top->peers) topology_free(p);
     top->peers.clear();
     if (!top->comms.empty() && rccl().ok)
@@ -2131,6 +2237,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "delta") top->delta = value;
     else if (k == "slots") top->slotsOpt = (int)value;
     else if (k == "device") top->device = (int)value;
+    else if (k == "prepare_on_attach") top->prepOnAttach = value != 0;
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
     else if (k == "par_hubs") top->parHubs = (int64_t)value;
     else if (k == "batch") {

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace shdtopo {
 
@@ -24,12 +25,8 @@ constexpr int kSsspBlock = SHD_SSSP_BLOCK;  // threads per SSSP workgroup
 #endif
 constexpr int kBatchWgPerCu = SHD_BATCH_WGPCU;  // batch-kernel workgroups per CU (share its LDS)
 constexpr int kMaxHops = 48;      // per-thread path buffer depth (longer paths: O(h^2) walk)
-constexpr int kEpiR = 4;          // batch epilogue: rounds of results a lane may run ahead of the
-                                  // slowest lane of its wave (staged, then written coalesced)
-// doubles of the batch kernel's path buffer per slot: the chain losses [kMaxHops][kSsspBlock],
-// then the epilogue's staged {lat, rel} [kEpiR][kSsspBlock] and hops u16 [kEpiR][kSsspBlock]
-constexpr size_t kPathBufPerSlot = (size_t)kMaxHops * kSsspBlock + 2 * (size_t)kEpiR * kSsspBlock +
-                                   (size_t)kEpiR * kSsspBlock / 4;
+// doubles of the batch kernel's path buffer per slot: the chain losses [kMaxHops][kSsspBlock]
+constexpr size_t kPathBufPerSlot = (size_t)kMaxHops * kSsspBlock;
 #ifndef SHD_KAP_IN_REC
 #define SHD_KAP_IN_REC 1
 #endif
@@ -129,8 +126,7 @@ struct SlotWs {
     unsigned long long* best = nullptr;  // parent pass: min d[u] over candidates
     uint32_t* cnt = nullptr;             // parent pass: candidates at the min
     uint32_t* bslot = nullptr;           // parent pass: lowest adjacency slot at the min
-    double* pathbuf = nullptr;           // [slot][kPathBufPerSlot]: edge losses of a path, staged
-                                         // epilogue results
+    double* pathbuf = nullptr;           // [slot][kPathBufPerSlot]: edge losses of a path
     uint32_t* counters = nullptr;        // [slot][4]: batch tag, (unused)
     int K = 8;
     int64_t q_stride = 0;
@@ -180,6 +176,23 @@ struct ReplayWs {
     uint32_t* pathbuf = nullptr;
 };
 
+// Hub rows (ids < rows: the long rows of the degree order) cut into segments of at most kHubSeg
+// entries, one wavefront each in the row-parallel steps (graph preparation, the target-aware
+// kappa fixpoint): the longest rows (250 k entries on C4) no longer serialise on one wavefront.
+// A row cut into several segments leaves one partial result per segment, combined by a
+// finalize pass over `multi`.
+constexpr uint32_t kHubSeg = 4096;
+struct HubSegs {
+    uint32_t rows = 0;             // hub rows [0, rows); the rest take a thread each
+    const uint2* seg = nullptr;    // {row, first entry} per segment, rows ascending
+    uint32_t nseg = 0;
+    const uint4* multi = nullptr;  // {row, first segment, segments, 0} of the rows cut in several
+    uint32_t nmulti = 0;
+};
+// the segment tables of rows [0, rows) from the first rows + 1 entries of rowptr (host)
+void hub_segments(const uint32_t* rowptr_head, uint32_t rows, std::vector<uint2>& seg,
+                  std::vector<uint4>& multi);
+
 // LDS plan of one batched SSSP workgroup: H hub distance rows (+ their queue masks) and P
 // parent hints, sized to the CU's 160 KiB.
 struct SsspLdsPlan {
@@ -197,9 +210,11 @@ hipError_t launch_mark_targets(uint32_t* adjk, int64_t nadj, const uint32_t* tbi
                                hipStream_t stream);
 // target-aware kappa fixpoint (topo_sssp_batch.hip): one step K_out = F(K_in) (K_in nullptr:
 // kappa0), then the f16 kappa field of the relaxation copy's records := K(column)
+// part: scratch of hs.nseg doubles (the per-segment minima of cut rows)
 hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const double* pot,
                             const uint32_t* tbits, const double* Kin, double* Kout, int64_t V,
-                            uint32_t nwave, unsigned int* changed, hipStream_t stream);
+                            const HubSegs& hs, double* part, unsigned int* changed,
+                            hipStream_t stream);
 hipError_t launch_kfix_store(uint32_t* adjk, int64_t nadj, const double* K, hipStream_t stream);
 // re-sort every row of the relaxation copy (records, kappa array, probes, kappa0) by the
 // target-aware key kap' of the current target set (tbits) and K
@@ -262,13 +277,13 @@ hipError_t prep_adjacency(int64_t V, int64_t E, int64_t nadj, const int32_t* eu,
 hipError_t prep_h0_distances(int64_t V, const uint32_t* rowptr, const uint32_t* adj, double* pot,
                              int* iterations, hipStream_t st);
 // h0 tree (sptPar u32[V], spt {parent, slot in v's row, f64 w}[V]), the records' pi / kappa0
-// field, *piMax = the largest finite pi; rows < nwave take a wavefront each
-hipError_t prep_tree(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* rowptr,
+// field, *piMax = the largest finite pi; hub rows by segments (hs)
+hipError_t prep_tree(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t* rowptr,
                      uint32_t* adj, const double* aloss, const double* pot, uint32_t* sptPar,
                      uint32_t* spt, double* sptLoss, double* piMax, hipStream_t st);
 // the plain kappa-sorted relaxation copy (adjk, kap, ksum, kap0) of adj: also restores it after
 // a target-aware re-sort when the target-aware order no longer applies
-hipError_t launch_kappa_copy(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* rowptr,
+hipError_t launch_kappa_copy(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t* rowptr,
                              const uint32_t* adj, const double* pot, const uint32_t* sptPar,
                              uint32_t* adjk, float* kap, float* ksum, float* kap0,
                              hipStream_t st);

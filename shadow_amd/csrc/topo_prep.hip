@@ -22,8 +22,8 @@
 //      field, pi max;
 //   7. the kappa-sorted relaxation copy: rows sorted by f32(w - pi(col)) rounded down (one global
 //      radix sort on (row, key)), the h0-tree edge flagged, kappa probes and kappa0.
-// Row-parallel steps take a wavefront per hub row (ids < nwave, the long rows after step 2) and a
-// thread per tail row.
+// Row-parallel steps take a wavefront per segment of a hub row (ids < hs.rows, the long rows after
+// step 2; at most kHubSeg entries per segment, HubSegs) and a thread per tail row.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -318,11 +318,10 @@ __device__ __forceinline__ bool tb_less(const TreeBest& a, const TreeBest& b) {
     return a.du < b.du || (a.du == b.du && a.u < b.u);
 }
 
-__device__ __forceinline__ void tree_scan(const uint32_t* rowptr, const uint32_t* adj,
-                                          const double* pot, uint32_t v, double dv, uint32_t k0,
-                                          uint32_t step, TreeBest& best, double& kmin) {
-    const uint32_t r1 = rowptr[v + 1];
-    for (uint32_t k = rowptr[v] + k0; k < r1; k += step) {
+__device__ __forceinline__ void tree_scan(const uint32_t* adj, const double* pot, uint32_t v,
+                                          double dv, uint32_t b, uint32_t e, uint32_t step,
+                                          TreeBest& best, double& kmin) {
+    for (uint32_t k = b; k < e; k += step) {
         const uint32_t u = adj[kAdjWords * k];
         const double w = rec_w(adj, k);
         const double du = pot[u];
@@ -347,46 +346,84 @@ __device__ __forceinline__ void tree_store(uint32_t v, const TreeBest& best, con
     kap0d[v] = kmin;
 }
 
+__device__ __forceinline__ void tb_wave_min(TreeBest& best, double& kmin) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        TreeBest y;
+        y.du = __shfl_xor(best.du, o, 64);
+        y.u = __shfl_xor(best.u, o, 64);
+        y.k = __shfl_xor(best.k, o, 64);
+        if (tb_less(y, best)) best = y;
+        const double km = __shfl_xor(kmin, o, 64);
+        kmin = km < kmin ? km : kmin;
+    }
+}
+
 __global__ void __launch_bounds__(kPB)
-prep_tree_kernel(int64_t V, uint32_t nwave, const uint32_t* __restrict__ rowptr,
+prep_tree_kernel(int64_t V, HubSegs hs, const uint32_t* __restrict__ rowptr,
                  const uint32_t* __restrict__ adj, const double* __restrict__ aloss,
                  const double* __restrict__ pot, uint32_t* __restrict__ sptPar,
                  uint32_t* __restrict__ spt, double* __restrict__ sptLoss,
-                 double* __restrict__ kap0d, unsigned long long* __restrict__ pimax) {
+                 double* __restrict__ kap0d, unsigned long long* __restrict__ pimax,
+                 TreeBest* __restrict__ pbest, double* __restrict__ pkmin) {
     const uint32_t lane = threadIdx.x & 63u;
     const int64_t nw = gstride() >> 6;
     const TreeBest none{~0ull, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    // hub rows: a wavefront each
-    for (int64_t v = gtid() >> 6; v < (int64_t)nwave; v += nw) {
+    // hub rows: a wavefront per segment; a row cut in several leaves partials (prep_tree_multi)
+    for (int64_t s = gtid() >> 6; s < (int64_t)hs.nseg; s += nw) {
+        const uint2 sg = hs.seg[s];
+        const uint32_t v = sg.x, r0 = rowptr[v], r1 = rowptr[v + 1];
+        const uint32_t e = min(sg.y + kHubSeg, r1);
         TreeBest best = none;
         double kmin = INFINITY;
         const double dv = pot[v];
-        tree_scan(rowptr, adj, pot, (uint32_t)v, v == 0 ? -INFINITY : dv, lane, 64u, best, kmin);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            TreeBest y;
-            y.du = __shfl_xor(best.du, o, 64);
-            y.u = __shfl_xor(best.u, o, 64);
-            y.k = __shfl_xor(best.k, o, 64);
-            if (tb_less(y, best)) best = y;
-            const double km = __shfl_xor(kmin, o, 64);
-            kmin = km < kmin ? km : kmin;
+        tree_scan(adj, pot, v, v == 0 ? -INFINITY : dv, sg.y + lane, e, 64u, best, kmin);
+        tb_wave_min(best, kmin);
+        if (lane == 0) {
+            if (sg.y == r0 && e == r1) {
+                tree_store(v, best, adj, aloss, sptPar, spt, sptLoss, kmin, kap0d);
+            } else {
+                pbest[s] = best;
+                pkmin[s] = kmin;
+            }
         }
-        if (lane == 0) tree_store((uint32_t)v, best, adj, aloss, sptPar, spt, sptLoss, kmin, kap0d);
     }
     // tail rows: a thread each
     unsigned long long pm = 0;
     for (int64_t v = gtid(); v < V; v += gstride()) {
         const double dv = pot[v];
         if (isfinite(dv)) pm = d2bits(dv) > pm ? d2bits(dv) : pm;
-        if (v < (int64_t)nwave) continue;
+        if (v < (int64_t)hs.rows) continue;
         TreeBest best = none;
         double kmin = INFINITY;
-        tree_scan(rowptr, adj, pot, (uint32_t)v, dv, 0u, 1u, best, kmin);
+        tree_scan(adj, pot, (uint32_t)v, dv, rowptr[v], rowptr[v + 1], 1u, best, kmin);
         tree_store((uint32_t)v, best, adj, aloss, sptPar, spt, sptLoss, kmin, kap0d);
     }
     pm = wave_min_u64(~pm);
     if (lane == 0 && pm != ~0ull) atomicMax(pimax, ~pm);
+}
+
+// the rows cut in several segments: a wavefront each combines its segments' partials
+__global__ void __launch_bounds__(kPB)
+prep_tree_multi_kernel(HubSegs hs, const uint32_t* __restrict__ adj,
+                       const double* __restrict__ aloss, uint32_t* __restrict__ sptPar,
+                       uint32_t* __restrict__ spt, double* __restrict__ sptLoss,
+                       double* __restrict__ kap0d, const TreeBest* __restrict__ pbest,
+                       const double* __restrict__ pkmin) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (int64_t m = gtid() >> 6; m < (int64_t)hs.nmulti; m += gstride() >> 6) {
+        const uint4 mr = hs.multi[m];
+        TreeBest best{~0ull, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        double kmin = INFINITY;
+        for (uint32_t i = lane; i < mr.z; i += 64u) {
+            const TreeBest c = pbest[mr.y + i];
+            if (tb_less(c, best)) best = c;
+            const double km = pkmin[mr.y + i];
+            kmin = km < kmin ? km : kmin;
+        }
+        tb_wave_min(best, kmin);
+        if (lane == 0) tree_store(mr.x, best, adj, aloss, sptPar, spt, sptLoss, kmin, kap0d);
+    }
 }
 
 // the records' 32-bit field: {f16 pi(col) rounded up, f16 kappa0(col) rounded down} (or the f32 pi
@@ -408,7 +445,7 @@ __global__ void prep_recfield_kernel(int64_t nadj, uint32_t* __restrict__ adj,
 // 7. kappa-sorted relaxation copy
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(kPB)
-kap_key_kernel(int64_t V, uint32_t nwave, const uint32_t* __restrict__ rowptr,
+kap_key_kernel(int64_t V, HubSegs hs, const uint32_t* __restrict__ rowptr,
                const uint32_t* __restrict__ adj, const double* __restrict__ pot,
                unsigned long long* __restrict__ key, uint32_t* __restrict__ idx) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -419,9 +456,12 @@ kap_key_kernel(int64_t V, uint32_t nwave, const uint32_t* __restrict__ rowptr,
         key[k] = ((unsigned long long)v << 32) | f32_order(f32_dn(kd));
         idx[k] = k;
     };
-    for (int64_t v = gtid() >> 6; v < (int64_t)nwave; v += nw)
-        for (uint32_t k = rowptr[v] + lane; k < rowptr[v + 1]; k += 64u) one((uint32_t)v, k);
-    for (int64_t v = (int64_t)nwave + gtid(); v < V; v += gstride())
+    for (int64_t s = gtid() >> 6; s < (int64_t)hs.nseg; s += nw) {
+        const uint2 sg = hs.seg[s];
+        const uint32_t e = min(sg.y + kHubSeg, rowptr[sg.x + 1]);
+        for (uint32_t k = sg.y + lane; k < e; k += 64u) one(sg.x, k);
+    }
+    for (int64_t v = (int64_t)hs.rows + gtid(); v < V; v += gstride())
         for (uint32_t k = rowptr[v]; k < rowptr[v + 1]; k++) one((uint32_t)v, k);
 }
 
@@ -677,19 +717,43 @@ hipError_t prep_h0_distances(int64_t V, const uint32_t* rowptr, const uint32_t* 
     return hipSuccess;
 }
 
-hipError_t prep_tree(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* rowptr,
+void hub_segments(const uint32_t* rowptr_head, uint32_t rows, std::vector<uint2>& seg,
+                  std::vector<uint4>& multi) {
+    seg.clear();
+    multi.clear();
+    for (uint32_t v = 0; v < rows; v++) {
+        const uint32_t r0 = rowptr_head[v], r1 = rowptr_head[v + 1];
+        const uint32_t first = (uint32_t)seg.size();
+        uint32_t b = r0;
+        do {
+            seg.push_back(make_uint2(v, b));
+            b += kHubSeg;
+        } while (b < r1);
+        const uint32_t n = (uint32_t)seg.size() - first;
+        if (n > 1) multi.push_back(make_uint4(v, first, n, 0u));
+    }
+}
+
+hipError_t prep_tree(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t* rowptr,
                      uint32_t* adj, const double* aloss, const double* pot, uint32_t* sptPar,
                      uint32_t* spt, double* sptLoss, double* piMax, hipStream_t st) {
-    Tmp<double> kap0d;
+    Tmp<double> kap0d, pkmin;
     Tmp<unsigned long long> pm;
+    Tmp<TreeBest> pbest;
     PCHK(kap0d.alloc(V));
     PCHK(pm.alloc(1));
+    PCHK(pbest.alloc(std::max<uint32_t>(1, hs.nseg)));
+    PCHK(pkmin.alloc(std::max<uint32_t>(1, hs.nseg)));
     PCHK(hipMemsetAsync(pm.p, 0, 8, st));
-    nwave = (uint32_t)std::min<int64_t>(nwave, V);
-    const unsigned g = std::max(grid_for(V), (unsigned)std::min<int64_t>((nwave + 3) / 4, 256 * 64));
-    hipLaunchKernelGGL(prep_tree_kernel, dim3(g), dim3(kPB), 0, st, V, nwave, rowptr, adj, aloss,
-                       pot, sptPar, spt, sptLoss, kap0d.p, pm.p);
+    const unsigned g = std::max(grid_for(V), (unsigned)std::min<int64_t>((hs.nseg + 3) / 4, 256 * 64));
+    hipLaunchKernelGGL(prep_tree_kernel, dim3(g), dim3(kPB), 0, st, V, hs, rowptr, adj, aloss,
+                       pot, sptPar, spt, sptLoss, kap0d.p, pm.p, pbest.p, pkmin.p);
     PCHK(hipGetLastError());
+    if (hs.nmulti > 0) {
+        hipLaunchKernelGGL(prep_tree_multi_kernel, dim3((hs.nmulti + 3) / 4), dim3(kPB), 0, st, hs,
+                           adj, aloss, sptPar, spt, sptLoss, kap0d.p, pbest.p, pkmin.p);
+        PCHK(hipGetLastError());
+    }
     if (nadj > 0)
         hipLaunchKernelGGL(prep_recfield_kernel, dim3(grid_for(nadj)), dim3(kPB), 0, st, nadj, adj,
                            pot, kap0d.p);
@@ -703,7 +767,7 @@ hipError_t prep_tree(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* ro
     return hipSuccess;
 }
 
-hipError_t launch_kappa_copy(int64_t V, int64_t nadj, uint32_t nwave, const uint32_t* rowptr,
+hipError_t launch_kappa_copy(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t* rowptr,
                              const uint32_t* adj, const double* pot, const uint32_t* sptPar,
                              uint32_t* adjk, float* kap, float* ksum, float* kap0,
                              hipStream_t st) {
@@ -715,9 +779,8 @@ hipError_t launch_kappa_copy(int64_t V, int64_t nadj, uint32_t nwave, const uint
     PCHK(k1.alloc(nadj));
     PCHK(i0.alloc(nadj));
     PCHK(i1.alloc(nadj));
-    nwave = (uint32_t)std::min<int64_t>(nwave, V);
-    const unsigned g = std::max(grid_for(V), (unsigned)std::min<int64_t>((nwave + 3) / 4, 256 * 64));
-    hipLaunchKernelGGL(kap_key_kernel, dim3(g), dim3(kPB), 0, st, V, nwave, rowptr, adj, pot, k0.p,
+    const unsigned g = std::max(grid_for(V), (unsigned)std::min<int64_t>((hs.nseg + 3) / 4, 256 * 64));
+    hipLaunchKernelGGL(kap_key_kernel, dim3(g), dim3(kPB), 0, st, V, hs, rowptr, adj, pot, k0.p,
                        i0.p);
     PCHK(hipGetLastError());
     const int endbit = 32 + bitlen((uint64_t)V);

@@ -1649,20 +1649,26 @@ __device__ __forceinline__ double kfix_term(const uint32_t* adj, const double* p
     return t;
 }
 
-// A wavefront per hub row (ids < nwave: the long rows of the degree order), a thread per tail row
-// (a wavefront per row left 54 of 64 lanes idle on the C4 tail: 6.2 ms per step).
+// A wavefront per segment of a hub row (ids < hs.rows: the long rows of the degree order; a row cut
+// in several segments leaves per-segment minima for kfix_multi_kernel), a thread per tail row (a
+// wavefront per row left 54 of 64 lanes idle on the C4 tail: 6.2 ms per step; a wavefront per
+// whole hub row left the top hub's 250 k entries on one wavefront: 4.4 ms per step).
 __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
                                  const uint32_t* __restrict__ adj, const double* __restrict__ pot,
                                  const uint32_t* __restrict__ tbits,
                                  const double* __restrict__ Kin, double* __restrict__ Kout,
-                                 int64_t V, uint32_t nwave, unsigned int* __restrict__ changed) {
+                                 int64_t V, HubSegs hs, double* __restrict__ part,
+                                 unsigned int* __restrict__ changed) {
     const uint32_t lane = threadIdx.x & 63u;
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t gs = (int64_t)gridDim.x * blockDim.x;
     bool ch = false;
-    for (int64_t x = gt >> 6; x < (int64_t)nwave; x += gs >> 6) {
+    for (int64_t s = gt >> 6; s < (int64_t)hs.nseg; s += gs >> 6) {
+        const uint2 sg = hs.seg[s];
+        const uint32_t x = sg.x, r0 = rowptr[x], r1 = rowptr[x + 1];
+        const uint32_t e = min(sg.y + kHubSeg, r1);
         double m = INFINITY;
-        for (uint32_t k = rowptr[x] + lane; k < rowptr[x + 1]; k += 64u) {
+        for (uint32_t k = sg.y + lane; k < e; k += 64u) {
             const double t = kfix_term(adj, pot, tbits, Kin, k);
             m = t < m ? t : m;
         }
@@ -1672,11 +1678,15 @@ __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
             m = y < m ? y : m;
         }
         if (lane == 0) {
-            ch |= Kin && !(m == Kin[x]);
-            Kout[x] = m;
+            if (sg.y == r0 && e == r1) {
+                ch |= Kin && !(m == Kin[x]);
+                Kout[x] = m;
+            } else {
+                part[s] = m;
+            }
         }
     }
-    for (int64_t x = (int64_t)nwave + gt; x < V; x += gs) {
+    for (int64_t x = (int64_t)hs.rows + gt; x < V; x += gs) {
         double m = INFINITY;
         for (uint32_t k = rowptr[x]; k < rowptr[x + 1]; k++) {
             const double t = kfix_term(adj, pot, tbits, Kin, k);
@@ -1686,6 +1696,34 @@ __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
         Kout[x] = m;
     }
     if (__ballot(ch) && lane == 0) atomicOr(changed, 1u);  // one atomic per wave
+}
+
+// the hub rows cut in several segments: a wavefront each takes the minimum of its partials
+__global__ void kfix_multi_kernel(const double* __restrict__ Kin, double* __restrict__ Kout,
+                                  HubSegs hs, const double* __restrict__ part,
+                                  unsigned int* __restrict__ changed) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    bool ch = false;
+    for (int64_t i = gt >> 6; i < (int64_t)hs.nmulti; i += gs >> 6) {
+        const uint4 mr = hs.multi[i];
+        double m = INFINITY;
+        for (uint32_t k = lane; k < mr.z; k += 64u) {
+            const double t = part[mr.y + k];
+            m = t < m ? t : m;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double y = __shfl_xor(m, o, 64);
+            m = y < m ? y : m;
+        }
+        if (lane == 0) {
+            ch |= Kin && !(m == Kin[mr.x]);
+            Kout[mr.x] = m;
+        }
+    }
+    if (__ballot(ch) && lane == 0) atomicOr(changed, 1u);
 }
 
 // largest half <= x (NaN: -inf)
@@ -1715,12 +1753,15 @@ __global__ void kfix_store_kernel(uint32_t* __restrict__ adjk, int64_t nadj,
 
 hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const double* pot,
                             const uint32_t* tbits, const double* Kin, double* Kout, int64_t V,
-                            uint32_t nwave, unsigned int* changed, hipStream_t stream) {
+                            const HubSegs& hs, double* part, unsigned int* changed,
+                            hipStream_t stream) {
     if (V <= 0) return hipSuccess;
-    nwave = (uint32_t)std::min<int64_t>(nwave, V);
-    const int64_t g = std::min<int64_t>(std::max<int64_t>((V + 255) / 256, (nwave + 3) / 4), 256 * 32);
+    const int64_t g = std::min<int64_t>(std::max<int64_t>((V + 255) / 256, (hs.nseg + 3) / 4), 256 * 32);
     hipLaunchKernelGGL(kfix_step_kernel, dim3((unsigned)g), dim3(256), 0, stream, rowptr, adj,
-                       pot, tbits, Kin, Kout, V, nwave, changed);
+                       pot, tbits, Kin, Kout, V, hs, part, changed);
+    if (hs.nmulti > 0)
+        hipLaunchKernelGGL(kfix_multi_kernel, dim3((hs.nmulti + 3) / 4), dim3(256), 0, stream, Kin,
+                           Kout, hs, part, changed);
     return hipGetLastError();
 }
 

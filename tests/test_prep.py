@@ -6,6 +6,8 @@ fixpoint) and the h0 tree (argmin (d(u), u) over tight edges with d(u) < d(v)).
 These arrays only shape performance -- every table is checked against the oracle elsewhere -- but
 the relabel, rows and pi must be exactly what DESIGN.md describes for the kernels' bounds to hold.
 """
+import time
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -73,3 +75,25 @@ def test_gpu_prep_matches_restatement(n_routers, n_poi, n_edges):
     assert want[0] == 0xFFFFFFFF and np.count_nonzero(want == 0xFFFFFFFF) == 1
     st = top.stats()
     assert st["csr_h0_rounds"] > 0
+
+
+def test_attach_time_preparation_matches_build_time():
+    """Option prepare_on_attach (default on): device init + graph preparation start in a
+    background thread at the first attach and the first build waits for it under the build lock.
+    The table must be bit-identical to a build that prepares everything itself, and only the
+    former reports a background preparation."""
+    tables = []
+    for on in (1, 0):
+        top = sa.Topology.synthetic(seed=43, n_routers=40000, n_poi=400, n_edges=250000)
+        top.set_option("prepare_on_attach", on)
+        top.synth_packets(5, 2000, 10, 10**9, 10**7)
+        time.sleep(3.0)  # let the background preparation win the build lock (it takes ~0.2 s)
+        A, lat, rel, hops = top.table()
+        st = top.stats()
+        if on:
+            assert st["attach_prep_ms"] > 0.0 and st["csr_ms"] == 0.0
+        else:
+            assert st["attach_prep_ms"] == 0.0 and st["csr_ms"] > 0.0
+        tables.append((np.asarray(A), lat.view(np.uint64), rel.view(np.uint64), hops))
+    for x, y in zip(*tables):
+        assert np.array_equal(x, y)
