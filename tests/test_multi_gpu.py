@@ -91,6 +91,7 @@ def test_multi_device_build_prepares_the_graph_once(devices):
     next build, and the peers' tables equal the owner's (checked against the oracle above)."""
     top, g = synthetic_pair(seed=37, n_routers=2500, n_poi=120, n_edges=25000)
     top.set_option("devices", devices)
+    top.set_option("prepare_on_attach", 0)  # the build itself prepares the graph (counted below)
     otop, ips, verts = attach_hosts(top, g, 200, type_hints=["client", "relay"])
     top.build()
     st = top.stats()
