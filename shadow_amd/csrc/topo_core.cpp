@@ -1634,18 +1634,32 @@ int build_multi(Topology* top) {
             if (r) return r;
             (void)default_delta(top);  // the mean latency, once (peers copy it)
         }
+        // the peers in parallel: a device's first stream costs ~80 ms of HIP queue setup
+        std::vector<int> prc((size_t)N, 0);
+        std::vector<uint8_t> pdid((size_t)N, 0);
+        std::vector<std::thread> pth;
+        for (int d = 1; d < N; d++)
+            pth.emplace_back([&, d]() {
+                auto one = [&]() -> int {
+                    Topology* T = slot_engine(top, d);
+                    reset_build_stats(T);
+                    HIPCHK(hipSetDevice(phys[(size_t)d]));
+                    int rr = dev_init(T);
+                    if (rr) return rr;
+                    T->meanLat = top->meanLat;
+                    if (!top->isComplete && !T->csrUploaded) {
+                        rr = copy_csr_from(T, phys[(size_t)d], top, phys[0]);
+                        if (rr) return rr;
+                        pdid[(size_t)d] = 1;
+                    }
+                    return 0;
+                };
+                prc[(size_t)d] = one();
+            });
+        for (auto& x : pth) x.join();
         for (int d = 1; d < N; d++) {
-            Topology* T = slot_engine(top, d);
-            reset_build_stats(T);
-            HIPCHK(hipSetDevice(phys[(size_t)d]));
-            r = dev_init(T);
-            if (r) return r;
-            T->meanLat = top->meanLat;
-            if (!top->isComplete && !T->csrUploaded) {
-                r = copy_csr_from(T, phys[(size_t)d], top, phys[0]);
-                if (r) return r;
-                did = true;
-            }
+            if (prc[(size_t)d]) return prc[(size_t)d];
+            did = did || pdid[(size_t)d];
         }
         HIPCHK(hipSetDevice(phys[0]));
         if (did)  // preparation + the peers' copies

@@ -151,7 +151,11 @@ __shared__ uint32_t rp_sv[kRpT];
 // The heap of one source: keys (igraph's data = -dist) and vertices, positions < kRpT in LDS,
 // the rest as 16-B nodes {f64 key, u32 vertex, pad} in this slot's HBM (one line per node
 // access); the position of a queued vertex lives in its 16-B vertex record
-// {f64 dist, u32 parent slot, u32 heap position} (one line per relaxation target).
+// {f64 dist, u32 parent slot, u32 heap position} (one line per relaxation target).  For a vertex
+// in the LDS levels the record only says so (some position < kRpT): moves inside the LDS levels
+// (half of every sink path) store no position -- each would be a 4-B write to a random line --
+// and a modify of such a vertex finds it by a wave-wide search of the LDS vertex array
+// (rp_lds_find).
 struct RpHeap {
     uint4* gn;
     uint4* vr;
@@ -167,9 +171,11 @@ struct RpHeap {
             v = q.z;
         }
     }
-    __device__ __forceinline__ void put(uint32_t p, double k, uint32_t v, int cat) const {
+    // node (k, v) to position p; its vertex record's position is stored only when `pos` (the
+    // element crossed into or out of the LDS levels, moved inside the HBM levels, or is new)
+    __device__ __forceinline__ void put(uint32_t p, double k, uint32_t v, int cat, bool pos = true) const {
         rp_lines(nl, cat, p >= kRpT, gn + p);
-        rp_lines(nl, cat, true, vr + 4 * (size_t)__lane_id() + v);  // random: one line each
+        rp_lines(nl, cat, pos, vr + 4 * (size_t)__lane_id() + v);  // random: one line each
         if (p < kRpT) {
             rp_sk[p] = k;
             rp_sv[p] = v;
@@ -177,7 +183,7 @@ struct RpHeap {
             const unsigned long long b = d2bits(k);
             gn[p] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), v, 0u);
         }
-        reinterpret_cast<uint32_t*>(vr + v)[3] = p;
+        if (pos) reinterpret_cast<uint32_t*>(vr + v)[3] = p;
     }
 };
 
@@ -186,6 +192,23 @@ __device__ __forceinline__ uint32_t rp_sub_pos(uint32_t head, int lane) {
     const uint32_t rr = (uint32_t)lane + 2u;  // BFS index + 1 of this lane's subtree node
     const int dl = 31 - __clz(rr);            // its depth below the hole (1..kRpLA)
     return ((head + 1u) << dl) - 1u + (rr - (1u << dl));
+}
+
+// Position of vertex t among the heap's LDS levels (positions < min(size, kRpT)): every lane
+// checks its share of the LDS vertex array, one ballot.  ~0u: not there (cannot happen for a
+// vertex whose record says it is).
+__device__ __forceinline__ uint32_t rp_lds_find(uint32_t t, uint32_t size, int lane) {
+    const uint32_t n = size < kRpT ? size : kRpT;
+    uint32_t found = 0xFFFFFFFFu;
+    for (uint32_t b = 0; b < n; b += 64u) {
+        const uint32_t p = b + (uint32_t)lane;
+        const unsigned long long m = __ballot(p < n && rp_sv[p] == t);
+        if (m) {
+            found = b + (uint32_t)(__ffsll((long long)m) - 1);
+            break;
+        }
+    }
+    return found;
 }
 
 // igraph_2wheap_sink of element (xk, xv) from position `head` (a hole) in a heap of `size`.
@@ -382,8 +405,11 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
     }
     RP_STICK(1);
     const uint32_t up = __shfl_up(pp, 1);  // the parent's position (path node lane - 1)
-    if (lane < stop) H.put(lane == 0 ? 0u : up, pk, pv, RPL_SINK_ST);
-    if (lane == 0) H.put(stop == 0 ? 0u : rl_u32(pp, stop - 1), xk, xv, RPL_SINK_ST);
+    if (lane < stop) H.put(lane == 0 ? 0u : up, pk, pv, RPL_SINK_ST, pp >= kRpT);
+    if (lane == 0) {
+        const uint32_t xp = stop == 0 ? 0u : rl_u32(pp, stop - 1);
+        H.put(xp, xk, xv, RPL_SINK_ST, xp >= kRpT || size >= kRpT);  // x came from position size
+    }
     RP_STICK(2);
 }
 
@@ -392,14 +418,14 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
 // Most shift-ups stop below the parent: it is read first (one node), the whole chain only when x
 // rises past it.  check = false: the caller knows x rises past the parent.
 __device__ __forceinline__ int rp_shift_up(const RpHeap& H, uint32_t pos, double xk, uint32_t xv,
-                                           int lane, uint32_t& mv, uint32_t& mp,
+                                           int lane, uint32_t& mv, uint32_t& mp, bool fresh,
                                            bool check = true) {
     if (SHD_RP_PROG && check && pos > 0) {
         double k0;
         uint32_t v0;
         H.node((pos - 1u) >> 1, k0, v0, RPL_SHIFT_LD);
-        if (xk < uni_f64(k0)) {  // data[x] < data[parent]: stays
-            if (lane == 0) H.put(pos, xk, xv, RPL_SHIFT_ST);
+        if (xk < uni_f64(k0)) {  // data[x] < data[parent]: stays (a pushed vertex is new)
+            if (lane == 0) H.put(pos, xk, xv, RPL_SHIFT_ST, fresh);
             return 0;
         }
     }
@@ -414,9 +440,9 @@ __device__ __forceinline__ int rp_shift_up(const RpHeap& H, uint32_t pos, double
     const unsigned long long stopm = __ballot(valid && xk < ak);
     const int f = stopm ? __ffsll((long long)stopm) - 1 : (int)depth;
     const uint32_t c = lane == 0 ? pos : (valid ? ((pos + 1u) >> (uint32_t)lane) - 1u : 0u);
-    if (lane < f) H.put(c, ak, av, RPL_SHIFT_ST);
+    if (lane < f) H.put(c, ak, av, RPL_SHIFT_ST, c >= kRpT);  // ancestors move down to c
     const uint32_t fp = f == 0 ? pos : ((pos + 1u) >> (uint32_t)f) - 1u;
-    if (lane == 0) H.put(fp, xk, xv, RPL_SHIFT_ST);
+    if (lane == 0) H.put(fp, xk, xv, RPL_SHIFT_ST, fresh || (f > 0 && (fp >= kRpT || pos >= kRpT)));
     mv = av;
     mp = c;
     return f;
@@ -570,11 +596,14 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                 double pk = INFINITY;
                 if (first) ppos = size + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
                 else if (impr) ppos = mypos;
-                if ((first || impr) && ppos > 0) {
+                // a vertex in the LDS levels: its record's position is only a marker (found by
+                // rp_lds_find at its operation, its parent read then)
+                bool stale = impr && mypos < kRpT;
+                if ((first || impr) && ppos > 0 && !stale) {
                     uint32_t pv;
                     H.node((ppos - 1u) >> 1, pk, pv, RPL_SHIFT_LD);
                 }
-                bool stale = false, dirty = false;
+                bool dirty = false;
                 while (m) {
                     const int l = __ffsll((long long)m) - 1;
                     m &= m - 1ull;
@@ -591,19 +620,21 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                         n_push++;
                     } else {  // igraph_2wheap_modify (its sink is a no-op for a larger key)
                         pos = rl_u32(mypos, l);
+                        if (pos < kRpT) pos = rp_lds_find(tv, size, lane);
                         n_mod++;
                     }
+                    const bool fresh = (fm >> l) & 1ull;
                     uint32_t mv = 0, mp = 0;
                     int f;
                     if (SHD_RP_PROG && !dirty && pos > 0 && !__shfl(stale, l)) {
                         if (xkey < rl_f64(pk, l)) {  // stays: data[x] < data[parent]
-                            if (lane == 0) H.put(pos, xkey, tv, RPL_SHIFT_ST);
+                            if (lane == 0) H.put(pos, xkey, tv, RPL_SHIFT_ST, fresh);
                             f = 0;
                         } else {
-                            f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp, false);
+                            f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp, fresh, false);
                         }
                     } else {
-                        f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp);
+                        f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp, fresh);
                     }
                     if (f > 0) dirty = true;
                     else if (ppos > 0 && ((ppos - 1u) >> 1) == pos) stale = true;
