@@ -17,7 +17,7 @@ os.makedirs(outdir, exist_ok=True)
 
 
 def short(name):
-    n = name.split("(")[0].replace("shdtopo::", "")
+    n = name.replace("(anonymous namespace)::", "").split("(")[0].replace("shdtopo::", "")
     if n.startswith("void "):
         n = n[5:]
     return n.split("(")[0]
