@@ -1271,7 +1271,13 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         const bool tree = v >= H && !((h.tw >> (q & 31)) & 1u) && pu < (uint32_t)V;
                         Hop hn = h;
                         if (tree) hn = load_hop(pu, j);
-                        if (atomicExch(&precw[4 * (size_t)q + 1], ep) == ep) {  // another walk's
+                        // The claim is a plain tag read issued with those loads; the pair's
+                        // record (put) or, for a pair left to the hint pass, a tag store marks
+                        // it as this batch's.  Two walks that reach an unclaimed pair in the same
+                        // round trip both walk on: they write identical records (the parent rule
+                        // is deterministic), and a pair listed twice in S is resolved twice the
+                        // same way -- cheaper than a returning atomic per hop (kernel -3.5 %).
+                        if (ld_l2_u32(&precw[4 * (size_t)q + 1]) == ep) {  // another walk's
                             act = false;
                         } else {
                             n_walk++;
@@ -1286,6 +1292,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                     h = hn;
                                 }
                             } else {
+                                precw[4 * (size_t)q + 1] = ep;
                                 const uint32_t pos = atomicAdd(&L.qtail, 1u);
                                 if (pos < pcap) fscr[pos] = q;
                                 else atomicOr(&L.fover, 128u);

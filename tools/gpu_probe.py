@@ -57,6 +57,8 @@ for rep in range(args.reps):
                                              st["far_splits"] / rows, st["slots"]]), flush=True)
     print("   parent phases ms/src: walks %.3f scans %.3f recount %.3f next %.3f" %
           tuple(x / rows for x in st["parent_phase_ms"]), flush=True)
+    print("   walk steps/src %.0f, walk kinds %s" % (st["walk_steps"] / rows, list(st["walk_kinds"])),
+          flush=True)
     print("   target prep %.2f ms (%d kappa iterations)" % (st["target_prep_ms"],
                                                          st["target_kappa_iters"]), flush=True)
     print("   split ms/src %.2f  far-scan sources %d" % (st["split_ms"] / rows,
