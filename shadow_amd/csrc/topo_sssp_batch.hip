@@ -843,35 +843,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // no landmark bound until h0 is reached (the sweeps test kappa0 against L.dh0)
         if (tid < (uint32_t)K) L.dh0[tid] = INFINITY;
         if (tid == 0) L.invd = B.inv_delta;
-        {
-            // the distance lines the previous batch of this slot lowered from +inf back to +inf:
-            // only touched tail vertices (their bit in D.touch), not the whole [V][K] block
-            // (64 MB at K = 8 per batch)
-            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-            u64x2* d2 = reinterpret_cast<u64x2*>(D.dist);
-            const u64x2 inf2 = {kInfBits, kInfBits};
-            unsigned long long nt = 0;
-            for (uint32_t wi = H / 32 + tid; wi < pw; wi += kSsspBlock) {
-                uint32_t w = ld_l2_u32(&D.touch[wi]);
-                if (!w) continue;
-                D.touch[wi] = 0u;
-                nt += (unsigned long long)__popc(w);
-                while (w) {
-                    const uint32_t v = wi * 32u + (uint32_t)__ffs(w) - 1u;
-                    w &= w - 1u;
-#pragma unroll
-                    for (int h = 0; h < K / 2; h++) {
-                        if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + (size_t)v * (K / 2) + h);
-                        else d2[(size_t)v * (K / 2) + h] = inf2;
-                    }
-                    // the vertex's K tie bits (whole bytes for K >= 8)
-                    if (K == 8) reinterpret_cast<uint8_t*>(D.tie)[v] = 0u;
-                    else if (K == 16) reinterpret_cast<uint16_t*>(D.tie)[v] = 0u;
-                }
-            }
-            nt = wave_sum_u64(nt);
-            if ((tid & 63) == 0 && nt) atomicAdd(&L.touched, nt);
-        }
         if (tid == 0) {
             L.fminb = kNoBucket;
             L.fover = 0;
@@ -1567,6 +1538,38 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         }
         __syncthreads();
         { unsigned long long t = wall_clock64(); t_tgt += t - tk; tk = t; }
+        {
+            // the distance lines this batch lowered from +inf back to +inf: only touched tail
+            // vertices (their bit in D.touch), not the whole [V][K] block (64 MB at K = 8 per
+            // batch).  Done at the batch's end (its time counts as setup): the next batch's
+            // setup waits for these stores; a one-round shard no longer has every slot resetting
+            // at its kernel's start.
+            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+            u64x2* d2 = reinterpret_cast<u64x2*>(D.dist);
+            const u64x2 inf2 = {kInfBits, kInfBits};
+            unsigned long long nt = 0;
+            for (uint32_t wi = H / 32 + tid; wi < pw; wi += kSsspBlock) {
+                uint32_t w = ld_l2_u32(&D.touch[wi]);
+                if (!w) continue;
+                D.touch[wi] = 0u;
+                nt += (unsigned long long)__popc(w);
+                while (w) {
+                    const uint32_t v = wi * 32u + (uint32_t)__ffs(w) - 1u;
+                    w &= w - 1u;
+#pragma unroll
+                    for (int h = 0; h < K / 2; h++) {
+                        if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + (size_t)v * (K / 2) + h);
+                        else d2[(size_t)v * (K / 2) + h] = inf2;
+                    }
+                    // the vertex's K tie bits (whole bytes for K >= 8)
+                    if (K == 8) reinterpret_cast<uint8_t*>(D.tie)[v] = 0u;
+                    else if (K == 16) reinterpret_cast<uint16_t*>(D.tie)[v] = 0u;
+                }
+            }
+            nt = wave_sum_u64(nt);
+            if ((tid & 63) == 0 && nt) atomicAdd(&L.touched, nt);
+        }
+        { unsigned long long t = wall_clock64(); t_init += t - tk; tk = t; }
         if (ws.btrace && tid == 0) {
             unsigned long long* b = ws.btrace + 8 * (size_t)bidx;
             b[1] = tk;
