@@ -264,6 +264,7 @@ struct _Topology {
     DevBuf<uint2> d_hseg;
     DevBuf<uint4> d_hmulti;
     uint32_t hsegRows = 0, hsegN = 0, hmultiN = 0;
+    int slotsUsed = 0;  // workgroups of the last batched launch (<= slots)
     DevBuf<unsigned int> d_kfChanged;
     DevBuf<uint32_t> d_rowmap, d_bsrc;  // batch order: output row and source of each position
     // cache of the last batch order (enqueue_rows): the rows' sources, batch fill and options
@@ -1150,6 +1151,9 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     if (rows <= (int64_t)K * S) kf = (int)std::min<int64_t>(K, (rows + S - 1) / S);
                 }
                 top->stats.batch_fill = kf;
+                // workgroups the launch uses: the batches, at most the workspace's slots (it
+                // may hold more: sized for a full table by the attach-time preparation)
+                top->slotsUsed = (int)std::min<int64_t>(ws.slots, (rows + kf - 1) / kf);
                 const double delta = default_delta(top);
                 // the order, the row map and the bucket shifts depend only on the sources, the
                 // batch fill and the options: a rebuild of the same rows reuses them
@@ -1384,7 +1388,7 @@ int collect_row_stats(Topology* top) {
     top->stats.near_iterations = (int64_t)h[ST_NEAR_IT];
     top->stats.far_splits = (int64_t)h[ST_SPLITS];
     for (int i = 0; i < 8; i++) top->stats.events[i] = (int64_t)h[ST_EV0 + i];
-    top->stats.slots = top->isComplete ? 0 : top->slots;
+    top->stats.slots = top->isComplete ? 0 : (top->slotsUsed > 0 ? top->slotsUsed : top->slots);
     double gm;
     memcpy(&gm, &h[ST_GLOBAL_MIN], sizeof gm);
     top->eagerMin = std::isinf(gm) ? -1.0 : gm;
@@ -2115,6 +2119,8 @@ void host_off(Topology* top, int32_t v) {
 }
 
 // shd-topology.c:1154-1166: g_hash_table_replace(virtualIP, ip, vertex)
+int ensure_workspace(Topology* top, int nsrc);
+
 // The attach-time preparation (Topology::prepOnAttach): device init + graph preparation in a
 // background thread holding buildMu; a build (or any other buildMu holder) that comes first does
 // the work itself and the thread then finds nothing left to do.  Complete and directed topologies
@@ -2132,6 +2138,9 @@ void start_attach_prep(Topology* top) {
         }
         int r = dev_init(top);
         if (!r) r = upload_csr(top);
+        // the batched SSSP's workspace too, sized for a full table (a build with fewer sources
+        // uses a part of it; a different batch width re-allocates)
+        if (!r) r = ensure_workspace(top, 1 << 30);
         if (!r) r = hipStreamSynchronize(top->stream) == hipSuccess ? 0 : -1;
         top->prepBgRc = r;
         top->prepBgMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
