@@ -553,7 +553,8 @@ def main():
             # by heap_replay_kernel (its time is inside ms_per_step and stated separately here)
             "replay": dict(rows=st["replay_rows"], ms=round(r_ms, 3),
                            pops=st["replay_pops"], pushes=st["replay_pushes"],
-                           modifies=st["replay_modifies"], slots=st["replay_slots"]),
+                           modifies=st["replay_modifies"], slots=st["replay_slots"],
+                           int_keys=st["replay_int_keys"]),
             "slots": st["slots"],
         }
         print(json.dumps(out), flush=True)

@@ -109,7 +109,9 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * kernel with event counters), "tie_replay" (1: rows whose target chains cross a d-tied parent
  * are recomputed by the exact heap replay; 0: reported only), "replay_all" (test hook: every row
  * through the replay), "replay_slots" (concurrent replay wavefronts, 0 = auto), "replay_landmark"
- * (1: the replay skips relaxations into vertices a landmark bound proves popped), "tie_dense"
+ * (1: the replay skips relaxations into vertices a landmark bound proves popped),
+ * "replay_int_keys" (1: u32 heap keys when every latency is an integer and V x max latency
+ * < 2^32 - 1 -- exact; 0: always f64 keys), "tie_dense"
  * (-1 auto / 0 / 1: every row through the replay, no batch kernel, once a build replayed >= 90 %
  * of its rows), "devices" (N:
  * the table is built by N GPUs of this process -- rows sharded, RCCL all-gather of the rows and
@@ -296,6 +298,8 @@ typedef struct {
                                    "prepare_on_attach": device init + graph preparation in a
                                    background thread from the first attach on, overlapping the
                                    host's attach phase; 0 if it did not run) */
+    int64_t replay_int_keys;    /* 1: the last replay ran on u32 heap keys (every latency an
+                                   integer, V x max latency < 2^32 - 1: exact), 0: f64 keys */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

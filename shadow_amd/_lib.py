@@ -50,7 +50,7 @@ class ShdStats(ctypes.Structure):
                 ("workspace_ms", dbl), ("csr_step_ms", dbl * 8), ("module_load_ms", dbl),
                 ("build_wall_ms", dbl), ("walk_steps", i64), ("build_step_ms", dbl * 8),
                 ("exchange_kind", i64), ("walk_kinds", i64 * 4),
-                ("build_wait_ms", dbl), ("attach_prep_ms", dbl)]
+                ("build_wait_ms", dbl), ("attach_prep_ms", dbl), ("replay_int_keys", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):

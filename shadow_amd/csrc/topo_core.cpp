@@ -237,6 +237,8 @@ struct _Topology {
     int replaySlotsOpt = 0;   // option "replay_slots" (0 = sized from the CUs and free HBM)
     bool replayLandmark = true;  // option "replay_landmark": skip edges into vertices the
                                  // landmark bound proves popped (topo_replay.hip)
+    bool replayIntOpt = true;    // option "replay_int_keys": u32 heap keys when replayIntOk
+    bool replayIntOk = false;    // every latency an integer and V x max < 2^32 - 1 (upload_replay)
     int sourceOrder = 2;      // option "source_order": batch kernel source grouping (0 = row
                               // order, 1 = by the hub their h0-tree path enters the core, then
                               // pi, 2 = preorder of the h0 shortest-path tree)
@@ -861,6 +863,20 @@ int upload_replay_impl(Topology* top) {
     const int64_t V = g.V, E = g.E;
     const bool dir = top->isDirected;
     const size_t cap = std::max<size_t>(1, (size_t)(dir ? E : 2 * E));
+    // u32 heap keys are exact when every relaxed latency (self loops never relax) is a
+    // non-negative integer and no tentative distance du + w <= V x max reaches 2^32 - 1 (the
+    // unreached marker): then every f64 sum the reference forms is an exact integer
+    {
+        bool ok = true;
+        double wmax = 0.0;
+        for (int64_t e = 0; e < E && ok; e++) {
+            if (g.eu[(size_t)e] == g.ev[(size_t)e]) continue;
+            const double w = g.elat[(size_t)e];
+            if (!(w >= 0.0) || w != std::floor(w)) ok = false;
+            else wmax = std::max(wmax, w);
+        }
+        top->replayIntOk = ok && (double)V * wmax < 4294967295.0;
+    }
     HIPCHK(top->d_rrow.ensure((size_t)V + 1));
     HIPCHK(top->d_rrec.ensure(cap));
     HIPCHK(top->d_rown.ensure(cap));
@@ -884,6 +900,7 @@ ReplayCSR replay_csr(Topology* top) {
     c.own = top->d_rown.p;
     // pi values exist for undirected topologies (upload_csr: d(h0, .) from relabelled vertex 0)
     c.landmark = (!top->isDirected && top->replayLandmark && top->hp && !top->hp->pot.empty()) ? 0 : -1;
+    c.intKeys = (top->replayIntOpt && top->replayIntOk) ? 1 : 0;
     c.hop = top->d_rhop.p;
     c.vloss = top->d_vloss.p;
     c.selfLat = top->d_selfLat.p;
@@ -903,7 +920,7 @@ int ensure_replay_ws(Topology* top, int nrows) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, top->device));
     // wavefronts per CU: 20, or as many as the CU's LDS holds (each its heap's top levels)
-    const int lds = (replay_lds_bytes() + 255) & ~255;
+    const int lds = (replay_lds_bytes(top->replayIntOpt && top->replayIntOk ? 1 : 0) + 255) & ~255;
     const int per_cu = std::max(1, std::min(20, (int)(prop.sharedMemPerMultiprocessor > 0 ? prop.sharedMemPerMultiprocessor : 163840) / lds));
     int want = top->replaySlotsOpt > 0 ? top->replaySlotsOpt : prop.multiProcessorCount * per_cu;
     size_t freeb = 0, totalb = 0;
@@ -1420,6 +1437,7 @@ int collect_row_stats(Topology* top) {
         top->stats.batch_edges_b = (int64_t)h[ST_BT0 + 7];
     }
     top->stats.replay_slots = top->stats.replay_rows ? std::min(top->rslots, top->rslotsUse) : 0;
+    top->stats.replay_int_keys = top->stats.replay_rows && top->replayIntOpt && top->replayIntOk ? 1 : 0;
     {
         int khz = 0;
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->device) != hipSuccess || khz <= 0)
@@ -1534,6 +1552,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->tieDense = p->tieDense || top->tieDense;
     p->replaySlotsOpt = top->replaySlotsOpt;
     p->replayLandmark = top->replayLandmark;
+    p->replayIntOpt = top->replayIntOpt;
     p->sourceOrder = top->sourceOrder;
     p->batchOrder = top->batchOrder;
     p->batchFill = top->batchFill;
@@ -2273,6 +2292,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "replay_all") top->replayAll = value != 0;
     else if (k == "replay_slots") top->replaySlotsOpt = (int)value;
     else if (k == "replay_landmark") top->replayLandmark = value != 0;
+    else if (k == "replay_int_keys") top->replayIntOpt = value != 0;
     else if (k == "tie_dense") top->tieDenseOpt = value < 0 ? -1 : (value != 0 ? 1 : 0);
     else if (k == "source_order") top->sourceOrder = (int)value;
     else if (k == "batch_order") top->batchOrder = (int)value;

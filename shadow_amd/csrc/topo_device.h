@@ -162,12 +162,16 @@ struct ReplayCSR {
     const uint32_t* tbits = nullptr;  // target (attached vertex) bitmap over V
     int64_t ntargets = 0;             // distinct targets (igraph's to_reach)
     int32_t landmark = -1;            // vertex the rec pi values are measured from (-1: none)
+    // 1: u32 heap keys (every latency an integer, V x max latency < 2^32 - 1: exact, see
+    // topo_replay.hip RpKey); 0: f64 keys
+    int32_t intKeys = 0;
 };
 
 // per-slot workspace of the heap replay (one wavefront = one slot), slot-major [slot][V]:
 // vertex records {f64 dist (-1 = unreached), u32 parent (replay-CSR slot of the parent edge),
 // u32 heap position} and heap nodes {f64 key, u32 vertex, pad} (positions >= the LDS part),
-// 16 B each (one line per access), and a path buffer [kMaxHops][64] per slot.
+// 16 B each (one line per access; u32 keys: {u32 dist, pad, ...} and 8-B nodes {u32 key, u32
+// vertex} in the first half of the node block), and a path buffer [kMaxHops][64] per slot.
 // 32 B x V + 12 KiB per slot.
 struct ReplayWs {
     int slots = 0;
@@ -235,8 +239,8 @@ hipError_t launch_heap_replay(const ReplayCSR& g, const ReplayWs& ws, const uint
                               int full, double2* out_lr, uint16_t* out_hops, double* out_rowmin,
                               unsigned long long* d_stats, double* dbg_dist, int32_t* dbg_par,
                               hipStream_t stream);
-int replay_lds_levels();
-int replay_lds_bytes();  // LDS of one replay wavefront (its heap's top levels)
+int replay_lds_levels(int int_keys);
+int replay_lds_bytes(int int_keys);  // LDS of one replay wavefront (its heap's top levels)
 
 hipError_t launch_pair_table_complete(int A, int64_t row0, int64_t rows, const double* elatAA,
                                       const double* elossAA, const double* vlossA, double2* out_lr,

@@ -57,10 +57,10 @@ namespace {
 using namespace dev;
 
 #ifndef SHD_RP_LDS_LEVELS
-#define SHD_RP_LDS_LEVELS 9
+#define SHD_RP_LDS_LEVELS 9       // f64 keys: 511 x 12 B in LDS per wavefront
 #endif
-#ifndef SHD_RP_PROG
-#define SHD_RP_PROG 1  // shift-up reads the parent first, the whole ancestor chain only if x rises
+#ifndef SHD_RP_LDS_LEVELS_INT
+#define SHD_RP_LDS_LEVELS_INT 9   // u32 keys: 511 x 8 B (10 levels, 8 KiB, lose occupancy: +28 %)
 #endif
 #ifndef SHD_RP_LINES
 #define SHD_RP_LINES 0  // profiling build: count the 64-B lines each part of the replay touches
@@ -79,37 +79,16 @@ using namespace dev;
 #else
 #define RP_STICK(i) do { } while (0)
 #endif
-#ifndef SHD_RP_SINK2
-#define SHD_RP_SINK2 1  // sink: path of larger children first (LDS levels while x is loaded)
-#endif
 #ifndef SHD_RP_PREF
 #define SHD_RP_PREF 1  // the next root's row bounds and target bit loaded right after the sink
 #endif
-#ifndef SHD_RP_LA
-#define SHD_RP_LA 5  // sink lookahead: heap levels loaded per round trip (<= 5: 62 nodes)
-#endif
-constexpr uint32_t kRpT = (1u << SHD_RP_LDS_LEVELS) - 1u;  // heap positions held in LDS
-constexpr int kRpLA = SHD_RP_LA;
-constexpr int kRpLaNodes = (2 << kRpLA) - 2;               // subtree nodes below the hole
-static_assert(kRpLA >= 1 && kRpLaNodes <= 64, "one node per lane");
+constexpr int kRpLA = 5;  // LDS walk of the sink: heap levels per LDS round (62 nodes)
 #ifndef SHD_RP_HL
 #define SHD_RP_HL 5  // levels per HBM round of the path-first sink (6: two nodes per lane)
 #endif
 constexpr int kHL = SHD_RP_HL;
 constexpr int kHNodes = (2 << kHL) - 2;
 static_assert(kHL >= 1 && kHNodes <= 128, "at most two nodes per lane");
-#ifndef SHD_RP_LA_HBM
-#define SHD_RP_LA_HBM SHD_RP_LA  // lookahead of a round whose subtree reaches the HBM levels
-#endif
-constexpr int kRpLaH = SHD_RP_LA_HBM;
-static_assert(kRpLaH >= 1 && kRpLaH <= kRpLA, "HBM lookahead");
-
-// levels loaded by a sink round from `head`: kRpLA while the subtree is in LDS (cheap), kRpLaH
-// once it reaches HBM (a level d below the hole costs 2^d x 16 B of lines; one more round trip
-// against fewer lines)
-__device__ __forceinline__ int rp_la(uint32_t head) {
-    return (((head + 2u) << kRpLA) - 2u) < kRpT ? kRpLA : kRpLaH;
-}
 
 __device__ __forceinline__ uint32_t rl_u32(uint32_t x, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
@@ -123,6 +102,71 @@ __device__ __forceinline__ uint32_t uni_u32(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
 }
 __device__ __forceinline__ double uni_f64(double x) { return rl_f64(x, 0); }
+
+// Heap keys.  igraph's two-way heap holds data = -dist (a max-heap).  Two exact encodings:
+//   * f64 (any latencies): key = -dist, 16-B HBM nodes {f64 key, u32 vertex, pad};
+//   * u32 (option replay_int_keys, when every latency is an integer and V x max latency fits in
+//     u32 -- upload_replay checks it): dist is an integer < 2^32 - 1, every f64 sum the reference
+//     forms is exact, and key = ~dist orders as -dist does (~ reverses the u32 order), so every
+//     comparison -- ties included -- is the f64 one.  8-B nodes {u32 key, u32 vertex}: a sink
+//     round's 62-node subtree is half the lines, and the readlane walks move one word per key.
+// Vertex records stay 16 B {dist, pad | f64 dist, u32 parent slot, u32 heap position}.
+template <bool I> struct RpKey;
+template <> struct RpKey<false> {
+    using T = double;
+    using Node = uint4;
+    static constexpr int kLevels = SHD_RP_LDS_LEVELS;
+    static constexpr unsigned long long kUnreached = 0xBFF0000000000000ull;  // dist = -1.0
+    __device__ static T lo() { return -INFINITY; }
+    __device__ static T hi() { return INFINITY; }
+    __device__ static T rl(T x, int l) { return rl_f64(x, l); }
+    __device__ static T uni(T x) { return uni_f64(x); }
+    __device__ static Node pack(T k, uint32_t v) {
+        const unsigned long long b = d2bits(k);
+        return make_uint4((uint32_t)b, (uint32_t)(b >> 32), v, 0u);
+    }
+    __device__ static void unpack(const Node& q, T& k, uint32_t& v) {
+        k = __hiloint2double((int)q.y, (int)q.x);
+        v = q.z;
+    }
+    __device__ static T dist(const uint4& x) { return __hiloint2double((int)x.y, (int)x.x); }
+    __device__ static bool reached(T d) { return d >= 0.0; }
+    __device__ static T key_of(T d) { return -d; }
+    __device__ static T dist_of_key(T k) { return -k; }
+    __device__ static T src_key() { return 0.0; }
+    __device__ static double f64(T d) { return d; }
+    __device__ static T add(T d, double w) { return __dadd_rn(d, w); }
+    __device__ static uint3 rec(T d, uint32_t j) {
+        const unsigned long long b = d2bits(d);
+        return make_uint3((uint32_t)b, (uint32_t)(b >> 32), j);
+    }
+    __device__ static void set_dist(uint4* r, T d) { *reinterpret_cast<double*>(r) = d; }
+};
+template <> struct RpKey<true> {
+    using T = uint32_t;
+    using Node = uint2;
+    static constexpr int kLevels = SHD_RP_LDS_LEVELS_INT;
+    static constexpr unsigned long long kUnreached = ~0ull;  // dist word = 0xFFFFFFFF
+    __device__ static T lo() { return 0u; }
+    __device__ static T hi() { return 0xFFFFFFFFu; }
+    __device__ static T rl(T x, int l) { return rl_u32(x, l); }
+    __device__ static T uni(T x) { return uni_u32(x); }
+    __device__ static Node pack(T k, uint32_t v) { return make_uint2(k, v); }
+    __device__ static void unpack(const Node& q, T& k, uint32_t& v) {
+        k = q.x;
+        v = q.y;
+    }
+    __device__ static T dist(const uint4& x) { return x.x; }
+    __device__ static bool reached(T d) { return d != 0xFFFFFFFFu; }
+    __device__ static T key_of(T d) { return ~d; }
+    __device__ static T dist_of_key(T k) { return ~k; }
+    __device__ static T src_key() { return ~0u; }
+    __device__ static double f64(T d) { return (double)d; }
+    // w is an integer-valued f64 and du + w < 2^32 - 1 (the host's bound): exact
+    __device__ static T add(T d, double w) { return d + (uint32_t)w; }
+    __device__ static uint3 rec(T d, uint32_t j) { return make_uint3(d, 0xFFFFFFFFu, j); }
+    __device__ static void set_dist(uint4* r, T d) { *reinterpret_cast<uint32_t*>(r) = d; }
+};
 
 // 64-B lines touched by one wave-wide access (active lanes, addresses ascending in lane order
 // for the heap's subtree / chain accesses; a random gather counts one line per lane).
@@ -141,48 +185,69 @@ __device__ __forceinline__ void rp_lines(unsigned long long* nl, int cat, bool a
 #endif
 }
 
-// The heap's top levels (positions < kRpT) of this workgroup's (= wavefront's) source, in LDS.
-// File-scope __shared__: every access is a ds_read/ds_write (a generic pointer let the compiler
-// merge the LDS and HBM branches of a node access into flat loads, which wait on both counters
-// and serialised the sink behind outstanding HBM loads: -4 to -7 %).
-__shared__ double rp_sk[kRpT];
-__shared__ uint32_t rp_sv[kRpT];
+// The heap's top levels (positions < kT) of this workgroup's (= wavefront's) source, in LDS.
+// File-scope __shared__ reached only through these accessors: every access is a ds_read /
+// ds_write (a generic pointer let the compiler merge the LDS and HBM branches of a node access
+// into flat loads, which wait on both counters and serialised the sink behind outstanding HBM
+// loads: -4 to -7 %).  Each kernel instantiation references (and is allocated) one pair.
+constexpr uint32_t kRpTF = (1u << SHD_RP_LDS_LEVELS) - 1u;
+constexpr uint32_t kRpTI = (1u << SHD_RP_LDS_LEVELS_INT) - 1u;
+__shared__ double rp_sk[kRpTF];
+__shared__ uint32_t rp_sv[kRpTF];
+__shared__ uint32_t rp_ik[kRpTI];
+__shared__ uint32_t rp_iv[kRpTI];
+template <bool I>
+__device__ __forceinline__ typename RpKey<I>::T lds_k(uint32_t p) {
+    if constexpr (I) return rp_ik[p];
+    else return rp_sk[p];
+}
+template <bool I>
+__device__ __forceinline__ uint32_t lds_v(uint32_t p) {
+    if constexpr (I) return rp_iv[p];
+    else return rp_sv[p];
+}
+template <bool I>
+__device__ __forceinline__ void lds_put(uint32_t p, typename RpKey<I>::T k, uint32_t v) {
+    if constexpr (I) {
+        rp_ik[p] = k;
+        rp_iv[p] = v;
+    } else {
+        rp_sk[p] = k;
+        rp_sv[p] = v;
+    }
+}
 
-// The heap of one source: keys (igraph's data = -dist) and vertices, positions < kRpT in LDS,
-// the rest as 16-B nodes {f64 key, u32 vertex, pad} in this slot's HBM (one line per node
-// access); the position of a queued vertex lives in its 16-B vertex record
-// {f64 dist, u32 parent slot, u32 heap position} (one line per relaxation target).  For a vertex
-// in the LDS levels the record only says so (some position < kRpT): moves inside the LDS levels
-// (half of every sink path) store no position -- each would be a 4-B write to a random line --
-// and a modify of such a vertex finds it by a wave-wide search of the LDS vertex array
-// (rp_lds_find).
+// The heap of one source: keys (igraph's data = -dist, encoded per RpKey) and vertices,
+// positions < kT in LDS, the rest as nodes in this slot's HBM (one line per node access); the
+// position of a queued vertex lives in its 16-B vertex record (one line per relaxation target).
+// For a vertex in the LDS levels the record only says so (some position < kT): moves inside
+// the LDS levels (half of every sink path) store no position -- each would be a 4-B write to a
+// random line -- and a modify of such a vertex finds it by a wave-wide search of the LDS vertex
+// array (rp_lds_find).
+template <bool I>
 struct RpHeap {
-    uint4* gn;
+    using K = RpKey<I>;
+    using T = typename K::T;
+    static constexpr uint32_t kT = (1u << K::kLevels) - 1u;
+    typename K::Node* gn;
     uint4* vr;
     unsigned long long* nl;
-    __device__ __forceinline__ void node(uint32_t p, double& k, uint32_t& v, int cat) const {
-        rp_lines(nl, cat, p >= kRpT, gn + p);
-        if (p < kRpT) {
-            k = rp_sk[p];
-            v = rp_sv[p];
+    __device__ __forceinline__ void node(uint32_t p, T& k, uint32_t& v, int cat) const {
+        rp_lines(nl, cat, p >= kT, gn + p);
+        if (p < kT) {
+            k = lds_k<I>(p);
+            v = lds_v<I>(p);
         } else {
-            const uint4 q = gn[p];
-            k = __hiloint2double((int)q.y, (int)q.x);
-            v = q.z;
+            K::unpack(gn[p], k, v);
         }
     }
     // node (k, v) to position p; its vertex record's position is stored only when `pos` (the
     // element crossed into or out of the LDS levels, moved inside the HBM levels, or is new)
-    __device__ __forceinline__ void put(uint32_t p, double k, uint32_t v, int cat, bool pos = true) const {
-        rp_lines(nl, cat, p >= kRpT, gn + p);
+    __device__ __forceinline__ void put(uint32_t p, T k, uint32_t v, int cat, bool pos = true) const {
+        rp_lines(nl, cat, p >= kT, gn + p);
         rp_lines(nl, cat, pos, vr + 4 * (size_t)__lane_id() + v);  // random: one line each
-        if (p < kRpT) {
-            rp_sk[p] = k;
-            rp_sv[p] = v;
-        } else {
-            const unsigned long long b = d2bits(k);
-            gn[p] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), v, 0u);
-        }
+        if (p < kT) lds_put<I>(p, k, v);
+        else gn[p] = K::pack(k, v);
         if (pos) reinterpret_cast<uint32_t*>(vr + v)[3] = p;
     }
 };
@@ -194,15 +259,17 @@ __device__ __forceinline__ uint32_t rp_sub_pos(uint32_t head, int lane) {
     return ((head + 1u) << dl) - 1u + (rr - (1u << dl));
 }
 
-// Position of vertex t among the heap's LDS levels (positions < min(size, kRpT)): every lane
+// Position of vertex t among the heap's LDS levels (positions < min(size, kT)): every lane
 // checks its share of the LDS vertex array, one ballot.  ~0u: not there (cannot happen for a
 // vertex whose record says it is).
+template <bool I>
 __device__ __forceinline__ uint32_t rp_lds_find(uint32_t t, uint32_t size, int lane) {
-    const uint32_t n = size < kRpT ? size : kRpT;
+    constexpr uint32_t kT = RpHeap<I>::kT;
+    const uint32_t n = size < kT ? size : kT;
     uint32_t found = 0xFFFFFFFFu;
     for (uint32_t b = 0; b < n; b += 64u) {
         const uint32_t p = b + (uint32_t)lane;
-        const unsigned long long m = __ballot(p < n && rp_sv[p] == t);
+        const unsigned long long m = __ballot(p < n && lds_v<I>(p) == t);
         if (m) {
             found = b + (uint32_t)(__ffsll((long long)m) - 1);
             break;
@@ -211,93 +278,40 @@ __device__ __forceinline__ uint32_t rp_lds_find(uint32_t t, uint32_t size, int l
     return found;
 }
 
-// igraph_2wheap_sink of element (xk, xv) from position `head` (a hole) in a heap of `size`.
-// The path of larger children does not depend on x, so the subtree kRpLA levels below the hole
-// is loaded in one round trip; x stops where it is not smaller than the chosen child.  (k, v):
-// the first round's subtree (rp_la(head) levels), loaded by the caller with its other loads.
-__device__ __forceinline__ void rp_sink(const RpHeap& H, uint32_t head, uint32_t size, double xk,
-                                        uint32_t xv, int lane, double k, uint32_t v) {
-    int la = rp_la(head);  // the caller loaded that many levels
-    for (;;) {
-#if SHD_RP_TIME
-        H.nl[6]++;  // sink rounds
-#endif
-        const uint32_t p = rp_sub_pos(head, lane);
-        uint32_t cur = head, q = 0;
-        bool stop = false;
-        unsigned long long path = 0;
-#pragma unroll
-        for (int s = 0; s < kRpLA; ++s) {
-            if (s >= la) break;
-            const uint32_t L = 2u * cur + 1u;
-            if (L >= size) {
-                stop = true;
-                break;
-            }
-            const int li = (int)(2u * q);  // lane of the left child (BFS 2q+1)
-            const double kL = rl_f64(k, li);
-            int ci = li;
-            uint32_t c = L;
-            double kc = kL;
-            if (L + 1u < size) {
-                const double kR = rl_f64(k, li + 1);
-                if (!(kL >= kR)) {
-                    ci = li + 1;
-                    c = L + 1u;
-                    kc = kR;
-                }
-            }
-            if (xk < kc) {
-                path |= 1ull << ci;
-                cur = c;
-                q = (uint32_t)ci + 1u;
-            } else {
-                stop = true;
-                break;
-            }
-        }
-        // every chosen child moves up to its parent's position
-        if ((path >> lane) & 1ull) H.put((p - 1u) >> 1, k, v, RPL_SINK_ST);
-        head = cur;
-        if (stop) break;
-        const uint32_t pn = rp_sub_pos(head, lane);  // below the last moved node: not written above
-        k = -INFINITY;
-        v = 0;
-        la = rp_la(head);
-        if (lane < (2 << la) - 2 && pn < size) H.node(pn, k, v, RPL_SINK_LD);
-    }
-    if (lane == 0) H.put(head, xk, xv, RPL_SINK_ST);
-}
-
 // igraph_2wheap_delete_max's sink of x = the last element from the root (a hole) in a heap of
-// `size` (after the removal).  The path of larger children does not depend on x, so it is found
-// first: the LDS levels by uniform LDS reads while x's load is in flight, then the HBM levels
-// kRpLA per round trip (the first round is issued before x is waited for).  x stops at the first
-// path node it is not smaller than; the path nodes above the stop move up one level, in parallel
-// (lane i holds path node i).  (kx, vx): x in lane 63, loaded by the caller.
-__device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int lane, double kx,
-                                            uint32_t vx) {
+// `size` (after the removal): igraph_2wheap_sink takes the left child if right == size or
+// data[L] >= data[R] and swaps while data[head] < data[child].  The path of larger children does
+// not depend on x, so it is found first: the LDS levels by lane-parallel LDS reads while x's
+// load is in flight, then the HBM levels kHL per round trip.  x stops at the first path node it
+// is not smaller than; the path nodes above the stop move up one level, in parallel (lane i
+// holds path node i).  (kx, vx): x in lane 63, loaded by the caller.
+template <bool I>
+__device__ __forceinline__ void rp_pop_sink(const RpHeap<I>& H, uint32_t size, int lane,
+                                            typename RpKey<I>::T kx, uint32_t vx) {
+    using K = RpKey<I>;
+    using T = typename K::T;
+    constexpr uint32_t kT = RpHeap<I>::kT;
 #if SHD_RP_TIME
     H.nl[12] = wall_clock64();
 #endif
     uint32_t pp = 0, pv = 0;  // this lane's path node: position, vertex, key
-    double pk = INFINITY;
+    T pk = K::hi();
     int np = 0;
     uint32_t cur = 0;
     bool bottom = false;
     // LDS levels, kRpLA per round: every lane reads its subtree node (one LDS round trip), the
     // path is walked with readlanes
     for (;;) {
-        const int dcur = 31 - __clz(cur + 1u);          // level of cur
-        const int nlds = SHD_RP_LDS_LEVELS - 1 - dcur;  // LDS levels below it
+        const int dcur = 31 - __clz(cur + 1u);   // level of cur
+        const int nlds = K::kLevels - 1 - dcur;  // LDS levels below it
         if (nlds <= 0) break;
         const int la = nlds < kRpLA ? nlds : kRpLA;
         const uint32_t p = rp_sub_pos(cur, lane);
-        double k = -INFINITY;
+        T k = K::lo();
         uint32_t v = 0;
         if (lane < (2 << la) - 2 && p < size) {
-            k = rp_sk[p];
-            v = rp_sv[p];
+            k = lds_k<I>(p);
+            v = lds_v<I>(p);
         }
         uint32_t q = 0;
         for (int s = 0; s < la; ++s) {
@@ -307,12 +321,12 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
                 break;
             }
             const int li = (int)(2u * q);  // BFS index of the left child
-            const double kL = rl_f64(k, li);
+            const T kL = K::rl(k, li);
             int ci = li;
             uint32_t c = L;
-            double kc = kL;
+            T kc = kL;
             if (L + 1u < size) {
-                const double kR = rl_f64(k, li + 1);
+                const T kR = K::rl(k, li + 1);
                 if (!(kL >= kR)) {
                     ci = li + 1;
                     c = L + 1u;
@@ -332,7 +346,7 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
         if (bottom) break;
     }
     RP_STICK(0);
-    double xk = 0.0;
+    T xk = K::lo();
     uint32_t xv = 0;
     bool havex = false;
     int stop = -1;  // first path index x is not smaller than
@@ -341,7 +355,7 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
         H.nl[6]++;  // HBM sink rounds
 #endif
         const uint32_t p = rp_sub_pos(cur, lane);
-        double k = -INFINITY, k2 = -INFINITY;
+        T k = K::lo(), k2 = K::lo();
         uint32_t v = 0, v2 = 0;
         if (lane < kHNodes && p < size) H.node(p, k, v, RPL_SINK_LD);
         if (kHNodes > 64) {  // BFS nodes 64.. in a second register
@@ -349,7 +363,7 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
             if (lane + 64 < kHNodes && p2 < size) H.node(p2, k2, v2, RPL_SINK_LD);
         }
         if (!havex) {
-            xk = rl_f64(kx, 63);
+            xk = K::rl(kx, 63);
             xv = rl_u32(vx, 63);
             havex = true;
             const unsigned long long sm = __ballot(lane < np && !(xk < pk));
@@ -367,12 +381,12 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
                 break;
             }
             const int li = (int)(2u * q);  // BFS index of the left child (2q+1 - 1)
-            const double kL = li < 64 ? rl_f64(k, li) : rl_f64(k2, li - 64);
+            const T kL = li < 64 ? K::rl(k, li) : K::rl(k2, li - 64);
             int ci = li;
             uint32_t c = L;
-            double kc = kL;
+            T kc = kL;
             if (L + 1u < size) {
-                const double kR = li + 1 < 64 ? rl_f64(k, li + 1) : rl_f64(k2, li + 1 - 64);
+                const T kR = li + 1 < 64 ? K::rl(k, li + 1) : K::rl(k2, li + 1 - 64);
                 if (!(kL >= kR)) {
                     ci = li + 1;
                     c = L + 1u;
@@ -396,7 +410,7 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
         if (stop >= 0) break;
     }
     if (!havex) {
-        xk = rl_f64(kx, 63);
+        xk = K::rl(kx, 63);
         xv = rl_u32(vx, 63);
         const unsigned long long sm = __ballot(lane < np && !(xk < pk));
         stop = sm ? __ffsll((long long)sm) - 1 : np;
@@ -405,10 +419,10 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
     }
     RP_STICK(1);
     const uint32_t up = __shfl_up(pp, 1);  // the parent's position (path node lane - 1)
-    if (lane < stop) H.put(lane == 0 ? 0u : up, pk, pv, RPL_SINK_ST, pp >= kRpT);
+    if (lane < stop) H.put(lane == 0 ? 0u : up, pk, pv, RPL_SINK_ST, pp >= kT);
     if (lane == 0) {
         const uint32_t xp = stop == 0 ? 0u : rl_u32(pp, stop - 1);
-        H.put(xp, xk, xv, RPL_SINK_ST, xp >= kRpT || size >= kRpT);  // x came from position size
+        H.put(xp, xk, xv, RPL_SINK_ST, xp >= kT || size >= kT);  // x came from position size
     }
     RP_STICK(2);
 }
@@ -417,14 +431,19 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap& H, uint32_t size, int 
 // of ancestors moved down one level; lane i < f holds the moved vertex (mv) and its new position.
 // Most shift-ups stop below the parent: it is read first (one node), the whole chain only when x
 // rises past it.  check = false: the caller knows x rises past the parent.
-__device__ __forceinline__ int rp_shift_up(const RpHeap& H, uint32_t pos, double xk, uint32_t xv,
-                                           int lane, uint32_t& mv, uint32_t& mp, bool fresh,
+template <bool I>
+__device__ __forceinline__ int rp_shift_up(const RpHeap<I>& H, uint32_t pos,
+                                           typename RpKey<I>::T xk, uint32_t xv, int lane,
+                                           uint32_t& mv, uint32_t& mp, bool fresh,
                                            bool check = true) {
-    if (SHD_RP_PROG && check && pos > 0) {
-        double k0;
+    using K = RpKey<I>;
+    using T = typename K::T;
+    constexpr uint32_t kT = RpHeap<I>::kT;
+    if (check && pos > 0) {
+        T k0;
         uint32_t v0;
         H.node((pos - 1u) >> 1, k0, v0, RPL_SHIFT_LD);
-        if (xk < uni_f64(k0)) {  // data[x] < data[parent]: stays (a pushed vertex is new)
+        if (xk < K::uni(k0)) {  // data[x] < data[parent]: stays (a pushed vertex is new)
             if (lane == 0) H.put(pos, xk, xv, RPL_SHIFT_ST, fresh);
             return 0;
         }
@@ -433,16 +452,16 @@ __device__ __forceinline__ int rp_shift_up(const RpHeap& H, uint32_t pos, double
     const bool valid = (uint32_t)lane < depth;
     const uint32_t sh = valid ? (uint32_t)lane + 1u : 0u;
     const uint32_t a = ((pos + 1u) >> sh) - 1u;
-    double ak = INFINITY;
+    T ak = K::hi();
     uint32_t av = 0;
     if (valid) H.node(a, ak, av, RPL_SHIFT_LD);
     // x rises past every ancestor with key <= x and stops below the first one with key > x
     const unsigned long long stopm = __ballot(valid && xk < ak);
     const int f = stopm ? __ffsll((long long)stopm) - 1 : (int)depth;
     const uint32_t c = lane == 0 ? pos : (valid ? ((pos + 1u) >> (uint32_t)lane) - 1u : 0u);
-    if (lane < f) H.put(c, ak, av, RPL_SHIFT_ST, c >= kRpT);  // ancestors move down to c
+    if (lane < f) H.put(c, ak, av, RPL_SHIFT_ST, c >= kT);  // ancestors move down to c
     const uint32_t fp = f == 0 ? pos : ((pos + 1u) >> (uint32_t)f) - 1u;
-    if (lane == 0) H.put(fp, xk, xv, RPL_SHIFT_ST, fresh || (f > 0 && (fp >= kRpT || pos >= kRpT)));
+    if (lane == 0) H.put(fp, xk, xv, RPL_SHIFT_ST, fresh || (f > 0 && (fp >= kT || pos >= kT)));
     mv = av;
     mp = c;
     return f;
@@ -450,12 +469,16 @@ __device__ __forceinline__ int rp_shift_up(const RpHeap& H, uint32_t pos, double
 
 __device__ __forceinline__ uint32_t vr_par(const uint4* vr, uint32_t v) { return vr[v].z; }
 
+template <bool I>
 __global__ void __launch_bounds__(64, 4)
 heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ sources,
                    const uint32_t* __restrict__ rows, int nrows,
                    const uint32_t* __restrict__ targets, int A, int full, double2* out_lr,
                    uint16_t* out_hops, double* out_rowmin, unsigned long long* stats,
                    double* dbg_dist, int32_t* dbg_par) {
+    using K = RpKey<I>;
+    using T = typename K::T;
+    constexpr uint32_t kT = RpHeap<I>::kT;
     const int lane = (int)threadIdx.x;
     const size_t V = (size_t)g.V;
     const size_t slot = blockIdx.x;
@@ -464,7 +487,8 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 #if SHD_RP_TIME
     unsigned long long tph[4] = {0, 0, 0, 0}, tlast = wall_clock64();
 #endif
-    RpHeap H{ws.node + slot * V, vr, nl};
+    // node storage: V x 16 B per slot, of which the u32-key heap uses the first half
+    RpHeap<I> H{reinterpret_cast<typename K::Node*>(ws.node + slot * V), vr, nl};
     uint32_t* pbuf = ws.pathbuf + slot * (size_t)kMaxHops * 64;
     unsigned long long n_pop = 0, n_push = 0, n_mod = 0, n_rows = 0, n_skip = 0;
 
@@ -478,15 +502,12 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
         n_rows++;
 
         // ---- igraph_get_shortest_paths_dijkstra ----
-        {
-            const unsigned long long m1 = d2bits(-1.0);
-            for (size_t i = (size_t)lane; i < V; i += 64)
-                *reinterpret_cast<unsigned long long*>(vr + i) = m1;  // dist = -1
-        }
+        for (size_t i = (size_t)lane; i < V; i += 64)
+            *reinterpret_cast<unsigned long long*>(vr + i) = K::kUnreached;  // dist = -1
         uint32_t size = 1;
         if (lane == 0) {
-            *reinterpret_cast<double*>(vr + src) = 0.0;
-            H.put(0, 0.0, src, RPL_SINK_ST);
+            K::set_dist(vr + src, T(0));
+            H.put(0, K::src_key(), src, RPL_SINK_ST);
         }
         int64_t to_reach = full ? (int64_t)V + 1 : (int64_t)g.ntargets;
         // The root after a sink is the next pop's u unless a shift-up of the relaxation reaches
@@ -497,22 +518,15 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
         while (size > 0 && to_reach > 0) {
             // igraph_2wheap_delete_max
             RP_TICK(3);
-            const uint32_t u = uni_u32(rp_sv[0]);
-            const double du = -uni_f64(rp_sk[0]);  // mindist = -data[0]
+            const uint32_t u = uni_u32(lds_v<I>(0));
+            const T du = K::dist_of_key(K::uni(lds_k<I>(0)));  // mindist = -data[0]
+            const double duf = K::f64(du);
             const uint32_t lastp = size - 1u;
-            // one round trip: the sink's first subtree (lanes < kRpLaNodes), the last node (lane
-            // 63) and, independent of the heap, u's target bit, row bounds and first 64 records
-            double k1 = -INFINITY;
+            // one round trip: the last node (lane 63) and, independent of the heap, u's target
+            // bit, row bounds and first 64 records
+            T k1 = K::lo();
             uint32_t v1 = 0;
-#if SHD_RP_SINK2
             if (lane == 63) H.node(lastp, k1, v1, RPL_SINK_LD);
-#else
-            {
-                const uint32_t p1 = rp_sub_pos(0, lane);
-                if (lane < kRpLaNodes && p1 < lastp) H.node(p1, k1, v1, RPL_SINK_LD);
-                else if (lane == 63) H.node(lastp, k1, v1, RPL_SINK_LD);
-            }
-#endif
             uint32_t tb, rb, re;
             if (SHD_RP_PREF && u == pf_u) {
 #if SHD_RP_TIME
@@ -532,16 +546,12 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 #if SHD_RP_TIME
             nl[7] += size;  // heap size at the pop
 #endif
-            if (u == (uint32_t)g.landmark) dh0 = du;
-#if SHD_RP_SINK2
-            if (size > 0) rp_pop_sink(H, size, lane, k1, v1);
-#else
-            if (size > 0) rp_sink(H, 0, size, rl_f64(k1, 63), rl_u32(v1, 63), lane, k1, v1);
-#endif
+            if (u == (uint32_t)g.landmark) dh0 = duf;
+            if (size > 0) rp_pop_sink<I>(H, size, lane, k1, v1);
             n_pop++;
             RP_TICK(0);
             if (SHD_RP_PREF && size > 0) {
-                pf_u = uni_u32(rp_sv[0]);
+                pf_u = uni_u32(lds_v<I>(0));
                 if (lane < 2) pf_r = g.rowptr[pf_u + (uint32_t)lane];
                 if (lane == 0) pf_t = g.tbits[pf_u >> 5];
             }
@@ -555,10 +565,11 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                 const uint32_t j = base + (uint32_t)lane;
                 const bool act = j < re;
                 uint32_t t = 0, mypos = 0;
-                double w = 0.0, cur = 0.0;
+                double w = 0.0;
+                T cur = T(0);
                 rp_lines(nl, RPL_RELAX_LD, act, g.rec + j);
 #if SHD_RP_LINES
-                rp_lines(nl, RPL_RELAX_LD, act && !(__dmul_rn(__dadd_rn(dh0, (double)__uint_as_float(g.rec[act ? j : 0].y)), 1.000001) < du),
+                rp_lines(nl, RPL_RELAX_LD, act && !(__dmul_rn(__dadd_rn(dh0, (double)__uint_as_float(g.rec[act ? j : 0].y)), 1.000001) < duf),
                          vr + 4 * (size_t)lane + (act ? g.rec[j].x : 0));
 #endif
                 bool live = act;
@@ -569,22 +580,20 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                     // landmark skip: d(t) <= d(h0) + pi(t) (the walk s -> h0 -> t; pi rounded
                     // up, rounding of the sums far inside the 1e-6 margin) below du proves t
                     // popped, and relaxing a popped vertex changes nothing: its record is not read
-                    live = !(__dmul_rn(__dadd_rn(dh0, (double)__uint_as_float(r.y)), 1.000001) < du);
+                    live = !(__dmul_rn(__dadd_rn(dh0, (double)__uint_as_float(r.y)), 1.000001) < duf);
                 }
                 if (live) {
                     const uint4 x = vr[t];  // {dist, parent slot, heap position}
-                    cur = __hiloint2double((int)x.y, (int)x.x);
+                    cur = K::dist(x);
                     mypos = x.w;
                 }
                 n_skip += (unsigned long long)__popcll(__ballot(act && !live));
-                const double alt = __dadd_rn(du, w);
-                const bool first = live && cur < 0.0;
+                const T alt = K::add(du, w);
+                const bool first = live && !K::reached(cur);
                 const bool impr = live && !first && alt < cur;
                 rp_lines(nl, RPL_RELAX_ST, first || impr, vr + 4 * (size_t)lane + t);
-                if (first || impr) {  // dist and parent in one 12-B store
-                    const unsigned long long b = d2bits(alt);
-                    *reinterpret_cast<uint3*>(vr + t) = make_uint3((uint32_t)b, (uint32_t)(b >> 32), j);
-                }
+                if (first || impr)  // dist and parent in one 12-B store
+                    *reinterpret_cast<uint3*>(vr + t) = K::rec(alt, j);
                 unsigned long long m = __ballot(first || impr);
                 const unsigned long long fm = __ballot(first);
                 RP_TICK(1);
@@ -593,12 +602,12 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                 // pushes before it, a modify at its vertex's position.  A read stays valid until
                 // an earlier operation moves nodes (dirty) or places its element at that parent.
                 uint32_t ppos = 0;
-                double pk = INFINITY;
+                T pk = K::hi();
                 if (first) ppos = size + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
                 else if (impr) ppos = mypos;
                 // a vertex in the LDS levels: its record's position is only a marker (found by
                 // rp_lds_find at its operation, its parent read then)
-                bool stale = impr && mypos < kRpT;
+                bool stale = impr && mypos < kT;
                 if ((first || impr) && ppos > 0 && !stale) {
                     uint32_t pv;
                     H.node((ppos - 1u) >> 1, pk, pv, RPL_SHIFT_LD);
@@ -608,7 +617,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                     const int l = __ffsll((long long)m) - 1;
                     m &= m - 1ull;
                     const uint32_t tv = rl_u32(t, l);
-                    const double xkey = -rl_f64(alt, l);
+                    const T xkey = K::key_of(K::rl(alt, l));
                     uint32_t pos;
                     if ((fm >> l) & 1ull) {  // igraph_2wheap_push_with_index
                         if (size >= (uint32_t)V) {  // cannot happen (each vertex queued once)
@@ -620,21 +629,21 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                         n_push++;
                     } else {  // igraph_2wheap_modify (its sink is a no-op for a larger key)
                         pos = rl_u32(mypos, l);
-                        if (pos < kRpT) pos = rp_lds_find(tv, size, lane);
+                        if (pos < kT) pos = rp_lds_find<I>(tv, size, lane);
                         n_mod++;
                     }
                     const bool fresh = (fm >> l) & 1ull;
                     uint32_t mv = 0, mp = 0;
                     int f;
-                    if (SHD_RP_PROG && !dirty && pos > 0 && !__shfl(stale, l)) {
-                        if (xkey < rl_f64(pk, l)) {  // stays: data[x] < data[parent]
+                    if (!dirty && pos > 0 && !__shfl(stale, l)) {
+                        if (xkey < K::rl(pk, l)) {  // stays: data[x] < data[parent]
                             if (lane == 0) H.put(pos, xkey, tv, RPL_SHIFT_ST, fresh);
                             f = 0;
                         } else {
-                            f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp, fresh, false);
+                            f = rp_shift_up<I>(H, pos, xkey, tv, lane, mv, mp, fresh, false);
                         }
                     } else {
-                        f = rp_shift_up(H, pos, xkey, tv, lane, mv, mp, fresh);
+                        f = rp_shift_up<I>(H, pos, xkey, tv, lane, mv, mp, fresh);
                     }
                     if (f > 0) dirty = true;
                     else if (ppos > 0 && ((ppos - 1u) >> 1) == pos) stale = true;
@@ -651,7 +660,8 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
         if (dbg_dist) {  // test hook: the replay's dist / parent vertex in relabelled ids
             for (size_t i = (size_t)lane; i < V; i += 64) {
                 const uint4 x = vr[i];
-                const double d = __hiloint2double((int)x.y, (int)x.x);
+                const T dt = K::dist(x);
+                const double d = K::reached(dt) ? K::f64(dt) : -1.0;
                 dbg_dist[i] = d;
                 dbg_par[i] = (d >= 0.0 && i != src) ? (int32_t)g.own[x.z] : -1;
             }
@@ -679,7 +689,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
                     h = 1;
                 }
             } else {
-                bool bad = !(*reinterpret_cast<const double*>(vr + t) >= 0.0);
+                bool bad = !K::reached(K::dist(vr[t]));
                 uint32_t v = t;
                 while (!bad && v != src) {
                     const uint32_t j = vr_par(vr, v);
@@ -750,8 +760,8 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 
 }  // namespace
 
-int replay_lds_levels() { return SHD_RP_LDS_LEVELS; }
-int replay_lds_bytes() { return (int)kRpT * 12; }
+int replay_lds_levels(int int_keys) { return int_keys ? SHD_RP_LDS_LEVELS_INT : SHD_RP_LDS_LEVELS; }
+int replay_lds_bytes(int int_keys) { return int_keys ? (int)kRpTI * 8 : (int)kRpTF * 12; }
 
 hipError_t launch_heap_replay(const ReplayCSR& g, const ReplayWs& ws, const uint32_t* d_sources,
                               const uint32_t* d_rows, int nrows, const uint32_t* d_targets, int A,
@@ -761,15 +771,22 @@ hipError_t launch_heap_replay(const ReplayCSR& g, const ReplayWs& ws, const uint
     const int grid = ws.slots < nrows ? ws.slots : nrows;
     if (grid < 1) return hipSuccess;
     if (g.V <= 0 || (dbg_dist && nrows != 1)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(heap_replay_kernel, dim3(grid), dim3(64), 0, stream, g, ws, d_sources,
-                       d_rows, nrows, d_targets, A, full, out_lr, out_hops, out_rowmin, d_stats,
-                       dbg_dist, dbg_par);
+    if (g.intKeys)
+        hipLaunchKernelGGL(heap_replay_kernel<true>, dim3(grid), dim3(64), 0, stream, g, ws,
+                           d_sources, d_rows, nrows, d_targets, A, full, out_lr, out_hops,
+                           out_rowmin, d_stats, dbg_dist, dbg_par);
+    else
+        hipLaunchKernelGGL(heap_replay_kernel<false>, dim3(grid), dim3(64), 0, stream, g, ws,
+                           d_sources, d_rows, nrows, d_targets, A, full, out_lr, out_hops,
+                           out_rowmin, d_stats, dbg_dist, dbg_par);
     return hipGetLastError();
 }
 
 hipError_t preload_replay_module() {
     hipFuncAttributes a;
-    return hipFuncGetAttributes(&a, (const void*)heap_replay_kernel);
+    const hipError_t e = hipFuncGetAttributes(&a, (const void*)heap_replay_kernel<false>);
+    if (e != hipSuccess) return e;
+    return hipFuncGetAttributes(&a, (const void*)heap_replay_kernel<true>);
 }
 
 }  // namespace shdtopo

@@ -94,12 +94,14 @@ def graphml_doc(nodes, edges, directed=False):
 
 
 def random_topology_graphml(n_routers=600, n_poi=60, extra=2400, seed=3, integer=False,
-                            directed=False, parallel=0):
+                            directed=False, parallel=0, lat_scale=1):
     """A connected router graph (a cycle, both directions when directed, plus `extra` random
     edges), poi vertices with an uplink (a pair of opposite edges when directed) and a self loop.
-    `parallel` extra edges duplicate existing router edges with other latencies (multigraph)."""
+    `parallel` extra edges duplicate existing router edges with other latencies (multigraph).
+    Router latencies are U{1..100} x lat_scale (integer) or U[1, 100)."""
     rng = np.random.default_rng(seed)
-    lat = (lambda: int(rng.integers(1, 101))) if integer else (lambda: rng.uniform(1, 100))
+    lat = ((lambda: int(rng.integers(1, 101)) * lat_scale) if integer
+           else (lambda: rng.uniform(1, 100)))
     nodes = [("pop-%d" % i, "pop", 0.0) for i in range(n_routers)]
     nodes += [("poi-%d" % k, ("client", "relay", "server")[k % 3], rng.uniform(0, 0.05))
               for k in range(n_poi)]

@@ -16,11 +16,12 @@ from helpers import attach_hosts, random_topology_graphml, synthetic_pair
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("integer", [True, False])
-def test_replay_full_dijkstra_parents_match_oracle(integer):
+@pytest.mark.parametrize("integer,int_keys", [(True, 1), (True, 0), (False, 1)])
+def test_replay_full_dijkstra_parents_match_oracle(integer, int_keys):
     """Full Dijkstra (no early exit): dist bit-exact and the parent of EVERY vertex equal to the
-    oracle heap's, ties included."""
+    oracle heap's, ties included -- on the u32-key heap (integer latencies) and the f64 one."""
     top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
+    top.set_option("replay_int_keys", int_keys)
     otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay", "server"])
     srcs = sorted(set(verts))[:4] + [0, g.V // 2]
     nties = 0
@@ -90,9 +91,25 @@ def test_replay_all_equals_oracle_continuous():
     st = top.stats()
     oa, olat, orel, ohops = g.table(verts)
     assert st["replay_rows"] == len(a) and st["errors"] == 0
+    assert st["replay_int_keys"] == 0  # continuous latencies: f64 keys
     assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(hops, ohops.astype(np.uint16))
     assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+
+
+@pytest.mark.parametrize("scale,int_keys", [(60000, 1), (1 << 23, 0)])
+def test_replay_int_key_bound(scale, int_keys):
+    """u32 heap keys only while V x max latency < 2^32 - 1 (660 x 100 x 60000 = 3.96e9 fits;
+    x 2^23 does not and falls back to f64 keys); every pair bit-exact either way."""
+    data = random_topology_graphml(n_routers=600, n_poi=60, extra=2400, seed=4, integer=True,
+                                   lat_scale=scale)
+    top = sa.Topology.from_buffer(data)
+    top.set_option("replay_all", 1)
+    g = oracle.OGraph.from_graphml(data)
+    otop, ips, verts = attach_hosts(top, g, 100, type_hints=["client", "relay"])
+    st = _table_bit_exact(top, g, verts)
+    assert st["errors"] == 0 and st["replay_rows"] == len(top.attached_vertices())
+    assert st["replay_int_keys"] == int_keys
 
 
 @pytest.mark.parametrize("integer", [False, True])
@@ -152,17 +169,19 @@ def _table_bit_exact(top, g, verts):
     return top.stats()
 
 
-@pytest.mark.parametrize("landmark", [1, 0])
-def test_tie_dense_replay_landmark_skip(landmark):
+@pytest.mark.parametrize("landmark,int_keys", [(1, 1), (0, 1), (1, 0)])
+def test_tie_dense_replay_landmark_skip(landmark, int_keys):
     """tie_dense = 1: no batch kernel, every row through the replay; the replay's landmark skip
     (relaxations into vertices d(h0) + pi(t) < du proves popped: their record is not read) on or
-    off -- every pair bit-exact against the oracle either way."""
+    off, u32 or f64 heap keys -- every pair bit-exact against the oracle either way."""
     top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=True)
     top.set_option("tie_dense", 1)
     top.set_option("replay_landmark", landmark)
+    top.set_option("replay_int_keys", int_keys)
     otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
     st = _table_bit_exact(top, g, verts)
     assert st["tie_dense"] == 1 and st["errors"] == 0
+    assert st["replay_int_keys"] == int_keys
     assert st["replay_rows"] == len(top.attached_vertices())
     assert st["ambiguous_pairs"] == 0  # the batch kernel did not run
     if landmark:

@@ -1,6 +1,6 @@
 """Probe: heap-replay cost on C4-int (integer latencies) for a row range, per row and per heap op.
-usage: python tools/replay_probe.py ROWS [SLOTS] [all] [LANDMARK]  (all: only the replay_all mode;
-LANDMARK 0: no landmark skip)"""
+usage: python tools/replay_probe.py ROWS [SLOTS] [all] [LANDMARK] [INT_KEYS]  (all: only the
+replay_all mode; LANDMARK 0: no landmark skip; INT_KEYS 0: f64 heap keys)"""
 import sys
 import time
 
@@ -20,6 +20,8 @@ if slots:
     top.set_option("replay_slots", slots)
 if len(sys.argv) > 4:
     top.set_option("replay_landmark", int(sys.argv[4]))
+if len(sys.argv) > 5:
+    top.set_option("replay_int_keys", int(sys.argv[5]))
 lr = torch.empty((rows, A, 2), dtype=torch.float64, device="cuda")
 hp = torch.empty((rows, A), dtype=torch.int16, device="cuda")
 modes = ("replay_all",) if len(sys.argv) > 3 and sys.argv[3] == "all" else ("batch+replay", "replay_all")
