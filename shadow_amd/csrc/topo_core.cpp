@@ -849,6 +849,30 @@ SlotWs slot_ws(Topology* top) {
 // heap history, topo_replay.hip) and the lowest edge id's latency/loss for the hop
 // (igraph_get_eid as orc_get_eid).  Built on the GPU (prep_replay_csr) from the parsed edges
 // upload_csr keeps in HBM.
+// One host pass over the parsed edges (the graph is immutable once loaded), run by the attach-time
+// preparation thread or else by the first build that needs it:
+//   * meanLat, the mean non-loop latency (the batch kernel's bucket width, default_delta);
+//   * replayIntOk: u32 heap keys are exact when every relaxed latency (self loops never relax)
+//     is a non-negative integer and no tentative distance du + w <= V x max reaches 2^32 - 1
+//     (the unreached marker): then every f64 sum the reference forms is an exact integer.
+void edge_scan(Topology* top) {
+    if (top->meanLat >= 0) return;
+    const HostGraph& g = top->g;
+    double s = 0.0, wmax = 0.0;
+    int64_t n = 0;
+    bool ints = true;
+    for (int64_t e = 0; e < g.E; e++) {
+        if (g.eu[(size_t)e] == g.ev[(size_t)e]) continue;
+        const double w = g.elat[(size_t)e];
+        s += w;
+        n++;
+        if (!(w >= 0.0) || w != std::floor(w)) ints = false;
+        else wmax = std::max(wmax, w);
+    }
+    top->replayIntOk = ints && (double)g.V * wmax < 4294967295.0;
+    top->meanLat = n ? s / (double)n : 1.0;
+}
+
 int upload_replay_impl(Topology* top);
 int upload_replay(Topology* top) {
     if (top->replayUploaded) return 0;
@@ -863,20 +887,7 @@ int upload_replay_impl(Topology* top) {
     const int64_t V = g.V, E = g.E;
     const bool dir = top->isDirected;
     const size_t cap = std::max<size_t>(1, (size_t)(dir ? E : 2 * E));
-    // u32 heap keys are exact when every relaxed latency (self loops never relax) is a
-    // non-negative integer and no tentative distance du + w <= V x max reaches 2^32 - 1 (the
-    // unreached marker): then every f64 sum the reference forms is an exact integer
-    {
-        bool ok = true;
-        double wmax = 0.0;
-        for (int64_t e = 0; e < E && ok; e++) {
-            if (g.eu[(size_t)e] == g.ev[(size_t)e]) continue;
-            const double w = g.elat[(size_t)e];
-            if (!(w >= 0.0) || w != std::floor(w)) ok = false;
-            else wmax = std::max(wmax, w);
-        }
-        top->replayIntOk = ok && (double)V * wmax < 4294967295.0;
-    }
+    edge_scan(top);
     HIPCHK(top->d_rrow.ensure((size_t)V + 1));
     HIPCHK(top->d_rrec.ensure(cap));
     HIPCHK(top->d_rown.ensure(cap));
@@ -1000,14 +1011,7 @@ uint64_t compute_geometry(Topology* top) {
 
 double default_delta(Topology* top) {
     if (top->delta > 0) return top->delta;
-    if (!(top->meanLat >= 0)) {  // the graph is immutable once loaded: one pass over the edges
-        const HostGraph& g = top->g;
-        double s = 0;
-        int64_t n = 0;
-        for (int64_t e = 0; e < g.E; e++)
-            if (g.eu[(size_t)e] != g.ev[(size_t)e]) { s += g.elat[(size_t)e]; n++; }
-        top->meanLat = n ? s / (double)n : 1.0;
-    }
+    edge_scan(top);
     const double mean = top->meanLat;
     // tuned on C4: single-source 0.06 x mean (~3 ms); the batch kernel gains from
     // wider buckets (sources of a batch share more expansions) up to 0.2 x mean (~10 ms)
@@ -1553,6 +1557,10 @@ void sync_peer(Topology* top, Topology* p) {
     p->replaySlotsOpt = top->replaySlotsOpt;
     p->replayLandmark = top->replayLandmark;
     p->replayIntOpt = top->replayIntOpt;
+    if (top->meanLat >= 0 && !(p->meanLat >= 0)) {  // the owner's edge scan (same graph)
+        p->meanLat = top->meanLat;
+        p->replayIntOk = top->replayIntOk;
+    }
     p->sourceOrder = top->sourceOrder;
     p->batchOrder = top->batchOrder;
     p->batchFill = top->batchFill;
@@ -2157,6 +2165,7 @@ void start_attach_prep(Topology* top) {
         }
         int r = dev_init(top);
         if (!r) r = upload_csr(top);
+        edge_scan(top);  // mean latency (bucket width) and the replay's integer-key check
         // the batched SSSP's workspace too, sized for a full table (a build with fewer sources
         // uses a part of it; a different batch width re-allocates)
         if (!r) r = ensure_workspace(top, 1 << 30);
