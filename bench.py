@@ -43,7 +43,7 @@ from shadow_amd import sharding  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SEED = 20261015
-PROFILE_TAG = "r03"            # profiles/<tag>_*_pmc.json: the committed counter passes
+PROFILE_TAG = "r04"            # profiles/<tag>_*_pmc.json: the committed counter passes
 
 
 def log(rank, *a):
@@ -72,9 +72,10 @@ def cpu_share():
 
 def cpu_baseline(top, attached, n_sample, n_sample_mt, nthreads_mt):
     """The reference path's CPU restatement (oracle: igraph-0.7 binary-heap Dijkstra + helper),
-    timed on this host on bounded samples of sources: 1 thread (the reference's concurrency:
-    Dijkstra runs under the global graphLock) and every thread of the job's CPU
-    share (sources are independent); each extrapolated linearly by source count."""
+    timed on this host on bounded samples of sources (BASELINE.md's plan: 64 sources): 1 thread
+    (the reference's concurrency: Dijkstra runs under the global graphLock) and
+    every thread of the job's CPU share (sources are independent).  The sample's own rate is
+    `value`; the linear extrapolation to the full table is reported apart from it."""
     import oracle
     V, eu, ev, elat, eloss, vloss = top.export_graph()
     t0 = time.time()
@@ -86,9 +87,11 @@ def cpu_baseline(top, attached, n_sample, n_sample_mt, nthreads_mt):
     g.source_rows(srcs, attached, nthreads=1)
     t = time.time() - t0
     out = dict(value=len(srcs) * E / t / 1e9, unit="GTEPS", cores=1, kind="port",
-               sample="%d of %d sources x %d targets (Dijkstra + per-target helper) on 1 thread, "
-                      "%.1f s; extrapolated linearly to the full table: %.0f s" %
-                      (len(srcs), A, A, t, t / len(srcs) * A),
+               sample="%d of %d sources x %d targets (Dijkstra + per-target helper) on 1 thread: "
+                      "%.1f s measured" % (len(srcs), A, A, t),
+               sample_sources=len(srcs), sample_s=round(t, 2),
+               extrapolated=dict(full_table_s=round(t / len(srcs) * A, 1),
+                                 note="linear in the source count (%d sources)" % A),
                seconds_per_source=t / len(srcs), oracle_setup_s=t_setup)
     if n_sample_mt > 0 and nthreads_mt > 1:
         srcs = attached[n_sample:n_sample + n_sample_mt]
@@ -97,18 +100,34 @@ def cpu_baseline(top, attached, n_sample, n_sample_mt, nthreads_mt):
         t = time.time() - t0
         out["all_cores"] = dict(
             value=len(srcs) * E / t / 1e9, unit="GTEPS", cores=nthreads_mt,
-            sample="%d sources x %d targets on %d threads (the job's CPU share), %.1f s; "
-                   "extrapolated to the full table: %.0f s" % (len(srcs), A, nthreads_mt, t,
-                                                               t / len(srcs) * A),
+            sample="%d sources x %d targets on %d threads (the job's CPU share): %.1f s measured"
+                   % (len(srcs), A, nthreads_mt, t),
+            sample_sources=len(srcs), sample_s=round(t, 2),
+            extrapolated=dict(full_table_s=round(t / len(srcs) * A, 1),
+                              note="linear in the source count"),
             seconds_per_source=t / len(srcs))
     return out
 
 
-def complete_table_lines(repeats=20):
+def _chunks(n, k):
+    b = [n * i // k for i in range(k + 1)]
+    return [(b[i], b[i + 1]) for i in range(k) if b[i + 1] > b[i]]
+
+
+def parallel_calls(fn, n, nthreads):
+    """fn(lo, hi) over nthreads contiguous chunks of [0, n) in threads (the oracle's ctypes calls
+    release the GIL, so the chunks run on separate cores)."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=nthreads) as ex:
+        return list(ex.map(lambda c: fn(*c), _chunks(n, nthreads)))
+
+
+def complete_table_lines(repeats=20, nthreads=1):
     """BASELINE configs 2 (plab, 303 x 303) and 3 (full Internet, 183 x 183): the complete-graph
     pair table (_topology_lookupPath for every attached pair, shd-topology.c:835-873) on the
-    GPU vs the oracle's restatement on one CPU thread.  One host per vertex via its unique
-    geocode hint.  34 B per pair (roofline of pair_table_complete_kernel)."""
+    GPU vs the oracle's restatement on one CPU thread and on every thread of the job's share.
+    One host per vertex via its unique geocode hint.  34 B per pair (roofline
+    of pair_table_complete_kernel)."""
     import lzma
     import oracle
     out = {}
@@ -136,9 +155,13 @@ def complete_table_lines(repeats=20):
         k_ms = float(np.median(ms))
         a = np.asarray(sorted(set(top.attached_vertices().tolist())), np.int32)
         S, D = np.meshgrid(a, a, indexing="ij")
+        Sr, Dr = S.ravel(), D.ravel()
         t0 = time.perf_counter()
-        g.complete_pairs(S.ravel(), D.ravel())
+        g.complete_pairs(Sr, Dr)
         t_cpu = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        parallel_calls(lambda lo, hi: g.complete_pairs(Sr[lo:hi], Dr[lo:hi]), len(Sr), nthreads)
+        t_cpu_mt = time.perf_counter() - t0
         pairs = A * A
         out[cfg] = dict(topology=name, attached=A, pairs=pairs,
                         gpu_pairs_per_s=round(pairs / (k_ms / 1e3), 1), kernel_ms=round(k_ms, 4),
@@ -148,15 +171,20 @@ def complete_table_lines(repeats=20):
                                       peak=HBM_PEAK_GBS, unit="GB/s",
                                       frac=round(pairs * 34 / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)),
                         cpu_pairs_per_s=round(pairs / t_cpu, 1), cpu_cores=1,
+                        cpu_all_cores=dict(pairs_per_s=round(pairs / t_cpu_mt, 1),
+                                           cores=nthreads),
                         note="launch-bound: %d pairs are a few microseconds of HBM time" % pairs)
     return out
 
 
-def cpu_route_baseline(lat, rel, payload, state, now, jump):
+def cpu_route_baseline(lat, rel, payload, state, now, jump, nthreads=1):
+    """worker_schedulePacket's restatement (oracle) over the whole window: packets/s."""
     import oracle
-    t0 = time.time()
-    oracle.route_packets(lat, rel, payload, state, now, jump, 1)
-    return len(lat) / (time.time() - t0)
+    t0 = time.perf_counter()
+    parallel_calls(lambda lo, hi: oracle.route_packets(lat[lo:hi], rel[lo:hi], payload[lo:hi],
+                                                       state[lo:hi], now[lo:hi], jump, 1),
+                   len(lat), nthreads)
+    return len(lat) / (time.perf_counter() - t0)
 
 
 def load_pmc(path, key):
@@ -208,8 +236,8 @@ def main():
     ap.add_argument("--hosts", type=int, default=100_000)
     ap.add_argument("--packets", type=int, default=10_000_000)
     ap.add_argument("--route-steps", type=int, default=20)
-    ap.add_argument("--cpu-sample", type=int, default=24,
-                    help="sources timed on 1 CPU thread (about 1 s each)")
+    ap.add_argument("--cpu-sample", type=int, default=64,
+                    help="sources timed on 1 CPU thread (about 1 s each; BASELINE.md: 64)")
     ap.add_argument("--cpu-sample-mt", type=int, default=256,
                     help="sources timed on all threads of the job's CPU share")
     ap.add_argument("--no-graphml", action="store_true",
@@ -296,11 +324,14 @@ def main():
     if library and ngpu > 1:
         top.set_option("devices", ngpu)
     window0 = 10_000_000  # Shadow's default 10 ms window until the runahead is known
-    pk = top.synth_packets(SEED, args.hosts, args.packets, 10**9, window0)
+    # ---- the attach phase (Shadow creates its hosts: topology_attach per host), timed as wall
+    # clock; the first table is built right after it, as Shadow's first packet would trigger it,
+    # so any part of the attach-time preparation the attaches do not hide shows in the build ----
+    t_att0 = time.perf_counter()
+    top.synth_packets(SEED, args.hosts, 0, 10**9, window0)
+    attach_phase_s = time.perf_counter() - t_att0
     attached = top.attached_vertices()
     A, V, E = len(attached), top.num_vertices, top.num_edges
-    log(rank, "workload ready in %.1fs: V=%d E=%d A=%d packets=%d, %d GPU(s), mode %s" %
-        (time.time() - t0, V, E, A, args.packets, ngpu, args.mode))
 
     kernel_ms, replay_ms = [], []
     if library:
@@ -344,13 +375,21 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    # ---- cold build: the first table of the loaded topology ----
+    # ---- cold build: the first table of the loaded topology, right after the attach phase ----
     barrier()
     t0 = time.perf_counter()
     step()
     barrier()
-    cold_s = max_over_ranks(time.perf_counter() - t0)
+    t1 = time.perf_counter()
+    cold_s = max_over_ranks(t1 - t0)
+    attach_to_table_s = max_over_ranks(t1 - t_att0)
     st_cold = top.stats()
+    # the packet window (same seed chain: every host re-attaches to the same vertex, the table
+    # stays valid), then the timed steps
+    tw0 = time.time()
+    pk = top.synth_packets(SEED, args.hosts, args.packets, 10**9, window0)
+    log(rank, "workload ready (window of %d packets in %.1fs): V=%d E=%d A=%d, %d GPU(s), mode %s"
+        % (args.packets, time.time() - tw0, V, E, A, ngpu, args.mode))
     kernel_ms.clear()
     replay_ms.clear()
     for _ in range(args.warmup):
@@ -472,14 +511,23 @@ def main():
             module_load_ms=round(cs["module_load_ms"], 2),
             build_wait_ms=round(cs["build_wait_ms"], 2),
             attach_prep_ms=round(cs["attach_prep_ms"], 2),
+            attach_phase_ms=round(attach_phase_s * 1e3, 2),
+            first_attach_to_table_ms=round(attach_to_table_s * 1e3, 2),
+            library_first_attach_to_table_ms=round(cs["first_attach_to_table_ms"], 2),
+            serialised_ms=round(cs["attach_prep_ms"] + cold_s * 1e3 - cs["build_wait_ms"], 2),
+            tie_probe=dict(rows=int(cs["tie_probe_rows"]), flagged=int(cs["tie_probe_flagged"]),
+                           ms=round(cs["tie_probe_ms"], 2)),
             host_ms=round(host_ms, 2), host_frac=round(host_ms / (cold_s * 1e3), 4),
             host_preparations=int(cs["csr_host_runs"]),
-            note="ms = the first build call (topology loaded and hosts attached -> first table "
-                 "installed); device init and graph preparation run from the first attach on in "
-                 "a background thread (attach_prep_ms, overlapping the attach phase; the build "
-                 "waits build_wait_ms for it) and then show 0 here; host_ms = host work of the "
-                 "cold build (graph preparation copies + host compute, source ordering, replay "
-                 "CSR); the rest runs on the GPU(s)")
+            note="ms = the first build call, made right after the attach phase (attach_phase_ms: "
+                 "%d hosts, wall clock); device init, graph preparation and the workspace run "
+                 "from the first attach on in a background thread (attach_prep_ms) that overlaps "
+                 "the attaches, and the build waits build_wait_ms for the rest of it; "
+                 "first_attach_to_table_ms = first attach -> first table installed (wall clock); "
+                 "serialised_ms = the preparation and the build one after the other (nothing "
+                 "overlapped); host_ms = host work of the cold build (graph preparation copies + "
+                 "host compute, source ordering, replay CSR); the rest runs on the GPU(s)" %
+                 args.hosts)
         route_roof = None
         if sl:
             rkey = "C5-%d-%d-%d-%s-packet_route_kernel" % (sl[0]["n"], A, ngpu, srch)
@@ -498,17 +546,22 @@ def main():
             log(rank, "cpu baseline: %d sources on 1 thread, %d on %d threads..." % (
                 args.cpu_sample, args.cpu_sample_mt, nt))
             cpu = cpu_baseline(top, attached, args.cpu_sample, args.cpu_sample_mt, nt)
-            nr = min(args.packets, 2_000_000)
+            # C5: the whole window over the pre-built table (the table gather is done first,
+            # outside the timed region), 1 thread and every thread of the job's share
             a_, lat_t, rel_t_, _ = top.table()
+            rl = lat_t[pk["src_col"], pk["dst_col"]]
+            rr = rel_t_[pk["src_col"], pk["dst_col"]]
+            del lat_t, rel_t_
             cpu["packet_routes_per_s"] = cpu_route_baseline(
-                lat_t[pk["src_col"][:nr], pk["dst_col"][:nr]],
-                rel_t_[pk["src_col"][:nr], pk["dst_col"][:nr]], pk["payload"][:nr],
-                pk["state_in"][:nr], pk["now"][:nr], jump)
+                rl, rr, pk["payload"], pk["state_in"], pk["now"], jump, 1)
+            cpu["packet_routes_per_s_all_cores"] = cpu_route_baseline(
+                rl, rr, pk["payload"], pk["state_in"], pk["now"], jump, nt)
+            cpu["packet_route_sample"] = "the whole %d-packet window" % len(rl)
             cpu["host_nproc"] = os.cpu_count()
             cpu["job_cpu_share"] = nt
         complete = None
         if ngpu == 1 and not args.no_complete:
-            complete = complete_table_lines()
+            complete = complete_table_lines(nthreads=cpu_share())
         out = {
             "metric": "routing-table build GTEPS + packet-routes/sec at 1/2/4/8 MI355X "
                       "(%HBM roofline)",
@@ -548,7 +601,12 @@ def main():
             "ambiguous_pairs": st["ambiguous_pairs"],
             "exchange": dict(kind={0: "none", 1: "rccl", 2: "peer copies"}.get(
                 int(st["exchange_kind"]), "?") if library else "torch.distributed",
-                             ms=round(st["exchange_ms"], 2)),
+                             ms=round(st["exchange_ms"], 2),
+                             bytes_per_device=int(st["exchange_bytes"]) if library else
+                             int((world - 1) * (table.r1 - table.r0) * (A * 18 + 8)),
+                             gb_per_s_per_device=round(int(st["exchange_bytes"]) / 1e6 /
+                                                       max(1e-9, st["exchange_ms"]), 2)
+                             if library and st["exchange_ms"] > 0 else None),
             # rows whose target chains cross a d-tied parent, recomputed in igraph's heap pop order
             # by heap_replay_kernel (its time is inside ms_per_step and stated separately here)
             "replay": dict(rows=st["replay_rows"], ms=round(r_ms, 3),

@@ -113,11 +113,12 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * "replay_int_keys" (1: u32 heap keys when every latency is an integer and V x max latency
  * < 2^32 - 1 -- exact; 0: always f64 keys), "tie_dense"
  * (-1 auto / 0 / 1: every row through the replay, no batch kernel, once a build replayed >= 90 %
- * of its rows), "devices" (N:
+ * of its rows or, on integer latencies, a 64-row probe before the first batched build found
+ * >= 90 % of its rows crossing a tie), "devices" (N:
  * the table is built by N GPUs of this process -- rows sharded, RCCL all-gather of the rows and
  * all-reduce(MIN) of the minimum; devices device..device+N-1), "rccl" (1: use that exchange even
- * with one device), "batch" (sources per SSSP workgroup: 8; 2 / 4 / 16; 1 = single-source
- * kernel), "batch_fill" (sources per batch, <= batch; 0 = auto: the fewest that finish the rows
+ * with one device), "batch" (sources per SSSP workgroup: 8; 2 / 4 / 16; any other value is
+ * rejected), "batch_fill" (sources per batch, <= batch; 0 = auto: the fewest that finish the rows
  * in the same rounds of the slots), "source_order" / "batch_order" (row grouping and batch
  * dequeue order), "target_skip" (1: the batch relaxation drops pairs into
  * non-target vertices that would relax nothing reaching a target), "target_kappa" (iterations of
@@ -177,6 +178,13 @@ int shdtopo_route_batch_vertices(Topology* top, const int32_t* srcVertex, const 
                                  const uint32_t* payloadLength, const uint32_t* rngState,
                                  const uint64_t* now, size_t n, uint64_t jumpNs,
                                  int clampInterHost, TopoPacketOut* out);
+/* Window bookkeeping of the engine-side adapter (include/shd_topology_window.h): while at least
+ * one window is registered (hold +1 at topowindow_new, -1 at topowindow_free), a vertex that
+ * loses its last host keeps its table column until shdtopo_window_release (called by every
+ * flush after it routed), so the packets it emitted in the window are routed as the reference
+ * routed them at emit.  Returns 0, -1 on a NULL topology. */
+int shdtopo_window_hold(Topology* top, int delta);
+int shdtopo_window_release(Topology* top);
 
 /* Route n packets whose inputs are resident in HBM (SoA, attached-column indices). */
 int shdtopo_route_batch_device(Topology* top, const int32_t* d_srcCol, const int32_t* d_dstCol,
@@ -218,7 +226,7 @@ typedef struct {
                                  entries skipped (events 1, 2, 6, 7 need option "events") */
     int64_t far_scan_sources; /* sources that overflowed a queue (scanning buckets instead) */
     double split_ms;          /* bucket changes + refills, summed over workgroups (in phase 1) */
-    int64_t batch;            /* sources per SSSP workgroup of the last build (1 = single-source) */
+    int64_t batch;            /* sources per SSSP workgroup of the last build (0: complete graph) */
     int64_t lds_hubs;         /* LDS-resident hub rows of the last SSSP launch */
     int64_t replay_rows;      /* rows recomputed by the exact igraph heap replay (rows with a
                                  d-tied parent on a target chain; every row of a directed graph) */
@@ -300,6 +308,18 @@ typedef struct {
                                    host's attach phase; 0 if it did not run) */
     int64_t replay_int_keys;    /* 1: the last replay ran on u32 heap keys (every latency an
                                    integer, V x max latency < 2^32 - 1: exact), 0: f64 keys */
+    int64_t tie_probe_rows;     /* the last build's tie probe (integer latencies, before the first
+                                   batched build): sample rows run through the batch kernel, */
+    int64_t tie_probe_flagged;  /*   of which crossing a d-tied parent (>= 90 %: tie-dense, every
+                                     row goes straight to the heap replay) */
+    double tie_probe_ms;        /*   and its wall time */
+    double first_attach_to_table_ms; /* wall time from the first attach to the first table
+                                        installed (once per topology; 0 before) */
+    int64_t exchange_bytes;     /* bytes each device received in the last row exchange (all-gather
+                                   of the other devices' rows, hops and row minima) */
+    int64_t csr_host_runs_total; /* host-side graph preparations since the topology was loaded,
+                                    the owner's and every peer engine's, the attach-time
+                                    preparation thread's included */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

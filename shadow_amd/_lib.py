@@ -50,7 +50,10 @@ class ShdStats(ctypes.Structure):
                 ("workspace_ms", dbl), ("csr_step_ms", dbl * 8), ("module_load_ms", dbl),
                 ("build_wall_ms", dbl), ("walk_steps", i64), ("build_step_ms", dbl * 8),
                 ("exchange_kind", i64), ("walk_kinds", i64 * 4),
-                ("build_wait_ms", dbl), ("attach_prep_ms", dbl), ("replay_int_keys", i64)]
+                ("build_wait_ms", dbl), ("attach_prep_ms", dbl), ("replay_int_keys", i64),
+                ("tie_probe_rows", i64), ("tie_probe_flagged", i64), ("tie_probe_ms", dbl),
+                ("first_attach_to_table_ms", dbl), ("exchange_bytes", i64),
+                ("csr_host_runs_total", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):
@@ -95,6 +98,8 @@ SIGNATURES = {
                                                   P, P, P]),
     "shdtopo_route_batch_device_slot": (ctypes.c_int, [P, ctypes.c_int, P, P, P, P, P, i64, u64,
                                                        ctypes.c_int, P, P, P, P]),
+    "shdtopo_window_hold": (ctypes.c_int, [P, ctypes.c_int]),
+    "shdtopo_window_release": (ctypes.c_int, [P]),
     "shdtopo_route_batch_vertices": (ctypes.c_int, [P, P, P, P, P, P, ctypes.c_size_t, u64,
                                                     ctypes.c_int, P]),
     "shdtopo_get_lazy_minimum_latency": (dbl, [P]),
@@ -144,8 +149,10 @@ class LibraryMissing(RuntimeError):
     pass
 
 
-def _bind(L, sigs):
+def _bind(L, sigs, optional=False):
     for name, (res, args) in sigs.items():
+        if optional and not hasattr(L, name):
+            continue  # an A/B build of an older revision (SHDTOPO_LIB) lacks newer entry points
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -164,5 +171,5 @@ def load():
     _shim = ctypes.CDLL(SHIM_PATH, mode=ctypes.RTLD_GLOBAL)
     _bind(_shim, SHIM_SIGNATURES)
     _lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-    _bind(_lib, SIGNATURES)
+    _bind(_lib, SIGNATURES, optional=bool(os.environ.get("SHDTOPO_LIB")))
     return _lib, _shim

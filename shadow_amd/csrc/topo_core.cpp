@@ -3,7 +3,8 @@
 // Reference: src/topology/shd-topology.c (Shadow v1.11.1).  What changes against the reference:
 //   * paths are not computed lazily one igraph Dijkstra at a time under a global lock
 //     (shd-topology.c:673-833); the whole attached-vertex table is built on the
-//     GPU on first use after the attach set settles (sssp_rows_kernel / pair_table_complete);
+//     GPU on first use after the attach set settles (sssp_batch_kernel + heap_replay_kernel /
+//     pair_table_complete_kernel);
 //   * getters read an immutable table; the reference's first-rooted-wins cache behaviour
 //     (shd-topology.c:894-915) is reproduced with per-source "materialised"
 //     flags (lazy mode, default) so answers and the min-latency trajectory are bit-identical
@@ -175,6 +176,11 @@ struct _Topology {
     std::atomic<bool> prepStarted{false};
     std::thread prepThread;
     double prepBgMs = 0.0;       // the thread's wall time
+    // wall clock of the first attach, and whether the first table since then was installed
+    // (ShdStats.first_attach_to_table_ms)
+    std::chrono::steady_clock::time_point firstAttachT;
+    std::atomic<bool> firstAttachSet{false};
+    bool firstTableDone = false;
     int prepBgRc = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
@@ -184,9 +190,9 @@ struct _Topology {
     // multi-GPU build, which copy the device CSR from this engine instead of preparing it again
     std::shared_ptr<HostPrep> hp;
     int64_t csrHostRuns = 0;    // host-side preparations (peers that copied count none)
-    DevBuf<uint32_t> d_spt;     // per vertex {parent, slot of (v -> parent) in v's row, f64 latency}
+    // per vertex, 32 B: {parent, slot of (v -> parent) in v's row, f64 latency, f64 loss, pad}
+    DevBuf<uint32_t> d_spt;
     DevBuf<uint32_t> d_sptPar;  // per vertex: h0-tree parent
-    DevBuf<double> d_sptLoss;   // per vertex: loss of the h0-tree edge (the parent pass' record)
     // the parsed edge arrays (document order) and old -> new ids, kept in HBM after the graph
     // preparation: the heap replay's CSR is built from them (prep_replay_csr)
     DevBuf<int32_t> d_eu, d_ev;
@@ -194,6 +200,7 @@ struct _Topology {
     DevBuf<uint32_t> d_inv;
     int wsK = 0;                // batch width the workspace was laid out for
     int64_t wsRing = 0;
+    size_t wsHpar = 0;          // hub-hint entries per slot the workspace was sized for
     DevBuf<uint32_t> d_rowptr, d_adj;
     DevBuf<uint32_t> d_adjk;  // rows re-sorted by kappa = w - pi(col) (batch relaxation copy)
     DevBuf<float> d_kap, d_ksum, d_kap0;  // kappa of d_adjk (f32, rounded down), per-vertex probes
@@ -231,9 +238,14 @@ struct _Topology {
     bool replayAll = false;   // option "replay_all" (test hook: every row through the replay)
     // option "tie_dense": -1 auto, 0 never, 1 always.  A tie-dense topology (integer latencies:
     // C4-int replays every row) skips the batch kernel, whose rows the replay would recompute
-    // anyway; auto turns it on after a build of >= 64 rows that replayed >= 90 % of them.
+    // anyway; auto turns it on after a build of >= 64 rows that replayed >= 90 % of them, or
+    // before the first batched build of an integer-latency topology when a probe of
+    // kTieProbeRows sample rows (batch kernel) finds >= 90 % of them crossing a tie.
     int tieDenseOpt = -1;
     bool tieDense = false;
+    bool tieProbed = false;
+    DevBuf<uint32_t> d_probeSrc;
+    DevBuf<double> d_probeSh;
     int replaySlotsOpt = 0;   // option "replay_slots" (0 = sized from the CUs and free HBM)
     bool replayLandmark = true;  // option "replay_landmark": skip edges into vertices the
                                  // landmark bound proves popped (topo_replay.hip)
@@ -316,6 +328,10 @@ struct _Topology {
     // a miss.  Epochs are ipGen values: per vertex the attach intervals [start, end) of "at
     // least one host on it", per source vertex the epochs it was materialised at.
     std::vector<uint32_t> hostsOn;                             // hosts per vertex (ipMu)
+    // window adapters registered (shdtopo_window_hold) and the vertices that lost their last
+    // host since the last flush: they stay table columns until shdtopo_window_release (ipMu)
+    int windows = 0;
+    std::vector<int32_t> deferredOff;
     std::unordered_map<int32_t, std::vector<std::pair<uint64_t, uint64_t>>> ivals;  // (ipMu)
     std::atomic<uint64_t> lastNewEpoch{0};                     // latest interval start
     std::unique_ptr<std::atomic<uint64_t>[]> matGen;          // per vertex: latest epoch
@@ -527,6 +543,8 @@ int upload_csr(Topology* top) {
 // among the first kGroupHubs vertices of the degree order (the count the former single-source
 // kernel held in LDS, where the grouping was tuned).
 constexpr int64_t kGroupHubs = 16565;
+// sample rows of the tie probe (enqueue_rows): 8 batches of 8, one short launch
+constexpr int64_t kTieProbeRows = 64;
 
 // Graph preparation.  Directed topologies only run the heap replay (its out-edge
 // rows, upload_replay) and keep their labels.  Undirected ones are prepared on the GPU
@@ -671,10 +689,9 @@ int upload_csr_impl(Topology* top) {
     top->stats.csr_h0_rounds = iters;
     step_done(3);
     HIPCHK(top->d_sptPar.ensure((size_t)V));
-    HIPCHK(top->d_spt.ensure(4 * (size_t)V));
-    HIPCHK(top->d_sptLoss.ensure((size_t)V));
+    HIPCHK(top->d_spt.ensure(8 * (size_t)V));
     HIPCHK(prep_tree(V, nadj, hub_segs(top), top->d_rowptr.p, top->d_adj.p, top->d_aloss.p, top->d_pot.p,
-                     top->d_sptPar.p, top->d_spt.p, top->d_sptLoss.p, &top->hp->piMax, st));
+                     top->d_sptPar.p, top->d_spt.p, &top->hp->piMax, st));
     step_done(4);
     // 4) the kappa-sorted relaxation copy
     HIPCHK(top->d_adjk.ensure(4 * (size_t)nadj));
@@ -726,7 +743,6 @@ DevCSR dev_csr(Topology* top) {
     c.ksum = reinterpret_cast<const float4*>(top->d_ksum.p);
     c.kap0 = top->d_kap0.p;
     c.spt = top->d_spt.p;
-    c.sptLoss = top->d_sptLoss.p;
     c.piMax = top->hp->piMax;
     c.aloss = top->d_aloss.p;
     c.vloss = top->d_vloss.p;
@@ -740,13 +756,13 @@ DevCSR dev_csr(Topology* top) {
 int batch_k(Topology* top) { return top->batchK; }  // 2, 4, 8 or 16 (shdtopo_set_option)
 
 // Per-slot u32 scratch after the parent pass' V * K pair list: the merged vertex list (V), the
-// sweep's pending bitmap, the (vertex, source) tie bitmap and the touched-line bitmap (a tail
-// vertex whose distance line the batch lowered from +inf: only those lines are reset for the
-// next batch).
+// sweep's pending bitmap and the touched-line bitmap (a tail vertex whose distance line the batch
+// lowered from +inf: only those lines are reset for the next batch).  Ties live in the pair
+// records' tag words (topo_sssp_batch.hip kTagTie).
 int64_t bitmap_words(int64_t n) { return (n + 31) / 32 + 64; }
 int64_t ring_entries(Topology* top, int K) {
     const int64_t V = top->g.V;
-    return V * (K + 1) + bitmap_words(V) + bitmap_words(V * K) + bitmap_words(V);
+    return V * (K + 1) + bitmap_words(V) + bitmap_words(V);
 }
 int64_t queue_stride(Topology* top, int K) {  // u64 per slot of each near queue / pair list
     const int64_t V = top->g.V;
@@ -781,7 +797,9 @@ int ensure_workspace(Topology* top, int nsrc) {
     int memcap = (int)std::max<size_t>(1, ((freeb + held) * 3 / 5) / per_slot);
     want = std::min(want, memcap);
     want = std::max(1, std::min(want, std::max(1, units)));
-    if (top->slots >= want && top->wsK == K && top->wsRing == ringE) return 0;
+    // hparN follows par_hubs: the kernel indexes the hints at slot * P * K with the current P
+    if (top->slots >= want && top->wsK == K && top->wsRing == ringE && top->wsHpar >= hparN)
+        return 0;
     const auto tw0 = std::chrono::steady_clock::now();
     if (top->slots > 0) {
         // layout change: release before re-allocating
@@ -818,6 +836,7 @@ int ensure_workspace(Topology* top, int nsrc) {
     top->slots = want;
     top->wsK = K;
     top->wsRing = ringE;
+    top->wsHpar = hparN;
     top->stats.slots = want;
     top->stats.workspace_ms = std::chrono::duration<double, std::milli>(
         std::chrono::steady_clock::now() - tw0).count();
@@ -990,6 +1009,7 @@ uint64_t compute_geometry(Topology* top) {
         vs.reserve(top->virtualIP.size());
         for (auto& kv : top->virtualIP)
             if (kv.second >= 0) vs.push_back(kv.second);
+        vs.insert(vs.end(), top->deferredOff.begin(), top->deferredOff.end());
     }
     std::sort(vs.begin(), vs.end());
     vs.erase(std::unique(vs.begin(), vs.end()), vs.end());
@@ -1013,9 +1033,9 @@ double default_delta(Topology* top) {
     if (top->delta > 0) return top->delta;
     edge_scan(top);
     const double mean = top->meanLat;
-    // tuned on C4: single-source 0.06 x mean (~3 ms); the batch kernel gains from
-    // wider buckets (sources of a batch share more expansions) up to 0.2 x mean (~10 ms)
-    return std::max(1e-9, (batch_k(top) > 1 ? 0.2 : 0.06) * mean);
+    // tuned on C4: the batch kernel gains from wide buckets (the sources of a batch
+    // share more expansions) up to 0.2 x mean (~10 ms)
+    return std::max(1e-9, 0.2 * mean);
 }
 
 // wall checkpoints of a whole-table build (ShdStats.build_step_ms): the time since the previous
@@ -1033,6 +1053,8 @@ void reset_build_stats(Topology* top) {
     top->stats.order_ms = top->stats.replay_prep_ms = top->stats.target_prep_ms = 0.0;
     top->stats.workspace_ms = 0.0;
     top->stats.csr_host_runs = 0;
+    top->stats.tie_probe_rows = top->stats.tie_probe_flagged = 0;
+    top->stats.tie_probe_ms = 0.0;
 }
 
 // Enqueue rows [row0,row1) into out buffers (device pointers) on `st`.
@@ -1081,7 +1103,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         const bool dense = top->tieReplay && (top->tieDenseOpt == 1 ||
                                               (top->tieDenseOpt < 0 && top->tieDense));
         const bool allReplay = top->isDirected || top->replayAll || top->hasMultiEdges || dense;
-        top->stats.tie_dense = dense ? 1 : 0;
+        bool probeDense = false;  // the tie probe below found the topology tie-dense
         std::vector<uint32_t> src((size_t)rows), tgt((size_t)A);
         for (int64_t i = 0; i < rows; i++) src[(size_t)i] = (uint32_t)top->hp->inv[(size_t)top->attached[(size_t)(row0 + i)]];
         for (int64_t i = 0; i < A; i++) tgt[(size_t)i] = (uint32_t)top->hp->inv[(size_t)top->attached[(size_t)i]];
@@ -1158,7 +1180,57 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 top->adjkPlain = false;
                 top->adjkResorted = top->targetResort;
             }
-            {
+            // Tie probe (integer latencies, before the first batched build of the topology):
+            // the batch kernel on kTieProbeRows sample rows (the range's first rows, written in
+            // place); if >= 90 % of them cross a d-tied parent the topology is tie-dense and
+            // every row goes straight to the heap replay -- the batch kernel would only compute
+            // rows the replay recomputes (C4-int: 0.93 s of batch kernel per first build).
+            if (top->tieReplay && top->tieDenseOpt < 0 && !top->tieDense && !top->tieProbed &&
+                rows >= 2 * kTieProbeRows) {
+                edge_scan(top);
+                if (top->replayIntOk) {
+                    top->tieProbed = true;
+                    const auto tq0 = std::chrono::steady_clock::now();
+                    const int64_t P = kTieProbeRows;
+                    const double delta = default_delta(top);
+                    const double pmax = top->hp->piMax;
+                    std::vector<double> sh((size_t)P);
+                    for (int64_t i = 0; i < P; i++) {
+                        const double pp = top->hp->pot[(size_t)src[(size_t)i]];
+                        sh[(size_t)i] = (pmax - (std::isfinite(pp) ? pp : pmax)) + 2.0 * delta;
+                    }
+                    HIPCHK(top->d_probeSrc.ensure((size_t)P));
+                    HIPCHK(top->d_probeSh.ensure((size_t)P));
+                    HIPCHK(hipMemcpyAsync(top->d_probeSrc.p, src.data(), 4 * (size_t)P, hipMemcpyHostToDevice, st));
+                    HIPCHK(hipMemcpyAsync(top->d_probeSh.p, sh.data(), 8 * (size_t)P, hipMemcpyHostToDevice, st));
+                    SlotWs pws = ws;
+                    pws.rowmap = nullptr;  // sample row i -> output row i
+                    const SsspLdsPlan bp = sssp_batch_lds_plan(
+                        K, top->hubLimit, (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 20)),
+                        top->g.V);
+                    HIPCHK(launch_sssp_batch(K, dev_csr(top), pws, top->d_probeSrc.p, top->d_probeSh.p,
+                                             (int)P, K, top->d_targets.p, (int)A, delta, bp,
+                                             top->iterGuard, out_lr, out_hops, out_rowmin,
+                                             top->d_stats.p, st));
+                    std::vector<uint8_t> fl((size_t)P);
+                    HIPCHK(hipMemcpyAsync(fl.data(), top->d_rowflag.p, (size_t)P, hipMemcpyDeviceToHost, st));
+                    HIPCHK(hipStreamSynchronize(st));
+                    int64_t nf = 0;
+                    for (uint8_t x : fl) nf += x ? 1 : 0;
+                    top->stats.tie_probe_rows = P;
+                    top->stats.tie_probe_flagged = nf;
+                    if (nf * 10 >= P * 9) top->tieDense = true;
+                    // the build's statistics and row flags start over (the rows are recomputed)
+                    HIPCHK(hipMemsetAsync(top->d_stats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
+                    HIPCHK(launch_fill_u64(top->d_stats.p + ST_GLOBAL_MIN, 0x7FF0000000000000ull, 1, st));
+                    HIPCHK(hipMemsetAsync(top->d_rowflag.p, 0, (size_t)rows, st));
+                    HIPCHK(hipStreamSynchronize(st));
+                    top->stats.tie_probe_ms = std::chrono::duration<double, std::milli>(
+                        std::chrono::steady_clock::now() - tq0).count();
+                }
+            }
+            probeDense = top->tieReplay && top->tieDenseOpt < 0 && top->tieDense;
+            if (!probeDense) {
                 const auto to0 = std::chrono::steady_clock::now();
                 // sources per batch: a shard that leaves slots idle at K (8-GPU builds: 1250
                 // rows = 157 batches for 256 slots) spreads over every slot with fewer sources
@@ -1314,8 +1386,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                                          delta, bp, top->iterGuard, out_lr, out_hops,
                                          out_rowmin, top->d_stats.p, st));
                 HIPCHK(hipEventRecord(top->ev1, st));
+                HIPCHK(hipStreamSynchronize(st));  // the kernel's wall time goes to step 3
                 bstep_mark(top, 3);
-                HIPCHK(hipStreamSynchronize(st));  // sh must outlive the async copy
                 if (ws.btrace) {
                     std::vector<unsigned long long> bt((size_t)nbt * 8);
                     HIPCHK(hipMemcpy(bt.data(), ws.btrace, 64 * (size_t)nbt, hipMemcpyDeviceToHost));
@@ -1340,7 +1412,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         HIPCHK(hipStreamSynchronize(st));
         // rows that need igraph's heap pop order: replayed exactly on the GPU
         std::vector<uint32_t> rlist;
-        if (allReplay) {
+        top->stats.tie_dense = dense || probeDense ? 1 : 0;
+        if (allReplay || probeDense) {
             rlist.resize((size_t)rows);
             std::iota(rlist.begin(), rlist.end(), 0u);
         } else if (top->tieReplay) {
@@ -1599,7 +1672,6 @@ int copy_csr_from(Topology* p, int pdev, Topology* o, int odev) {
     HIPCHK(peer_copy(p->d_kap0, pdev, o->d_kap0, odev, st));
     HIPCHK(peer_copy(p->d_spt, pdev, o->d_spt, odev, st));
     HIPCHK(peer_copy(p->d_sptPar, pdev, o->d_sptPar, odev, st));
-    HIPCHK(peer_copy(p->d_sptLoss, pdev, o->d_sptLoss, odev, st));
     HIPCHK(peer_copy(p->d_pot, pdev, o->d_pot, odev, st));
     HIPCHK(peer_copy(p->d_aloss, pdev, o->d_aloss, odev, st));
     HIPCHK(peer_copy(p->d_vloss, pdev, o->d_vloss, odev, st));
@@ -1678,6 +1750,7 @@ int build_multi(Topology* top) {
                     int rr = dev_init(T);
                     if (rr) return rr;
                     T->meanLat = top->meanLat;
+                    T->replayIntOk = top->replayIntOk;  // the owner's edge scan (same graph)
                     if (!top->isComplete && !T->csrUploaded) {
                         rr = copy_csr_from(T, phys[(size_t)d], top, phys[0]);
                         if (rr) return rr;
@@ -1755,6 +1828,8 @@ int build_multi(Topology* top) {
         }
     }
     top->stats.exchange_kind = N > 1 || top->forceRccl ? (useRccl ? 1 : 2) : 0;
+    // per device: the other devices' rows ({lat, rel} + hops) and row minima
+    top->stats.exchange_bytes = (int64_t)(N - 1) * R * (A * (int64_t)(sizeof(double2) + 2) + 8);
     if (useRccl) {
         RcclApi& api = rccl();
         NCCLCHK(api.groupStart());
@@ -1847,6 +1922,7 @@ int ensure_table(Topology* top) {
     for (Topology* p : top->peers) runs0 += p->csrHostRuns;
     top->stats.devices = 1;
     top->stats.exchange_ms = 0.0;
+    top->stats.exchange_bytes = 0;
     if (A > 0 && (top->devicesOpt > 1 || top->forceRccl)) {
         r = build_multi(top);
         if (r) return r;
@@ -1875,11 +1951,17 @@ int ensure_table(Topology* top) {
     int64_t runs1 = top->csrHostRuns;
     for (Topology* p : top->peers) runs1 += p->csrHostRuns;
     top->stats.csr_host_runs = runs1 - runs0;
+    top->stats.csr_host_runs_total = runs1;
     top->stats.build_wall_ms = std::chrono::duration<double, std::milli>(
         std::chrono::steady_clock::now() - tb0).count();
     top->tableGen.store(sg, std::memory_order_release);
     top->tableSerial.fetch_add(1);
     top->tableValid.store(true, std::memory_order_release);
+    if (!top->firstTableDone && top->firstAttachSet.load()) {
+        top->firstTableDone = true;
+        top->stats.first_attach_to_table_ms = std::chrono::duration<double, std::milli>(
+            std::chrono::steady_clock::now() - top->firstAttachT).count();
+    }
     if (!top->lazy && A > 0) push_min_to_engine(top->eagerMin);
     return 0;
 }
@@ -2141,6 +2223,12 @@ void host_off(Topology* top, int32_t v) {
     if (--top->hostsOn[(size_t)v] == 0) {
         auto& iv = top->ivals[v];
         if (!iv.empty()) iv.back().second = top->ipGen;
+        if (top->windows > 0) {
+            // a window adapter may hold packets this vertex emitted or was sent: the column stays
+            // until the flush (shdtopo_window_release), the table stays valid
+            top->deferredOff.push_back(v);
+            return;
+        }
         top->setGen.fetch_add(1);
     }
 }
@@ -2176,6 +2264,13 @@ void start_attach_prep(Topology* top) {
 }
 
 void do_attach(Topology* top, uint32_t ip, int32_t v, uint64_t* bwDownOut, uint64_t* bwUpOut) {
+    if (!top->firstAttachSet.load(std::memory_order_relaxed)) {
+        std::unique_lock<std::shared_mutex> lk(top->ipMu);
+        if (!top->firstAttachSet.load()) {
+            top->firstAttachT = std::chrono::steady_clock::now();
+            top->firstAttachSet.store(true);
+        }
+    }
     start_attach_prep(top);
     {
         std::unique_lock<std::shared_mutex> lk(top->ipMu);
@@ -2283,11 +2378,17 @@ void topology_free(Topology* top) {
 int shdtopo_set_option(Topology* top, const char* key, double value) {
     if (!top || !key) return -1;
     std::string k(key);
+    // the attach-time preparation thread and the builders read the options under buildMu
+    std::lock_guard<std::mutex> lk(top->buildMu);
     if (k == "abort_on_error") top->abortOnError = value != 0;
     else if (k == "lazy") top->lazy = value != 0;
     else if (k == "delta") top->delta = value;
     else if (k == "slots") top->slotsOpt = (int)value;
-    else if (k == "device") top->device = (int)value;
+    else if (k == "device") {
+        // the device is fixed once the attach-time preparation (or a build) initialised it
+        if ((top->prepStarted.load() || top->devInit) && (int)value != top->device) return -1;
+        top->device = (int)value;
+    }
     else if (k == "prepare_on_attach") top->prepOnAttach = value != 0;
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
     else if (k == "par_hubs") top->parHubs = (int64_t)value;
@@ -2312,11 +2413,9 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "devices") {
         const int n = (int)value;
         if (n < 1 || n > 64) return -1;
-        std::lock_guard<std::mutex> lk(top->buildMu);
         if (n != top->devicesOpt) top->tableValid.store(false);
         top->devicesOpt = n;
     } else if (k == "rccl") {
-        std::lock_guard<std::mutex> lk(top->buildMu);
         top->forceRccl = value != 0;
         top->tableValid.store(false);
     }
@@ -2452,6 +2551,24 @@ int shdtopo_build_rows(Topology* top, int64_t row0, int64_t row1, void* d_lr, vo
     top->bstepT = std::chrono::steady_clock::now();
     const int64_t runs0 = top->csrHostRuns;
     hipStream_t st = stream ? (hipStream_t)stream : top->stream;
+    if (top->extLr) {
+        // rows written into a table bound by reference (shdtopo_bind_table_ref): the bound table
+        // is no longer a finished table, so the getters must not read it until it is bound again
+        const char* b0 = (const char*)top->extLr;
+        const char* b1 = b0 + sizeof(double2) * (size_t)(top->A * top->A);
+        const char* h0 = (const char*)top->extHops;
+        const char* h1 = h0 + sizeof(uint16_t) * (size_t)(top->A * top->A);
+        const size_t nr = (size_t)((row1 - row0) * top->A);  // d_lr / d_hops: row row0's output
+        const char* o0 = (const char*)d_lr;
+        const char* o1 = o0 + sizeof(double2) * nr;
+        const char* p0 = (const char*)d_hops;
+        const char* p1 = p0 + sizeof(uint16_t) * nr;
+        if ((o0 < b1 && b0 < o1) || (p0 < h1 && h0 < p1)) {
+            top->tableValid.store(false);
+            top->extLr = nullptr;
+            top->extHops = nullptr;
+        }
+    }
     r = enqueue_rows(top, row0, row1, (double2*)d_lr, (uint16_t*)d_hops, (double*)d_rowmin, st);
     if (r) return r;
     top->stats.csr_host_runs = top->csrHostRuns - runs0;
@@ -2687,6 +2804,23 @@ int topology_routePacketBatch(Topology* top, const TopoPacketIn* in, TopoPacketO
     return r < 0 ? (int)r : (int)std::min<int64_t>(r, INT32_MAX);
 }
 
+int shdtopo_window_hold(Topology* top, int delta) {
+    if (!top) return -1;
+    std::unique_lock<std::shared_mutex> lk(top->ipMu);
+    top->windows = std::max(0, top->windows + delta);
+    return 0;
+}
+
+int shdtopo_window_release(Topology* top) {
+    if (!top) return -1;
+    std::unique_lock<std::shared_mutex> lk(top->ipMu);
+    if (top->deferredOff.empty()) return 0;
+    top->deferredOff.clear();
+    top->ipGen++;  // the columns change: recomputed (and the table rebuilt) on the next query
+    top->setGen.fetch_add(1);
+    return 0;
+}
+
 int shdtopo_route_batch_vertices(Topology* top, const int32_t* srcVertex, const int32_t* dstVertex,
                                  const uint32_t* payloadLength, const uint32_t* rngState,
                                  const uint64_t* now, size_t n, uint64_t jumpNs,
@@ -2846,10 +2980,21 @@ int shdtopo_synth_packets(Topology* top, uint64_t seed, int64_t n_hosts, int64_t
     }
     if (relays.empty()) relays.push_back(0);
     if (servers.empty()) servers = relays;
+    if (n_packets <= 0) return 0;  // the attach phase only
+    // the table's columns (ascending attached vertex) from the attach table itself: the harness
+    // takes no build lock, so any wait for the attach-time preparation shows in the build
+    std::vector<int32_t> cols;
     {
-        std::lock_guard<std::mutex> lk(top->buildMu);
-        compute_geometry(top);
+        std::shared_lock<std::shared_mutex> lk(top->ipMu);
+        cols.reserve(top->virtualIP.size());
+        for (auto& kv : top->virtualIP)
+            if (kv.second >= 0) cols.push_back(kv.second);
     }
+    std::sort(cols.begin(), cols.end());
+    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+    auto colOf = [&](int32_t v) {
+        return (int32_t)(std::lower_bound(cols.begin(), cols.end(), v) - cols.begin());
+    };
     SplitMix rng(seed ^ 0x5eed5eed5eedull);
     for (int64_t k = 0; k < n_packets; k++) {
         int64_t s = (int64_t)rng.below((uint64_t)n_hosts);
@@ -2860,8 +3005,8 @@ int shdtopo_synth_packets(Topology* top, uint64_t seed, int64_t n_hosts, int64_t
             else d = (rng.below(2) == 0) ? relays[(size_t)rng.below(relays.size())]
                                          : servers[(size_t)rng.below(servers.size())];
         } while (d == s && n_hosts > 1 && relays.size() + servers.size() > 1);
-        srcCol[k] = top->colOf[(size_t)hostVertex[(size_t)s]];
-        dstCol[k] = top->colOf[(size_t)hostVertex[(size_t)d]];
+        srcCol[k] = colOf(hostVertex[(size_t)s]);
+        dstCol[k] = colOf(hostVertex[(size_t)d]);
         payload[k] = rng.uniform() < 0.8 ? 1448u : 0u;
         stateIn[k] = hostState[(size_t)s];
         (void)glibc_rand_r(&hostState[(size_t)s]);  // the route's draw advances the host stream

@@ -98,8 +98,9 @@ struct DevCSR {
     const float4* ksum = nullptr;   // per vertex: kappa at row positions 0, 1, 3, 7[, 15, 31, 63,
                                     // 127] (kKProbes floats, +inf past the row)
     const float* kap0 = nullptr;    // per vertex: smallest kappa of its row (+inf: empty row)
-    const uint32_t* spt = nullptr;  // per vertex {h0-tree parent, its slot in v's row, f64 w}
-    const double* sptLoss = nullptr; // per vertex: packet loss of that h0-tree edge
+    // per vertex, 32 B: {h0-tree parent, its slot in v's row, f64 w, f64 packet loss of that
+    // edge, pad} (one line per walk hop)
+    const uint32_t* spt = nullptr;
     double piMax = 0.0;             // largest finite pi
     const double* aloss = nullptr;
     const double* vloss = nullptr;
@@ -280,11 +281,11 @@ hipError_t prep_adjacency(int64_t V, int64_t E, int64_t nadj, const int32_t* eu,
 // pi = d(h0, .) from vertex 0 (f64[V], +inf = unreached); *iterations = frontier rounds
 hipError_t prep_h0_distances(int64_t V, const uint32_t* rowptr, const uint32_t* adj, double* pot,
                              int* iterations, hipStream_t st);
-// h0 tree (sptPar u32[V], spt {parent, slot in v's row, f64 w}[V]), the records' pi / kappa0
-// field, *piMax = the largest finite pi; hub rows by segments (hs)
+// h0 tree (sptPar u32[V], spt {parent, slot in v's row, f64 w, f64 loss, pad} 32 B [V]), the
+// records' pi / kappa0 field, *piMax = the largest finite pi; hub rows by segments (hs)
 hipError_t prep_tree(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t* rowptr,
                      uint32_t* adj, const double* aloss, const double* pot, uint32_t* sptPar,
-                     uint32_t* spt, double* sptLoss, double* piMax, hipStream_t st);
+                     uint32_t* spt, double* piMax, hipStream_t st);
 // the plain kappa-sorted relaxation copy (adjk, kap, ksum, kap0) of adj: also restores it after
 // a target-aware re-sort when the target-aware order no longer applies
 hipError_t launch_kappa_copy(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t* rowptr,

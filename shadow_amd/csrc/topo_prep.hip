@@ -336,13 +336,15 @@ __device__ __forceinline__ void tree_scan(const uint32_t* adj, const double* pot
 
 __device__ __forceinline__ void tree_store(uint32_t v, const TreeBest& best, const uint32_t* adj,
                                            const double* aloss, uint32_t* sptPar, uint32_t* spt,
-                                           double* sptLoss, double kmin, double* kap0d) {
+                                           double kmin, double* kap0d) {
     const bool ok = best.u != 0xFFFFFFFFu;
     sptPar[v] = ok ? best.u : 0xFFFFFFFFu;
-    sptLoss[v] = ok ? aloss[best.k] : 0.0;
+    // 32-B record {parent, slot, f64 w, f64 loss, pad}: a walk hop reads it as one line
+    const unsigned long long lb = ok ? d2bits(aloss[best.k]) : 0ull;
     uint4 r = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     if (ok) r = make_uint4(best.u, best.k, adj[kAdjWords * best.k + 2], adj[kAdjWords * best.k + 3]);
-    reinterpret_cast<uint4*>(spt)[v] = r;
+    reinterpret_cast<uint4*>(spt)[2 * (size_t)v] = r;
+    reinterpret_cast<uint4*>(spt)[2 * (size_t)v + 1] = make_uint4((uint32_t)lb, (uint32_t)(lb >> 32), 0u, 0u);
     kap0d[v] = kmin;
 }
 
@@ -363,8 +365,7 @@ __global__ void __launch_bounds__(kPB)
 prep_tree_kernel(int64_t V, HubSegs hs, const uint32_t* __restrict__ rowptr,
                  const uint32_t* __restrict__ adj, const double* __restrict__ aloss,
                  const double* __restrict__ pot, uint32_t* __restrict__ sptPar,
-                 uint32_t* __restrict__ spt, double* __restrict__ sptLoss,
-                 double* __restrict__ kap0d, unsigned long long* __restrict__ pimax,
+                 uint32_t* __restrict__ spt, double* __restrict__ kap0d, unsigned long long* __restrict__ pimax,
                  TreeBest* __restrict__ pbest, double* __restrict__ pkmin) {
     const uint32_t lane = threadIdx.x & 63u;
     const int64_t nw = gstride() >> 6;
@@ -381,7 +382,7 @@ prep_tree_kernel(int64_t V, HubSegs hs, const uint32_t* __restrict__ rowptr,
         tb_wave_min(best, kmin);
         if (lane == 0) {
             if (sg.y == r0 && e == r1) {
-                tree_store(v, best, adj, aloss, sptPar, spt, sptLoss, kmin, kap0d);
+                tree_store(v, best, adj, aloss, sptPar, spt, kmin, kap0d);
             } else {
                 pbest[s] = best;
                 pkmin[s] = kmin;
@@ -397,7 +398,7 @@ prep_tree_kernel(int64_t V, HubSegs hs, const uint32_t* __restrict__ rowptr,
         TreeBest best = none;
         double kmin = INFINITY;
         tree_scan(adj, pot, (uint32_t)v, dv, rowptr[v], rowptr[v + 1], 1u, best, kmin);
-        tree_store((uint32_t)v, best, adj, aloss, sptPar, spt, sptLoss, kmin, kap0d);
+        tree_store((uint32_t)v, best, adj, aloss, sptPar, spt, kmin, kap0d);
     }
     pm = wave_min_u64(~pm);
     if (lane == 0 && pm != ~0ull) atomicMax(pimax, ~pm);
@@ -407,8 +408,7 @@ prep_tree_kernel(int64_t V, HubSegs hs, const uint32_t* __restrict__ rowptr,
 __global__ void __launch_bounds__(kPB)
 prep_tree_multi_kernel(HubSegs hs, const uint32_t* __restrict__ adj,
                        const double* __restrict__ aloss, uint32_t* __restrict__ sptPar,
-                       uint32_t* __restrict__ spt, double* __restrict__ sptLoss,
-                       double* __restrict__ kap0d, const TreeBest* __restrict__ pbest,
+                       uint32_t* __restrict__ spt, double* __restrict__ kap0d, const TreeBest* __restrict__ pbest,
                        const double* __restrict__ pkmin) {
     const uint32_t lane = threadIdx.x & 63u;
     for (int64_t m = gtid() >> 6; m < (int64_t)hs.nmulti; m += gstride() >> 6) {
@@ -422,7 +422,7 @@ prep_tree_multi_kernel(HubSegs hs, const uint32_t* __restrict__ adj,
             kmin = km < kmin ? km : kmin;
         }
         tb_wave_min(best, kmin);
-        if (lane == 0) tree_store(mr.x, best, adj, aloss, sptPar, spt, sptLoss, kmin, kap0d);
+        if (lane == 0) tree_store(mr.x, best, adj, aloss, sptPar, spt, kmin, kap0d);
     }
 }
 
@@ -736,7 +736,7 @@ void hub_segments(const uint32_t* rowptr_head, uint32_t rows, std::vector<uint2>
 
 hipError_t prep_tree(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t* rowptr,
                      uint32_t* adj, const double* aloss, const double* pot, uint32_t* sptPar,
-                     uint32_t* spt, double* sptLoss, double* piMax, hipStream_t st) {
+                     uint32_t* spt, double* piMax, hipStream_t st) {
     Tmp<double> kap0d, pkmin;
     Tmp<unsigned long long> pm;
     Tmp<TreeBest> pbest;
@@ -747,11 +747,11 @@ hipError_t prep_tree(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t*
     PCHK(hipMemsetAsync(pm.p, 0, 8, st));
     const unsigned g = std::max(grid_for(V), (unsigned)std::min<int64_t>((hs.nseg + 3) / 4, 256 * 64));
     hipLaunchKernelGGL(prep_tree_kernel, dim3(g), dim3(kPB), 0, st, V, hs, rowptr, adj, aloss,
-                       pot, sptPar, spt, sptLoss, kap0d.p, pm.p, pbest.p, pkmin.p);
+                       pot, sptPar, spt, kap0d.p, pm.p, pbest.p, pkmin.p);
     PCHK(hipGetLastError());
     if (hs.nmulti > 0) {
         hipLaunchKernelGGL(prep_tree_multi_kernel, dim3((hs.nmulti + 3) / 4), dim3(kPB), 0, st, hs,
-                           adj, aloss, sptPar, spt, sptLoss, kap0d.p, pbest.p, pkmin.p);
+                           adj, aloss, sptPar, spt, kap0d.p, pbest.p, pkmin.p);
         PCHK(hipGetLastError());
     }
     if (nadj > 0)

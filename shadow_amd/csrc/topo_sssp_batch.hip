@@ -1,7 +1,7 @@
 // topo_sssp_batch.hip -- batched multi-source SSSP for gfx950: one persistent workgroup settles
 // K sources at once (K = 8: the K distances of a vertex are one 64-B line).
 //
-// Replaces, like sssp_rows_kernel, igraph_get_shortest_paths_dijkstra + the per-target helper
+// Replaces igraph_get_shortest_paths_dijkstra + the per-target helper
 // (src/topology/shd-topology.c:561-833): same distances (bit-exact: every latency add is one IEEE
 // add and any label-correcting order reaches the same monotone-rounding fixpoint), same parents
 // (the argmin d[u] rule of SURVEY.md A.3), same per-target epilogue.
@@ -131,6 +131,8 @@ struct LdsB {
     unsigned long long dg[4];   // diagnostic: hub edges, hub source-relaxations, first-iteration
                                 // edges, first-iteration source-relaxations
     unsigned long long touched; // tail lines reset (touched by the slot's previous batches)
+    unsigned long long wk[5];   // parent pass: walk steps; resolved by the h0-tree guess, a
+                                // tail's improver, a hub's improver; pairs sent to row scans
     unsigned long long bt[8];   // SHD_BATCH_TIME builds: wave ticks of tail / hub iterations in
                                 // chunk loads, phase A, phase B; phase-B rounds, active lanes
 };
@@ -170,11 +172,10 @@ struct BView {
     uint32_t* xb;              // LDS: (hub, source) expanded at its current distance
     uint32_t* hpar;            // HBM [P][K]: vertex whose relaxation last lowered hub v for j
     uint32_t* pend;            // HBM, 1 bit per vertex: a tail vertex with a pair pending past cb
-    uint32_t* tie;             // HBM, 1 bit per (tail vertex, source): a relaxation tied its value
     uint32_t* touch;           // HBM, 1 bit per tail vertex: the batch lowered its line from +inf
-    uint32_t* tpar;            // HBM [V][K] pair records (word 0): vertex whose relaxation last
+    uint32_t* tpar;            // HBM [V][K] pair records: word 0 = vertex whose relaxation last
                                // lowered the tail pair (SHD_TAIL_HINT; the parent field before
-                               // the parent pass)
+                               // the parent pass), word 1 = tag word (ties: kTagTie)
     uint32_t H, P;
     __device__ __forceinline__ unsigned long long get(uint32_t v, uint32_t j) const {
         return v < H ? hd[(size_t)v * K + j] : ld_l2_u64(&dist[(size_t)v * K + j]);
@@ -183,8 +184,23 @@ struct BView {
 
 struct BBuckets {
     double inv_delta;
-    uint32_t cb;  // the bucket being settled
+    uint32_t cb;       // the bucket being settled
+    uint32_t tie_tag;  // the batch's tag | kTagTie (pair records of tied tail pairs)
 };
+
+// Pair record tag word (word 1 of the 16-B record): the batch tag ep (30 bits, 1..kTagMask) |
+// kTagClaim once the parent pass resolved or claimed the pair | kTagTie when a relaxation of this
+// batch tied the pair's value (set during the SSSP, kept on a claim).  Tags of other batches match
+// nothing, so no per-batch clearing is needed.
+constexpr uint32_t kTagMask = 0x3FFFFFFFu;
+constexpr uint32_t kTagClaim = 0x40000000u;
+constexpr uint32_t kTagTie = 0x80000000u;
+__device__ __forceinline__ bool tag_claimed(uint32_t w, uint32_t ep) {
+    return (w & ~kTagTie) == (ep | kTagClaim);
+}
+__device__ __forceinline__ bool tag_tied(uint32_t w, uint32_t ep) {
+    return (w & kTagTie) && (w & kTagMask) == ep;
+}
 
 // End of the kappa-sorted row prefix that can pass threshold T: the first probe position
 // (0, 1, 3, 7[, 15, 31, 63, 127]) whose kappa exceeds T (an upper bound: the edges before it are
@@ -643,7 +659,9 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     const size_t wi = (size_t)n[rr] * K + jj;
                     const unsigned long long old = atomicMin(&D.dist[wi], ab[rr]);
                     im = ab[rr] < old;
-                    if (ab[rr] == old) atomicOr(&D.tie[wi >> 5], 1u << (wi & 31));
+                    // tie: the pair record's tag word := this batch's tag | kTagTie (a plain,
+                    // idempotent store; no bitmap to clear for the next batch)
+                    if (ab[rr] == old) D.tpar[4 * wi + 1] = B.tie_tag;
                     if (SHD_TAIL_HINT && im && !tree[rr]) D.tpar[4 * wi] = L.vx[lo[rr]];
                     cur[rr] = old;
                 }
@@ -794,20 +812,18 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     uint32_t* vscr = fscr + (size_t)V * K;  // parent-pass vertex list (V entries)
     const uint32_t pw = (uint32_t)((V + 31) / 32);  // words of the pending bitmap
     D.pend = vscr + (size_t)V;
-    const uint32_t tw = (uint32_t)((V * K + 31) / 32);  // words of the tie bitmap
-    D.tie = D.pend + pw + 64;
-    D.touch = D.tie + tw + 64;  // touched-line bitmap (one bit per tail vertex)
+    D.touch = D.pend + pw + 64;  // touched-line bitmap (one bit per tail vertex)
     const uint32_t pcap = (uint32_t)(V * K);
 
     uint32_t iter = ctr[0];
-    unsigned long long n_near = 0, n_sweep = 0, n_expand = 0, n_par = 0, n_walk = 0;
-    unsigned long long n_wk[4] = {0, 0, 0, 0};  // walk steps by kind (ST_WK0)
+    unsigned long long n_near = 0, n_sweep = 0, n_expand = 0, n_par = 0;
     unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, t_split = 0;
     if (tid < 4) L.cnt[tid] = 0;
     if (tid < 5) L.pt[tid] = 0;
     if (tid < 4) L.dg[tid] = 0;
     if (tid < 8) L.bt[tid] = 0;
     if (tid == 0) L.touched = 0;
+    if (tid < 5) L.wk[tid] = 0;
     unsigned long long tk = wall_clock64();
 
     for (;;) {
@@ -836,9 +852,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         for (uint32_t i = tid; i < tbw; i += kSsspBlock) D.tb[i] = 0u;
         for (uint32_t i = tid; i < xbw; i += kSsspBlock) D.xb[i] = 0u;
         for (uint32_t i = tid; i < pw; i += kSsspBlock) D.pend[i] = 0u;
-        // tie bits: set only on touched tail lines, so K >= 8 clears them with those lines below
-        if (K < 8)
-            for (uint32_t i = tid; i < tw; i += kSsspBlock) D.tie[i] = 0u;
+        // the batch's tag: claims of the parent pass, ties of the SSSP (pair records)
+        iter++;
+        const uint32_t ep = (iter - 1u) % kTagMask + 1u;
+        B.tie_tag = ep | kTagTie;
         if (tid < (uint32_t)K) L.sh[tid] = (int)tid < nk ? srcsh[r0 + tid] : 0.0;
         // no landmark bound until h0 is reached (the sweeps test kappa0 against L.dh0)
         if (tid < (uint32_t)K) L.dh0[tid] = INFINITY;
@@ -1071,7 +1088,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         }
                         __syncthreads();
                     }
-                    if (wi < pw) D.pend[wi] = sv[tid];
+                    // sv holds a subset of word's bits: an unchanged word needs no store
+                    if (wi < pw && sv[tid] != word) D.pend[wi] = sv[tid];
                     __syncthreads();
                 }
             }
@@ -1105,8 +1123,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // pairs with several candidates get a recount at the minimum.  All K sources' chains run
         // in the same levels, so the pass has K times the parallelism of one source's.
         if ((int)tid < nk) L.src[tid] = sources[r0 + tid];
-        iter++;
-        const uint32_t ep = iter;  // claim tag of this batch's pair records
+        const uint32_t ept = ep | kTagClaim;  // tag word of a resolved / claimed pair record
         if (tid == 0) L.qtail = 0;
         __syncthreads();
         uint32_t* pcur = qa;
@@ -1129,7 +1146,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // A pair's record: its parent, the batch's tag, the loss of the parent edge (one store)
         auto put = [&](uint32_t q, uint32_t u, double loss) {
             const unsigned long long lb = d2bits(loss);
-            prec[q] = make_uint4(u, ep, (uint32_t)lb, (uint32_t)(lb >> 32));
+            prec[q] = make_uint4(u, ept, (uint32_t)lb, (uint32_t)(lb >> 32));
         };
         // A guess certified without scanning a row, past the h0-tree guess of a tail (tried by
         // the walk itself): a tail's recorded improver (no tie bit, the edge is tight) or the
@@ -1138,11 +1155,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         auto try_hint = [&](uint32_t q, unsigned long long dv, uint32_t* pout) -> bool {
             const uint32_t v = q / K, j = q % K;
             if (v >= H) {
-                if ((D.tie[q >> 5] >> (q & 31)) & 1u) return false;
+                // the record {improver, tag word} (the walk's tag store kept the tie flag)
+                const uint2 rw = __hip_atomic_load(reinterpret_cast<const uint2*>(precw + 4 * (size_t)q),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tag_tied(rw.y, ep)) return false;
                 if (!SHD_TAIL_HINT || !g.rows_sorted) return false;
                 // second guess: the recorded improver u; the edge is found in v's own row (a
                 // tail: short) -- the same undirected edge, same latency and loss as u's slot
-                const uint32_t u = precw[4 * (size_t)q] & 0x3FFFFFFFu;
+                const uint32_t u = rw.x & 0x3FFFFFFFu;
                 if (u >= (uint32_t)V || u == v) return false;
                 const unsigned long long du = D.get(u, j);
                 uint32_t lo = g.rowptr[v], hi = g.rowptr[v + 1];
@@ -1178,26 +1198,25 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             return true;
         };
         // A walk hop's inputs at tail vertex v for source j: its h0-tree record {parent, slot,
-        // f64 w}, that edge's loss, the tie word of (v, j) and d_j(v) -- independent loads, all
-        // in one round trip.  Hubs: d_j(v) only (LDS).
+        // f64 w, f64 loss of that edge} (32 B, one line) and d_j(v) -- independent loads, in one
+        // round trip.  Hubs: d_j(v) only (LDS).
         struct Hop {
             uint4 sp;
             double sl;
-            uint32_t tw;
             unsigned long long d;
         };
         auto load_hop = [&](uint32_t v, uint32_t j) -> Hop {
             Hop h;
             const uint32_t q = v * K + j;
             if (v >= H) {
-                h.sp = reinterpret_cast<const uint4*>(g.spt)[v];
-                h.sl = g.sptLoss[v];
-                h.tw = D.tie[q >> 5];
+                const uint4* s = reinterpret_cast<const uint4*>(g.spt) + 2 * (size_t)v;
+                h.sp = s[0];
+                const uint2 l = *reinterpret_cast<const uint2*>(s + 1);
+                h.sl = __hiloint2double((int)l.y, (int)l.x);
                 h.d = ld_l2_u64(&D.dist[(size_t)q]);
             } else {
                 h.sp = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
                 h.sl = 0.0;
-                h.tw = 0u;
                 h.d = D.hd[(size_t)q];
             }
             return h;
@@ -1208,21 +1227,21 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             // Walks: chains are followed towards the source while the h0-tree guess certifies
             // parents (no level barriers); a chain stops at the source, at a pair another walk
             // claimed first (tag), or at a pair whose guess fails (-> S = fscr, claimed: the hint
-            // pass below resolves it).  One round trip per hop: the claim of q goes out with the
-            // loads of q's tree parent pu (d_j(pu) certifies the guess, pu's own hop inputs serve
-            // the next hop).  Flattened: a lane takes its next start pair as soon as its chain
-            // ends, so a wave runs for its busiest lane's total of hops, not for the sum over
-            // start pairs of the longest chain among its 64 lanes; the slower guesses (binary
-            // searches) are deferred so they do not stall the wave's other chains.
+            // pass below resolves it).  One round trip per hop: the tag word of q (claim, tie)
+            // goes out with the loads of q's tree parent pu (d_j(pu) certifies the guess, pu's
+            // own hop inputs serve the next hop).  Flattened: a lane takes its next start pair as
+            // soon as its chain ends, so a wave runs for its busiest lane's total of hops, not
+            // for the sum over start pairs of the longest chain among its 64 lanes; the slower
+            // guesses (binary searches) are deferred so they do not stall the wave's other chains.
             if (tid == 0) L.qtail = 0;
             __syncthreads();
             {
                 uint32_t i = tid, q = 0, j = 0;
+                uint32_t nw = 0, nw0 = 0;  // walk steps, of which certified by the tree guess
                 bool act = false, fresh = false;
                 Hop h;
                 h.sp = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
                 h.sl = 0.0;
-                h.tw = 0u;
                 h.d = 0ull;
                 for (;;) {
                     if (!act && i < nF) {
@@ -1239,7 +1258,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     } else if (act) {
                         const uint32_t v = q / K;
                         const uint32_t pu = h.sp.x;
-                        const bool tree = v >= H && !((h.tw >> (q & 31)) & 1u) && pu < (uint32_t)V;
+                        const bool tree = v >= H && pu < (uint32_t)V;
                         Hop hn = h;
                         if (tree) hn = load_hop(pu, j);
                         // The claim is a plain tag read issued with those loads; the pair's
@@ -1248,14 +1267,17 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         // round trip both walk on: they write identical records (the parent rule
                         // is deterministic), and a pair listed twice in S is resolved twice the
                         // same way -- cheaper than a returning atomic per hop (kernel -3.5 %).
-                        if (ld_l2_u32(&precw[4 * (size_t)q + 1]) == ep) {  // another walk's
+                        const uint32_t tw = ld_l2_u32(&precw[4 * (size_t)q + 1]);
+                        if (tag_claimed(tw, ep)) {  // another walk's
                             act = false;
                         } else {
-                            n_walk++;
-                            if (tree && __dadd_rn(bits2d(hn.d), __hiloint2double((int)h.sp.w, (int)h.sp.z)) ==
-                                            bits2d(h.d)) {
+                            nw++;
+                            const bool tied = tag_tied(tw, ep);
+                            if (tree && !tied &&
+                                __dadd_rn(bits2d(hn.d), __hiloint2double((int)h.sp.w, (int)h.sp.z)) ==
+                                    bits2d(h.d)) {
                                 put(q, pu, h.sl);
-                                n_wk[0]++;
+                                nw0++;
                                 if (pu == L.src[j]) {
                                     act = false;
                                 } else {
@@ -1263,7 +1285,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                     h = hn;
                                 }
                             } else {
-                                precw[4 * (size_t)q + 1] = ep;
+                                precw[4 * (size_t)q + 1] = ept | (tied ? kTagTie : 0u);
                                 const uint32_t pos = atomicAdd(&L.qtail, 1u);
                                 if (pos < pcap) fscr[pos] = q;
                                 else atomicOr(&L.fover, 128u);
@@ -1271,6 +1293,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                             }
                         }
                     }
+                }
+                const unsigned long long s0 = wave_sum_u64(nw), s1 = wave_sum_u64(nw0);
+                if ((tid & 63) == 0) {
+                    atomicAdd(&L.wk[0], s0);
+                    atomicAdd(&L.wk[1], s1);
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1293,7 +1320,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     q = fscr[i];
                     uint32_t u = 0;
                     const bool ok = try_hint(q, D.get(q / K, q % K), &u);
-                    n_wk[ok ? (q / K >= H ? 1 : 2) : 3]++;
+                    atomicAdd(&L.wk[ok ? (q / K >= H ? 2 : 3) : 4], 1ull);
                     if (!ok) {
                         best[q] = kInfBits;
                         cntc[q] = 0;
@@ -1411,10 +1438,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     const uint32_t c = ld_l2_u32(&cntc[q]);
                     if (jr == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
                         atomicAdd(&stats[ST_ERRORS], 1ull);
-                        prec[q] = make_uint4(L.src[q % K] | 0x40000000u, ep, 0u, 0u);
+                        prec[q] = make_uint4(L.src[q % K] | 0x40000000u, ept, 0u, 0u);
                     } else {
                         const unsigned long long lb = d2bits(g.aloss[jr]);
-                        prec[q] = make_uint4(adj_col(g, jr) | (c > 1 ? 0x80000000u : 0u), ep,
+                        prec[q] = make_uint4(adj_col(g, jr) | (c > 1 ? 0x80000000u : 0u), ept,
                                              (uint32_t)lb, (uint32_t)(lb >> 32));
                     }
                 }
@@ -1449,9 +1476,19 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         { unsigned long long t = wall_clock64(); t_par += t - tk; tk = t; }
 
         // ---------------- per-target latency / reliability / hops (shd-topology.c:561-671) ----
-        // items (source j, target k) of the whole batch; each thread walks its pairs' chains
+        // items (source j, target k) of the whole batch; each thread walks its pairs' chains.
+        // The hub distances move to their (otherwise unused) rows of the [V][K] block, so the
+        // hub LDS holds the first nl levels of the per-thread path buffer (the chain's edge
+        // losses, multiplied in path order after the walk); deeper levels go to HBM (pbuf).
         if ((int)tid < K) L.rmin[tid] = kInfBits;
+        for (uint32_t i = tid; i < H * K; i += kSsspBlock) D.dist[i] = D.hd[i];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        double* lpb = reinterpret_cast<double*>(D.hd);
+        const uint32_t nl = H * K / kSsspBlock;  // LDS levels of the path buffer
+        auto pb_at = [&](uint32_t x) -> double* {
+            return x < nl ? lpb + (size_t)x * kSsspBlock + tid : pbuf + (size_t)x * kSsspBlock + tid;
+        };
         for (uint32_t i = tid; i < (uint32_t)A * (uint32_t)nk; i += kSsspBlock) {
             const uint32_t j = i / (uint32_t)A;
             const uint32_t k = i - j * (uint32_t)A;
@@ -1474,7 +1511,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     h = 1;
                 }
             } else {
-                lat = bits2d(D.get(t, j));
+                lat = bits2d(ld_l2_u64(&D.dist[(size_t)t * K + j]));
                 bool amb = false, bad = false;
                 uint32_t v = t;
                 while (v != src) {
@@ -1483,12 +1520,12 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     const u32x4 rv = __builtin_nontemporal_load(
                         reinterpret_cast<const u32x4*>(prec) + (size_t)v * K + j);
                     const uint4 r = make_uint4(rv.x, rv.y, rv.z, rv.w);
-                    if (r.y != ep || (r.x & 0x40000000u)) {
+                    if (r.y != ept || (r.x & 0x40000000u)) {
                         bad = true;
                         break;
                     }
                     amb |= (r.x >> 31) != 0u;
-                    if (h < kMaxHops) pbuf[(size_t)h * kSsspBlock + tid] = __hiloint2double((int)r.w, (int)r.z);
+                    if (h < kMaxHops) *pb_at(h) = __hiloint2double((int)r.w, (int)r.z);
                     h++;
                     v = r.x & 0x3FFFFFFFu;
                     if (h > (uint32_t)V) { bad = true; break; }
@@ -1501,8 +1538,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     lat = -1.0;
                     rel = -1.0;
                 } else if (h <= (uint32_t)kMaxHops) {
-                    for (int x = (int)h - 1; x >= 0; --x)
-                        rel *= (1.0 - pbuf[(size_t)x * kSsspBlock + tid]);
+                    for (int x = (int)h - 1; x >= 0; --x) rel *= (1.0 - *pb_at((uint32_t)x));
                 } else {
                     atomicAdd(&stats[ST_LONGPATH], 1ull);
                     for (int x = (int)h - 1; x >= 0; --x) {  // edge at depth x from t
@@ -1544,26 +1580,37 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             // batch).  Done at the batch's end (its time counts as setup): the next batch's
             // setup waits for these stores; a one-round shard no longer has every slot resetting
             // at its kernel's start.
+            // A thread loads one touch word; the G = K / 2 lanes of a group then reset the
+            // group's G words' vertices together, lane p storing the p-th 16 B of each line, so
+            // one store instruction writes 64 / G whole lines (one write request per line, not
+            // one per 16 B).
             typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
             u64x2* d2 = reinterpret_cast<u64x2*>(D.dist);
             const u64x2 inf2 = {kInfBits, kInfBits};
+            constexpr uint32_t G = K / 2;
+            const uint32_t part = tid % G, gbase = (tid & 63u) - part;
             unsigned long long nt = 0;
-            for (uint32_t wi = H / 32 + tid; wi < pw; wi += kSsspBlock) {
-                uint32_t w = ld_l2_u32(&D.touch[wi]);
-                if (!w) continue;
-                D.touch[wi] = 0u;
-                nt += (unsigned long long)__popc(w);
-                while (w) {
-                    const uint32_t v = wi * 32u + (uint32_t)__ffs(w) - 1u;
-                    w &= w - 1u;
+            const uint32_t w0 = H / 32;
+            uint32_t nword = w0 + tid < pw ? ld_l2_u32(&D.touch[w0 + tid]) : 0u;
+            for (uint32_t wb = w0; wb < pw; wb += kSsspBlock) {
+                const uint32_t wi = wb + tid;
+                const uint32_t myw = nword;
+                nword = wi + kSsspBlock < pw ? ld_l2_u32(&D.touch[wi + kSsspBlock]) : 0u;
+                if (myw) {
+                    D.touch[wi] = 0u;
+                    nt += (unsigned long long)__popc(myw);
+                }
+                if (!__any(myw != 0u)) continue;
 #pragma unroll
-                    for (int h = 0; h < K / 2; h++) {
-                        if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + (size_t)v * (K / 2) + h);
-                        else d2[(size_t)v * (K / 2) + h] = inf2;
+                for (uint32_t p = 0; p < G; p++) {
+                    uint32_t w = __shfl(myw, (int)(gbase + p), 64);
+                    const uint32_t wv = wi - part + p;
+                    while (w) {
+                        const uint32_t v = wv * 32u + (uint32_t)__ffs(w) - 1u;
+                        w &= w - 1u;
+                        if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + (size_t)v * G + part);
+                        else d2[(size_t)v * G + part] = inf2;
                     }
-                    // the vertex's K tie bits (whole bytes for K >= 8)
-                    if (K == 8) reinterpret_cast<uint8_t*>(D.tie)[v] = 0u;
-                    else if (K == 16) reinterpret_cast<uint16_t*>(D.tie)[v] = 0u;
                 }
             }
             nt = wave_sum_u64(nt);
@@ -1580,13 +1627,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             b[7] = (unsigned long long)nk;
         }
     }
-    n_walk = wave_sum_u64(n_walk);
-    if ((tid & 63) == 0 && n_walk) atomicAdd(&stats[ST_WALK], n_walk);
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const unsigned long long x = wave_sum_u64(n_wk[i]);
-        if ((tid & 63) == 0 && x) atomicAdd(&stats[ST_WK0 + i], x);
-    }
+    __syncthreads();
     if (tid == 0) {
         ctr[0] = iter;
         atomicAdd(&stats[ST_RELAX], L.cnt[0]);
@@ -1610,6 +1651,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         atomicAdd(&stats[ST_EV0 + 5], 0ull);
         atomicAdd(&stats[ST_EV0 + 5], n_par);
         for (int i = 0; i < 4; i++) atomicAdd(&stats[ST_PT0 + i], L.pt[1 + i]);
+        atomicAdd(&stats[ST_WALK], L.wk[0]);
+        for (int i = 0; i < 4; i++) atomicAdd(&stats[ST_WK0 + i], L.wk[1 + i]);
         if (SHD_BATCH_TIME)
             for (int i = 0; i < 8; i++) atomicAdd(&stats[ST_BT0 + i], L.bt[i]);
     }

@@ -36,10 +36,16 @@ TopoWindow* topowindow_new(Topology* top) {
     if (!top) return nullptr;
     TopoWindow* w = new TopoWindow();
     w->top = top;
+    shdtopo_window_hold(top, +1);
     return w;
 }
 
-void topowindow_free(TopoWindow* w) { delete w; }
+void topowindow_free(TopoWindow* w) {
+    if (!w) return;
+    shdtopo_window_hold(w->top, -1);
+    shdtopo_window_release(w->top);
+    delete w;
+}
 
 int64_t topowindow_emit_state(TopoWindow* w, uint32_t srcIP, uint32_t dstIP,
                               uint32_t payloadLength, uint32_t preDrawState, uint64_t now,
@@ -81,7 +87,10 @@ int topowindow_flush(TopoWindow* w, uint64_t jumpNs, int multiThreaded, TopoWind
         std::lock_guard<std::mutex> lk(w->mu);
         in.swap(w->in);
     }
-    if (in.empty()) return 0;
+    if (in.empty()) {
+        shdtopo_window_release(w->top);
+        return 0;
+    }
     const size_t n = in.size();
     std::vector<int32_t> sv(n), dv(n);
     std::vector<uint32_t> pay(n), st(n);
@@ -94,7 +103,9 @@ int topowindow_flush(TopoWindow* w, uint64_t jumpNs, int multiThreaded, TopoWind
         now[i] = in[i].now;
     }
     w->out.resize(n);
-    // a packet whose vertex left the table (its last host detached) comes back undelivered
+    // a vertex detached during the window is still a column (shdtopo_window_hold): its packets
+    // are routed as at emit; only a packet whose vertex left before an earlier flush comes back
+    // undelivered
     const int r = shdtopo_route_batch_vertices(w->top, sv.data(), dv.data(), pay.data(), st.data(),
                                                now.data(), n, jumpNs, multiThreaded, w->out.data());
     if (r < 0) {
@@ -105,6 +116,8 @@ int topowindow_flush(TopoWindow* w, uint64_t jumpNs, int multiThreaded, TopoWind
         w->in.swap(in);
         return r;
     }
+    // the window's packets are routed: vertices detached during it may leave the table now
+    shdtopo_window_release(w->top);
     if (deliver)
         for (size_t i = 0; i < n; i++)
             deliver(ctx, in[i].packet, w->out[i].delivered, w->out[i].time);

@@ -130,3 +130,62 @@ def random_topology_graphml(n_routers=600, n_poi=60, extra=2400, seed=3, integer
         edges.append(("poi-%d" % k, "poi-%d" % k, 1.0, 0.0))
     order = rng.permutation(len(edges))  # edge ids not grouped by vertex
     return graphml_doc(nodes, [edges[i] for i in order], directed)
+
+
+def scipy_rows(graph, srcs, targets):
+    """The per-target helper (shd-topology.c:561-671) over scipy's shortest-path trees, an
+    implementation independent of the oracle: scipy.sparse.csgraph.dijkstra with predecessors on
+    the undirected non-loop graph.  latency = scipy's distance (the same left-to-right f64 sums
+    from the source), hops = the predecessor chain's length, reliability = ((1 * (1 - vloss[s]))
+    * (1 - vloss[t])) * prod(1 - loss(e)) in path order from the source; the self pair is the
+    self loop (latency 0 + its latency, reliability (1 - vloss) * (1 - loss), 1 hop)."""
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import dijkstra
+    V, eu, ev, elat, eloss, vloss = graph
+    eu, ev = np.asarray(eu, np.int64), np.asarray(ev, np.int64)
+    elat, eloss = np.asarray(elat, np.float64), np.asarray(eloss, np.float64)
+    vloss = np.asarray(vloss, np.float64)
+    nl = eu != ev
+    r = np.concatenate([eu[nl], ev[nl]])
+    c = np.concatenate([ev[nl], eu[nl]])
+    W = sp.csr_matrix((np.concatenate([elat[nl], elat[nl]]), (r, c)), shape=(V, V))
+    Lm = sp.csr_matrix((np.concatenate([eloss[nl], eloss[nl]]), (r, c)), shape=(V, V))
+    # no parallel edges (the csr would sum them) and no zero latency (scipy drops zeros)
+    assert W.nnz == 2 * int(nl.sum()) and bool((W.data > 0).all())
+    # self loops: the first (lowest edge id) per vertex, as igraph_get_eid
+    selfLat = np.full(V, np.nan)
+    selfLoss = np.zeros(V)
+    li = np.nonzero(~nl)[0][::-1]  # assigned last-to-first: the lowest edge id wins
+    selfLat[eu[li]] = elat[li]
+    selfLoss[eu[li]] = eloss[li]
+    dist, pred = dijkstra(W, directed=False, indices=np.asarray(srcs), return_predecessors=True)
+    targets = np.asarray(targets, np.int64)
+    A = len(targets)
+    lat = np.empty((len(srcs), A))
+    rel = np.empty((len(srcs), A))
+    hops = np.zeros((len(srcs), A), np.int64)
+    for i, s in enumerate(srcs):
+        lat[i] = dist[i, targets]
+        cur = targets.copy()
+        losses = []
+        act = cur != s
+        while act.any():
+            p = pred[i, cur]
+            p = np.where(act, p, cur)
+            assert bool((p[act] >= 0).all())
+            lo = np.zeros(A)
+            lo[act] = np.asarray(Lm[p[act], cur[act]]).ravel()
+            losses.append(lo)
+            hops[i] += act
+            cur = np.where(act, p, cur)
+            act = cur != s
+        rr = (1.0 * (1.0 - vloss[s])) * (1.0 - vloss[targets])
+        for k in range(len(losses) - 1, -1, -1):  # the edge at depth k from the target
+            rr = np.where(k < hops[i], rr * (1.0 - losses[k]), rr)
+        rel[i] = rr
+        lat[i] = np.where(lat[i] == 0.0, 1.0, lat[i])  # the helper's zero-latency rule
+        selfc = targets == s
+        lat[i, selfc] = 0.0 + selfLat[s]
+        rel[i, selfc] = (1.0 * (1.0 - vloss[s])) * (1.0 - selfLoss[s])
+        hops[i, selfc] = 1
+    return lat, rel, hops

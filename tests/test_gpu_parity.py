@@ -9,7 +9,7 @@ import pytest
 
 import oracle
 import shadow_amd as sa
-from helpers import attach_hosts, bundled_pair, host_ip, rel_close, synthetic_pair
+from helpers import attach_hosts, bundled_pair, host_ip, rel_close, scipy_rows, synthetic_pair
 
 pytestmark = pytest.mark.gpu
 
@@ -43,6 +43,7 @@ def test_sssp_synthetic_table(integer, hubs, fill):
     top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
     top.set_option("lds_hubs", hubs)
     top.set_option("batch_fill", fill)  # whole batches (auto would run 1 source per slot here)
+    top.set_option("tie_dense", 0)  # the batch kernel + flagged-row replay path (no tie probe)
     otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()
@@ -73,6 +74,7 @@ def test_target_skip_exact_across_target_sets(integer):
         top, g = synthetic_pair(seed=17, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
         top.set_option("target_skip", skip)
         top.set_option("batch_fill", 8)
+        top.set_option("tie_dense", 0)  # the batch kernel path (no tie probe)
         tops.append(top)
     verts = []
     st = 1
@@ -101,6 +103,7 @@ def test_single_slot_reuses_touched_lines(integer):
     top, g = synthetic_pair(seed=23, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
     top.set_option("slots", 1)
     top.set_option("batch_fill", 3)
+    top.set_option("tie_dense", 0)  # the batch kernel path (no tie probe)
     verts = []
     st = 7
     for lo, hi in ((0, 90), (90, 260)):
@@ -319,12 +322,10 @@ def _oracle_threads():
     return max(1, min(64, (os.cpu_count() or 8)))
 
 
-def test_sssp_full_size_c4_sampled_rows():
-    """BASELINE config 4 at full size (1M vertices / 10M edges, the bench workload): 128 seeded
-    rows bit-exact against the oracle's Dijkstra + helper (the box's host cores run them in a few
-    seconds), and size-independent properties of the whole 9,999 x 9,999 table: every latency
-    finite and > 0, reliability in (0, 1], the diagonal is the self loop (1 hop), no overflow
-    fallback, nothing to replay, and the kernel's row minima equal the table's."""
+@pytest.fixture(scope="module")
+def c4_table():
+    """BASELINE config 4 at full size (1M vertices / 10M edges, the bench workload): the whole
+    attached-vertex table built once for the tests below."""
     import torch
     top = sa.Topology.synthetic(seed=20261015)
     assert top.num_vertices == 1_000_000 and top.num_edges == 10_000_000
@@ -336,7 +337,22 @@ def test_sssp_full_size_c4_sampled_rows():
     rm = torch.empty((A,), dtype=torch.float64, device="cuda")
     top.build_rows_into(0, A, lr, hp, rm)
     torch.cuda.synchronize()
-    st = top.stats()
+    rows = np.sort(np.random.default_rng(20261015).choice(A, 128, replace=False))
+    yield dict(top=top, att=att, lr=lr, hp=hp, rm=rm, st=top.stats(), rows=rows,
+               graph=top.export_graph())
+    del lr, hp, rm
+    torch.cuda.empty_cache()
+
+
+def test_sssp_full_size_c4_sampled_rows(c4_table):
+    """BASELINE config 4 at full size: 128 seeded rows bit-exact against the oracle's Dijkstra +
+    helper (the box's host cores run them in a few seconds), and size-independent properties of
+    the whole 10,000 x 10,000 table: every latency finite and > 0, reliability in (0, 1], the
+    diagonal is the self loop (1 hop), no overflow fallback, nothing to replay, and the kernel's
+    row minima equal the table's."""
+    import torch
+    att, lr, hp, rm, st, rows = (c4_table[k] for k in ("att", "lr", "hp", "rm", "st", "rows"))
+    A = len(att)
     assert st["errors"] == 0 and st["ambiguous_pairs"] == 0 and st["far_scan_sources"] == 0
     assert st["replay_rows"] == 0
     lat = lr[..., 0]
@@ -346,8 +362,7 @@ def test_sssp_full_size_c4_sampled_rows():
     diag = torch.arange(A, device="cuda")
     assert bool((hp[diag, diag] == 1).all()) and bool((hp >= 1).all())
     assert torch.equal(rm, lat.min(dim=1).values)
-    rows = np.sort(np.random.default_rng(20261015).choice(A, 128, replace=False))
-    V, eu, ev, elat, eloss, vloss = top.export_graph()
+    V, eu, ev, elat, eloss, vloss = c4_table["graph"]
     g = oracle.OGraph(V, eu, ev, elat, eloss, vloss)
     olat, orel, ohops = g.source_rows(att[rows], att, nthreads=_oracle_threads())
     glr = lr[torch.from_numpy(rows).cuda()].cpu().numpy()
@@ -355,6 +370,27 @@ def test_sssp_full_size_c4_sampled_rows():
     assert np.array_equal(glr[..., 1].view(np.uint64), orel.view(np.uint64))
     ghp = hp[torch.from_numpy(rows).cuda()].cpu().numpy().view(np.uint16)
     assert np.array_equal(ghp, ohops.astype(np.uint16))
+
+
+@pytest.mark.timeout(600)
+def test_sssp_full_size_c4_rows_vs_scipy(c4_table):
+    """BASELINE config 4 at full size, pinned by an implementation independent of the oracle:
+    16 of the 128 sampled sources, every one of their 10,000 targets, against scipy's Dijkstra
+    predecessor trees + the reference helper (helpers.scipy_rows).  C4's latencies are continuous, so
+    every shortest path is unique (the build flags no d-tied parent: ambiguous_pairs == 0) and
+    scipy's tree is igraph's; latency, reliability and hops bit for bit.  (Ties stay "parity
+    unpinned": DESIGN.md 2.)"""
+    import torch
+    att, lr, hp, rows, st = (c4_table[k] for k in ("att", "lr", "hp", "rows", "st"))
+    assert st["ambiguous_pairs"] == 0
+    sub = rows[:: len(rows) // 16][:16]
+    slat, srel, shops = scipy_rows(c4_table["graph"], att[sub], att)
+    idx = torch.from_numpy(sub).cuda()
+    glr = lr[idx].cpu().numpy()
+    ghp = hp[idx].cpu().numpy().view(np.uint16)
+    assert np.array_equal(glr[..., 0].view(np.uint64), slat.view(np.uint64))
+    assert np.array_equal(glr[..., 1].view(np.uint64), srel.view(np.uint64))
+    assert np.array_equal(ghp, shops.astype(np.uint16))
 
 
 def test_sssp_full_size_c4_int_rows():

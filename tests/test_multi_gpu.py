@@ -139,3 +139,30 @@ def test_route_on_every_device_slot():
         assert np.array_equal(t_.view(np.uint64), ot)
         assert np.array_equal(s_.view(np.uint32), os_)
         assert np.array_equal(d_, od)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [2, 3])
+def test_multi_device_default_attach_prep_prepares_once(devices):
+    """The default path of a Shadow run (prepare_on_attach left on): the first attach starts the
+    attach-time preparation thread on the owner's device, and the devices = N build that follows
+    copies its graph to the peer engines -- one host preparation in all (attach-time thread +
+    builds, owner + peers), none in a rebuild, and every engine's table equals the oracle's."""
+    top, g = synthetic_pair(seed=41, n_routers=2500, n_poi=120, n_edges=25000)
+    top.set_option("devices", devices)
+    otop, ips, verts = attach_hosts(top, g, 200, type_hints=["client", "relay"])
+    top.build()
+    st = top.stats()
+    assert st["devices"] == devices and st["errors"] == 0
+    # by the attach-time thread (csr_host_runs 0), or by the build if it took the lock first
+    assert st["csr_host_runs_total"] == 1 and st["csr_host_runs"] in (0, 1)
+    top.rebuild()
+    st = top.stats()
+    assert st["csr_host_runs_total"] == 1 and st["csr_host_runs"] == 0
+    a, lat, rel, hops = top.table()
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(a, oa)
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+    assert top.getMinimumLatency() == olat.min()

@@ -221,3 +221,16 @@ def test_oracle_paths_pinned_by_scipy_on_tie_free_graph():
     assert np.array_equal(lat[other], z["lat"][other])
     assert np.array_equal(rel[other].view(np.uint64), z["rel"][other].view(np.uint64))
     assert np.array_equal(hops[other], z["hops"][other])
+
+
+def test_vectorised_scipy_helper_matches_golden_rows():
+    """tests/helpers.scipy_rows (the full-size C4 GPU test's independent pin: scipy predecessor
+    trees + the reference helper, vectorised over targets) reproduces the oracle's golden rows of
+    the tie-free graph bit for bit, self pairs included."""
+    from helpers import scipy_rows
+    z = np.load(os.path.join(GOLDEN, "synth_real.npz"))
+    graph = (int(z["V"]), z["eu"], z["ev"], z["elat"], z["eloss"], z["vloss"])
+    lat, rel, hops = scipy_rows(graph, z["sources"], z["targets"])
+    assert np.array_equal(lat.view(np.uint64), z["lat"].view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), z["rel"].view(np.uint64))
+    assert np.array_equal(hops, z["hops"])

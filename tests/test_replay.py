@@ -56,6 +56,7 @@ def test_integer_ties_table_bit_exact(fill):
     bit-exact against the oracle; the tie rows went through the replay."""
     top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=True)
     top.set_option("batch_fill", fill)
+    top.set_option("tie_dense", 0)  # the batch kernel + flagged-row replay path (no tie probe)
     otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()
@@ -191,12 +192,16 @@ def test_tie_dense_replay_landmark_skip(landmark, int_keys):
 
 
 def test_tie_dense_auto_switch():
-    """tie_dense auto (-1): a build that replays >= 90 % of >= 64 rows switches the topology to
-    replay-only builds; the rebuilt rows are bit-identical."""
+    """tie_dense auto (-1).  The first batched build of an integer-latency topology probes 64
+    sample rows with the batch kernel: if >= 90 % of them cross a d-tied parent the topology is
+    tie-dense before the full launch and every row goes straight to the heap replay (no batch
+    kernel over the table); otherwise a build that replays >= 90 % of >= 64 rows switches the
+    later builds.  Every build's rows are bit-identical (and equal the oracle's)."""
     import torch
-    top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=150, n_edges=30000, integer=True)
-    otop, ips, verts = attach_hosts(top, g, 400, type_hints=["client", "relay", "server"])
+    top, g = synthetic_pair(seed=11, n_routers=3000, n_poi=300, n_edges=30000, integer=True)
+    otop, ips, verts = attach_hosts(top, g, 800, type_hints=["client", "relay", "server"])
     A = len(top.attached_vertices())
+    assert A >= 128  # the probe needs twice its sample (A = 191 here)
     outs, sts = [], []
     for _ in range(2):
         lr = torch.empty((A, A, 2), dtype=torch.float64, device="cuda")
@@ -205,11 +210,17 @@ def test_tie_dense_auto_switch():
         torch.cuda.synchronize()
         outs.append((lr.cpu().numpy(), hp.cpu().numpy()))
         sts.append(top.stats())
-    dense = A >= 64 and sts[0]["replay_rows"] * 10 >= A * 9
-    assert sts[0]["tie_dense"] == 0
-    assert sts[1]["tie_dense"] == (1 if dense else 0)
+    st0, st1 = sts
+    assert st0["tie_probe_rows"] == 64 and st1["tie_probe_rows"] == 0  # once per topology
+    probe_dense = st0["tie_probe_flagged"] * 10 >= 64 * 9
+    assert st0["tie_dense"] == (1 if probe_dense else 0)
+    if probe_dense:
+        # decided before the full launch: every row replayed, none flagged by a batch launch
+        assert st0["replay_rows"] == A and st0["ambiguous_pairs"] == 0
+    dense = probe_dense or st0["replay_rows"] * 10 >= A * 9
+    assert st1["tie_dense"] == (1 if dense else 0)
     if dense:
-        assert sts[1]["replay_rows"] == A and sts[1]["ambiguous_pairs"] == 0
+        assert st1["replay_rows"] == A and st1["ambiguous_pairs"] == 0
     assert np.array_equal(outs[0][0].view(np.uint64), outs[1][0].view(np.uint64))
     assert np.array_equal(outs[0][1], outs[1][1])
     oa, olat, orel, ohops = g.table(verts)

@@ -83,3 +83,62 @@ def test_window_adapter_vs_reference(serial):
         assert top.lazyMinimumLatency() == otop.minimum_path_latency
         t0 += jump
     lib.topowindow_free(w)
+
+
+def test_window_routes_packets_of_a_host_detached_before_the_flush():
+    """a packet is routed at emit in the reference (shd-worker.c:345-369).  A host
+    that detaches (the last host on its vertex) after emitting or being sent packets in a window
+    keeps its vertex's table column until the window's flush (shdtopo_window_hold / _release),
+    so those packets come back exactly as the reference routed them; the column goes after the
+    flush (a later query rebuilds the table without it)."""
+    top, g = synthetic_pair(seed=33, n_routers=1500, n_poi=80, n_edges=15000)
+    lib, shim = _lib.load()
+    otop = oracle.OracleTopology(g)
+    hosts, verts = [], []
+    st = 9
+    for k in range(60):
+        st = (st * 1103515245 + 12345) & 0xFFFFFFFF
+        ip = host_ip(k + 1)
+        v1, s1 = top.attach_ip(ip, st, typeHint=("client", "relay")[k % 2])
+        v2, s2 = otop.attach(ip, st, type_hint=("client", "relay")[k % 2])
+        assert v1 == v2 and s1 == s2
+        hosts.append((ip, sa.Address(ip), sa.Random(s1)))
+        verts.append(v1)
+    # a host alone on its vertex
+    lone = next(i for i, v in enumerate(verts) if verts.count(v) == 1)
+    A0 = len(top.attached_vertices())
+    w = lib.topowindow_new(top._h)
+    jump = lib.topowindow_jump_ns(top._h, 0)
+    got = {}
+
+    @_lib.WINDOW_DELIVER
+    def deliver(ctx, packet, delivered, time):
+        got[int(packet)] = (delivered, time)
+
+    ref_state = [h[2].state for h in hosts]
+    ref = []
+    rng = np.random.default_rng(3)
+    t0 = 10**9
+    for k in range(400):
+        a = lone if k % 2 == 0 else int(rng.integers(0, len(hosts)))
+        b = int(rng.integers(0, len(hosts)))
+        s, d = (a, b) if k % 4 < 2 else (b, a)
+        if s == d:
+            d = (d + 1) % len(hosts)
+        pay = 1448
+        now = t0 + int(rng.integers(0, jump))
+        rel = otop.get_reliability(hosts[s][0], hosts[d][0])
+        r, ref_state[s] = oracle.next_double(ref_state[s])
+        dl = r <= rel
+        t = max(now + int(math.ceil(otop.get_latency(hosts[s][0], hosts[d][0]) * 1e6)),
+                now + jump) if dl else 0
+        ref.append((int(dl), t))
+        assert lib.topowindow_emit(w, hosts[s][1]._p, hosts[d][1]._p, pay, hosts[s][2]._p, now,
+                                   k + 1) == k
+    top.detach_ip(hosts[lone][0])  # the lone host leaves before the window's flush
+    assert lib.topowindow_flush(w, jump, 1, deliver, None) == 0
+    assert [got[k + 1] for k in range(len(ref))] == ref
+    assert any(x[0] for x in ref)
+    # after the flush the vertex is no longer a column
+    assert len(top.attached_vertices()) == A0 - 1
+    lib.topowindow_free(w)

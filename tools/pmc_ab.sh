@@ -1,8 +1,11 @@
 #!/bin/bash
 # Request-count comparison of kernel variants (run on the GPU box from the repo root):
 #   tools/pmc_ab.sh OUTDIR "name|lib|probe args" ...
-# One rocprofv3 pass per variant with the DRAM request counters (+ a kernel-trace pass).
+# One rocprofv3 pass per variant with the DRAM request counters; PMC="..." picks other counters
+# (one block's limits per pass, e.g. PMC=WRITE_SIZE) and TAG a suffix for the output names.
 set -u
+PMC=${PMC:-"TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_ATOMIC_sum"}
+TAG=${TAG:-}
 OUT=$1; shift
 ROOT=$(pwd)
 mkdir -p "$OUT"
@@ -11,8 +14,8 @@ for spec in "$@"; do
   IFS='|' read -r name lib args <<< "$spec"
   if [ "$lib" = "-" ]; then L=""; else L="$ROOT/abtest/$lib/libshdtopo.so"; fi
   export SHDTOPO_LIB="$L"
-  timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_ATOMIC_sum \
-      --output-format csv -d "$ROOT/$OUT/$name" -o "$name" -- \
-      python3 -u "$ROOT/tools/gpu_probe.py" $args > "$ROOT/$OUT/$name.log" 2>&1 || exit $?
-  echo "pmc $name ok"
+  timeout -s KILL 150 rocprofv3 --pmc $PMC \
+      --output-format csv -d "$ROOT/$OUT/$name$TAG" -o "$name$TAG" -- \
+      python3 -u "$ROOT/tools/gpu_probe.py" $args > "$ROOT/$OUT/$name$TAG.log" 2>&1 || exit $?
+  echo "pmc $name$TAG ok"
 done
