@@ -320,6 +320,17 @@ typedef struct {
     int64_t csr_host_runs_total; /* host-side graph preparations since the topology was loaded,
                                     the owner's and every peer engine's, the attach-time
                                     preparation thread's included */
+    int64_t sweep_events[4];    /* profiling builds (-DSHD_BATCH_TIME=1) only, else 0: the batch
+                                   kernel's bucket sweeps -- pending tail vertices visited, of which
+                                   queued, holding a pair in the opened bucket the kappa test kept
+                                   out, and kept pending */
+    int64_t write_lines[16];    /* profiling builds (-DSHD_BATCH_WRCOUNT=1) only, else 0: 64-B lines
+                                   the batch kernel's stores and atomics touched, by category
+                                   (topo_sssp_batch.hip WL_*): relaxation atomicMin, tie tags,
+                                   improver hints, pending atomics, touched atomics, near-mask
+                                   atomics; mask stores; pending words; line reset; touched-word
+                                   clears; pair records; parent scratch; table output; hub rows and
+                                   hints; queue appends; other */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -247,6 +247,8 @@ struct _Topology {
     DevBuf<uint32_t> d_probeSrc;
     DevBuf<double> d_probeSh;
     int replaySlotsOpt = 0;   // option "replay_slots" (0 = sized from the CUs and free HBM)
+    int replayWpc = 20;       // option "replay_wpc": replay wavefronts per CU (LDS and HBM allowing)
+    bool rwsInt = false;      // the replay workspace's node block is laid out for u32 keys
     bool replayLandmark = true;  // option "replay_landmark": skip edges into vertices the
                                  // landmark bound proves popped (topo_replay.hip)
     bool replayIntOpt = true;    // option "replay_int_keys": u32 heap keys when replayIntOk
@@ -755,10 +757,10 @@ DevCSR dev_csr(Topology* top) {
 
 int batch_k(Topology* top) { return top->batchK; }  // 2, 4, 8 or 16 (shdtopo_set_option)
 
-// Per-slot u32 scratch after the parent pass' V * K pair list: the merged vertex list (V), the
-// sweep's pending bitmap and the touched-line bitmap (a tail vertex whose distance line the batch
-// lowered from +inf: only those lines are reset for the next batch).  Ties live in the pair
-// records' tag words (topo_sssp_batch.hip kTagTie).
+// Per-slot u32 scratch after the parent pass' V * K pair list: the merged vertex list (V), then
+// 2 bits per vertex (16 per word): the sweep's pending bit and the touched bit (a tail vertex
+// whose distance line the batch lowered from +inf: only those lines are reset for the next
+// batch), sized as two bitmaps.  Ties live in the pair records' tag words (kTagTie).
 int64_t bitmap_words(int64_t n) { return (n + 31) / 32 + 64; }
 int64_t ring_entries(Topology* top, int K) {
     const int64_t V = top->g.V;
@@ -767,6 +769,17 @@ int64_t ring_entries(Topology* top, int K) {
 int64_t queue_stride(Topology* top, int K) {  // u64 per slot of each near queue / pair list
     const int64_t V = top->g.V;
     return std::max<int64_t>(2 * V, V * K / 2);
+}
+
+// The batched SSSP's workspace back to the allocator (a layout change, or a tie-dense topology
+// whose builds run only the heap replay: its HBM then holds more replay rows at once).
+void release_workspace(Topology* top) {
+    if (top->slots <= 0) return;
+    top->d_dist.release(); top->d_ring.release(); top->d_best.release();
+    top->d_prec.release(); top->d_cnt.release();
+    top->d_bslot.release(); top->d_pathbuf.release();
+    top->d_qa.release(); top->d_qb.release(); top->d_mask.release(); top->d_hpar.release();
+    top->slots = 0;
 }
 
 // Per-slot workspace of the batched SSSP: dist [V][K], two K-bit masks per
@@ -801,14 +814,7 @@ int ensure_workspace(Topology* top, int nsrc) {
     if (top->slots >= want && top->wsK == K && top->wsRing == ringE && top->wsHpar >= hparN)
         return 0;
     const auto tw0 = std::chrono::steady_clock::now();
-    if (top->slots > 0) {
-        // layout change: release before re-allocating
-        top->d_dist.release(); top->d_ring.release(); top->d_best.release();
-        top->d_prec.release(); top->d_cnt.release();
-        top->d_bslot.release(); top->d_pathbuf.release();
-        top->d_qa.release(); top->d_qb.release(); top->d_mask.release(); top->d_hpar.release();
-        top->slots = 0;
-    }
+    release_workspace(top);  // a layout change: released before re-allocating
     const size_t n = (size_t)want * (size_t)V;
     const size_t pn = n * (size_t)K;  // per-(vertex, source) arrays
     HIPCHK(top->d_dist.ensure(pn));
@@ -946,12 +952,15 @@ ReplayCSR replay_csr(Topology* top) {
 // finish the rows in the same number of rounds.
 int ensure_replay_ws(Topology* top, int nrows) {
     const size_t V = (size_t)top->g.V;
-    const size_t per_slot = 32 * V + (size_t)kMaxHops * 64 * 4 + 64;
+    const bool ik = top->replayIntOpt && top->replayIntOk;
+    const size_t nodeB = ik ? 8 : 16;  // heap node: {u32 key, u32 vertex} or {f64 key, u32 vertex, pad}
+    const size_t per_slot = 16 * V + nodeB * V + (size_t)kMaxHops * 64 * 4 + 64;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, top->device));
-    // wavefronts per CU: 20, or as many as the CU's LDS holds (each its heap's top levels)
-    const int lds = (replay_lds_bytes(top->replayIntOpt && top->replayIntOk ? 1 : 0) + 255) & ~255;
-    const int per_cu = std::max(1, std::min(20, (int)(prop.sharedMemPerMultiprocessor > 0 ? prop.sharedMemPerMultiprocessor : 163840) / lds));
+    // wavefronts per CU: replay_wpc (20), or as many as the CU's LDS holds (each its heap's top
+    // levels)
+    const int lds = (replay_lds_bytes(ik ? 1 : 0) + 255) & ~255;
+    const int per_cu = std::max(1, std::min(top->replayWpc, (int)(prop.sharedMemPerMultiprocessor > 0 ? prop.sharedMemPerMultiprocessor : 163840) / lds));
     int want = top->replaySlotsOpt > 0 ? top->replaySlotsOpt : prop.multiProcessorCount * per_cu;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
@@ -965,12 +974,13 @@ int ensure_replay_ws(Topology* top, int nrows) {
         want = (nrows + rounds - 1) / rounds;
     }
     top->rslotsUse = want;
-    if (top->rslots >= want) return 0;
+    if (top->rslots >= want && top->rwsInt == ik) return 0;
     top->d_rvrec.release(); top->d_rnode.release(); top->d_rpath.release();
     top->rslots = 0;
     const size_t n = (size_t)want * V;
     HIPCHK(top->d_rvrec.ensure(n));
-    HIPCHK(top->d_rnode.ensure(n));
+    HIPCHK(top->d_rnode.ensure(ik ? (n + 1) / 2 : n));  // uint4 units
+    top->rwsInt = ik;
     HIPCHK(top->d_rpath.ensure((size_t)want * kMaxHops * 64));
     top->rslots = want;
     return 0;
@@ -1424,6 +1434,9 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             if (rows >= 64 && (int64_t)rlist.size() * 10 >= rows * 9) top->tieDense = true;
         }
         top->replayPending = false;
+        // builds that run only the replay (tie-dense, directed, multigraph, replay_all): the
+        // batch workspace (~110 GB at C4) goes back so the replay can hold more rows at once
+        if (allReplay || probeDense) release_workspace(top);
         if (!rlist.empty()) {
             r = upload_replay(top);
             if (r) return r;
@@ -1512,6 +1525,8 @@ int collect_row_stats(Topology* top) {
         for (int i = 0; i < 6; i++) top->stats.batch_wave_ms[i] = (double)h[ST_BT0 + i] / (double)khz;
         top->stats.batch_rounds = (int64_t)h[ST_BT0 + 6];
         top->stats.batch_edges_b = (int64_t)h[ST_BT0 + 7];
+        for (int i = 0; i < 4; i++) top->stats.sweep_events[i] = (int64_t)h[ST_SW0 + i];
+        for (int i = 0; i < 16; i++) top->stats.write_lines[i] = (int64_t)h[ST_WL0 + i];
     }
     top->stats.replay_slots = top->stats.replay_rows ? std::min(top->rslots, top->rslotsUse) : 0;
     top->stats.replay_int_keys = top->stats.replay_rows && top->replayIntOpt && top->replayIntOk ? 1 : 0;
@@ -2401,6 +2416,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "tie_replay") top->tieReplay = value != 0;
     else if (k == "replay_all") top->replayAll = value != 0;
     else if (k == "replay_slots") top->replaySlotsOpt = (int)value;
+    else if (k == "replay_wpc") top->replayWpc = std::max(1, std::min(64, (int)value));
     else if (k == "replay_landmark") top->replayLandmark = value != 0;
     else if (k == "replay_int_keys") top->replayIntOpt = value != 0;
     else if (k == "tie_dense") top->tieDenseOpt = value < 0 ? -1 : (value != 0 ? 1 : 0);

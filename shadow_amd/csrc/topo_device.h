@@ -85,7 +85,12 @@ enum StatIdx {
     ST_WALK = 60,       // batch kernel parent pass: walk steps (pairs claimed and resolved)
     ST_WK0 = 61,        //   of which resolved by the h0-tree guess, by a tail's improver, by a
                         //   hub's improver, and pairs sent to row scans (4 slots)
-    ST_COUNT = 65
+    ST_SW0 = 65,        // batch kernel sweeps (SHD_BATCH_TIME builds): pending tail vertices
+                        //   visited, of which queued (a pair in the opened bucket), holding a
+                        //   pair in that bucket that the kappa test kept out, kept pending
+    ST_WL0 = 69,        // batch kernel (SHD_BATCH_WRCOUNT builds): 64-B lines written per
+                        //   category (16 slots, topo_sssp_batch.hip WL_*)
+    ST_COUNT = 85
 };
 
 struct DevCSR {
@@ -172,8 +177,8 @@ struct ReplayCSR {
 // vertex records {f64 dist (-1 = unreached), u32 parent (replay-CSR slot of the parent edge),
 // u32 heap position} and heap nodes {f64 key, u32 vertex, pad} (positions >= the LDS part),
 // 16 B each (one line per access; u32 keys: {u32 dist, pad, ...} and 8-B nodes {u32 key, u32
-// vertex} in the first half of the node block), and a path buffer [kMaxHops][64] per slot.
-// 32 B x V + 12 KiB per slot.
+// vertex}, the node block then V x 8 B per slot), and a path buffer [kMaxHops][64] per slot.
+// 32 B (u32 keys: 24 B) x V + 12 KiB per slot.
 struct ReplayWs {
     int slots = 0;
     uint4* vrec = nullptr;

@@ -469,8 +469,11 @@ __device__ __forceinline__ int rp_shift_up(const RpHeap<I>& H, uint32_t pos,
 
 __device__ __forceinline__ uint32_t vr_par(const uint4* vr, uint32_t v) { return vr[v].z; }
 
+#ifndef SHD_RP_WAVES_EU
+#define SHD_RP_WAVES_EU 4  // minimum waves per SIMD the register allocation must allow
+#endif
 template <bool I>
-__global__ void __launch_bounds__(64, 4)
+__global__ void __launch_bounds__(64, SHD_RP_WAVES_EU)
 heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ sources,
                    const uint32_t* __restrict__ rows, int nrows,
                    const uint32_t* __restrict__ targets, int A, int full, double2* out_lr,
@@ -488,7 +491,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
     unsigned long long tph[4] = {0, 0, 0, 0}, tlast = wall_clock64();
 #endif
     // node storage: V x 16 B per slot, of which the u32-key heap uses the first half
-    RpHeap<I> H{reinterpret_cast<typename K::Node*>(ws.node + slot * V), vr, nl};
+    RpHeap<I> H{reinterpret_cast<typename K::Node*>(ws.node) + slot * V, vr, nl};
     uint32_t* pbuf = ws.pathbuf + slot * (size_t)kMaxHops * 64;
     unsigned long long n_pop = 0, n_push = 0, n_mod = 0, n_rows = 0, n_skip = 0;
 

@@ -59,6 +59,12 @@ using namespace dev;
 #ifndef SHD_TAIL_HINT
 #define SHD_TAIL_HINT 1  // record each tail pair's improver during the SSSP (parent-pass guess)
 #endif
+#ifndef SHD_MASK_TAKE
+#define SHD_MASK_TAKE 0  // a queued tail vertex's mask read and cleared by one returning atomic
+#endif
+#ifndef SHD_BATCH_WRCOUNT
+#define SHD_BATCH_WRCOUNT 0  // profiling build: 64-B lines written per category (ST_WL0)
+#endif
 #ifndef SHD_BATCH_TIME
 #define SHD_BATCH_TIME 0  // profiling build: per-wave time of the near iterations' parts
 #endif
@@ -135,7 +141,73 @@ struct LdsB {
                                 // tail's improver, a hub's improver; pairs sent to row scans
     unsigned long long bt[8];   // SHD_BATCH_TIME builds: wave ticks of tail / hub iterations in
                                 // chunk loads, phase A, phase B; phase-B rounds, active lanes
+    unsigned long long sw[4];   // SHD_BATCH_TIME builds: sweep counts (ST_SW0)
+    // per-workgroup counters and phase ticks, kept here by thread 0 rather than in (uniform)
+    // registers: near iterations, sweeps, expansions, parent-pass pairs; ticks of init, SSSP,
+    // parents, targets, sweeps; the last tick
+    unsigned long long ev[4];
+    unsigned long long tm[5];
+    unsigned long long tk;
+    unsigned long long wl[16];  // SHD_BATCH_WRCOUNT builds: 64-B lines stored / atomically
+                                // written per category (WL_*)
 };
+
+// Write categories of SHD_BATCH_WRCOUNT builds (ShdStats.write_lines): each store / atomic
+// wave-instruction adds the 64-B lines its active lanes touch (a lane whose line equals its
+// predecessor's counts once, so coalesced runs count their lines and scattered lanes one each).
+enum {
+    WL_RELAX_MIN,    // relaxation: returning atomicMin of a tail distance
+    WL_RELAX_TIE,    //   tie tag stores
+    WL_RELAX_HINT,   //   improver hint stores
+    WL_RELAX_PEND,   //   (unused: pending and touched bits share one atomic, WL_RELAX_TOUCH)
+    WL_RELAX_TOUCH,  //   first-reach atomics (touched + pending bits)
+    WL_RELAX_MASK,   //   near-mask atomics (HBM)
+    WL_MASK_ST,      // mask stores (chunk loads clear, sweeps set)
+    WL_PEND_ST,      // pending words (batch init, sweep rewrites)
+    WL_RESET,        // touched distance lines reset to +inf
+    WL_TOUCH_CLR,    // touched words cleared
+    WL_PREC,         // pair records (walk puts, tags, hint puts, row-scan results)
+    WL_PSCR,         // parent-pass scratch (best / cnt / bslot, row-scan vertex masks)
+    WL_OUT,          // table rows, hops, row minima, row flags
+    WL_HUB,          // hub rows copied to their dist rows, hub parent hints
+    WL_QUEUE,        // queue / list appends (near queues, hub lists, pair lists)
+    WL_OTHER         // path buffer spill to HBM, source init
+};
+template <int K>
+__device__ __forceinline__ void wl_count(LdsB<K>& L, int cat, bool act, const void* a) {
+#if SHD_BATCH_WRCOUNT
+    const unsigned long long line = (unsigned long long)a >> 6;
+    const unsigned long long am = __ballot(act);
+    if (!am) return;
+    const int lane = (int)(threadIdx.x & 63u);
+    const unsigned long long prev = __shfl_up(line, 1, 64);
+    const bool dup = lane > 0 && ((am >> (lane - 1)) & 1ull) && prev == line;
+    const unsigned long long nm = __ballot(act && !dup);
+    if (lane == __ffsll((long long)am) - 1) atomicAdd(&L.wl[cat], (unsigned long long)__popcll(nm));
+#else
+    (void)L; (void)cat; (void)act; (void)a;
+#endif
+}
+
+// wave_push_t (topo_dev_common.h) that also counts its queue stores (SHD_BATCH_WRCOUNT)
+template <int K>
+__device__ __forceinline__ void wpush(LdsB<K>& L, bool pred, uint32_t val, uint32_t* q,
+                                      uint32_t* lds_tail, uint32_t cap, uint32_t* lds_over,
+                                      uint32_t code) {
+    unsigned long long m = __ballot(pred);
+    if (m == 0ull) return;
+    const int lane = (int)(threadIdx.x & 63u);
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(lds_tail, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    wl_count(L, WL_QUEUE, pred && pos < cap, q + pos);
+    if (pred) {
+        if (pos < cap) q[pos] = val;
+        else atomicOr(lds_over, code);
+    }
+}
 
 // Dynamic LDS after the control block: the hubs' (deferred) source masks, parent-tie bits of the
 // first P hubs (P*K bits), "expanded at its current value" bits of every (hub, source), then the
@@ -171,8 +243,10 @@ struct BView {
     uint32_t* tb;              // LDS parent-tie bits of (hub < P, source)
     uint32_t* xb;              // LDS: (hub, source) expanded at its current distance
     uint32_t* hpar;            // HBM [P][K]: vertex whose relaxation last lowered hub v for j
-    uint32_t* pend;            // HBM, 1 bit per vertex: a tail vertex with a pair pending past cb
-    uint32_t* touch;           // HBM, 1 bit per tail vertex: the batch lowered its line from +inf
+    // HBM, 2 bits per vertex (16 vertices per word): bit 2i a pair of vertex i pending past cb,
+    // bit 2i + 1 the batch lowered its line from +inf (touched: reset at the batch's end).  A
+    // pending vertex is always touched, so one atomic sets both and the reset clears both.
+    uint32_t* pt;
     uint32_t* tpar;            // HBM [V][K] pair records: word 0 = vertex whose relaxation last
                                // lowered the tail pair (SHD_TAIL_HINT; the parent field before
                                // the parent pass), word 1 = tag word (ties: kTagTie)
@@ -262,8 +336,14 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
                 if (m) atomicOr(&D.xb[(v * K) >> 5], m << ((v * K) & 31));
             }
         } else {
+#if SHD_MASK_TAKE
+            wl_count(L, WL_MASK_ST, true, mcur + v);
+            m = MO::take(mcur, v);  // read-and-clear: one returning atomic
+#else
             m = MO::get_l2(mcur, v);
+            wl_count(L, WL_MASK_ST, true, mcur + v);
             mcur[v] = 0;
+#endif
         }
         const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
         deg = m ? r1 - r0 : 0u;
@@ -396,7 +476,12 @@ __device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t
         const uint32_t v = qv;  // this lane's queue entry (loaded by the caller)
         // every load of the vertex in one round trip: its mask (a queued vertex's is almost
         // never empty), row bounds, kappa probes and K distances
+#if SHD_MASK_TAKE
+        wl_count(L, WL_MASK_ST, true, mcur + v);
+        const uint32_t m = MO::take(mcur, v);  // read-and-clear: one returning atomic
+#else
         const uint32_t m = MO::get_l2(mcur, v);
+#endif
         const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
         const float4 ks0 = g.ksum[kKProbes / 4 * (size_t)v];
         const float4 ks1 = kKProbes > 4 ? g.ksum[kKProbes / 4 * (size_t)v + 1] : ks0;
@@ -411,7 +496,10 @@ __device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t
                 dv[2 * h + 1] = bits2d(x.y);
             }
         }
+#if !SHD_MASK_TAKE
+        wl_count(L, WL_MASK_ST, true, mcur + v);
         mcur[v] = 0;
+#endif
         deg = m ? r1 - r0 : 0u;
         if (deg) {
             double T = -INFINITY;
@@ -634,53 +722,53 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 if (!kKapInRec) kz[rr] = g.kap0[t ? n[rr] : 0u];
                 cur[rr] = t ? x : 0ull;
             }
+            // Tail pairs: the queue bookkeeping (near mask, pending and touched bits) is issued in
+            // the same round trip as the returning atomicMin, decided on the pre-check value:
+            // a pair that improves now (ab < old <= cur) also had ab < cur, so the speculative
+            // bits cover every real one; a spurious bit (a concurrent relaxation lowered the
+            // line in between) only re-expands a vertex at its current value, resets an extra
+            // line or leaves an extra pending bit -- label-correcting, the fixpoint and every
+            // tie / parent hint (decided on the atomic's return) are unchanged.  All RB rounds'
+            // atomics are in flight together.
+            unsigned long long old[RB];
+            uint32_t pm[RB];  // the mask word's previous bits (first: push), or ~0: no mask op
+            bool hfv[RB];     // a hub's first deferral
 #pragma unroll
             for (int rr = 0; rr < RB; rr++) {
-                bool im = false;
                 const bool on = ab[rr] != ~0ull;
                 const uint32_t jj = jr[rr];
-                if (on && n[rr] < D.H) {
+                const bool hub = n[rr] < D.H;
+                bool nr = false, nf = false, ft = false;
+                old[rr] = ~0ull;
+                if (on && hub) {
                     const size_t wi = (size_t)n[rr] * K + jj;
-                    const unsigned long long old = atomicMin(&D.hd[wi], ab[rr]);
-                    im = ab[rr] < old;
+                    const unsigned long long o = atomicMin(&D.hd[wi], ab[rr]);
+                    const bool im = ab[rr] < o;
                     if (im) atomicAnd(&D.xb[wi >> 5], ~(1u << (wi & 31)));
                     if (n[rr] < D.P) {  // parent hint (see the parent pass)
+                        wl_count(L, WL_HUB, im, D.hpar + wi);
                         if (im) D.hpar[wi] = L.vx[lo[rr]];
-                        else if (ab[rr] == old) atomicOr(&D.tb[wi >> 5], 1u << (wi & 31));
+                        else if (ab[rr] == o) atomicOr(&D.tb[wi >> 5], 1u << (wi & 31));
+                    }
+                    if (im) {
+                        const uint32_t b = bkt(bits2d(ab[rr]), L.sh[jj], B.inv_delta);
+                        if (b <= B.cb) nr = true;
+                        else fm = b < fm ? b : fm;
                     }
                 } else if (on && ab[rr] <= cur[rr]) {
-                    // the edge's pairs: one coalesced atomic request per line.  Returning, so
-                    // that exactly one relaxation per value counts as its improver and every
-                    // other one producing the same value as a tie (tie bit): "no tie bit" then
-                    // certifies a unique parent candidate for the parent pass.  The improver is
-                    // the parent pass' second guess (a later improver's hint may be overwritten
-                    // by an earlier one's store: the pass verifies tightness; the h0-tree edge
-                    // needs no record: it is the pass' first guess)
-                    const size_t wi = (size_t)n[rr] * K + jj;
-                    const unsigned long long old = atomicMin(&D.dist[wi], ab[rr]);
-                    im = ab[rr] < old;
-                    // tie: the pair record's tag word := this batch's tag | kTagTie (a plain,
-                    // idempotent store; no bitmap to clear for the next batch)
-                    if (ab[rr] == old) D.tpar[4 * wi + 1] = B.tie_tag;
-                    if (SHD_TAIL_HINT && im && !tree[rr]) D.tpar[4 * wi] = L.vx[lo[rr]];
-                    cur[rr] = old;
-                }
-                bool nr = false, nf = false;
-                // first reach of a tail line (old value +inf): the line joins the batch's
-                // touched set, the only lines reset for the next batch
-                const bool ft = im && n[rr] >= D.H && cur[rr] == kInfBits;
-                if (im) {
-                    const uint32_t b = bkt(bits2d(ab[rr]), L.sh[jj], B.inv_delta);
-                    if (b <= B.cb) nr = n[rr] < D.H || kappa_useful(kz[rr], L.dh0[jj],
-                                                                    bits2d(ab[rr]), g.piMax);
-                    else {
-                        fm = b < fm ? b : fm;
-                        nf = cur[rr] == kInfBits;
+                    // the edge's pairs: one coalesced atomic request per line (returning: one
+                    // relaxation per value is its improver, every other one producing the same
+                    // value a tie -- see the consuming loop)
+                    wl_count(L, WL_RELAX_MIN, true, &D.dist[(size_t)n[rr] * K + jj]);
+                    old[rr] = atomicMin(&D.dist[(size_t)n[rr] * K + jj], ab[rr]);
+                    if (ab[rr] < cur[rr]) {
+                        const uint32_t b = bkt(bits2d(ab[rr]), L.sh[jj], B.inv_delta);
+                        const bool inf = cur[rr] == kInfBits;
+                        ft = inf;
+                        if (b <= B.cb) nr = kappa_useful(kz[rr], L.dh0[jj], bits2d(ab[rr]), g.piMax);
+                        else nf = inf;
                     }
                 }
-                // the edge's pairs sit in adjacent lanes (<= K of them): their near bits and
-                // first-reach flags are OR-ed into the segment's first lane, which does the
-                // edge's pend, touch and mask atomics once
                 uint32_t gm = nr ? 1u << jj : 0u, gf = (nf ? 1u : 0u) | (ft ? 2u : 0u);
 #pragma unroll
                 for (int o = 1; o < K; o <<= 1) {
@@ -690,15 +778,38 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 }
                 const uint32_t pe = __shfl_up(er[rr], 1, 64);
                 const bool head = on && (lane == 0 || pe != er[rr]);
-                if (head && (gf & 1u)) (void)atomicOr(&D.pend[n[rr] >> 5], 1u << (n[rr] & 31));
-                if (head && (gf & 2u)) (void)atomicOr(&D.touch[n[rr] >> 5], 1u << (n[rr] & 31));
-                bool first = false, hfirst = false;
+                // first reach: touched (bit 1), and pending when past cb (bit 0): one atomic
+                wl_count(L, WL_RELAX_TOUCH, head && gf, &D.pt[n[rr] >> 4]);
+                wl_count(L, WL_RELAX_MASK, head && gm && !hub, mnxt + n[rr]);
+                if (head && gf) (void)atomicOr(&D.pt[n[rr] >> 4], gf << (2u * (n[rr] & 15u)));
+                pm[rr] = ~0u;
+                hfv[rr] = false;
                 if (head && gm) {
-                    if (n[rr] < D.H) hfirst = MO::set(hdef, n[rr], gm) == 0u;
-                    else first = MO::set(mnxt, n[rr], gm) == 0u;
+                    if (hub) hfv[rr] = MO::set(hdef, n[rr], gm) == 0u;
+                    else pm[rr] = MO::set(mnxt, n[rr], gm);
                 }
-                wave_push_t<uint32_t>(first, n[rr], qout, &L.qtail, qcap, &L.fover, 1u);
-                wave_push_t<uint32_t>(hfirst, n[rr], hq, &L.htail, D.H, &L.fover, 1u);
+            }
+#pragma unroll
+            for (int rr = 0; rr < RB; rr++) {
+                const uint32_t jj = jr[rr];
+                if (old[rr] != ~0ull) {
+                    const size_t wi = (size_t)n[rr] * K + jj;
+                    const bool im = ab[rr] < old[rr];
+                    // tie: the pair record's tag word := this batch's tag | kTagTie (a plain,
+                    // idempotent store; no bitmap to clear for the next batch)
+                    wl_count(L, WL_RELAX_TIE, ab[rr] == old[rr], D.tpar + 4 * wi);
+                    if (ab[rr] == old[rr]) D.tpar[4 * wi + 1] = B.tie_tag;
+                    // the improver: the parent pass' second guess (verified there; the h0-tree
+                    // edge needs no record: it is the pass' first guess)
+                    wl_count(L, WL_RELAX_HINT, SHD_TAIL_HINT && im && !tree[rr], D.tpar + 4 * wi);
+                    if (SHD_TAIL_HINT && im && !tree[rr]) D.tpar[4 * wi] = L.vx[lo[rr]];
+                    if (im) {
+                        const uint32_t b = bkt(bits2d(ab[rr]), L.sh[jj], B.inv_delta);
+                        if (b > B.cb) fm = b < fm ? b : fm;
+                    }
+                }
+                wpush<K>(L, pm[rr] == 0u, n[rr], qout, &L.qtail, qcap, &L.fover, 1u);
+                wpush<K>(L, hfv[rr], n[rr], hq, &L.htail, D.H, &L.fover, 1u);
             }
             }
             if (__ballot(fm != kNoBucket)) {
@@ -810,21 +921,30 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     // then the merged vertex list
     uint32_t* fscr = reinterpret_cast<uint32_t*>(ws.ring) + (size_t)slot * ws.ring_entries;
     uint32_t* vscr = fscr + (size_t)V * K;  // parent-pass vertex list (V entries)
-    const uint32_t pw = (uint32_t)((V + 31) / 32);  // words of the pending bitmap
-    D.pend = vscr + (size_t)V;
-    D.touch = D.pend + pw + 64;  // touched-line bitmap (one bit per tail vertex)
+    const uint32_t pw = (uint32_t)((V + 15) / 16);  // words of the pending / touched bits
+    D.pt = vscr + (size_t)V;
     const uint32_t pcap = (uint32_t)(V * K);
 
     uint32_t iter = ctr[0];
-    unsigned long long n_near = 0, n_sweep = 0, n_expand = 0, n_par = 0;
-    unsigned long long t_init = 0, t_sssp = 0, t_par = 0, t_tgt = 0, t_split = 0;
     if (tid < 4) L.cnt[tid] = 0;
     if (tid < 5) L.pt[tid] = 0;
     if (tid < 4) L.dg[tid] = 0;
     if (tid < 8) L.bt[tid] = 0;
+    if (tid < 4) L.sw[tid] = 0;
+    if (tid < 16) L.wl[tid] = 0;
     if (tid == 0) L.touched = 0;
     if (tid < 5) L.wk[tid] = 0;
-    unsigned long long tk = wall_clock64();
+    if (tid < 4) L.ev[tid] = 0;
+    if (tid < 5) L.tm[tid] = 0;
+    // phase boundary (all threads pass it together): thread 0 charges the ticks since the last
+    // one to phase i
+    auto tick = [&](int i) {
+        if (tid == 0) {
+            const unsigned long long t = wall_clock64();
+            L.tm[i] += t - L.tk;
+            L.tk = t;
+        }
+    };
 
     for (;;) {
         if (tid == 0) L.idx = (uint32_t)atomicAdd(&stats[ST_DEQUEUE], 1ull);
@@ -836,11 +956,13 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         if ((int64_t)bidx * kf >= nsrc) break;
         const int r0 = (int)bidx * kf;
         const int nk = min(kf, nsrc - r0);
-        tk = wall_clock64();
-        const unsigned long long bt_near = n_near, bt_sweep = n_sweep, bt_exp = n_expand,
-                                 bt_rel = L.cnt[0];
+        if (tid == 0) L.tk = wall_clock64();
         if (ws.btrace && tid == 0) {
-            ws.btrace[8 * (size_t)bidx] = tk;
+            ws.btrace[8 * (size_t)bidx] = L.tk;
+            ws.btrace[8 * (size_t)bidx + 3] = L.ev[0];
+            ws.btrace[8 * (size_t)bidx + 4] = L.ev[1];
+            ws.btrace[8 * (size_t)bidx + 5] = L.ev[2];
+            ws.btrace[8 * (size_t)bidx + 6] = L.cnt[0];
             ws.btrace[8 * (size_t)bidx + 2] = (unsigned long long)slot;
         }
 
@@ -851,7 +973,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         }
         for (uint32_t i = tid; i < tbw; i += kSsspBlock) D.tb[i] = 0u;
         for (uint32_t i = tid; i < xbw; i += kSsspBlock) D.xb[i] = 0u;
-        for (uint32_t i = tid; i < pw; i += kSsspBlock) D.pend[i] = 0u;
+        // (the pending / touched words are zero: the previous batch's reset cleared every word
+        // it touched, and a pending vertex is always touched)
         // the batch's tag: claims of the parent pass, ties of the SSSP (pair records)
         iter++;
         const uint32_t ep = (iter - 1u) % kTagMask + 1u;
@@ -872,14 +995,13 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             if (s < H) D.hd[(size_t)s * K + tid] = 0ull;
             else {
                 D.dist[(size_t)s * K + tid] = 0ull;
-                atomicOr(&D.pend[s >> 5], 1u << (s & 31));
-                atomicOr(&D.touch[s >> 5], 1u << (s & 31));
+                atomicOr(&D.pt[s >> 4], 3u << (2u * (s & 15u)));
             }
             atomicMin(&L.fminb, bkt(0.0, L.sh[tid], B.inv_delta));
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        { unsigned long long t = wall_clock64(); t_init += t - tk; tk = t; }
+        tick(0);
 
         // ---------------- lock-step delta-stepping over the shifted buckets -------------------
         // L.fminb is exact at every bucket change: the sweep sets it to the smallest pending
@@ -912,7 +1034,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     if (hubs) L.htail = 0;
                 }
                 __syncthreads();
-                n_expand += ns;
+                if (tid == 0) L.ev[2] += ns;
                 const unsigned long long e0 = L.cnt[2], a0 = L.cnt[0];
                 const bool first_it = guard == 0 || just_swept;
 #ifndef SHD_BATCH_NOWAVE
@@ -931,7 +1053,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 just_swept = false;
                 { uint32_t* t = qin; qin = qout; qout = t; }
                 { M* t = mcur; mcur = mnxt; mnxt = t; }
-                n_near++;
+                if (tid == 0) L.ev[0]++;
                 if (++guard > iter_guard) {
                     aborted = true;
                     nq = 0;
@@ -993,7 +1115,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         const uint32_t v = (uint32_t)(2 * i / K);
                         const bool lead = (tid % LPV) == 0 && m != 0u && i < hpair;
                         if (lead) hdef[v] = (M)m;
-                        wave_push_t<uint32_t>(lead, v, hfill, &L.htail, H, &L.fover, 32u);
+                        wpush<K>(L, lead, v, hfill, &L.htail, H, &L.fover, 32u);
                     }
                     km = wave_min_u32(km);
                     if ((tid & 63) == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
@@ -1003,94 +1125,109 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 // thread, compacts the set bits' vertices into LDS (the chunk buffers are idle
                 // here), classifies their lines (LPV lanes x 16 B per vertex) and rewrites the
                 // words with the vertices that still hold a pair past nb.
-                constexpr uint32_t VPI = kSsspBlock / LPV;                 // vertices per pass
-                uint32_t* sv = reinterpret_cast<uint32_t*>(L.val);        // survivor words
-                uint32_t* cl = sv + kSsspBlock;                           // compacted vertices
-                constexpr uint32_t kCl = (uint32_t)(sizeof(L.val) / 4) - kSsspBlock;
-                static_assert(kCl >= 256, "sweep compaction buffer");
-                // the next round's bitmap word is loaded before this round's chain (a sweep does
-                // not race with relaxations: rounds only rewrite their own words)
-                uint32_t nword = H / 32 + tid < pw ? ld_l2_u32(&D.pend[H / 32 + tid]) : 0u;
-                for (uint32_t wb = H / 32; wb < pw; wb += kSsspBlock) {
-                    const uint32_t wi = wb + tid;
-                    const uint32_t word = nword;
-                    nword = wi + kSsspBlock < pw ? ld_l2_u32(&D.pend[wi + kSsspBlock]) : 0u;
-                    sv[tid] = 0u;
-                    uint32_t tot;
-                    const uint32_t off = block_excl_scan<kSsspBlock>((uint32_t)__popc(word), L.wave,
-                                                                     &tot);
-                    for (uint32_t p0 = 0; p0 < tot; p0 += kCl) {
-                        {
-                            uint32_t w = word, o = off;
-                            while (w) {
-                                const uint32_t b = (uint32_t)__ffs(w) - 1u;
-                                w &= w - 1u;
-                                if (o >= p0 && o < p0 + kCl) cl[o - p0] = wi * 32u + b;
-                                o++;
-                            }
-                        }
-                        __syncthreads();
-                        const uint32_t n = min(kCl, tot - p0);
-                        for (uint32_t vb = 0; vb < n; vb += VPI * SU) {
-                            unsigned long long d[SU][2];
-                            uint32_t vv[SU];
-                            float k0[SU];
-#pragma unroll
-                            for (int u = 0; u < SU; u++) {
-                                const uint32_t e = vb + (uint32_t)u * VPI + tid / LPV;
-                                vv[u] = e < n ? cl[e] : 0xFFFFFFFFu;
-                                k0[u] = g.kap0[e < n ? vv[u] : 0u];
-                                d[u][0] = d[u][1] = kInfBits;
-                                if (e < n) {
-                                    // L1-bypassing 16-B load: the words were lowered by atomics
-                                    typedef unsigned long long u64x2
-                                        __attribute__((ext_vector_type(2)));
-                                    const u64x2 x = __builtin_nontemporal_load(
-                                        reinterpret_cast<const u64x2*>(D.dist) +
-                                        (size_t)vv[u] * LPV + tid % LPV);
-                                    d[u][0] = x.x;
-                                    d[u][1] = x.y;
+                // Wave-parallel tail sweep: every wave owns blocks of 64 bitmap words (one per
+                // lane), compacts their set bits into its own LDS slice, classifies those lines
+                // and rewrites its own words -- no block barrier until the sweep ends.
+                {
+                    constexpr uint32_t NW = kSsspBlock / 64;
+                    constexpr uint32_t VPW = 64 / LPV;  // vertices per wave instruction
+                    uint32_t* svb = reinterpret_cast<uint32_t*>(L.val);   // survivor words
+                    constexpr uint32_t kClW = ((uint32_t)(sizeof(L.val) / 4) - NW * 64) / NW;
+                    static_assert(kClW >= 64, "sweep compaction slice");
+                    const uint32_t wv = tid >> 6, lane = tid & 63u;
+                    uint32_t* svw = svb + wv * 64u;
+                    uint32_t* clw = svb + NW * 64u + wv * kClW;
+                    const uint32_t w0 = H / 16;
+                    uint32_t nword = w0 + wv * 64u + lane < pw ? ld_l2_u32(&D.pt[w0 + wv * 64u + lane]) : 0u;
+                    for (uint32_t bb = w0 + wv * 64u; bb < pw; bb += NW * 64u) {
+                        const uint32_t wi = bb + lane;
+                        const uint32_t word = nword;
+                        const uint32_t pend = word & 0x55555555u;  // the pending bits
+                        nword = wi + NW * 64u < pw ? ld_l2_u32(&D.pt[wi + NW * 64u]) : 0u;
+                        svw[lane] = 0u;
+                        uint32_t tot;
+                        const uint32_t off = wave_excl_scan((uint32_t)__popc(pend), &tot);
+                        for (uint32_t p0 = 0; p0 < tot; p0 += kClW) {
+                            {
+                                uint32_t w = pend, o = off;
+                                while (w) {
+                                    const uint32_t b = (uint32_t)__ffs(w) - 1u;
+                                    w &= w - 1u;
+                                    if (o >= p0 && o < p0 + kClW) clw[o - p0] = wi * 16u + b / 2u;
+                                    o++;
                                 }
                             }
-                            uint32_t km = kNoBucket;
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            __builtin_amdgcn_wave_barrier();
+                            const uint32_t n = min(kClW, tot - p0);
+                            for (uint32_t vb = 0; vb < n; vb += VPW * SU) {
+                                unsigned long long d[SU][2];
+                                uint32_t vv[SU];
+                                float k0[SU];
 #pragma unroll
-                            for (int u = 0; u < SU; u++) {
-                                const uint32_t jl = 2 * (tid % LPV);
-                                uint32_t m = 0, keep = 0;
-#pragma unroll
-                                for (int h = 0; h < 2; h++) {
-                                    if (d[u][h] == kInfBits) continue;
-                                    const uint32_t b = bkt(bits2d(d[u][h]), L.sh[jl + h],
-                                                           B.inv_delta);
-                                    if (b == nb) {
-                                        if (kappa_useful(k0[u], L.dh0[jl + h],
-                                                         bits2d(d[u][h]), g.piMax))
-                                            m |= 1u << (jl + h);
-                                    } else if (b > nb) {
-                                        keep = 1u;
-                                        if (b < km) km = b;
+                                for (int u = 0; u < SU; u++) {
+                                    const uint32_t e = vb + (uint32_t)u * VPW + lane / LPV;
+                                    vv[u] = e < n ? clw[e] : 0xFFFFFFFFu;
+                                    k0[u] = g.kap0[e < n ? vv[u] : 0u];
+                                    d[u][0] = d[u][1] = kInfBits;
+                                    if (e < n) {
+                                        typedef unsigned long long u64x2
+                                            __attribute__((ext_vector_type(2)));
+                                        const u64x2 x = __builtin_nontemporal_load(
+                                            reinterpret_cast<const u64x2*>(D.dist) +
+                                            (size_t)vv[u] * LPV + lane % LPV);
+                                        d[u][0] = x.x;
+                                        d[u][1] = x.y;
                                     }
                                 }
+                                uint32_t km = kNoBucket;
 #pragma unroll
-                                for (uint32_t o = 1; o < LPV; o <<= 1) {
-                                    m |= __shfl_xor(m, (int)o, 64);
-                                    keep |= __shfl_xor(keep, (int)o, 64);
+                                for (int u = 0; u < SU; u++) {
+                                    const uint32_t jl = 2 * (lane % LPV);
+                                    uint32_t m = 0, keep = 0;
+#pragma unroll
+                                    for (int h = 0; h < 2; h++) {
+                                        if (d[u][h] == kInfBits) continue;
+                                        const uint32_t b = bkt(bits2d(d[u][h]), L.sh[jl + h],
+                                                               B.inv_delta);
+                                        if (b == nb) {
+                                            if (kappa_useful(k0[u], L.dh0[jl + h],
+                                                             bits2d(d[u][h]), g.piMax))
+                                                m |= 1u << (jl + h);
+                                        } else if (b > nb) {
+                                            keep = 1u;
+                                            if (b < km) km = b;
+                                        }
+                                    }
+#pragma unroll
+                                    for (uint32_t o = 1; o < LPV; o <<= 1) {
+                                        m |= __shfl_xor(m, (int)o, 64);
+                                        keep |= __shfl_xor(keep, (int)o, 64);
+                                    }
+                                    const uint32_t v = vv[u];
+                                    const bool ok = (lane % LPV) == 0 && v != 0xFFFFFFFFu;
+                                    const bool lead = ok && m != 0u;
+                                    wl_count(L, WL_MASK_ST, lead, mcur + (lead ? v : 0u));
+                                    if (lead) mcur[v] = (M)m;
+                                    if (ok && keep) atomicOr(&svw[v / 16 - bb], 1u << (2u * (v & 15u)));
+                                    wpush<K>(L, lead, v, qin, &L.qtail, cap, &L.fover, 32u);
                                 }
-                                const uint32_t v = vv[u];
-                                const bool ok = (tid % LPV) == 0 && v != 0xFFFFFFFFu;
-                                const bool lead = ok && m != 0u;
-                                if (lead) mcur[v] = (M)m;
-                                if (ok && keep) atomicOr(&sv[v / 32 - wb], 1u << (v & 31));
-                                wave_push_t<uint32_t>(lead, v, qin, &L.qtail, cap, &L.fover, 32u);
+                                km = wave_min_u32(km);
+                                if (lane == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
                             }
-                            km = wave_min_u32(km);
-                            if ((tid & 63) == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
+                            // the slice is refilled by the next pass
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            __builtin_amdgcn_wave_barrier();
                         }
-                        __syncthreads();
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        __builtin_amdgcn_wave_barrier();
+                        // the touched bits stay; svw holds a subset of the pending bits: an
+                        // unchanged word needs no store
+                        const uint32_t nw = (word & 0xAAAAAAAAu) | svw[lane];
+                        wl_count(L, WL_PEND_ST, wi < pw && nw != word, D.pt + wi);
+                        if (wi < pw && nw != word) D.pt[wi] = nw;
+                        __builtin_amdgcn_wave_barrier();
                     }
-                    // sv holds a subset of word's bits: an unchanged word needs no store
-                    if (wi < pw && sv[tid] != word) D.pend[wi] = sv[tid];
-                    __syncthreads();
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1099,8 +1236,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             if (tid == 0) L.cnt[1] += nq;
             B.cb = nb;
             just_swept = true;
-            n_sweep++;
-            t_split += wall_clock64() - ts0;
+            if (tid == 0) {
+                L.ev[1]++;
+                L.tm[4] += wall_clock64() - ts0;
+            }
             __syncthreads();
         }
         if (aborted) {
@@ -1114,7 +1253,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             atomicAdd(&stats[ST_FARSCAN], 1ull);
             atomicOr(&stats[ST_OVERSITE], (unsigned long long)L.fover);
         }
-        { unsigned long long t = wall_clock64(); t_sssp += t - tk; tk = t; }
+        tick(1);
 
         // ---------------- parents for the target chains of every source of the batch ---------
         // One level-synchronous pass over (vertex, source) pairs p = v * K + j (SURVEY.md A.3:
@@ -1138,7 +1277,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 q = t * K + j;
                 p = t != L.src[j];
             }
-            wave_push_t<uint32_t>(p, q, pcur, &L.qtail, pcap, &L.fover, 128u);
+            wpush<K>(L, p, q, pcur, &L.qtail, pcap, &L.fover, 128u);
         }
         __syncthreads();
         uint32_t nF = min(L.qtail, pcap);
@@ -1146,6 +1285,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // A pair's record: its parent, the batch's tag, the loss of the parent edge (one store)
         auto put = [&](uint32_t q, uint32_t u, double loss) {
             const unsigned long long lb = d2bits(loss);
+            wl_count(L, WL_PREC, true, prec + q);
             prec[q] = make_uint4(u, ept, (uint32_t)lb, (uint32_t)(lb >> 32));
         };
         // A guess certified without scanning a row, past the h0-tree guess of a tail (tried by
@@ -1222,7 +1362,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             return h;
         };
         while (nF > 0) {
-            n_par += nF;
+            if (tid == 0) L.ev[3] += nF;
             unsigned long long tp0 = wall_clock64();
             // Walks: chains are followed towards the source while the h0-tree guess certifies
             // parents (no level barriers); a chain stops at the source, at a pair another walk
@@ -1285,8 +1425,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                     h = hn;
                                 }
                             } else {
+                                wl_count(L, WL_PREC, true, precw + 4 * (size_t)q);
                                 precw[4 * (size_t)q + 1] = ept | (tied ? kTagTie : 0u);
                                 const uint32_t pos = atomicAdd(&L.qtail, 1u);
+                                wl_count(L, WL_QUEUE, pos < pcap, fscr + pos);
                                 if (pos < pcap) fscr[pos] = q;
                                 else atomicOr(&L.fover, 128u);
                                 act = false;
@@ -1322,13 +1464,16 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     const bool ok = try_hint(q, D.get(q / K, q % K), &u);
                     atomicAdd(&L.wk[ok ? (q / K >= H ? 2 : 3) : 4], 1ull);
                     if (!ok) {
+                        wl_count(L, WL_PSCR, true, best + q);
+                        wl_count(L, WL_PSCR, true, cntc + q);
+                        wl_count(L, WL_PSCR, true, bslot + q);
                         best[q] = kInfBits;
                         cntc[q] = 0;
                         bslot[q] = 0xFFFFFFFFu;
                         scan = true;
                     }
                 }
-                wave_push_t<uint32_t>(scan, q, pcur, &L.qtail, pcap, &L.fover, 128u);
+                wpush<K>(L, scan, q, pcur, &L.qtail, pcap, &L.fover, 128u);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -1347,9 +1492,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     if (i < nR) {
                         const uint32_t q = rl[i];
                         v = q / K;
+                        wl_count(L, WL_PSCR, v >= H, mA + v);
                         first = (v < H ? MO::set(hdef, v, 1u << (q % K)) : MO::set(mA, v, 1u << (q % K))) == 0u;
                     }
-                    wave_push_t<uint32_t>(first, v, vscr, &L.qtail, cap, &L.fover, 128u);
+                    wpush<K>(L, first, v, vscr, &L.qtail, cap, &L.fover, 128u);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
@@ -1386,6 +1532,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         for (int q = 0; q < K; q++) {
                             if (((m >> q) & 1u) && __dadd_rn(bits2d(du[q]), wt) == L.val[lo * K + q]) {
                                 const uint32_t pq = L.vx[lo] * K + (uint32_t)q;
+                                wl_count(L, WL_PSCR, true, best + pq);
+                                wl_count(L, WL_PSCR, true, cntc + pq);
+                                wl_count(L, WL_PSCR, true, bslot + pq);
                                 atomicMin(&best[pq], du[q]);
                                 atomicAdd(&cntc[pq], 1u);
                                 atomicMin(&bslot[pq], jr);
@@ -1407,12 +1556,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     if (i < nR) {
                         q = rl[i];
                         multi = ld_l2_u32(&cntc[q]) > 1u;
+                        wl_count(L, WL_PSCR, multi, cntc + q);
+                        wl_count(L, WL_PSCR, multi, bslot + q);
                         if (multi) {
                             atomicExch(&cntc[q], 0u);
                             atomicExch(&bslot[q], 0xFFFFFFFFu);
                         }
                     }
-                    wave_push_t<uint32_t>(multi, q, pnxt, &L.qtail, pcap, &L.fover, 128u);
+                    wpush<K>(L, multi, q, pnxt, &L.qtail, pcap, &L.fover, 128u);
                 }
                 __syncthreads();
                 const uint32_t nM = min(L.qtail, pcap);
@@ -1426,7 +1577,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                             double wt;
                             adj_load(g, jr, u, wt);
                             const unsigned long long du = D.get(u, q % K);
-                            if (__dadd_rn(bits2d(du), wt) == dv && du == ld_l2_u64(&best[q])) {
+                            const bool hit = __dadd_rn(bits2d(du), wt) == dv && du == ld_l2_u64(&best[q]);
+                            wl_count(L, WL_PSCR, hit, cntc + q);
+                            wl_count(L, WL_PSCR, hit, bslot + q);
+                            if (hit) {
                                 atomicAdd(&cntc[q], 1u);
                                 atomicMin(&bslot[q], jr);
                             }
@@ -1436,6 +1590,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     const uint32_t q = rl[i];
                     const uint32_t jr = ld_l2_u32(&bslot[q]);
                     const uint32_t c = ld_l2_u32(&cntc[q]);
+                    wl_count(L, WL_PREC, true, prec + q);
                     if (jr == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
                         atomicAdd(&stats[ST_ERRORS], 1ull);
                         prec[q] = make_uint4(L.src[q % K] | 0x40000000u, ept, 0u, 0u);
@@ -1465,7 +1620,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     q = u * K + j;
                     p = u != L.src[j];
                 }
-                wave_push_t<uint32_t>(p, q, pnxt, &L.qtail, pcap, &L.fover, 128u);
+                wpush<K>(L, p, q, pnxt, &L.qtail, pcap, &L.fover, 128u);
             }
             __syncthreads();
             nF = min(L.qtail, pcap);
@@ -1473,7 +1628,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             __syncthreads();
             if (tid == 0) L.pt[4] += wall_clock64() - tp0;  // next level
         }
-        { unsigned long long t = wall_clock64(); t_par += t - tk; tk = t; }
+        tick(2);
 
         // ---------------- per-target latency / reliability / hops (shd-topology.c:561-671) ----
         // items (source j, target k) of the whole batch; each thread walks its pairs' chains.
@@ -1481,7 +1636,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // hub LDS holds the first nl levels of the per-thread path buffer (the chain's edge
         // losses, multiplied in path order after the walk); deeper levels go to HBM (pbuf).
         if ((int)tid < K) L.rmin[tid] = kInfBits;
-        for (uint32_t i = tid; i < H * K; i += kSsspBlock) D.dist[i] = D.hd[i];
+        for (uint32_t i = tid; i < H * K; i += kSsspBlock) {
+            wl_count(L, WL_HUB, true, D.dist + i);
+            D.dist[i] = D.hd[i];
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         double* lpb = reinterpret_cast<double*>(D.hd);
@@ -1525,6 +1683,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         break;
                     }
                     amb |= (r.x >> 31) != 0u;
+                    wl_count(L, WL_OTHER, h < kMaxHops && h >= nl, pb_at(h));
                     if (h < kMaxHops) *pb_at(h) = __hiloint2double((int)r.w, (int)r.z);
                     h++;
                     v = r.x & 0x3FFFFFFFu;
@@ -1556,6 +1715,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             }
             const size_t o = (size_t)(ws.rowmap ? (int)ws.rowmap[r0 + (int)j] : r0 + (int)j) * (size_t)A + k;
             const uint16_t hh = (uint16_t)(h > 65535u ? 65535u : h);
+            wl_count(L, WL_OUT, true, out_lr + o);
+            wl_count(L, WL_OUT, true, out_hops + o);
             if (SHD_OUT_NT) {  // the table (1.8 GB per launch) is not re-read by the kernel
                 typedef double f64x2 __attribute__((ext_vector_type(2)));
                 const f64x2 r2 = {lat, rel};
@@ -1573,14 +1734,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             atomicMin(&stats[ST_GLOBAL_MIN], L.rmin[tid]);  // shd-topology.c:500-511
         }
         __syncthreads();
-        { unsigned long long t = wall_clock64(); t_tgt += t - tk; tk = t; }
+        tick(3);
         {
             // the distance lines this batch lowered from +inf back to +inf: only touched tail
-            // vertices (their bit in D.touch), not the whole [V][K] block (64 MB at K = 8 per
-            // batch).  Done at the batch's end (its time counts as setup): the next batch's
+            // vertices (their touched bit in D.pt), not the whole [V][K] block (64 MB at K = 8 per
+            // batch); the words are cleared, pending bits included.  Done at the batch's end (its time counts as setup): the next batch's
             // setup waits for these stores; a one-round shard no longer has every slot resetting
             // at its kernel's start.
-            // A thread loads one touch word; the G = K / 2 lanes of a group then reset the
+            // A thread loads one word (16 vertices); the G = K / 2 lanes of a group then reset the
             // group's G words' vertices together, lane p storing the p-th 16 B of each line, so
             // one store instruction writes 64 / G whole lines (one write request per line, not
             // one per 16 B).
@@ -1590,14 +1751,16 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             constexpr uint32_t G = K / 2;
             const uint32_t part = tid % G, gbase = (tid & 63u) - part;
             unsigned long long nt = 0;
-            const uint32_t w0 = H / 32;
-            uint32_t nword = w0 + tid < pw ? ld_l2_u32(&D.touch[w0 + tid]) : 0u;
+            const uint32_t w0 = H / 16;
+            uint32_t nword = w0 + tid < pw ? ld_l2_u32(&D.pt[w0 + tid]) : 0u;
             for (uint32_t wb = w0; wb < pw; wb += kSsspBlock) {
                 const uint32_t wi = wb + tid;
-                const uint32_t myw = nword;
-                nword = wi + kSsspBlock < pw ? ld_l2_u32(&D.touch[wi + kSsspBlock]) : 0u;
-                if (myw) {
-                    D.touch[wi] = 0u;
+                const uint32_t word = nword;
+                const uint32_t myw = word & 0xAAAAAAAAu;  // the touched bits
+                nword = wi + kSsspBlock < pw ? ld_l2_u32(&D.pt[wi + kSsspBlock]) : 0u;
+                wl_count(L, WL_TOUCH_CLR, word != 0u, D.pt + wi);
+                if (word) {
+                    D.pt[wi] = 0u;
                     nt += (unsigned long long)__popc(myw);
                 }
                 if (!__any(myw != 0u)) continue;
@@ -1606,8 +1769,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     uint32_t w = __shfl(myw, (int)(gbase + p), 64);
                     const uint32_t wv = wi - part + p;
                     while (w) {
-                        const uint32_t v = wv * 32u + (uint32_t)__ffs(w) - 1u;
+                        const uint32_t v = wv * 16u + ((uint32_t)__ffs(w) - 1u) / 2u;
                         w &= w - 1u;
+                        wl_count(L, WL_RESET, true, d2 + (size_t)v * G + part);
                         if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + (size_t)v * G + part);
                         else d2[(size_t)v * G + part] = inf2;
                     }
@@ -1616,14 +1780,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             nt = wave_sum_u64(nt);
             if ((tid & 63) == 0 && nt) atomicAdd(&L.touched, nt);
         }
-        { unsigned long long t = wall_clock64(); t_init += t - tk; tk = t; }
+        tick(0);
         if (ws.btrace && tid == 0) {
             unsigned long long* b = ws.btrace + 8 * (size_t)bidx;
-            b[1] = tk;
-            b[3] = n_near - bt_near;
-            b[4] = n_sweep - bt_sweep;
-            b[5] = n_expand - bt_exp;
-            b[6] = L.cnt[0] - bt_rel;
+            b[1] = L.tk;
+            b[3] = L.ev[0] - b[3];
+            b[4] = L.ev[1] - b[4];
+            b[5] = L.ev[2] - b[5];
+            b[6] = L.cnt[0] - b[6];
             b[7] = (unsigned long long)nk;
         }
     }
@@ -1631,14 +1795,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     if (tid == 0) {
         ctr[0] = iter;
         atomicAdd(&stats[ST_RELAX], L.cnt[0]);
-        atomicAdd(&stats[ST_T_INIT], t_init);
-        atomicAdd(&stats[ST_T_SSSP], t_sssp);
-        atomicAdd(&stats[ST_T_PARENT], t_par);
-        atomicAdd(&stats[ST_T_TARGET], t_tgt);
-        atomicAdd(&stats[ST_T_SPLIT], t_split);
-        atomicAdd(&stats[ST_NEAR_IT], n_near);
-        atomicAdd(&stats[ST_SPLITS], n_sweep);
-        atomicAdd(&stats[ST_EV0 + 0], n_expand);
+        atomicAdd(&stats[ST_T_INIT], L.tm[0]);
+        atomicAdd(&stats[ST_T_SSSP], L.tm[1]);
+        atomicAdd(&stats[ST_T_PARENT], L.tm[2]);
+        atomicAdd(&stats[ST_T_TARGET], L.tm[3]);
+        atomicAdd(&stats[ST_T_SPLIT], L.tm[4]);
+        atomicAdd(&stats[ST_NEAR_IT], L.ev[0]);
+        atomicAdd(&stats[ST_SPLITS], L.ev[1]);
+        atomicAdd(&stats[ST_EV0 + 0], L.ev[2]);
         atomicAdd(&stats[ST_EV0 + 3], L.cnt[1]);
         atomicAdd(&stats[ST_EV0 + 1], L.cnt[2]);
         atomicAdd(&stats[ST_EV0 + 6], L.cnt[3]);
@@ -1649,12 +1813,16 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         atomicAdd(&stats[ST_NEAR_IT + 0], 0ull);
         atomicAdd(&stats[ST_OVERSITE], 0ull);
         atomicAdd(&stats[ST_EV0 + 5], 0ull);
-        atomicAdd(&stats[ST_EV0 + 5], n_par);
+        atomicAdd(&stats[ST_EV0 + 5], L.ev[3]);
         for (int i = 0; i < 4; i++) atomicAdd(&stats[ST_PT0 + i], L.pt[1 + i]);
         atomicAdd(&stats[ST_WALK], L.wk[0]);
         for (int i = 0; i < 4; i++) atomicAdd(&stats[ST_WK0 + i], L.wk[1 + i]);
-        if (SHD_BATCH_TIME)
+        if (SHD_BATCH_TIME) {
             for (int i = 0; i < 8; i++) atomicAdd(&stats[ST_BT0 + i], L.bt[i]);
+            for (int i = 0; i < 4; i++) atomicAdd(&stats[ST_SW0 + i], L.sw[i]);
+        }
+        if (SHD_BATCH_WRCOUNT)
+            for (int i = 0; i < 16; i++) atomicAdd(&stats[ST_WL0 + i], L.wl[i]);
     }
 }
 

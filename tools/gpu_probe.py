@@ -70,6 +70,17 @@ for rep in range(args.reps):
                   [x / rows for x in w] + [st["batch_rounds"] / rows, st["batch_edges_b"] / rows,
                                            st["batch_edges_b"] / max(1, st["batch_rounds"])]),
               flush=True)
+    if any(st.get("sweep_events", [0])):
+        sw = st["sweep_events"]
+        print("   sweeps (SHD_BATCH_TIME) per source: pending visited %.0f, queued %.0f, kappa-held "
+              "%.0f, kept %.0f" % tuple(x / rows for x in sw), flush=True)
+    if any(st.get("write_lines", [0])):
+        names = ("relax_min", "relax_tie", "relax_hint", "relax_pend", "relax_touch", "relax_mask",
+                 "mask_st", "pend_st", "reset", "touch_clr", "prec", "pscr", "out", "hub", "queue",
+                 "other")
+        wl = st["write_lines"]
+        print("   write lines per source (SHD_BATCH_WRCOUNT): total %.0f %s" % (
+            sum(wl) / rows, {k: round(v / rows) for k, v in zip(names, wl)}), flush=True)
     print("   per-source events:", {k: "%.3g" % (v / rows) for k, v in st["events"].items()},
           flush=True)
 x = lr[..., 0].cpu().numpy()
