@@ -331,6 +331,9 @@ typedef struct {
                                    atomics; mask stores; pending words; line reset; touched-word
                                    clears; pair records; parent scratch; table output; hub rows and
                                    hints; queue appends; other */
+    int64_t read_lines[8];      /* the same builds: 64-B lines read, by category (RL_*): phase-B
+                                   pre-checks, phase-A records, chunk loads, sweeps, parent walks,
+                                   epilogue, reset, other (hint pass, row scans) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

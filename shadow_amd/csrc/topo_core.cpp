@@ -1527,6 +1527,7 @@ int collect_row_stats(Topology* top) {
         top->stats.batch_edges_b = (int64_t)h[ST_BT0 + 7];
         for (int i = 0; i < 4; i++) top->stats.sweep_events[i] = (int64_t)h[ST_SW0 + i];
         for (int i = 0; i < 16; i++) top->stats.write_lines[i] = (int64_t)h[ST_WL0 + i];
+        for (int i = 0; i < 8; i++) top->stats.read_lines[i] = (int64_t)h[ST_RL0 + i];
     }
     top->stats.replay_slots = top->stats.replay_rows ? std::min(top->rslots, top->rslotsUse) : 0;
     top->stats.replay_int_keys = top->stats.replay_rows && top->replayIntOpt && top->replayIntOk ? 1 : 0;

@@ -90,7 +90,8 @@ enum StatIdx {
                         //   pair in that bucket that the kappa test kept out, kept pending
     ST_WL0 = 69,        // batch kernel (SHD_BATCH_WRCOUNT builds): 64-B lines written per
                         //   category (16 slots, topo_sssp_batch.hip WL_*)
-    ST_COUNT = 85
+    ST_RL0 = 85,        //   then 64-B lines read per category (8 slots, RL_*)
+    ST_COUNT = 93
 };
 
 struct DevCSR {

@@ -36,6 +36,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdint>
 #include <type_traits>
 
@@ -59,8 +60,12 @@ using namespace dev;
 #ifndef SHD_TAIL_HINT
 #define SHD_TAIL_HINT 1  // record each tail pair's improver during the SSSP (parent-pass guess)
 #endif
+#ifndef SHD_SWEEP_K0LAZY
+#define SHD_SWEEP_K0LAZY 0  // sweeps load kappa0 only for vertices with a pair in the opened bucket
+#endif
 #ifndef SHD_MASK_TAKE
-#define SHD_MASK_TAKE 0  // a queued tail vertex's mask read and cleared by one returning atomic
+#define SHD_MASK_TAKE 1  // a queued tail vertex's mask read and cleared by one returning atomic
+                         // (r04: 94.7 -> 92.3 ms, same box)
 #endif
 #ifndef SHD_BATCH_WRCOUNT
 #define SHD_BATCH_WRCOUNT 0  // profiling build: 64-B lines written per category (ST_WL0)
@@ -149,7 +154,8 @@ struct LdsB {
     unsigned long long tm[5];
     unsigned long long tk;
     unsigned long long wl[16];  // SHD_BATCH_WRCOUNT builds: 64-B lines stored / atomically
-                                // written per category (WL_*)
+                                // written per category (WL_*), then read per category (RL_*)
+    unsigned long long rl[16];
 };
 
 // Write categories of SHD_BATCH_WRCOUNT builds (ShdStats.write_lines): each store / atomic
@@ -173,6 +179,32 @@ enum {
     WL_QUEUE,        // queue / list appends (near queues, hub lists, pair lists)
     WL_OTHER         // path buffer spill to HBM, source init
 };
+// Read categories of SHD_BATCH_WRCOUNT builds (ShdStats.read_lines), counted like the writes.
+enum {
+    RL_RELAX_PRE,  // phase B pre-check of the target's distance line
+    RL_PHASE_A,    // phase A adjacency records (kappa-sorted copy)
+    RL_CHUNK,      // chunk / sub-chunk loads: queue entries, masks, row bounds, probes, distances
+    RL_SWEEP,      // sweeps: bitmap words, kappa0, distance lines
+    RL_WALK,       // parent walks: start pairs, tag words, tree records, distances
+    RL_EPI,        // epilogue: targets, vertex arrays, distances, pair records
+    RL_RESET,      // reset: bitmap words
+    RL_OTHER       // hint pass and row scans
+};
+template <int K>
+__device__ __forceinline__ void rl_count(LdsB<K>& L, int cat, bool act, const void* a) {
+#if SHD_BATCH_WRCOUNT
+    const unsigned long long line = (unsigned long long)a >> 6;
+    const unsigned long long am = __ballot(act);
+    if (!am) return;
+    const int lane = (int)(threadIdx.x & 63u);
+    const unsigned long long prev = __shfl_up(line, 1, 64);
+    const bool dup = lane > 0 && ((am >> (lane - 1)) & 1ull) && prev == line;
+    const unsigned long long nm = __ballot(act && !dup);
+    if (lane == __ffsll((long long)am) - 1) atomicAdd(&L.rl[cat], (unsigned long long)__popcll(nm));
+#else
+    (void)L; (void)cat; (void)act; (void)a;
+#endif
+}
 template <int K>
 __device__ __forceinline__ void wl_count(LdsB<K>& L, int cat, bool act, const void* a) {
 #if SHD_BATCH_WRCOUNT
@@ -482,6 +514,10 @@ __device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t
 #else
         const uint32_t m = MO::get_l2(mcur, v);
 #endif
+        rl_count(L, RL_CHUNK, true, mcur + v);
+        rl_count(L, RL_CHUNK, true, g.rowptr + v);
+        rl_count(L, RL_CHUNK, true, g.ksum + kKProbes / 4 * (size_t)v);
+        rl_count(L, RL_CHUNK, true, D.dist + (size_t)v * K);
         const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
         const float4 ks0 = g.ksum[kKProbes / 4 * (size_t)v];
         const float4 ks1 = kKProbes > 4 ? g.ksum[kKProbes / 4 * (size_t)v + 1] : ks0;
@@ -571,6 +607,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
     if (WAVE) {
         if (lane == 0) nb0 = atomicAdd(&L.qhead, kBSub);
         nb0 = __shfl(nb0, 0, 64);
+        rl_count(L, RL_CHUNK, nb0 + lane < nq, Q + nb0 + lane);
         nqv = nb0 + lane < nq ? Q[nb0 + lane] : 0u;
     }
     for (uint32_t base = 0;; base += kBChunk) {
@@ -581,6 +618,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             cnt = min(kBSub, nq - b0);
             if (lane == 0) nb0 = atomicAdd(&L.qhead, kBSub);
             nb0 = __shfl(nb0, 0, 64);
+            rl_count(L, RL_CHUNK, nb0 + lane < nq, Q + nb0 + lane);
             nqv = nb0 + lane < nq ? Q[nb0 + lane] : 0u;
             total = load_sub<K>(qv, cnt, wb, g, L, D, mcur);
         } else {
@@ -602,6 +640,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                                : WAVE ? (int)(wb + slice_slot(L.off + wb, cnt, e))
                                       : chunk_slot<K>(L, cnt, e);
                 const uint32_t jr = valid ? L.rs[lo] + (e - L.off[lo]) : 0u;
+                rl_count(L, RL_PHASE_A, valid, g.adjk + kAdjWords * jr);
                 const AdjRec r = *reinterpret_cast<const AdjRec*>(g.adjk + kAdjWords * jr);
                 an[a] = r.a;
                 apb[a] = r.p;
@@ -718,6 +757,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 ab[rr] = on ? d2bits(abd) : ~0ull;
                 // pre-check: the edge's pairs read its target's line in one request
                 const bool t = on && n[rr] >= D.H;
+                rl_count(L, RL_RELAX_PRE, t, D.dist + (t ? (size_t)n[rr] : (size_t)0) * K + jj);
                 const unsigned long long x = D.dist[(t ? (size_t)n[rr] : (size_t)0) * K + jj];
                 if (!kKapInRec) kz[rr] = g.kap0[t ? n[rr] : 0u];
                 cur[rr] = t ? x : 0ull;
@@ -921,8 +961,13 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     // then the merged vertex list
     uint32_t* fscr = reinterpret_cast<uint32_t*>(ws.ring) + (size_t)slot * ws.ring_entries;
     uint32_t* vscr = fscr + (size_t)V * K;  // parent-pass vertex list (V entries)
-    const uint32_t pw = (uint32_t)((V + 15) / 16);  // words of the pending / touched bits
-    D.pt = vscr + (size_t)V;
+    // pending / touched bits, 8-B aligned (the ring keeps 64 words of slack per bitmap): the
+    // sweeps and the reset read them as pw pairs of words, 32 vertices per pair
+    D.pt = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(vscr + (size_t)V) + 7) &
+                                       ~(uintptr_t)7);
+    const uint32_t pw = (uint32_t)((V + 31) / 32);  // word pairs of the pending / touched bits
+    unsigned long long* const pt2 = reinterpret_cast<unsigned long long*>(D.pt);
+    constexpr unsigned long long kPendBits = 0x5555555555555555ull;
     const uint32_t pcap = (uint32_t)(V * K);
 
     uint32_t iter = ctr[0];
@@ -932,6 +977,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     if (tid < 8) L.bt[tid] = 0;
     if (tid < 4) L.sw[tid] = 0;
     if (tid < 16) L.wl[tid] = 0;
+    if (tid < 16) L.rl[tid] = 0;
     if (tid == 0) L.touched = 0;
     if (tid < 5) L.wk[tid] = 0;
     if (tid < 4) L.ev[tid] = 0;
@@ -1125,35 +1171,41 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 // thread, compacts the set bits' vertices into LDS (the chunk buffers are idle
                 // here), classifies their lines (LPV lanes x 16 B per vertex) and rewrites the
                 // words with the vertices that still hold a pair past nb.
-                // Wave-parallel tail sweep: every wave owns blocks of 64 bitmap words (one per
-                // lane), compacts their set bits into its own LDS slice, classifies those lines
-                // and rewrites its own words -- no block barrier until the sweep ends.
+                // Wave-parallel tail sweep: every wave owns blocks of 64 word pairs (one per lane,
+                // 32 vertices), compacts their pending bits into its own LDS slice, classifies
+                // those lines and rewrites its own words -- no block barrier until the sweep ends.
                 {
                     constexpr uint32_t NW = kSsspBlock / 64;
                     constexpr uint32_t VPW = 64 / LPV;  // vertices per wave instruction
-                    uint32_t* svb = reinterpret_cast<uint32_t*>(L.val);   // survivor words
-                    constexpr uint32_t kClW = ((uint32_t)(sizeof(L.val) / 4) - NW * 64) / NW;
+                    // the chunk buffers (off .. val, contiguous and idle here): survivor pairs,
+                    // then each wave's compaction slice
+                    unsigned long long* svb = reinterpret_cast<unsigned long long*>(L.off);
+                    constexpr uint32_t kSweepU32 =
+                        (uint32_t)((offsetof(LdsB<K>, val) + sizeof(L.val) - offsetof(LdsB<K>, off)) / 4);
+                    constexpr uint32_t kClW = (kSweepU32 - 2 * NW * 64) / NW;
                     static_assert(kClW >= 64, "sweep compaction slice");
                     const uint32_t wv = tid >> 6, lane = tid & 63u;
-                    uint32_t* svw = svb + wv * 64u;
-                    uint32_t* clw = svb + NW * 64u + wv * kClW;
-                    const uint32_t w0 = H / 16;
-                    uint32_t nword = w0 + wv * 64u + lane < pw ? ld_l2_u32(&D.pt[w0 + wv * 64u + lane]) : 0u;
+                    unsigned long long* svw = svb + wv * 64u;
+                    uint32_t* clw = reinterpret_cast<uint32_t*>(svb + NW * 64u) + wv * kClW;
+                    const uint32_t w0 = H / 32;
+                    unsigned long long nword = w0 + wv * 64u + lane < pw ? ld_l2_u64(&pt2[w0 + wv * 64u + lane]) : 0ull;
                     for (uint32_t bb = w0 + wv * 64u; bb < pw; bb += NW * 64u) {
                         const uint32_t wi = bb + lane;
-                        const uint32_t word = nword;
-                        const uint32_t pend = word & 0x55555555u;  // the pending bits
-                        nword = wi + NW * 64u < pw ? ld_l2_u32(&D.pt[wi + NW * 64u]) : 0u;
-                        svw[lane] = 0u;
+                        const unsigned long long word = nword;
+                        const unsigned long long pend = word & kPendBits;  // the pending bits
+                        rl_count(L, RL_SWEEP, wi + NW * 64u < pw, pt2 + wi + NW * 64u);
+                        nword = wi + NW * 64u < pw ? ld_l2_u64(&pt2[wi + NW * 64u]) : 0ull;
+                        svw[lane] = 0ull;
                         uint32_t tot;
-                        const uint32_t off = wave_excl_scan((uint32_t)__popc(pend), &tot);
+                        const uint32_t off = wave_excl_scan((uint32_t)__popcll(pend), &tot);
                         for (uint32_t p0 = 0; p0 < tot; p0 += kClW) {
                             {
-                                uint32_t w = pend, o = off;
+                                unsigned long long w = pend;
+                                uint32_t o = off;
                                 while (w) {
-                                    const uint32_t b = (uint32_t)__ffs(w) - 1u;
-                                    w &= w - 1u;
-                                    if (o >= p0 && o < p0 + kClW) clw[o - p0] = wi * 16u + b / 2u;
+                                    const uint32_t b = (uint32_t)__ffsll((long long)w) - 1u;
+                                    w &= w - 1ull;
+                                    if (o >= p0 && o < p0 + kClW) clw[o - p0] = wi * 32u + b / 2u;
                                     o++;
                                 }
                             }
@@ -1168,7 +1220,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                 for (int u = 0; u < SU; u++) {
                                     const uint32_t e = vb + (uint32_t)u * VPW + lane / LPV;
                                     vv[u] = e < n ? clw[e] : 0xFFFFFFFFu;
+                                    rl_count(L, RL_SWEEP, e < n, reinterpret_cast<const char*>(D.dist) + ((size_t)(e < n ? vv[u] : 0u) * LPV + lane % LPV) * 16);
+#if !SHD_SWEEP_K0LAZY
+                                    rl_count(L, RL_SWEEP, e < n, g.kap0 + (e < n ? vv[u] : 0u));
                                     k0[u] = g.kap0[e < n ? vv[u] : 0u];
+#endif
                                     d[u][0] = d[u][1] = kInfBits;
                                     if (e < n) {
                                         typedef unsigned long long u64x2
@@ -1180,6 +1236,24 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                         d[u][1] = x.y;
                                     }
                                 }
+#if SHD_SWEEP_K0LAZY
+                                // kappa0 only for the vertices with a pair in bucket nb (about
+                                // a third of those visited): one more round trip, fewer requests
+#pragma unroll
+                                for (int u = 0; u < SU; u++) {
+                                    const uint32_t jl = 2 * (lane % LPV);
+                                    uint32_t inb = 0;
+#pragma unroll
+                                    for (int h = 0; h < 2; h++)
+                                        if (d[u][h] != kInfBits &&
+                                            bkt(bits2d(d[u][h]), L.sh[jl + h], B.inv_delta) == nb)
+                                            inb = 1u;
+#pragma unroll
+                                    for (uint32_t o = 1; o < LPV; o <<= 1) inb |= __shfl_xor(inb, (int)o, 64);
+                                    rl_count(L, RL_SWEEP, inb != 0u, g.kap0 + (inb ? vv[u] : 0u));
+                                    k0[u] = inb ? g.kap0[vv[u]] : 0.f;
+                                }
+#endif
                                 uint32_t km = kNoBucket;
 #pragma unroll
                                 for (int u = 0; u < SU; u++) {
@@ -1209,7 +1283,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                     const bool lead = ok && m != 0u;
                                     wl_count(L, WL_MASK_ST, lead, mcur + (lead ? v : 0u));
                                     if (lead) mcur[v] = (M)m;
-                                    if (ok && keep) atomicOr(&svw[v / 16 - bb], 1u << (2u * (v & 15u)));
+                                    if (ok && keep) atomicOr(&svw[v / 32 - bb], 1ull << (2u * (v & 31u)));
                                     wpush<K>(L, lead, v, qin, &L.qtail, cap, &L.fover, 32u);
                                 }
                                 km = wave_min_u32(km);
@@ -1222,10 +1296,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                         __builtin_amdgcn_wave_barrier();
                         // the touched bits stay; svw holds a subset of the pending bits: an
-                        // unchanged word needs no store
-                        const uint32_t nw = (word & 0xAAAAAAAAu) | svw[lane];
-                        wl_count(L, WL_PEND_ST, wi < pw && nw != word, D.pt + wi);
-                        if (wi < pw && nw != word) D.pt[wi] = nw;
+                        // unchanged pair needs no store
+                        const unsigned long long nw = (word & ~kPendBits) | svw[lane];
+                        wl_count(L, WL_PEND_ST, wi < pw && nw != word, pt2 + wi);
+                        if (wi < pw && nw != word) pt2[wi] = nw;
                         __builtin_amdgcn_wave_barrier();
                     }
                 }
@@ -1348,6 +1422,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         auto load_hop = [&](uint32_t v, uint32_t j) -> Hop {
             Hop h;
             const uint32_t q = v * K + j;
+            rl_count(L, RL_WALK, v >= H, reinterpret_cast<const uint4*>(g.spt) + 2 * (size_t)v);
+            rl_count(L, RL_WALK, v >= H, D.dist + (size_t)q);
             if (v >= H) {
                 const uint4* s = reinterpret_cast<const uint4*>(g.spt) + 2 * (size_t)v;
                 h.sp = s[0];
@@ -1384,6 +1460,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 h.sl = 0.0;
                 h.d = 0ull;
                 for (;;) {
+                    rl_count(L, RL_WALK, !act && i < nF, pcur + (i < nF ? i : 0u));
                     if (!act && i < nF) {
                         q = pcur[i];
                         i += kSsspBlock;
@@ -1407,6 +1484,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         // round trip both walk on: they write identical records (the parent rule
                         // is deterministic), and a pair listed twice in S is resolved twice the
                         // same way -- cheaper than a returning atomic per hop (kernel -3.5 %).
+                        rl_count(L, RL_WALK, true, precw + 4 * (size_t)q);
                         const uint32_t tw = ld_l2_u32(&precw[4 * (size_t)q + 1]);
                         if (tag_claimed(tw, ep)) {  // another walk's
                             act = false;
@@ -1650,6 +1728,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         for (uint32_t i = tid; i < (uint32_t)A * (uint32_t)nk; i += kSsspBlock) {
             const uint32_t j = i / (uint32_t)A;
             const uint32_t k = i - j * (uint32_t)A;
+            rl_count(L, RL_EPI, true, targets + k);
             const uint32_t t = targets[k];
             const uint32_t src = L.src[j];
             double lat, rel;
@@ -1669,12 +1748,15 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     h = 1;
                 }
             } else {
+                rl_count(L, RL_EPI, true, D.dist + (size_t)t * K + j);
+                rl_count(L, RL_EPI, true, g.vloss + t);
                 lat = bits2d(ld_l2_u64(&D.dist[(size_t)t * K + j]));
                 bool amb = false, bad = false;
                 uint32_t v = t;
                 while (v != src) {
                     // the pair record, L1-bypassing (written by other waves of the workgroup)
                     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                    rl_count(L, RL_EPI, true, reinterpret_cast<const u32x4*>(prec) + (size_t)v * K + j);
                     const u32x4 rv = __builtin_nontemporal_load(
                         reinterpret_cast<const u32x4*>(prec) + (size_t)v * K + j);
                     const uint4 r = make_uint4(rv.x, rv.y, rv.z, rv.w);
@@ -1751,26 +1833,27 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             constexpr uint32_t G = K / 2;
             const uint32_t part = tid % G, gbase = (tid & 63u) - part;
             unsigned long long nt = 0;
-            const uint32_t w0 = H / 16;
-            uint32_t nword = w0 + tid < pw ? ld_l2_u32(&D.pt[w0 + tid]) : 0u;
+            const uint32_t w0 = H / 32;
+            unsigned long long nword = w0 + tid < pw ? ld_l2_u64(&pt2[w0 + tid]) : 0ull;
             for (uint32_t wb = w0; wb < pw; wb += kSsspBlock) {
                 const uint32_t wi = wb + tid;
-                const uint32_t word = nword;
-                const uint32_t myw = word & 0xAAAAAAAAu;  // the touched bits
-                nword = wi + kSsspBlock < pw ? ld_l2_u32(&D.pt[wi + kSsspBlock]) : 0u;
-                wl_count(L, WL_TOUCH_CLR, word != 0u, D.pt + wi);
+                const unsigned long long word = nword;
+                const unsigned long long myw = word & ~kPendBits;  // the touched bits
+                rl_count(L, RL_RESET, wi + kSsspBlock < pw, pt2 + wi + kSsspBlock);
+                nword = wi + kSsspBlock < pw ? ld_l2_u64(&pt2[wi + kSsspBlock]) : 0ull;
+                wl_count(L, WL_TOUCH_CLR, word != 0ull, pt2 + wi);
                 if (word) {
-                    D.pt[wi] = 0u;
-                    nt += (unsigned long long)__popc(myw);
+                    pt2[wi] = 0ull;
+                    nt += (unsigned long long)__popcll(myw);
                 }
-                if (!__any(myw != 0u)) continue;
+                if (!__any(myw != 0ull)) continue;
 #pragma unroll
                 for (uint32_t p = 0; p < G; p++) {
-                    uint32_t w = __shfl(myw, (int)(gbase + p), 64);
+                    unsigned long long w = __shfl(myw, (int)(gbase + p), 64);
                     const uint32_t wv = wi - part + p;
                     while (w) {
-                        const uint32_t v = wv * 16u + ((uint32_t)__ffs(w) - 1u) / 2u;
-                        w &= w - 1u;
+                        const uint32_t v = wv * 32u + ((uint32_t)__ffsll((long long)w) - 1u) / 2u;
+                        w &= w - 1ull;
                         wl_count(L, WL_RESET, true, d2 + (size_t)v * G + part);
                         if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + (size_t)v * G + part);
                         else d2[(size_t)v * G + part] = inf2;
@@ -1821,8 +1904,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             for (int i = 0; i < 8; i++) atomicAdd(&stats[ST_BT0 + i], L.bt[i]);
             for (int i = 0; i < 4; i++) atomicAdd(&stats[ST_SW0 + i], L.sw[i]);
         }
-        if (SHD_BATCH_WRCOUNT)
+        if (SHD_BATCH_WRCOUNT) {
             for (int i = 0; i < 16; i++) atomicAdd(&stats[ST_WL0 + i], L.wl[i]);
+            for (int i = 0; i < 8; i++) atomicAdd(&stats[ST_RL0 + i], L.rl[i]);
+        }
     }
 }
 

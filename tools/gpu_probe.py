@@ -81,6 +81,11 @@ for rep in range(args.reps):
         wl = st["write_lines"]
         print("   write lines per source (SHD_BATCH_WRCOUNT): total %.0f %s" % (
             sum(wl) / rows, {k: round(v / rows) for k, v in zip(names, wl)}), flush=True)
+        rl = st["read_lines"]
+        print("   read lines per source (SHD_BATCH_WRCOUNT): total %.0f %s" % (
+            sum(rl) / rows, {k: round(v / rows) for k, v in zip(
+                ("pre", "phase_a", "chunk", "sweep", "walk", "epi", "reset", "other"), rl)}),
+            flush=True)
     print("   per-source events:", {k: "%.3g" % (v / rows) for k, v in st["events"].items()},
           flush=True)
 x = lr[..., 0].cpu().numpy()
