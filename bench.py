@@ -518,6 +518,8 @@ def main():
             module_load_ms=round(cs["module_load_ms"], 2),
             build_wait_ms=round(cold_wait_ms, 2),
             attach_prep_ms=round(cs["attach_prep_ms"], 2),
+            attach_prep_steps_ms=dict(zip(("device_init", "graph_prep", "edge_scan", "workspace"),
+                                          [round(x, 2) for x in cs["attach_prep_step_ms"]])),
             attach_phase_ms=round(attach_phase_s * 1e3, 2),
             first_attach_to_table_ms=round(attach_to_table_s * 1e3, 2),
             library_first_attach_to_table_ms=round(cs["first_attach_to_table_ms"], 2),

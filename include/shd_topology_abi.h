@@ -334,6 +334,9 @@ typedef struct {
     int64_t read_lines[8];      /* the same builds: 64-B lines read, by category (RL_*): phase-B
                                    pre-checks, phase-A records, chunk loads, sweeps, parent walks,
                                    epilogue, reset, other (hint pass, row scans) */
+    double attach_prep_step_ms[4]; /* the attach-time preparation's parts (wall): device init (HIP
+                                      queues, code objects), graph preparation, edge scan, the
+                                      batched SSSP's workspace (allocation + initialisation) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

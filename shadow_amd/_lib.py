@@ -54,7 +54,8 @@ class ShdStats(ctypes.Structure):
                 ("tie_probe_rows", i64), ("tie_probe_flagged", i64), ("tie_probe_ms", dbl),
                 ("first_attach_to_table_ms", dbl), ("exchange_bytes", i64),
                 ("csr_host_runs_total", i64), ("sweep_events", i64 * 4),
-                ("write_lines", i64 * 16), ("read_lines", i64 * 8)]
+                ("write_lines", i64 * 16), ("read_lines", i64 * 8),
+                ("attach_prep_step_ms", dbl * 4)]
 
 
 class ShdSynthParams(ctypes.Structure):

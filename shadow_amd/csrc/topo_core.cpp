@@ -176,6 +176,8 @@ struct _Topology {
     std::atomic<bool> prepStarted{false};
     std::thread prepThread;
     double prepBgMs = 0.0;       // the thread's wall time
+    double prepStepMs[4] = {0, 0, 0, 0};  // of which device init, graph preparation, edge scan,
+                                          // SSSP workspace
     // wall clock of the first attach, and whether the first table since then was installed
     // (ShdStats.first_attach_to_table_ms)
     std::chrono::steady_clock::time_point firstAttachT;
@@ -954,7 +956,8 @@ int ensure_replay_ws(Topology* top, int nrows) {
     const size_t V = (size_t)top->g.V;
     const bool ik = top->replayIntOpt && top->replayIntOk;
     const size_t nodeB = ik ? 8 : 16;  // heap node: {u32 key, u32 vertex} or {f64 key, u32 vertex, pad}
-    const size_t per_slot = 16 * V + nodeB * V + (size_t)kMaxHops * 64 * 4 + 64;
+    const ReplayLayout lay = replay_layout(ik ? 1 : 0, (uint32_t)V);
+    const size_t per_slot = 16 * V + nodeB * lay.nodeCap + (size_t)kMaxHops * 64 * 4 + 64;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, top->device));
     // wavefronts per CU: replay_wpc (20), or as many as the CU's LDS holds (each its heap's top
@@ -978,8 +981,9 @@ int ensure_replay_ws(Topology* top, int nrows) {
     top->d_rvrec.release(); top->d_rnode.release(); top->d_rpath.release();
     top->rslots = 0;
     const size_t n = (size_t)want * V;
+    const size_t nn = (size_t)want * lay.nodeCap;
     HIPCHK(top->d_rvrec.ensure(n));
-    HIPCHK(top->d_rnode.ensure(ik ? (n + 1) / 2 : n));  // uint4 units
+    HIPCHK(top->d_rnode.ensure(ik ? (nn + 1) / 2 : nn));  // uint4 units
     top->rwsInt = ik;
     HIPCHK(top->d_rpath.ensure((size_t)want * kMaxHops * 64));
     top->rslots = want;
@@ -992,6 +996,10 @@ ReplayWs replay_ws(Topology* top) {
     w.vrec = top->d_rvrec.p;
     w.node = top->d_rnode.p;
     w.pathbuf = top->d_rpath.p;
+    const ReplayLayout lay = replay_layout(top->rwsInt ? 1 : 0, (uint32_t)top->g.V);
+    w.nodeCap = lay.nodeCap;
+    w.stdPos = lay.stdPos;
+    w.stdBase = lay.stdBase;
     return w;
 }
 
@@ -1250,8 +1258,14 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 if (top->batchFill > 0) {
                     kf = std::min(K, top->batchFill);
                 } else {
+                    // the fewest sources per batch that still finish the rows in the fewest
+                    // rounds of the slots: a batch's time grows with its sources, so equal
+                    // rounds of smaller batches beat a last round of a few full ones (2,500
+                    // rows on 256 slots: 500 batches of 5, two even rounds, instead of 313
+                    // batches of 8 whose last 57 form a second round on their own)
                     const int64_t S = std::max(1, ws.slots);
-                    if (rows <= (int64_t)K * S) kf = (int)std::min<int64_t>(K, (rows + S - 1) / S);
+                    const int64_t rounds = (rows + (int64_t)K * S - 1) / ((int64_t)K * S);
+                    kf = (int)std::max<int64_t>(1, std::min<int64_t>(K, (rows + rounds * S - 1) / (rounds * S)));
                 }
                 top->stats.batch_fill = kf;
                 // workgroups the launch uses: the batches, at most the workspace's slots (it
@@ -1922,6 +1936,7 @@ int ensure_table(Topology* top) {
     // (waiting for the attach-time preparation thread, or another builder)
     top->stats.build_wait_ms = std::chrono::duration<double, std::milli>(tb0 - tw0).count();
     top->stats.attach_prep_ms = top->prepBgMs;
+    for (int i = 0; i < 4; i++) top->stats.attach_prep_step_ms[i] = top->prepStepMs[i];
     for (double& x : top->stats.build_step_ms) x = 0.0;
     top->bstepT = tb0;
     auto bstep = [&](int i) { bstep_mark(top, i); };
@@ -2267,13 +2282,23 @@ void start_attach_prep(Topology* top) {
             (void)hipGetLastError();
             return;  // no GPU here: the first build reports it
         }
+        auto tq = t0;
+        auto step = [&](int i) {
+            const auto t = std::chrono::steady_clock::now();
+            top->prepStepMs[i] = std::chrono::duration<double, std::milli>(t - tq).count();
+            tq = t;
+        };
         int r = dev_init(top);
+        step(0);
         if (!r) r = upload_csr(top);
+        step(1);
         edge_scan(top);  // mean latency (bucket width) and the replay's integer-key check
+        step(2);
         // the batched SSSP's workspace too, sized for a full table (a build with fewer sources
         // uses a part of it; a different batch width re-allocates)
         if (!r) r = ensure_workspace(top, 1 << 30);
         if (!r) r = hipStreamSynchronize(top->stream) == hipSuccess ? 0 : -1;
+        step(3);
         top->prepBgRc = r;
         top->prepBgMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });

@@ -183,9 +183,19 @@ struct ReplayCSR {
 struct ReplayWs {
     int slots = 0;
     uint4* vrec = nullptr;
-    uint4* node = nullptr;
+    uint4* node = nullptr;     // nodeCap heap nodes per slot (node size: 8 B u32 keys, 16 B f64)
     uint32_t* pathbuf = nullptr;
+    uint32_t nodeCap = 0;      // physical heap nodes per slot (replay_layout)
+    uint32_t stdPos = 0;       // first heap position stored position-major (past the blocked bands)
+    uint32_t stdBase = 0;      // its physical node index
 };
+// Physical layout of a replay heap's HBM levels (topo_replay.hip, RpHeap::phys): the levels below the
+// LDS ones in bands of one sink round's height, each band root's subtree contiguous; the levels
+// past the last band the heap can fill, position-major.
+struct ReplayLayout {
+    uint32_t stdPos, stdBase, nodeCap;
+};
+ReplayLayout replay_layout(int int_keys, uint32_t V);
 
 // Hub rows (ids < rows: the long rows of the degree order) cut into segments of at most kHubSeg
 // entries, one wavefront each in the row-parallel steps (graph preparation, the target-aware

@@ -45,6 +45,7 @@
 // sums) proves t popped, and its record is not read: on C4-int 31-46 % of the relaxations.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 
@@ -87,6 +88,14 @@ constexpr int kRpLA = 5;  // LDS walk of the sink: heap levels per LDS round (62
 #define SHD_RP_HL 5  // levels per HBM round of the path-first sink (6: two nodes per lane)
 #endif
 constexpr int kHL = SHD_RP_HL;
+#ifndef SHD_RP_BLOCKED
+#define SHD_RP_BLOCKED 1  // HBM heap levels stored as contiguous sink-round subtrees (RpHeap::phys)
+#endif
+// Blocks (of 2 << kHL nodes) in the bands before band b: band b' has one per node of its root
+// level L0 - 1 + kHL b'.
+__host__ __device__ __forceinline__ uint32_t rp_band_base(uint32_t L0, uint32_t b) {
+    return (1u << (L0 - 1u)) * (((1u << (kHL * b)) - 1u) / ((1u << kHL) - 1u));
+}
 constexpr int kHNodes = (2 << kHL) - 2;
 static_assert(kHL >= 1 && kHNodes <= 128, "at most two nodes per lane");
 
@@ -232,22 +241,43 @@ struct RpHeap {
     typename K::Node* gn;
     uint4* vr;
     unsigned long long* nl;
+    uint32_t stdPos, stdBase;
+    // Physical node of HBM position p.  Positions below stdPos sit in bands of kHL levels: the
+    // 2^(kHL+1) - 2 descendants of a band root r (level L0 - 1 + kHL b) -- exactly the nodes one
+    // sink round loads below its path end -- are one contiguous block in the BFS order of
+    // rp_sub_pos, so a round reads 8 whole lines (u32 keys; 16 for f64) instead of ~12 (~21)
+    // across five position-major levels, and a path's moves inside the band share lines.
+    __device__ __forceinline__ uint32_t phys(uint32_t p) const {
+        if (p >= stdPos) return p - stdPos + stdBase;
+        const uint32_t l = 31u - (uint32_t)__clz(p + 1u);  // level of p (>= L0)
+        const uint32_t b = (l - (uint32_t)K::kLevels) / (uint32_t)kHL;
+        const uint32_t r = (uint32_t)K::kLevels - 1u + (uint32_t)kHL * b;  // band root level
+        const uint32_t dl = l - r;                                          // 1..kHL below it
+        const uint32_t a = ((p + 1u) >> dl) - 1u;                           // the band root
+        return (rp_band_base(K::kLevels, b) + (a + 1u - (1u << r))) * (2u << kHL) +
+               (p + 1u) - ((a + 1u) << dl) + (1u << dl) - 2u;
+    }
     __device__ __forceinline__ void node(uint32_t p, T& k, uint32_t& v, int cat) const {
-        rp_lines(nl, cat, p >= kT, gn + p);
         if (p < kT) {
             k = lds_k<I>(p);
             v = lds_v<I>(p);
         } else {
-            K::unpack(gn[p], k, v);
+            const uint32_t x = phys(p);
+            rp_lines(nl, cat, true, gn + x);
+            K::unpack(gn[x], k, v);
         }
     }
     // node (k, v) to position p; its vertex record's position is stored only when `pos` (the
     // element crossed into or out of the LDS levels, moved inside the HBM levels, or is new)
     __device__ __forceinline__ void put(uint32_t p, T k, uint32_t v, int cat, bool pos = true) const {
-        rp_lines(nl, cat, p >= kT, gn + p);
         rp_lines(nl, cat, pos, vr + 4 * (size_t)__lane_id() + v);  // random: one line each
-        if (p < kT) lds_put<I>(p, k, v);
-        else gn[p] = K::pack(k, v);
+        if (p < kT) {
+            lds_put<I>(p, k, v);
+        } else {
+            const uint32_t x = phys(p);
+            rp_lines(nl, cat, true, gn + x);
+            gn[x] = K::pack(k, v);
+        }
         if (pos) reinterpret_cast<uint32_t*>(vr + v)[3] = p;
     }
 };
@@ -490,8 +520,9 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 #if SHD_RP_TIME
     unsigned long long tph[4] = {0, 0, 0, 0}, tlast = wall_clock64();
 #endif
-    // node storage: V x 16 B per slot, of which the u32-key heap uses the first half
-    RpHeap<I> H{reinterpret_cast<typename K::Node*>(ws.node) + slot * V, vr, nl};
+    // node storage: ws.nodeCap nodes per slot (replay_layout)
+    RpHeap<I> H{reinterpret_cast<typename K::Node*>(ws.node) + slot * (size_t)ws.nodeCap, vr, nl,
+                ws.stdPos, ws.stdBase};
     uint32_t* pbuf = ws.pathbuf + slot * (size_t)kMaxHops * 64;
     unsigned long long n_pop = 0, n_push = 0, n_mod = 0, n_rows = 0, n_skip = 0;
 
@@ -762,6 +793,20 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 }
 
 }  // namespace
+
+ReplayLayout replay_layout(int int_keys, uint32_t V) {
+    const uint32_t L0 = (uint32_t)replay_lds_levels(int_keys);
+    uint32_t lmax = 0;  // level of the deepest position a heap of V elements can use
+    while (V > 1 && ((2ull << lmax) - 1ull) < (unsigned long long)V) lmax++;
+    uint32_t nb = 0;    // bands whose levels all lie within [L0, lmax]
+    while (SHD_RP_BLOCKED && L0 + (uint32_t)kHL * (nb + 1) - 1 <= lmax && L0 + (uint32_t)kHL * (nb + 1) < 31) nb++;
+    ReplayLayout r;
+    r.stdPos = (uint32_t)((1ull << (L0 + (uint32_t)kHL * nb)) - 1ull);
+    r.stdBase = rp_band_base(L0, nb) * (2u << kHL);  // positions < kT live in LDS only
+    const unsigned long long cap = (unsigned long long)r.stdBase + (V > r.stdPos ? V - r.stdPos : 0u);
+    r.nodeCap = (uint32_t)((std::max<unsigned long long>(cap, 64) + 63ull) & ~63ull);  // blocks stay aligned per slot
+    return r;
+}
 
 int replay_lds_levels(int int_keys) { return int_keys ? SHD_RP_LDS_LEVELS_INT : SHD_RP_LDS_LEVELS; }
 int replay_lds_bytes(int int_keys) { return int_keys ? (int)kRpTI * 8 : (int)kRpTF * 12; }

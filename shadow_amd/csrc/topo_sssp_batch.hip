@@ -79,6 +79,9 @@ using namespace dev;
 #else
 #define BT_TICK(i) do { } while (0)
 #endif
+#ifndef SHD_TGT_MAJOR
+#define SHD_TGT_MAJOR 1  // parent walks and epilogue items numbered target-major (a target's K sources in adjacent lanes)
+#endif
 #ifndef SHD_INIT_NT
 #define SHD_INIT_NT 1  // the batch's [V][K] distance reset with nontemporal stores
 #endif
@@ -1341,6 +1344,26 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         __syncthreads();
         uint32_t* pcur = qa;
         uint32_t* pnxt = qb;
+#if SHD_TGT_MAJOR
+        // Target-major start list, K entries per target (kNoPair for the sources past nk and a
+        // target that is the source): a target's chains for the K sources share their tail part
+        // (the h0-tree guess is source-independent), so the K lanes of an aligned group walk the
+        // same vertices in the same round trip and one line serves the group's tree records,
+        // distances and pair records.  The first level's walks keep the groups together (a lane
+        // takes its next start pair when its whole group is idle).
+        constexpr uint32_t kNoPair = 0xFFFFFFFFu;
+        for (uint32_t i = tid; i < (uint32_t)A * K; i += kSsspBlock) {
+            const uint32_t j = i % K;
+            const uint32_t t = targets[i / K];
+            const bool p = j < (uint32_t)nk && t != L.src[j];
+            wl_count(L, WL_QUEUE, true, pcur + i);
+            pcur[i] = p ? t * K + j : kNoPair;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        uint32_t nF = (uint32_t)A * K;
+        bool gsync = true;
+#else
         for (uint32_t ib = 0; ib < (uint32_t)A * (uint32_t)nk; ib += kSsspBlock) {
             const uint32_t i = ib + tid;
             bool p = false;
@@ -1356,6 +1379,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         __syncthreads();
         uint32_t nF = min(L.qtail, pcap);
         __syncthreads();
+        constexpr uint32_t kNoPair = 0xFFFFFFFFu;
+        constexpr bool gsync = false;
+#endif
         // A pair's record: its parent, the batch's tag, the loss of the parent edge (one store)
         auto put = [&](uint32_t q, uint32_t u, double loss) {
             const unsigned long long lb = d2bits(loss);
@@ -1460,15 +1486,21 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 h.sl = 0.0;
                 h.d = 0ull;
                 for (;;) {
-                    rl_count(L, RL_WALK, !act && i < nF, pcur + (i < nF ? i : 0u));
-                    if (!act && i < nF) {
+                    bool take = !act && i < nF;
+                    if (gsync) {  // the lane's group of K (one target) takes its starts together
+                        const unsigned long long am = __ballot(act);
+                        take = take && ((am >> ((tid & 63u) & ~(uint32_t)(K - 1))) & ((1ull << K) - 1ull)) == 0ull;
+                    }
+                    rl_count(L, RL_WALK, take, pcur + (take ? i : 0u));
+                    if (take) {
                         q = pcur[i];
                         i += kSsspBlock;
                         j = q % K;
-                        act = true;
-                        fresh = true;
+                        act = q != kNoPair;
+                        fresh = act;
                     }
-                    if (!__any(act)) break;
+                    if (!__any(act || i < nF)) break;
+                    if (!act) continue;
                     if (act && fresh) {
                         h = load_hop(q / K, j);
                         fresh = false;
@@ -1703,6 +1735,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             __syncthreads();
             nF = min(L.qtail, pcap);
             { uint32_t* t = pcur; pcur = pnxt; pnxt = t; }
+#if SHD_TGT_MAJOR
+            gsync = false;  // later levels start at the scanned pairs' parents (compacted)
+#endif
             __syncthreads();
             if (tid == 0) L.pt[4] += wall_clock64() - tp0;  // next level
         }
@@ -1726,8 +1761,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             return x < nl ? lpb + (size_t)x * kSsspBlock + tid : pbuf + (size_t)x * kSsspBlock + tid;
         };
         for (uint32_t i = tid; i < (uint32_t)A * (uint32_t)nk; i += kSsspBlock) {
-            const uint32_t j = i / (uint32_t)A;
-            const uint32_t k = i - j * (uint32_t)A;
+            // target-major (as the walks): the group's chains coincide up to the core, so each
+            // lockstep hop reads one target's K pair records (two lines), not K lines
+            const uint32_t j = SHD_TGT_MAJOR ? i % (uint32_t)nk : i / (uint32_t)A;
+            const uint32_t k = SHD_TGT_MAJOR ? i / (uint32_t)nk : i - j * (uint32_t)A;
             rl_count(L, RL_EPI, true, targets + k);
             const uint32_t t = targets[k];
             const uint32_t src = L.src[j];

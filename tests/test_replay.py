@@ -35,6 +35,21 @@ def test_replay_full_dijkstra_parents_match_oracle(integer, int_keys):
         assert nties > 50  # the case the replay exists for
 
 
+@pytest.mark.parametrize("int_keys", [1, 0])
+def test_replay_deep_heap_blocked_layout_matches_oracle(int_keys):
+    """A graph large enough (V > 2^14) that the heap's HBM levels 9-13 sit in the blocked
+    sink-round layout (topo_replay.hip RpHeap::phys) and deeper levels position-major: full
+    Dijkstra from three sources, distances and every parent equal to the oracle's."""
+    top, g = synthetic_pair(seed=21, n_routers=40000, n_poi=200, n_edges=300000, integer=True)
+    top.set_option("replay_int_keys", int_keys)
+    attach_hosts(top, g, 200, type_hints=["client", "relay"])
+    for s in [0, g.V // 3, g.V - 1]:
+        d, p = top.replay_source(s, full=True)
+        od, opv, _, _ = g.dijkstra(s)
+        assert np.array_equal(d.view(np.uint64), od.view(np.uint64)), s
+        assert np.array_equal(p, opv), (s, int(np.sum(p != opv)))
+
+
 def test_replay_early_exit_matches_oracle():
     """The reference's early exit (all attached targets popped): every vertex popped before it
     has the oracle's parent."""
