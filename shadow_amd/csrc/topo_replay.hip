@@ -89,7 +89,7 @@ constexpr int kRpLA = 5;  // LDS walk of the sink: heap levels per LDS round (62
 #endif
 constexpr int kHL = SHD_RP_HL;
 #ifndef SHD_RP_BLOCKED
-#define SHD_RP_BLOCKED 1  // HBM heap levels stored as contiguous sink-round subtrees (RpHeap::phys)
+#define SHD_RP_BLOCKED 0  // (1: slower) HBM heap levels stored as contiguous sink-round subtrees (RpHeap::phys)
 #endif
 // Blocks (of 2 << kHL nodes) in the bands before band b: band b' has one per node of its root
 // level L0 - 1 + kHL b'.
@@ -257,6 +257,24 @@ struct RpHeap {
         return (rp_band_base(K::kLevels, b) + (a + 1u - (1u << r))) * (2u << kHL) +
                (p + 1u) - ((a + 1u) << dl) + (1u << dl) - 2u;
     }
+    // Physical node of the first of the 2^(kHL+1) - 2 descendants of band root `cur` (uniform),
+    // when they all lie in the blocked bands (then descendant BFS index i + 1 is node base + i);
+    // ~0u otherwise.
+    __device__ __forceinline__ uint32_t sub_base(uint32_t cur) const {
+        if (((unsigned long long)(cur + 1u) << kHL) > stdPos) return 0xFFFFFFFFu;  // past the bands
+        const uint32_t r = 31u - (uint32_t)__clz(cur + 1u);
+        const uint32_t b = (r + 1u - (uint32_t)K::kLevels) / (uint32_t)kHL;
+        return (rp_band_base(K::kLevels, b) + (cur + 1u - (1u << r))) * (2u << kHL);
+    }
+    // the sink round's node load: physical node x (x != ~0u) or position p
+    __device__ __forceinline__ void node_at(uint32_t x, uint32_t p, T& k, uint32_t& v, int cat) const {
+        if (x == 0xFFFFFFFFu) {
+            node(p, k, v, cat);
+        } else {
+            rp_lines(nl, cat, true, gn + x);
+            K::unpack(gn[x], k, v);
+        }
+    }
     __device__ __forceinline__ void node(uint32_t p, T& k, uint32_t& v, int cat) const {
         if (p < kT) {
             k = lds_k<I>(p);
@@ -385,12 +403,16 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap<I>& H, uint32_t size, i
         H.nl[6]++;  // HBM sink rounds
 #endif
         const uint32_t p = rp_sub_pos(cur, lane);
+        // cur is a band root here (the LDS walk ends at level L0 - 1, rounds take kHL levels)
+        const uint32_t xb = SHD_RP_BLOCKED ? H.sub_base(cur) : 0xFFFFFFFFu;
         T k = K::lo(), k2 = K::lo();
         uint32_t v = 0, v2 = 0;
-        if (lane < kHNodes && p < size) H.node(p, k, v, RPL_SINK_LD);
+        if (lane < kHNodes && p < size)
+            H.node_at(xb == 0xFFFFFFFFu ? xb : xb + (uint32_t)lane, p, k, v, RPL_SINK_LD);
         if (kHNodes > 64) {  // BFS nodes 64.. in a second register
             const uint32_t p2 = rp_sub_pos(cur, lane + 64);
-            if (lane + 64 < kHNodes && p2 < size) H.node(p2, k2, v2, RPL_SINK_LD);
+            if (lane + 64 < kHNodes && p2 < size)
+                H.node_at(xb == 0xFFFFFFFFu ? xb : xb + (uint32_t)lane + 64u, p2, k2, v2, RPL_SINK_LD);
         }
         if (!havex) {
             xk = K::rl(kx, 63);
