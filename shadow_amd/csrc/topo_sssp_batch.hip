@@ -60,9 +60,6 @@ using namespace dev;
 #ifndef SHD_TAIL_HINT
 #define SHD_TAIL_HINT 1  // record each tail pair's improver during the SSSP (parent-pass guess)
 #endif
-#ifndef SHD_SWEEP_K0LAZY
-#define SHD_SWEEP_K0LAZY 0  // sweeps load kappa0 only for vertices with a pair in the opened bucket
-#endif
 #ifndef SHD_MASK_TAKE
 #define SHD_MASK_TAKE 1  // a queued tail vertex's mask read and cleared by one returning atomic
                          // (r04: 94.7 -> 92.3 ms, same box)
@@ -1174,42 +1171,61 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 // thread, compacts the set bits' vertices into LDS (the chunk buffers are idle
                 // here), classifies their lines (LPV lanes x 16 B per vertex) and rewrites the
                 // words with the vertices that still hold a pair past nb.
-                // Wave-parallel tail sweep: every wave owns blocks of 64 word pairs (one per lane,
-                // 32 vertices), compacts their pending bits into its own LDS slice, classifies
-                // those lines and rewrites its own words -- no block barrier until the sweep ends.
+                // Wave-parallel tail sweep: every wave owns blocks of SG x 64 word pairs (SG per
+                // lane, 32 vertices each), compacts their pending bits into its own LDS slice,
+                // classifies those lines and rewrites its own words -- no block barrier until the
+                // sweep ends.  ~1.7 % of the vertices are pending per sweep, so a block of 64
+                // word pairs yields ~35 vertices; SG blocks share one round trip of line loads.
                 {
+#ifndef SHD_SWEEP_G
+#define SHD_SWEEP_G 2  // 2: -2.9 % full table; 4 spills (+4 %)
+#endif
+                    constexpr uint32_t SG = SHD_SWEEP_G;  // word pairs per lane and block
                     constexpr uint32_t NW = kSsspBlock / 64;
                     constexpr uint32_t VPW = 64 / LPV;  // vertices per wave instruction
-                    // the chunk buffers (off .. val, contiguous and idle here): survivor pairs,
-                    // then each wave's compaction slice
-                    unsigned long long* svb = reinterpret_cast<unsigned long long*>(L.off);
+                    constexpr uint32_t kKeep = 0x80000000u;  // slice entry: the vertex stays pending
+                    // the chunk buffers (off .. val, contiguous and idle here): each wave's
+                    // compaction slice
                     constexpr uint32_t kSweepU32 =
                         (uint32_t)((offsetof(LdsB<K>, val) + sizeof(L.val) - offsetof(LdsB<K>, off)) / 4);
-                    constexpr uint32_t kClW = (kSweepU32 - 2 * NW * 64) / NW;
+                    constexpr uint32_t kClW = kSweepU32 / NW;
                     static_assert(kClW >= 64, "sweep compaction slice");
                     const uint32_t wv = tid >> 6, lane = tid & 63u;
-                    unsigned long long* svw = svb + wv * 64u;
-                    uint32_t* clw = reinterpret_cast<uint32_t*>(svb + NW * 64u) + wv * kClW;
+                    uint32_t* clw = L.off + wv * kClW;
                     const uint32_t w0 = H / 32;
-                    unsigned long long nword = w0 + wv * 64u + lane < pw ? ld_l2_u64(&pt2[w0 + wv * 64u + lane]) : 0ull;
-                    for (uint32_t bb = w0 + wv * 64u; bb < pw; bb += NW * 64u) {
-                        const uint32_t wi = bb + lane;
-                        const unsigned long long word = nword;
-                        const unsigned long long pend = word & kPendBits;  // the pending bits
-                        rl_count(L, RL_SWEEP, wi + NW * 64u < pw, pt2 + wi + NW * 64u);
-                        nword = wi + NW * 64u < pw ? ld_l2_u64(&pt2[wi + NW * 64u]) : 0ull;
-                        svw[lane] = 0ull;
+                    unsigned long long nword[SG];
+#pragma unroll
+                    for (uint32_t gi = 0; gi < SG; gi++) {
+                        const uint32_t wi = w0 + wv * 64u * SG + gi * 64u + lane;
+                        nword[gi] = wi < pw ? ld_l2_u64(&pt2[wi]) : 0ull;
+                    }
+                    for (uint32_t bb = w0 + wv * 64u * SG; bb < pw; bb += NW * 64u * SG) {
+                        unsigned long long word[SG], surv[SG];
+                        uint32_t cnt = 0;
+#pragma unroll
+                        for (uint32_t gi = 0; gi < SG; gi++) {
+                            word[gi] = nword[gi];
+                            surv[gi] = 0ull;
+                            cnt += (uint32_t)__popcll(word[gi] & kPendBits);
+                            const uint32_t wn = bb + NW * 64u * SG + gi * 64u + lane;
+                            rl_count(L, RL_SWEEP, wn < pw, pt2 + (wn < pw ? wn : 0u));
+                            nword[gi] = wn < pw ? ld_l2_u64(&pt2[wn]) : 0ull;
+                        }
                         uint32_t tot;
-                        const uint32_t off = wave_excl_scan((uint32_t)__popcll(pend), &tot);
+                        const uint32_t off = wave_excl_scan(cnt, &tot);
                         for (uint32_t p0 = 0; p0 < tot; p0 += kClW) {
                             {
-                                unsigned long long w = pend;
                                 uint32_t o = off;
-                                while (w) {
-                                    const uint32_t b = (uint32_t)__ffsll((long long)w) - 1u;
-                                    w &= w - 1ull;
-                                    if (o >= p0 && o < p0 + kClW) clw[o - p0] = wi * 32u + b / 2u;
-                                    o++;
+#pragma unroll
+                                for (uint32_t gi = 0; gi < SG; gi++) {
+                                    unsigned long long w = word[gi] & kPendBits;
+                                    const uint32_t wi = bb + gi * 64u + lane;
+                                    while (w) {
+                                        const uint32_t b = (uint32_t)__ffsll((long long)w) - 1u;
+                                        w &= w - 1ull;
+                                        if (o >= p0 && o < p0 + kClW) clw[o - p0] = wi * 32u + b / 2u;
+                                        o++;
+                                    }
                                 }
                             }
                             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1224,10 +1240,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                     const uint32_t e = vb + (uint32_t)u * VPW + lane / LPV;
                                     vv[u] = e < n ? clw[e] : 0xFFFFFFFFu;
                                     rl_count(L, RL_SWEEP, e < n, reinterpret_cast<const char*>(D.dist) + ((size_t)(e < n ? vv[u] : 0u) * LPV + lane % LPV) * 16);
-#if !SHD_SWEEP_K0LAZY
                                     rl_count(L, RL_SWEEP, e < n, g.kap0 + (e < n ? vv[u] : 0u));
                                     k0[u] = g.kap0[e < n ? vv[u] : 0u];
-#endif
                                     d[u][0] = d[u][1] = kInfBits;
                                     if (e < n) {
                                         typedef unsigned long long u64x2
@@ -1239,24 +1253,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                         d[u][1] = x.y;
                                     }
                                 }
-#if SHD_SWEEP_K0LAZY
-                                // kappa0 only for the vertices with a pair in bucket nb (about
-                                // a third of those visited): one more round trip, fewer requests
-#pragma unroll
-                                for (int u = 0; u < SU; u++) {
-                                    const uint32_t jl = 2 * (lane % LPV);
-                                    uint32_t inb = 0;
-#pragma unroll
-                                    for (int h = 0; h < 2; h++)
-                                        if (d[u][h] != kInfBits &&
-                                            bkt(bits2d(d[u][h]), L.sh[jl + h], B.inv_delta) == nb)
-                                            inb = 1u;
-#pragma unroll
-                                    for (uint32_t o = 1; o < LPV; o <<= 1) inb |= __shfl_xor(inb, (int)o, 64);
-                                    rl_count(L, RL_SWEEP, inb != 0u, g.kap0 + (inb ? vv[u] : 0u));
-                                    k0[u] = inb ? g.kap0[vv[u]] : 0.f;
-                                }
-#endif
                                 uint32_t km = kNoBucket;
 #pragma unroll
                                 for (int u = 0; u < SU; u++) {
@@ -1282,28 +1278,47 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                         keep |= __shfl_xor(keep, (int)o, 64);
                                     }
                                     const uint32_t v = vv[u];
+                                    const uint32_t e = vb + (uint32_t)u * VPW + lane / LPV;
                                     const bool ok = (lane % LPV) == 0 && v != 0xFFFFFFFFu;
                                     const bool lead = ok && m != 0u;
                                     wl_count(L, WL_MASK_ST, lead, mcur + (lead ? v : 0u));
                                     if (lead) mcur[v] = (M)m;
-                                    if (ok && keep) atomicOr(&svw[v / 32 - bb], 1ull << (2u * (v & 31u)));
+                                    if (ok && keep) clw[e] = v | kKeep;
                                     wpush<K>(L, lead, v, qin, &L.qtail, cap, &L.fover, 32u);
                                 }
                                 km = wave_min_u32(km);
                                 if (lane == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
                             }
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            __builtin_amdgcn_wave_barrier();
+                            // this pass's survivors back into the lanes' words (same bit order)
+                            {
+                                uint32_t o = off;
+#pragma unroll
+                                for (uint32_t gi = 0; gi < SG; gi++) {
+                                    unsigned long long w = word[gi] & kPendBits;
+                                    while (w) {
+                                        const uint32_t b = (uint32_t)__ffsll((long long)w) - 1u;
+                                        w &= w - 1ull;
+                                        if (o >= p0 && o < p0 + kClW && (clw[o - p0] & kKeep))
+                                            surv[gi] |= 1ull << b;
+                                        o++;
+                                    }
+                                }
+                            }
                             // the slice is refilled by the next pass
                             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                             __builtin_amdgcn_wave_barrier();
                         }
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        __builtin_amdgcn_wave_barrier();
-                        // the touched bits stay; svw holds a subset of the pending bits: an
+                        // the touched bits stay; surv holds a subset of the pending bits: an
                         // unchanged pair needs no store
-                        const unsigned long long nw = (word & ~kPendBits) | svw[lane];
-                        wl_count(L, WL_PEND_ST, wi < pw && nw != word, pt2 + wi);
-                        if (wi < pw && nw != word) pt2[wi] = nw;
-                        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                        for (uint32_t gi = 0; gi < SG; gi++) {
+                            const uint32_t wi = bb + gi * 64u + lane;
+                            const unsigned long long nw = (word[gi] & ~kPendBits) | surv[gi];
+                            wl_count(L, WL_PEND_ST, wi < pw && nw != word[gi], pt2 + wi);
+                            if (wi < pw && nw != word[gi]) pt2[wi] = nw;
+                        }
                     }
                 }
             }

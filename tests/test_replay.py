@@ -36,10 +36,11 @@ def test_replay_full_dijkstra_parents_match_oracle(integer, int_keys):
 
 
 @pytest.mark.parametrize("int_keys", [1, 0])
-def test_replay_deep_heap_blocked_layout_matches_oracle(int_keys):
-    """A graph large enough (V > 2^14) that the heap's HBM levels 9-13 sit in the blocked
-    sink-round layout (topo_replay.hip RpHeap::phys) and deeper levels position-major: full
-    Dijkstra from three sources, distances and every parent equal to the oracle's."""
+def test_replay_deep_heap_matches_oracle(int_keys):
+    """A graph large enough (V > 2^15) that the heap grows well past its 9 LDS levels into the HBM
+    levels -- in a SHD_RP_BLOCKED build the blocked sink-round layout of levels 9-13
+    (topo_replay.hip RpHeap::phys) and position-major levels below: full Dijkstra from three
+    sources, distances and every parent equal to the oracle's."""
     top, g = synthetic_pair(seed=21, n_routers=40000, n_poi=200, n_edges=300000, integer=True)
     top.set_option("replay_int_keys", int_keys)
     attach_hosts(top, g, 200, type_hints=["client", "relay"])
