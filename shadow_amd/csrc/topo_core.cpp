@@ -260,8 +260,9 @@ struct _Topology {
                               // pi, 2 = preorder of the h0 shortest-path tree)
     int batchFill = 0;        // option "batch_fill": sources per batch (0 = auto: the fewest per
                               // batch that finish the rows in the same rounds of the slots)
-    int batchOrder = 2;       // option "batch_order": 0 grouped order, 1 shuffled, 2 / 3 by mean
-                              // pi descending / ascending
+    int batchOrder = 5;       // option "batch_order": 0 grouped order, 1 shuffled, 2 / 3 by mean
+                              // pi descending / ascending, 4 by mean h0-tree depth descending,
+                              // 5 auto (4 past 3 rounds of the slots, else 2)
     bool targetSkip = true;   // option "target_skip": target bits in the relaxation copy; pairs
                               // into non-target tail vertices that would expand nothing are
                               // dropped (topo_sssp_batch.hip)
@@ -1274,8 +1275,11 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 const double delta = default_delta(top);
                 // the order, the row map and the bucket shifts depend only on the sources, the
                 // batch fill and the options: a rebuild of the same rows reuses them
+                const int64_t nbat = (rows + kf - 1) / kf;
+                const int border = top->batchOrder != 5 ? top->batchOrder
+                                   : nbat > 3 * (int64_t)std::max(1, ws.slots) ? 4 : 2;
                 const bool cached = top->ordHp == top->hp.get() && top->ordKf == kf &&
-                                    top->ordSO == top->sourceOrder && top->ordBO == top->batchOrder &&
+                                    top->ordSO == top->sourceOrder && top->ordBO == border &&
                                     top->ordDelta == delta && top->ordSrc == src;
                 if (!cached) {
                 // Batches of K sources settle in lock-step and share an expansion when their
@@ -1328,11 +1332,15 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 }
                 // order of the batches (groups of kf consecutive positions) in the dequeue: the
                 // kernel ends with the slowest slot, so the last batches decide its tail
-                if (top->batchOrder != 0 && rows > kf) {
-                    const int64_t nb = (rows + kf - 1) / kf;
+                // batch_order 5 (auto): by depth when the batches fill more than 3 rounds of the
+                // slots -- longest-predicted first shortens the tail of a many-round launch (full
+                // table: 71.1 -> 68.5 ms) -- else by pi: with two rounds the order only pairs
+                // batches, and the depth predictor pairs them worse (2,500 rows: 25.9 -> 28.6 ms)
+                if (border != 0 && rows > kf) {
+                    const int64_t nb = nbat;
                     std::vector<uint32_t> bo((size_t)nb);
                     std::iota(bo.begin(), bo.end(), 0u);
-                    if (top->batchOrder == 1) {
+                    if (border == 1) {
                         SplitMix rng(0x5eedull);
                         for (int64_t i = nb - 1; i > 0; i--) std::swap(bo[(size_t)i], bo[(size_t)rng.below((uint64_t)i + 1)]);
                     } else {
@@ -1340,12 +1348,25 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                         for (int64_t b = 0; b < nb; b++) {
                             int64_t c = 0;
                             for (int64_t i = b * kf; i < std::min(rows, (b + 1) * kf); i++, c++) {
-                                const double p = top->hp->pot[(size_t)src[(size_t)perm[(size_t)i]]];
-                                mp[(size_t)b] += std::isfinite(p) ? p : 0.0;
+                                const uint32_t s = src[(size_t)perm[(size_t)i]];
+                                if (border == 4) {
+                                    // the source's depth in the h0 shortest-path tree: deeper
+                                    // sources relax more pairs (C4: corr 0.59 with the batch's
+                                    // duration, against 0.25 for mean pi)
+                                    uint32_t v = s, dep = 0;
+                                    while (dep <= (uint32_t)top->g.V && top->hp->sptPar[v] != 0xFFFFFFFFu) {
+                                        v = top->hp->sptPar[v];
+                                        dep++;
+                                    }
+                                    mp[(size_t)b] += (double)dep;
+                                } else {
+                                    const double p = top->hp->pot[(size_t)s];
+                                    mp[(size_t)b] += std::isfinite(p) ? p : 0.0;
+                                }
                             }
                             mp[(size_t)b] /= (double)std::max<int64_t>(1, c);
                         }
-                        const bool desc = top->batchOrder == 2;
+                        const bool desc = border != 3;
                         std::stable_sort(bo.begin(), bo.end(), [&](uint32_t a, uint32_t b) {
                             return desc ? mp[a] > mp[b] : mp[a] < mp[b];
                         });
@@ -1386,7 +1407,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 top->ordHp = top->hp.get();
                 top->ordKf = kf;
                 top->ordSO = top->sourceOrder;
-                top->ordBO = top->batchOrder;
+                top->ordBO = border;
                 top->ordDelta = delta;
                 }
                 ws.rowmap = top->d_rowmap.p;

@@ -72,4 +72,5 @@ print("per source: dur ms p50 %.2f p90 %.2f max %.2f | relax p50 %.3g max %.3g |
 for name, y in (("relax", rel), ("exp", exp), ("dur", dur)):
     print("corr(%s, x): " % name + ", ".join("%s %.2f" % (k, np.corrcoef(y, v)[0, 1])
                                            for k, v in feats.items() if np.std(v) > 0))
-np.savez(out, src=src, dur=dur, rel=rel, exp=exp, **feats)
+np.savez(out, src=src, dur=dur, rel=rel, exp=exp, tree_parent=csr["tree_parent"], pot=pot,
+         deg_all=deg.astype(np.int32), **feats)
