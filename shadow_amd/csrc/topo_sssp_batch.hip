@@ -76,6 +76,12 @@ using namespace dev;
 #else
 #define BT_TICK(i) do { } while (0)
 #endif
+#ifndef SHD_PB_SPLIT
+#define SHD_PB_SPLIT 1  // phase-B rounds of tail-target pairs first, then rounds of LDS-hub pairs
+#endif
+#ifndef SHD_PA_SKIP
+#define SHD_PA_SKIP 1  // the target skip decided in phase A (dropped pairs take no phase-B lane)
+#endif
 #ifndef SHD_TGT_MAJOR
 #define SHD_TGT_MAJOR 1  // parent walks and epilogue items numbered target-major (a target's K sources in adjacent lanes)
 #endif
@@ -146,7 +152,8 @@ struct LdsB {
                                 // tail's improver, a hub's improver; pairs sent to row scans
     unsigned long long bt[8];   // SHD_BATCH_TIME builds: wave ticks of tail / hub iterations in
                                 // chunk loads, phase A, phase B; phase-B rounds, active lanes
-    unsigned long long sw[4];   // SHD_BATCH_TIME builds: sweep counts (ST_SW0)
+    unsigned long long sw[4];   // SHD_BATCH_TIME builds (ST_SW0): phase-B rounds with a tail
+                                // target, tail-target pairs, hub-target pairs, (unused)
     // per-workgroup counters and phase ticks, kept here by thread 0 rather than in (uniform)
     // registers: near iterations, sweeps, expansions, parent-pass pairs; ticks of init, SSSP,
     // parents, targets, sweeps; the last tick
@@ -590,6 +597,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                                               uint32_t qcap, uint32_t* hq, const BBuckets& B) {
     using MO = MaskOps<K>;
     static_assert(64 % K == 0, "a wave holds whole edge groups");
+    static_assert(UA >= 1 && (UA & (UA - 1)) == 0, "the phase-B edge search halves UA * 64");
     constexpr int RB = SHD_BATCH_RB;     // phase-B rounds whose loads are in flight together
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
@@ -656,17 +664,23 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             // is dropped from the edge (91 % of the tail relaxations on C4).  Every relaxation
             // that sets or ties a final value is still performed: distances, parent hints and
             // tie bits are unchanged.
+            // The target skip (phase B's comment below) is decided here too, per (edge, source):
+            // a dropped pair takes no phase-B lane (C4: 21 % of the pairs).
 #pragma unroll
             for (int a = 0; a < UA; a++) {
                 uint32_t mk = amk[a];
                 const double w = __hiloint2double((int)awh[a], (int)awl[a]);
                 const double pv = rec_pi(apb[a]);
+                const bool skippable = SHD_PA_SKIP && kKapInRec && g.tflags &&
+                                       (an[a] & 0x3FFFFFFFu) >= D.H && !((an[a] >> 30) & 1u);
+                const float kz0 = rec_kap0(apb[a]);
                 while (mk) {
                     const uint32_t jj = (uint32_t)__ffs(mk) - 1u;
                     mk &= mk - 1u;
                     const double ad = __dadd_rn(L.val[alo[a] * K + jj], w);
                     const double bnd = __dmul_rn(__dadd_rn(L.dh0[jj], pv), 1.000001);
-                    if (ad > bnd) amk[a] &= ~(1u << jj);
+                    if (ad > bnd || (skippable && !kappa_useful(kz0, L.dh0[jj], ad, g.piMax)))
+                        amk[a] &= ~(1u << jj);
                 }
             }
             // Pair compaction: the wave's surviving (edge, source) pairs, in edge order (edge
@@ -675,14 +689,28 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             // search over the offsets by shuffles), its source the matching set bit of the
             // edge's mask.  The pairs of one edge sit in adjacent lanes: their loads and atomics
             // on the target's 64-B line of K distances still go out as one request.
-            uint32_t po[UA];  // exclusive pair offset of edge (a, lane)
-            uint32_t npair = 0;
+            // Two classes of pairs, numbered apart: pairs into tail vertices (HBM line: pre-check
+            // load, returning atomicMin) fill the first rounds, pairs into LDS hubs the rest.  A
+            // hub round then issues no HBM load or returning atomic at all (LDS atomics and
+            // fire-and-forget stores only), instead of waiting on the tail pairs it was mixed with.
+            // exclusive pair offsets of edge (a, lane) among the tail-class pairs (po) and the
+            // hub-class pairs (ph): each non-decreasing in edge order, an edge of the other class
+            // counting 0 pairs (the search takes the last edge at or below a pair's index)
+            uint32_t po[UA], ph[UA];
+            uint32_t npt = 0, nph = 0;  // tail-class, hub-class pairs
 #pragma unroll
             for (int a = 0; a < UA; a++) {
-                uint32_t t_;
-                po[a] = npair + wave_excl_scan((uint32_t)__popc(amk[a]), &t_);
-                npair += t_;
+                const uint32_t c = (uint32_t)__popc(amk[a]);
+                const bool tl = !SHD_PB_SPLIT ||
+                                (an[a] & (g.tflags ? 0x3FFFFFFFu : 0x7FFFFFFFu)) >= D.H;
+                uint32_t tt, th = 0;
+                po[a] = npt + wave_excl_scan(tl ? c : 0u, &tt);
+                ph[a] = SHD_PB_SPLIT ? nph + wave_excl_scan(tl ? 0u : c, &th) : 0u;
+                npt += tt;
+                nph += th;
             }
+            const uint32_t rT = (npt + 63u) / 64u;               // tail rounds
+            const uint32_t nround = rT + (nph + 63u) / 64u;      // then hub rounds
             // the edge's data for the shuffles: (col | tree bit), (chunk slot | mask << 16)
             uint32_t alm[UA];
 #pragma unroll
@@ -690,20 +718,28 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             BT_TICK(1);
 #if SHD_BATCH_TIME
             if (lane == 0) {
-                atomicAdd(&L.bt[6], (unsigned long long)((npair + 63) / 64));
-                atomicAdd(&L.bt[7], (unsigned long long)npair);
+                atomicAdd(&L.bt[6], (unsigned long long)nround);
+                atomicAdd(&L.bt[7], (unsigned long long)(npt + nph));
             }
 #endif
             uint32_t fm = kNoBucket;
-            for (uint32_t p0 = 0; p0 < npair; p0 += 64u * RB) {
+            for (uint32_t r0 = 0; r0 < nround; r0 += RB) {
             uint32_t n[RB], lo[RB], jr[RB], er[RB];
             unsigned long long ab[RB], cur[RB];  // ab = ~0: no pair in this lane
             float kz[RB];                         // kappa0 of the edge's target
             uint32_t tree[RB];
 #pragma unroll
             for (int rr = 0; rr < RB; rr++) {
-                const uint32_t q = p0 + (uint32_t)rr * 64u + lane;
-                // last edge E (of UA * 64) with offset <= q (uniform shuffles, per-lane index)
+                // round r (uniform): class tail below rT, else hub; q = the pair in its class
+                const uint32_t r = r0 + (uint32_t)rr;
+                const bool hubr = r >= rT;
+                const uint32_t q = (hubr ? r - rT : r) * 64u + lane;
+                const uint32_t lim = r >= nround ? 0u : hubr ? nph : npt;
+                // last edge E (of UA * 64) whose offset in the round's class is <= q (uniform
+                // shuffles, per-lane index)
+                uint32_t pc[UA];
+#pragma unroll
+                for (int a = 0; a < UA; a++) pc[a] = hubr ? ph[a] : po[a];
                 uint32_t e = 0;
 #pragma unroll
                 for (uint32_t st = (uint32_t)UA * 32u; st >= 1u; st >>= 1) {
@@ -711,7 +747,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     uint32_t oc = 0;
 #pragma unroll
                     for (int a = 0; a < UA; a++) {
-                        const uint32_t x = __shfl(po[a], (int)(c & 63u), 64);
+                        const uint32_t x = __shfl(pc[a], (int)(c & 63u), 64);
                         if ((c >> 6) == (uint32_t)a) oc = x;
                     }
                     if (oc <= q) e = c;
@@ -723,12 +759,12 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     const uint32_t t0 = __shfl(an[a], el, 64), t1 = __shfl(alm[a], el, 64);
                     const uint32_t t2 = __shfl(awl[a], el, 64), t3 = __shfl(awh[a], el, 64);
                     const uint32_t t4 = kKapInRec ? __shfl(apb[a], el, 64) : 0u;
-                    const uint32_t t5 = __shfl(po[a], el, 64);
+                    const uint32_t t5 = __shfl(pc[a], el, 64);
                     if ((e >> 6) == (uint32_t)a) {
                         xn = t0; xlm = t1; xwl = t2; xwh = t3; xpb = t4; xo = t5;
                     }
                 }
-                bool on = q < npair;
+                bool on = q < lim;
                 // source: the (q - offset)-th set bit of the edge's mask
                 uint32_t mk = xlm >> 16, k = q - xo, jj = 0;
 #pragma unroll
@@ -750,7 +786,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 // its final distance (its chain edge passes the filter), so every relaxation that
                 // sets or ties its final value passes this test (a larger, stale d_j(h0) only
                 // widens it).  The pair is dropped before its pre-check load and atomics.
-                if (kKapInRec && g.tflags && on && n[rr] >= D.H && !((xn >> 30) & 1u) &&
+                if (!SHD_PA_SKIP && kKapInRec && g.tflags && on && n[rr] >= D.H && !((xn >> 30) & 1u) &&
                     !kappa_useful(kz[rr], L.dh0[jj], abd, g.piMax))
                     on = false;
                 er[rr] = on ? e : 0x10000u + lane;  // segment key (no segment across empty lanes)
@@ -759,6 +795,16 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 const bool t = on && n[rr] >= D.H;
                 rl_count(L, RL_RELAX_PRE, t, D.dist + (t ? (size_t)n[rr] : (size_t)0) * K + jj);
                 const unsigned long long x = D.dist[(t ? (size_t)n[rr] : (size_t)0) * K + jj];
+#if SHD_BATCH_TIME
+                {
+                    const unsigned long long tb = __ballot(t), hb = __ballot(on && !t);
+                    if (lane == 0) {
+                        if (tb) atomicAdd(&L.sw[0], 1ull);
+                        atomicAdd(&L.sw[1], (unsigned long long)__popcll(tb));
+                        atomicAdd(&L.sw[2], (unsigned long long)__popcll(hb));
+                    }
+                }
+#endif
                 if (!kKapInRec) kz[rr] = g.kap0[t ? n[rr] : 0u];
                 cur[rr] = t ? x : 0ull;
             }

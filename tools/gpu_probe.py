@@ -72,8 +72,8 @@ for rep in range(args.reps):
               flush=True)
     if any(st.get("sweep_events", [0])):
         sw = st["sweep_events"]
-        print("   sweeps (SHD_BATCH_TIME) per source: pending visited %.0f, queued %.0f, kappa-held "
-              "%.0f, kept %.0f" % tuple(x / rows for x in sw), flush=True)
+        print("   phase B (SHD_BATCH_TIME) per source: rounds with a tail target %.0f, tail-target "
+              "pairs %.0f, hub-target pairs %.0f" % tuple(x / rows for x in sw[:3]), flush=True)
     if any(st.get("write_lines", [0])):
         names = ("relax_min", "relax_tie", "relax_hint", "relax_pend", "relax_touch", "relax_mask",
                  "mask_st", "pend_st", "reset", "touch_clr", "prec", "pscr", "out", "hub", "queue",
