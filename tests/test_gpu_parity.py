@@ -203,6 +203,30 @@ def test_sssp_batch_fill(fill, integer):
     assert np.array_equal(hops, ohops.astype(np.uint16))
 
 
+@pytest.mark.parametrize("order,slots,fill", [(2, 8, 0), (4, 8, 0), (5, 8, 0), (5, 64, 0),
+                                              (3, 8, 5), (1, 8, 2)])
+def test_sssp_batch_order_and_rounds(order, slots, fill):
+    """The batch dequeue order (batch_order 1 shuffled, 2 / 3 mean pi, 4 h0-tree depth, 5 auto:
+    depth past 3 rounds of the slots) and the auto fill by equal rounds on few slots (many
+    rounds, ragged last batches) settle the same table, bit-exact against the oracle."""
+    top, g = synthetic_pair(seed=23, n_routers=2000, n_poi=101, n_edges=20000)
+    top.set_option("batch_order", order)
+    top.set_option("slots", slots)
+    top.set_option("batch_fill", fill)
+    otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay", "server"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    assert st["errors"] == 0
+    if fill == 0:  # equal rounds: the fewest sources per batch that keep the round count
+        S = st["slots"]
+        rounds = -(-len(a) // (8 * S))
+        assert st["batch_fill"] == min(8, -(-len(a) // (rounds * S)))
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+
+
 def test_sssp_rows_shard_equals_full():
     """build_rows on a row range == the same rows of the full table (sharding correctness)."""
     import torch
