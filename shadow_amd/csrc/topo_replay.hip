@@ -326,6 +326,57 @@ __device__ __forceinline__ uint32_t rp_lds_find(uint32_t t, uint32_t size, int l
     return found;
 }
 
+#ifndef SHD_RP_PARPATH
+#define SHD_RP_PARPATH 1  // a sink round's path of larger children found lane-parallel (ballots)
+#endif
+// One sink round's path of larger children, lane-parallel: lane i holds node rr = i + 2 of the
+// subtree below the round's head (BFS, head = 1; `valid`: the node exists, i.e. its position is
+// below the heap size).  igraph_2wheap_sink goes left when data[L] >= data[R] (or R does not
+// exist): every node compares itself with its sibling (one shuffle) -- the winners form one
+// ballot -- and a node is on the path iff it and all its ancestors below the head won (bit tests
+// of that ballot).  A second ballot is the path, one node per depth; path lanes np .. np + m - 1
+// receive node (position, key, vertex) of depth 1 .. m by one shuffle each.  No readlane chain:
+// a few dozen VALU and three ballots instead of la dependent readlane steps.  Returns m (levels
+// taken: < la when the path ends inside the round); *cur becomes the deepest path node.
+template <bool I>
+__device__ __forceinline__ int rp_round_path(uint32_t& cur, int lane, bool valid,
+                                             typename RpKey<I>::T k, uint32_t v, uint32_t p,
+                                             int np, uint32_t& pp, typename RpKey<I>::T& pk,
+                                             uint32_t& pv) {
+    using T = typename RpKey<I>::T;
+    const uint32_t rr = (uint32_t)lane + 2u;
+    const T ks = __shfl_xor(k, 1, 64);
+    const bool vs = __shfl_xor(valid ? 1 : 0, 1, 64) != 0;
+    // left (rr even) wins if it exists and (no right sibling or k_L >= k_R); right wins if both
+    // exist and !(k_L >= k_R)
+    const bool win = (rr & 1u) == 0u ? (valid && (!vs || k >= ks)) : (valid && vs && !(ks >= k));
+    const unsigned long long W = __ballot(win);
+    bool on = win;
+#pragma unroll
+    for (int t = 1; t < kRpLA; t++) {
+        const uint32_t a = rr >> t;  // ancestor at t levels up (a >= 2: below the head)
+        if (a >= 2u) on = on && ((W >> (a - 2u)) & 1ull);
+    }
+    const unsigned long long P = __ballot(on);
+    const int m = __popcll(P);
+    // lane np + d - 1 takes the path node of depth d (lanes rr in [2^d, 2^(d+1)))
+    const int d = lane - np + 1;
+    int src = 0;
+    if (d >= 1 && d <= m) {
+        const unsigned long long rng = ((2ull << ((1u << d) - 1u)) - 1ull) << ((1u << d) - 2u);
+        src = __ffsll((long long)(P & rng)) - 1;
+    }
+    const T ksrc = __shfl(k, src, 64);
+    const uint32_t vsrc = __shfl(v, src, 64), psrc = __shfl(p, src, 64);
+    if (d >= 1 && d <= m) {
+        pp = psrc;
+        pk = ksrc;
+        pv = vsrc;
+    }
+    if (m > 0) cur = rl_u32(p, 63 - __clzll((long long)P));
+    return m;
+}
+
 // igraph_2wheap_delete_max's sink of x = the last element from the root (a hole) in a heap of
 // `size` (after the removal): igraph_2wheap_sink takes the left child if right == size or
 // data[L] >= data[R] and swaps while data[head] < data[child].  The path of larger children does
@@ -357,10 +408,22 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap<I>& H, uint32_t size, i
         const uint32_t p = rp_sub_pos(cur, lane);
         T k = K::lo();
         uint32_t v = 0;
-        if (lane < (2 << la) - 2 && p < size) {
+        const bool valid = lane < (2 << la) - 2 && p < size;
+        if (valid) {
             k = lds_k<I>(p);
             v = lds_v<I>(p);
         }
+#if SHD_RP_PARPATH
+        {
+            const int m = rp_round_path<I>(cur, lane, valid, k, v, p, np, pp, pk, pv);
+            np += m;
+            if (m < la) {
+                bottom = true;
+                break;
+            }
+            continue;
+        }
+#endif
         uint32_t q = 0;
         for (int s = 0; s < la; ++s) {
             const uint32_t L = 2u * cur + 1u;
@@ -424,6 +487,22 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap<I>& H, uint32_t size, i
                 break;
             }
         }
+#if SHD_RP_PARPATH
+        if (kHNodes <= 64) {
+            // the round's path at once; x stops at the first of its nodes it is not smaller than
+            const bool valid = lane < kHNodes && p < size;
+            const int np0 = np;
+            const int m = rp_round_path<I>(cur, lane, valid, k, v, p, np, pp, pk, pv);
+            np += m;
+            const unsigned long long sm = __ballot(lane >= np0 && lane < np && !(xk < pk));
+            if (sm) {
+                stop = __ffsll((long long)sm) - 1;
+                break;
+            }
+            if (m < kHL) bottom = true;
+            continue;
+        }
+#endif
         uint32_t q = 0;
 #pragma unroll
         for (int s = 0; s < kHL; ++s) {
