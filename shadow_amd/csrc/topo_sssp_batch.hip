@@ -1450,53 +1450,96 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             prec[q] = make_uint4(u, ept, (uint32_t)lb, (uint32_t)(lb >> 32));
         };
         // A guess certified without scanning a row, past the h0-tree guess of a tail (tried by
-        // the walk itself): a tail's recorded improver (no tie bit, the edge is tight) or the
-        // first P hubs' recorded improver (LDS hint, no tie bit).  Writes the pair record and
-        // returns the parent in *pout; false: the pair needs a row scan.  dv = d_j(v).
-        auto try_hint = [&](uint32_t q, unsigned long long dv, uint32_t* pout) -> bool {
-            const uint32_t v = q / K, j = q % K;
-            if (v >= H) {
-                // the record {improver, tag word} (the walk's tag store kept the tie flag)
-                const uint2 rw = __hip_atomic_load(reinterpret_cast<const uint2*>(precw + 4 * (size_t)q),
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (tag_tied(rw.y, ep)) return false;
-                if (!SHD_TAIL_HINT || !g.rows_sorted) return false;
-                // second guess: the recorded improver u; the edge is found in v's own row (a
-                // tail: short) -- the same undirected edge, same latency and loss as u's slot
-                const uint32_t u = rw.x & 0x3FFFFFFFu;
-                if (u >= (uint32_t)V || u == v) return false;
-                const unsigned long long du = D.get(u, j);
-                uint32_t lo = g.rowptr[v], hi = g.rowptr[v + 1];
-                const uint32_t end = hi;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (adj_col(g, mid) < u) lo = mid + 1; else hi = mid;
+        // the walk itself): a tail's recorded improver u (no tie bit; the edge is found in v's own
+        // row -- a tail: short -- the same undirected edge, same latency and loss as u's slot) or
+        // the first P hubs' recorded improver (LDS hint, no tie bit; the edge in u's row).  The
+        // hint pass runs two pairs per thread with their dependent loads interleaved (record ->
+        // row bounds and d_j(u) -> binary search -> edge record and loss): half the serial round
+        // trips of one pair at a time.  A certified pair's record is written (put).
+        constexpr int kHP = 2;  // pairs per thread in flight
+        auto hint_pass = [&](const uint32_t* S, uint32_t nS, uint32_t ib, bool* scan, uint32_t* qo) {
+            uint32_t q[kHP], uu[kHP], key[kHP], lo[kHP], hi[kHP], end[kHP];
+            unsigned long long dv[kHP], du[kHP];
+            bool has[kHP], live[kHP];
+            uint2 rw[kHP];
+            uint32_t hp[kHP], tbit[kHP];
+#pragma unroll
+            for (int h = 0; h < kHP; h++) {
+                const uint32_t i = ib + (uint32_t)h * kSsspBlock + tid;
+                has[h] = i < nS;
+                q[h] = has[h] ? S[i] : 0u;
+                qo[h] = q[h];
+                const uint32_t v = q[h] / K, j = q[h] % K;
+                dv[h] = has[h] ? D.get(v, j) : 0ull;
+                rw[h] = make_uint2(0u, 0u);
+                hp[h] = 0xFFFFFFFFu;
+                tbit[h] = 1u;
+                if (has[h] && v >= H) {
+                    // the record {improver, tag word} (the walk's tag store kept the tie flag)
+                    rw[h] = __hip_atomic_load(reinterpret_cast<const uint2*>(precw + 4 * (size_t)q[h]),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else if (has[h] && v < P) {
+                    tbit[h] = (D.tb[q[h] >> 5] >> (q[h] & 31)) & 1u;
+                    hp[h] = D.hpar[q[h]];
                 }
-                if (lo >= end || adj_col(g, lo) != u) return false;
-                uint32_t c;
-                double wt;
-                adj_load(g, lo, c, wt);
-                if (__dadd_rn(bits2d(du), wt) != bits2d(dv)) return false;
-                put(q, u, g.aloss[lo]);
-                *pout = u;
-                return true;
             }
-            if (!g.rows_sorted || v >= P || ((D.tb[q >> 5] >> (q & 31)) & 1u)) return false;
-            const uint32_t u = D.hpar[q];
-            if (u >= (uint32_t)V) return false;
-            uint32_t lo = g.rowptr[u], hi = g.rowptr[u + 1];
-            while (lo < hi) {  // rows are sorted by neighbour
-                const uint32_t mid = (lo + hi) >> 1;
-                if (adj_col(g, mid) < v) lo = mid + 1; else hi = mid;
+#pragma unroll
+            for (int h = 0; h < kHP; h++) {
+                const uint32_t v = q[h] / K, j = q[h] % K;
+                live[h] = false;
+                uu[h] = 0xFFFFFFFFu;
+                key[h] = 0u;
+                uint32_t row = 0;
+                if (has[h] && g.rows_sorted) {
+                    if (v >= H) {
+                        const uint32_t u = rw[h].x & 0x3FFFFFFFu;
+                        if (SHD_TAIL_HINT && !tag_tied(rw[h].y, ep) && u < (uint32_t)V && u != v) {
+                            live[h] = true;
+                            uu[h] = u;
+                            key[h] = u;
+                            row = v;
+                        }
+                    } else if (v < P && !tbit[h] && hp[h] < (uint32_t)V) {
+                        live[h] = true;
+                        uu[h] = hp[h];
+                        key[h] = v;
+                        row = hp[h];
+                    }
+                }
+                lo[h] = live[h] ? g.rowptr[row] : 0u;
+                hi[h] = live[h] ? g.rowptr[row + 1] : 0u;
+                du[h] = live[h] ? D.get(uu[h], j) : 0ull;
+                end[h] = hi[h];
             }
-            if (lo >= g.rowptr[u + 1] || adj_col(g, lo) != v) return false;
-            uint32_t c;
-            double wt;
-            adj_load(g, lo, c, wt);
-            if (__dadd_rn(bits2d(D.get(u, j)), wt) != bits2d(dv)) return false;
-            put(q, u, g.aloss[lo]);
-            *pout = u;
-            return true;
+            // binary searches of the rows (sorted by neighbour), side by side
+            for (;;) {
+                bool any = false;
+                uint32_t mid[kHP], c[kHP];
+#pragma unroll
+                for (int h = 0; h < kHP; h++) {
+                    const bool go = live[h] && lo[h] < hi[h];
+                    mid[h] = (lo[h] + hi[h]) >> 1;
+                    c[h] = go ? adj_col(g, mid[h]) : 0u;
+                    any = any || go;
+                }
+                if (!any) break;
+#pragma unroll
+                for (int h = 0; h < kHP; h++) {
+                    if (!(live[h] && lo[h] < hi[h])) continue;
+                    if (c[h] < key[h]) lo[h] = mid[h] + 1u; else hi[h] = mid[h];
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < kHP; h++) {
+                scan[h] = has[h];
+                if (!live[h] || lo[h] >= end[h]) continue;
+                const AdjRec ar = adj_rec(g, lo[h]);
+                const double ls = g.aloss[lo[h]];
+                if (ar.a != key[h]) continue;
+                if (__dadd_rn(bits2d(du[h]), rec_wt(ar)) != bits2d(dv[h])) continue;
+                put(q[h], uu[h], ls);
+                scan[h] = false;
+            }
         };
         // A walk hop's inputs at tail vertex v for source j: its h0-tree record {parent, slot,
         // f64 w, f64 loss of that edge} (32 B, one line) and d_j(v) -- independent loads, in one
@@ -1625,26 +1668,33 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             // (consumed by the walks)
             if (tid == 0) L.qtail = 0;
             __syncthreads();
-            for (uint32_t ib = 0; ib < nS; ib += kSsspBlock) {
-                const uint32_t i = ib + tid;
-                bool scan = false;
-                uint32_t q = 0;
-                if (i < nS) {
-                    q = fscr[i];
-                    uint32_t u = 0;
-                    const bool ok = try_hint(q, D.get(q / K, q % K), &u);
-                    atomicAdd(&L.wk[ok ? (q / K >= H ? 2 : 3) : 4], 1ull);
-                    if (!ok) {
+            for (uint32_t ib = 0; ib < nS; ib += (uint32_t)kHP * kSsspBlock) {
+                bool scan[kHP];
+                uint32_t qs[kHP];
+                hint_pass(fscr, nS, ib, scan, qs);
+#pragma unroll
+                for (int h = 0; h < kHP; h++) {
+                    const uint32_t q = qs[h];
+                    const bool in = ib + (uint32_t)h * kSsspBlock + tid < nS;
+                    // counters (walk kinds): tail hint, hub hint, row scan -- one LDS atomic per wave
+                    const unsigned long long bt = __ballot(in && !scan[h] && q / K >= H);
+                    const unsigned long long bh = __ballot(in && !scan[h] && q / K < H);
+                    const unsigned long long bs = __ballot(in && scan[h]);
+                    if ((tid & 63u) == 0u) {
+                        if (bt) atomicAdd(&L.wk[2], (unsigned long long)__popcll(bt));
+                        if (bh) atomicAdd(&L.wk[3], (unsigned long long)__popcll(bh));
+                        if (bs) atomicAdd(&L.wk[4], (unsigned long long)__popcll(bs));
+                    }
+                    if (in && scan[h]) {
                         wl_count(L, WL_PSCR, true, best + q);
                         wl_count(L, WL_PSCR, true, cntc + q);
                         wl_count(L, WL_PSCR, true, bslot + q);
                         best[q] = kInfBits;
                         cntc[q] = 0;
                         bslot[q] = 0xFFFFFFFFu;
-                        scan = true;
                     }
+                    wpush<K>(L, in && scan[h], q, pcur, &L.qtail, pcap, &L.fover, 128u);
                 }
-                wpush<K>(L, scan, q, pcur, &L.qtail, pcap, &L.fover, 128u);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
