@@ -321,9 +321,8 @@ typedef struct {
                                     the owner's and every peer engine's, the attach-time
                                     preparation thread's included */
     int64_t sweep_events[4];    /* profiling builds (-DSHD_BATCH_TIME=1) only, else 0: the batch
-                                   kernel's bucket sweeps -- pending tail vertices visited, of which
-                                   queued, holding a pair in the opened bucket the kappa test kept
-                                   out, and kept pending */
+                                   kernel's phase-B rounds holding a tail-target pair, tail-target
+                                   pairs, hub-target pairs, (unused) */
     int64_t write_lines[16];    /* profiling builds (-DSHD_BATCH_WRCOUNT=1) only, else 0: 64-B lines
                                    the batch kernel's stores and atomics touched, by category
                                    (topo_sssp_batch.hip WL_*): relaxation atomicMin, tie tags,
