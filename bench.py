@@ -122,12 +122,16 @@ def parallel_calls(fn, n, nthreads):
         return list(ex.map(lambda c: fn(*c), _chunks(n, nthreads)))
 
 
-def complete_table_lines(repeats=20, nthreads=1):
-    """BASELINE configs 2 (plab, 303 x 303) and 3 (full Internet, 183 x 183): the complete-graph
-    pair table (_topology_lookupPath for every attached pair, shd-topology.c:835-873) on the
-    GPU vs the oracle's restatement on one CPU thread and on every thread of the job's share.
-    One host per vertex via its unique geocode hint.  34 B per pair (roofline
-    of pair_table_complete_kernel)."""
+def complete_table_lines(repeats=20, nthreads=1, devices=1, cpu=True):
+    """BASELINE configs 2 (plab, 303 x 303, "on 1 MI355X") and 3 (full Internet, 183 x 183, "on 8
+    MI355X"): the complete-graph pair table (_topology_lookupPath for every attached pair,
+    shd-topology.c:835-873) built by shdtopo_rebuild -- the whole-table build Shadow's first
+    getter triggers: on `devices` GPUs the rows are sharded over the library's engines and
+    exchanged (RCCL all-gather + all-reduce(MIN)).  One host per vertex via its unique geocode
+    hint.  Reported: the build call's wall time (build_ms), the pair kernel's
+    event time (kernel_ms: the slowest device's), per device its shard kernel and rows, and the
+    exchange; 34 B per pair (roofline of pair_table_complete_kernel).  CPU: the oracle's
+    restatement on one thread and on every thread of the job's share (N = 1 runs only)."""
     import lzma
     import oracle
     out = {}
@@ -137,6 +141,8 @@ def complete_table_lines(repeats=20, nthreads=1):
             data = f.read()
         top = sa.Topology.from_buffer(data)
         g = oracle.OGraph.from_graphml(data)
+        if devices > 1:
+            top.set_option("devices", devices)
         geos = list(g.vattrs["geocode"])
         st = 1
         for k, geo in enumerate(geos):
@@ -144,36 +150,50 @@ def complete_table_lines(repeats=20, nthreads=1):
             top.attach_ip(sa.ip_to_network("11.%d.%d.%d" % (k >> 16, (k >> 8) & 255, k & 255)),
                           st, geocodeHint=geo)
         A = len(top.attached_vertices())
-        lr = torch.empty((A, A, 2), dtype=torch.float64, device="cuda")
-        hp = torch.empty((A, A), dtype=torch.int16, device="cuda")
-        rm = torch.empty((A,), dtype=torch.float64, device="cuda")
-        ms = []
+        ms, wall, dk, xm = [], [], [], []
         for i in range(repeats + 2):
-            top.build_rows_into(0, A, lr, hp, rm)
+            top.rebuild()
+            s_ = top.stats()
             if i >= 2:
-                ms.append(top.stats()["sssp_kernel_ms"])
+                ms.append(s_["sssp_kernel_ms"])
+                wall.append(s_["build_wall_ms"])
+                dk.append(s_["device_kernel_ms"][:max(1, min(8, devices))])
+                xm.append(s_["exchange_ms"])
         k_ms = float(np.median(ms))
-        a = np.asarray(sorted(set(top.attached_vertices().tolist())), np.int32)
-        S, D = np.meshgrid(a, a, indexing="ij")
-        Sr, Dr = S.ravel(), D.ravel()
-        t0 = time.perf_counter()
-        g.complete_pairs(Sr, Dr)
-        t_cpu = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        parallel_calls(lambda lo, hi: g.complete_pairs(Sr[lo:hi], Dr[lo:hi]), len(Sr), nthreads)
-        t_cpu_mt = time.perf_counter() - t0
         pairs = A * A
-        out[cfg] = dict(topology=name, attached=A, pairs=pairs,
-                        gpu_pairs_per_s=round(pairs / (k_ms / 1e3), 1), kernel_ms=round(k_ms, 4),
-                        kernel="pair_table_complete_kernel + row_min_kernel",
-                        roofline=dict(bound="hbm", bytes_per_unit=34, units_per_launch=pairs,
-                                      achieved=round(pairs * 34 / (k_ms / 1e3) / 1e9, 2),
-                                      peak=HBM_PEAK_GBS, unit="GB/s",
-                                      frac=round(pairs * 34 / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)),
-                        cpu_pairs_per_s=round(pairs / t_cpu, 1), cpu_cores=1,
-                        cpu_all_cores=dict(pairs_per_s=round(pairs / t_cpu_mt, 1),
-                                           cores=nthreads),
-                        note="launch-bound: %d pairs are a few microseconds of HBM time" % pairs)
+        line = dict(topology=name, attached=A, pairs=pairs, devices=devices,
+                    build_ms=round(float(np.median(wall)), 4), kernel_ms=round(k_ms, 4),
+                    gpu_pairs_per_s=round(pairs / (float(np.median(wall)) / 1e3), 1),
+                    kernel_pairs_per_s=round(pairs / (k_ms / 1e3), 1),
+                    kernel="pair_table_complete_kernel (records, hops, row minima, global "
+                           "minimum: one launch per device)",
+                    pair_matrix_builds=int(s_["pair_matrix_builds"]),
+                    roofline=dict(bound="hbm", bytes_per_unit=34, units_per_launch=pairs,
+                                  achieved=round(pairs * 34 / (k_ms / 1e3) / 1e9, 2),
+                                  peak=HBM_PEAK_GBS, unit="GB/s",
+                                  frac=round(pairs * 34 / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)),
+                    note="launch-bound: %d pairs are a few microseconds of HBM time; the edge "
+                         "matrices stay resident while the attached set is unchanged" % pairs)
+        if devices > 1:
+            line["device_kernel_ms"] = [round(float(x), 4) for x in np.median(np.asarray(dk), axis=0)]
+            line["device_rows"] = list(s_["device_rows"][:min(8, devices)])
+            line["exchange"] = dict(kind={0: "none", 1: "rccl", 2: "peer copies"}.get(
+                int(s_["exchange_kind"]), "?"), ms=round(float(np.median(xm)), 4),
+                bytes_per_device=int(s_["exchange_bytes"]))
+        if cpu:
+            a = np.asarray(sorted(set(top.attached_vertices().tolist())), np.int32)
+            S, D = np.meshgrid(a, a, indexing="ij")
+            Sr, Dr = S.ravel(), D.ravel()
+            t0 = time.perf_counter()
+            g.complete_pairs(Sr, Dr)
+            t_cpu = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            parallel_calls(lambda lo, hi: g.complete_pairs(Sr[lo:hi], Dr[lo:hi]), len(Sr), nthreads)
+            t_cpu_mt = time.perf_counter() - t0
+            line.update(cpu_pairs_per_s=round(pairs / t_cpu, 1), cpu_cores=1,
+                        cpu_all_cores=dict(pairs_per_s=round(pairs / t_cpu_mt, 1), cores=nthreads))
+        top.free()
+        out[cfg] = line
     return out
 
 
@@ -569,8 +589,11 @@ def main():
             cpu["host_nproc"] = os.cpu_count()
             cpu["job_cpu_share"] = nt
         complete = None
-        if ngpu == 1 and not args.no_complete:
-            complete = complete_table_lines(nthreads=cpu_share())
+        if library and not args.no_complete:
+            # configs 2 / 3 on the job's GPUs (option devices = N; "--opt devices=N" rehearses the
+            # N-engine path on one GPU, the engines then sharing it)
+            ndev = int(float(dict(kv.split("=") for kv in args.opt).get("devices", ngpu)))
+            complete = complete_table_lines(nthreads=cpu_share(), devices=ndev, cpu=ngpu == 1)
         out = {
             "metric": "routing-table build GTEPS + packet-routes/sec at 1/2/4/8 MI355X "
                       "(%HBM roofline)",
@@ -611,6 +634,15 @@ def main():
             "exchange": dict(kind={0: "none", 1: "rccl", 2: "peer copies"}.get(
                 int(st["exchange_kind"]), "?") if library else "torch.distributed",
                              ms=round(st["exchange_ms"], 2),
+                             devices=int(st["devices"]) if library else world,
+                             device_kernel_ms=[round(x, 3) for x in
+                                               st["device_kernel_ms"][:min(8, int(st["devices"]))]]
+                             if library and st["devices"] > 1 else None,
+                             device_build_ms=[round(x, 3) for x in
+                                              st["device_build_ms"][:min(8, int(st["devices"]))]]
+                             if library and st["devices"] > 1 else None,
+                             device_rows=st["device_rows"][:min(8, int(st["devices"]))]
+                             if library and st["devices"] > 1 else None,
                              bytes_per_device=int(st["exchange_bytes"]) if library else
                              int((world - 1) * (table.r1 - table.r0) * (A * 18 + 8)),
                              gb_per_s_per_device=round(int(st["exchange_bytes"]) / 1e6 /

@@ -336,6 +336,21 @@ typedef struct {
     double attach_prep_step_ms[4]; /* the attach-time preparation's parts (wall): device init (HIP
                                       queues, code objects), graph preparation, edge scan, the
                                       batched SSSP's workspace (allocation + initialisation) */
+    int64_t pair_matrix_builds; /* complete topologies: times the resident A x A direct-edge
+                                   matrices were (re)built (once per attached set; cumulative) */
+    double device_kernel_ms[8]; /* the last multi-device build (option "devices"), per device slot
+                                   (first 8): event time of its row shard's kernels (SSSP or pair
+                                   kernel, + heap replay), */
+    double device_build_ms[8];  /*   wall time of its row shard's build, */
+    int64_t device_rows[8];     /*   and its rows */
+    int64_t dev_inits;          /* device initialisations of this topology (HIP stream, events, code
+                                   objects): 1, or 2 when the "device" option moved it */
+    double init_bg_ms;          /* wall time of topology_new's background device init (overlaps the
+                                   GraphML parse; 0 if it did not run) */
+    double path_seconds_total;  /* shortestPathTotalTime of the reference (shd-topology.c:792): wall
+                                   seconds of every table / row build so far */
+    int64_t paths_computed;     /* shortestPathCount (shd-topology.c:793): source rows built so far;
+                                   both are logged at topology_free (:445-446) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

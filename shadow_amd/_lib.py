@@ -55,7 +55,10 @@ class ShdStats(ctypes.Structure):
                 ("first_attach_to_table_ms", dbl), ("exchange_bytes", i64),
                 ("csr_host_runs_total", i64), ("sweep_events", i64 * 4),
                 ("write_lines", i64 * 16), ("read_lines", i64 * 8),
-                ("attach_prep_step_ms", dbl * 4)]
+                ("attach_prep_step_ms", dbl * 4), ("pair_matrix_builds", i64),
+                ("device_kernel_ms", dbl * 8), ("device_build_ms", dbl * 8),
+                ("device_rows", i64 * 8), ("dev_inits", i64), ("init_bg_ms", dbl),
+                ("path_seconds_total", dbl), ("paths_computed", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):
@@ -141,6 +144,11 @@ SHIM_SIGNATURES = {
     "shim_next_min_jump": (u64, []),
     "shim_min_updates": (ctypes.c_int, []),
     "shim_reset": (None, []),
+    "logging_log": (None, [cstr, ctypes.c_int, cstr, cstr, ctypes.c_int, cstr]),
+    "shim_log_count": (ctypes.c_int, []),
+    "shim_log_get": (ctypes.c_int, [ctypes.c_int, P, ctypes.c_char_p, ctypes.c_int,
+                                    ctypes.c_char_p, ctypes.c_int]),
+    "shim_log_reset": (None, []),
 }
 
 _lib = None

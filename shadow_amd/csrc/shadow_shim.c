@@ -6,9 +6,14 @@
  *   address_toNetworkIP       src/topology/shd-address.c:114-117  (Address holds a network-order IP)
  *   random_new / nextDouble   src/utility/shd-random.c:13-37      (glibc rand_r stream)
  *   worker_updateMinTimeJump  src/engine/shd-worker.c:459 -> shd-master.c:113-124 (recorded)
+ *   logging_log               src/support/shd-logging.c:127-135 (recorded; printed to stderr at
+ *                             the SHDTOPO_LOG level: 1 critical + warning, 2 + message, 3 + info)
  */
+#include <stdarg.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 struct _Address {
     uint32_t ip; /* network order */
@@ -60,3 +65,48 @@ void shim_reset(void) {
     g_next_min_jump = 0;
     g_updates = 0;
 }
+
+/* logging_log: the last kLogRing messages {GLib level, function, formatted text} are kept for tests
+ * (tests/c/log_capture.c) */
+#define kLogRing 64
+typedef struct {
+    int level;
+    char func[64];
+    char text[512];
+} ShimLog;
+static ShimLog g_log[kLogRing];
+static int g_log_n = 0; /* messages logged since the last reset */
+void logging_log(const char* log_domain, int log_level, const char* fileName,
+                 const char* functionName, int lineNumber, const char* format, ...) {
+    (void)log_domain;
+    (void)fileName;
+    (void)lineNumber;
+    ShimLog* e = &g_log[g_log_n % kLogRing];
+    va_list ap;
+    va_start(ap, format);
+    vsnprintf(e->text, sizeof e->text, format, ap);
+    va_end(ap);
+    e->level = log_level;
+    snprintf(e->func, sizeof e->func, "%s", functionName ? functionName : "n/a");
+    g_log_n++;
+    const char* env = getenv("SHDTOPO_LOG");
+    const int want = env ? atoi(env) : 1;
+    const int lvl = log_level <= (1 << 4) ? 1 : (log_level == (1 << 5) ? 2 : 3);
+    if (lvl <= want) {
+        const char* tag = log_level == (1 << 3) ? "critical"
+                          : log_level == (1 << 4) ? "warning"
+                          : log_level == (1 << 5) ? "message" : "info";
+        fprintf(stderr, "[shadow] %s: [%s] %s\n", tag, e->func, e->text);
+    }
+}
+int shim_log_count(void) { return g_log_n; }
+/* the i-th most recent message (0 = last): its text, level and function; -1 if not kept */
+int shim_log_get(int i, int* level, char* func, int funcCap, char* text, int textCap) {
+    if (i < 0 || i >= g_log_n || i >= kLogRing) return -1;
+    const ShimLog* e = &g_log[(g_log_n - 1 - i) % kLogRing];
+    if (level) *level = e->level;
+    if (func && funcCap > 0) snprintf(func, (size_t)funcCap, "%s", e->func);
+    if (text && textCap > 0) snprintf(text, (size_t)textCap, "%s", e->text);
+    return 0;
+}
+void shim_log_reset(void) { g_log_n = 0; }

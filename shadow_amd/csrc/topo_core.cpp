@@ -38,8 +38,12 @@ extern "C" {
 __attribute__((weak)) uint32_t address_toNetworkIP(Address* address);
 __attribute__((weak)) double random_nextDouble(Random* random);
 __attribute__((weak)) void worker_updateMinTimeJump(double minPathLatency);
+// src/support/shd-logging.h:122-124 (GLogLevelFlags passed as int): Shadow's logger prefixes the
+// real time, the simulated time and the host, and applies the configured log-level filter
+__attribute__((weak)) void logging_log(const char* log_domain, int log_level, const char* fileName,
+                                       const char* functionName, int lineNumber,
+                                       const char* format, ...);
 }
-
 using namespace shdtopo;
 
 namespace shdtopo {
@@ -77,6 +81,8 @@ void pinned_free(void* p) {
 
 namespace {
 
+// Standalone filter (no Shadow logger): SHDTOPO_LOG = 0 silent, 1 critical + warning (default),
+// 2 + message, 3 + info
 int log_level() {
     static int lvl = [] {
         const char* e = getenv("SHDTOPO_LOG");
@@ -85,18 +91,34 @@ int log_level() {
     return lvl;
 }
 
-void logf(int lvl, const char* tag, const char* fmt, ...) {
-    if (lvl > log_level()) return;
+// GLib log levels (G_LOG_LEVEL_CRITICAL / WARNING / MESSAGE / INFO)
+[[maybe_unused]] constexpr int kLogCritical = 1 << 3, kLogWarning = 1 << 4, kLogMessage = 1 << 5,
+                                kLogInfo = 1 << 6;
+
+// The reference's critical() / warning() / message() (shd-logging.h:24-59): inside Shadow the
+// message goes through logging_log, which filters by the configured level and adds the run's
+// prefix; standalone it goes to stderr, filtered by SHDTOPO_LOG.
+void shd_log(int glevel, const char* file, const char* func, int line, const char* fmt, ...) {
+    const int lvl = glevel <= kLogWarning ? 1 : (glevel == kLogMessage ? 2 : 3);
+    if (!logging_log && lvl > log_level()) return;
+    char buf[1024];
     va_list ap;
     va_start(ap, fmt);
-    fprintf(stderr, "[shdtopo] %s: ", tag);
-    vfprintf(stderr, fmt, ap);
-    fputc('\n', stderr);
+    vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
+    if (logging_log) {
+        logging_log("shadow", glevel, file, func, line, "%s", buf);
+        return;
+    }
+    const char* tag = glevel == kLogCritical ? "critical"
+                      : glevel == kLogWarning ? "warning"
+                      : glevel == kLogMessage ? "message" : "info";
+    fprintf(stderr, "[shdtopo] %s: %s\n", tag, buf);
 }
-#define CRITICAL(...) logf(1, "critical", __VA_ARGS__)
-#define WARNING(...) logf(1, "warning", __VA_ARGS__)
-#define MESSAGE(...) logf(2, "message", __VA_ARGS__)
+#define CRITICAL(...) shd_log(kLogCritical, __FILE__, __FUNCTION__, __LINE__, __VA_ARGS__)
+#define WARNING(...) shd_log(kLogWarning, __FILE__, __FUNCTION__, __LINE__, __VA_ARGS__)
+#define MESSAGE(...) shd_log(kLogMessage, __FILE__, __FUNCTION__, __LINE__, __VA_ARGS__)
+#define INFO(...) shd_log(kLogInfo, __FILE__, __FUNCTION__, __LINE__, __VA_ARGS__)
 
 #define HIPCHK(expr)                                                                        \
     do {                                                                                    \
@@ -139,11 +161,12 @@ struct _Topology {
 
     bool isComplete = false;
     bool isDirected = false;
+    bool isPeer = false;  // a peer engine of a multi-GPU build (make_peer), not a caller's topology
     bool hasMultiEdges = false;
 
-    // options
-    bool abortOnError = true;
-    bool lazy = true;
+    // options ("abort_on_error" and "lazy" are read by getters on worker threads without a lock)
+    std::atomic<bool> abortOnError{true};
+    std::atomic<bool> lazy{true};
     double delta = 0.0;  // 0 = auto
     int slotsOpt = 0;
     int device = 0;
@@ -168,6 +191,13 @@ struct _Topology {
     // device state
     bool devInit = false;
     int devId = 0;               // the device dev_init bound (every later entry re-binds it)
+    int64_t devInits = 0;        // dev_init runs (a "device" change before the first attach
+                                 // re-initialises on the new device)
+    // Device init at topology_new (shd-topology.c:1237): a background thread holding buildMu
+    // initialises the default device (SHDTOPO_DEVICE, else 0) while the GraphML is parsed, so the
+    // first attach and the first build no longer pay the HIP context, queues and code objects.
+    std::thread initThread;
+    double initBgMs = 0.0;       // its wall time
     // Preparation at the first attach (option "prepare_on_attach", default on): a background
     // thread initialises the device and prepares the graph (upload_csr) under buildMu while the
     // host attaches its hosts, so the first table build -- whose lock waits for the thread --
@@ -201,6 +231,9 @@ struct _Topology {
     DevBuf<double> d_elat, d_eloss;
     DevBuf<uint32_t> d_inv;
     int wsK = 0;                // batch width the workspace was laid out for
+    uint32_t wsHubRows = 0;     // rows [0, wsHubRows) of every slot's dist block may hold a
+                                // launch's hub distances (the epilogue copies them there): a
+                                // launch with fewer LDS hubs refills [H, wsHubRows) with +inf
     int64_t wsRing = 0;
     size_t wsHpar = 0;          // hub-hint entries per slot the workspace was sized for
     DevBuf<uint32_t> d_rowptr, d_adj;
@@ -223,6 +256,7 @@ struct _Topology {
     const uint16_t* extHops = nullptr;
     DevBuf<double> d_rowmin;
     DevBuf<double> d_elatAA, d_elossAA, d_vlossA;
+    std::vector<int32_t> aaCols;  // the columns the resident A x A edge matrices were built for
     DevBuf<uint32_t> d_sources, d_targets;
     DevBuf<double> d_srcsh;
     DevBuf<uint8_t> d_mask;
@@ -347,6 +381,11 @@ struct _Topology {
     std::mutex minMu;
     double lazyMin = 0.0;  // top->minimumPathLatency
 
+    // the reference's shortestPathTotalTime / shortestPathCount (shd-topology.c:46-47,792-793),
+    // logged when the topology is freed (:445-446): rows built and the builds' wall time
+    double spTotalSec = 0.0;
+    uint64_t spCount = 0;
+
     // stats
     bool rowsPending = false;  // a launch whose stats have not been read back yet
     bool routePending = false;
@@ -460,12 +499,22 @@ bool check_graph(Topology* top) {
     return true;
 }
 
+extern "C" void topology_free(Topology* top);
+void start_device_init(Topology* top);
+
 Topology* finish_new(Topology* top) {
     if (!check_graph(top)) {
-        delete top;
+        topology_free(top);  // joins the device-init thread, releases the device
         return nullptr;
     }
+    return top;
+}
+
+// a new Topology: its device is SHDTOPO_DEVICE (else 0) unless the "device" option changes it
+Topology* new_topology(bool earlyInit) {
+    Topology* top = new Topology();
     if (const char* d = getenv("SHDTOPO_DEVICE")) top->device = atoi(d);
+    if (earlyInit) start_device_init(top);
     return top;
 }
 
@@ -522,7 +571,43 @@ int dev_init(Topology* top) {
     top->stats.module_load_ms = std::chrono::duration<double, std::milli>(
         std::chrono::steady_clock::now() - t0).count();
     top->devInit = true;
+    top->devInits++;
     return 0;
+}
+
+// Undo dev_init: the "device" option changed after topology_new's background init bound the
+// default device (before the first attach).  The next dev_init binds the new device.
+void dev_release(Topology* top) {
+    if (!top->devInit) return;
+    (void)hipSetDevice(top->devId);
+    (void)hipStreamSynchronize(top->stream);
+    for (hipEvent_t e : {top->ev0, top->ev1, top->ev2, top->ev3, top->evr0, top->evr1})
+        (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(top->stream);
+    top->stream = nullptr;
+    top->ev0 = top->ev1 = top->ev2 = top->ev3 = top->evr0 = top->evr1 = nullptr;
+    top->d_stats.release();
+    top->devInit = false;
+}
+
+// topology_new's background device init (Topology::initThread): the HIP context, the library's
+// stream and events and the kernels' code objects on the default device while the GraphML is
+// parsed (C4: 2.8 s of parsing hide ~150 ms of device init).  Holds buildMu, so an early
+// set_option or build waits for it.  No device present: nothing to do (the first build reports).
+void start_device_init(Topology* top) {
+    if (getenv("SHDTOPO_NO_EARLY_INIT")) return;
+    top->initThread = std::thread([top]() {
+        std::lock_guard<std::mutex> lk(top->buildMu);
+        const auto t0 = std::chrono::steady_clock::now();
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+            (void)hipGetLastError();
+            return;
+        }
+        if (dev_init(top) != 0) (void)hipGetLastError();
+        top->initBgMs = std::chrono::duration<double, std::milli>(
+            std::chrono::steady_clock::now() - t0).count();
+    });
 }
 
 HubSegs hub_segs(Topology* top) {
@@ -844,11 +929,25 @@ int ensure_workspace(Topology* top, int nsrc) {
     HIPCHK(hipStreamSynchronize(top->stream));
     top->slots = want;
     top->wsK = K;
+    top->wsHubRows = 0;  // every row +inf
     top->wsRing = ringE;
     top->wsHpar = hparN;
     top->stats.slots = want;
     top->stats.workspace_ms = std::chrono::duration<double, std::milli>(
         std::chrono::steady_clock::now() - tw0).count();
+    return 0;
+}
+
+// Before a batched launch with H LDS hubs: rows [H, wsHubRows) of every slot's dist block may
+// still hold hub distances an earlier launch with more hubs copied there (its epilogue); this
+// launch treats those vertices as tail vertices, whose lines must start at +inf.
+int hub_rows_ready(Topology* top, uint32_t H, hipStream_t st) {
+    if (H < top->wsHubRows) {
+        const int64_t V = top->g.V, K = top->wsK;
+        HIPCHK(launch_fill_u64_strided(top->d_dist.p + (size_t)H * (size_t)K, 0x7FF0000000000000ull,
+                                       top->slots, V * K, (int64_t)(top->wsHubRows - H) * K, st));
+    }
+    top->wsHubRows = H;
     return 0;
 }
 
@@ -1085,33 +1184,38 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
     HIPCHK(hipMemsetAsync(top->d_stats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
     HIPCHK(launch_fill_u64(top->d_stats.p + ST_GLOBAL_MIN, 0x7FF0000000000000ull, 1, st));
     if (top->isComplete) {
-        // dense A x A direct-edge matrices (lowest edge id wins, as orc_get_eid)
-        std::vector<double> elat((size_t)(A * A), -1.0), eloss((size_t)(A * A), 0.0), vl((size_t)A);
-        const HostGraph& g = top->g;
-        for (int64_t e = 0; e < g.E; e++) {
-            int32_t ca = top->colOf[(size_t)g.eu[(size_t)e]], cb = top->colOf[(size_t)g.ev[(size_t)e]];
-            if (ca < 0 || cb < 0) continue;
-            size_t k1 = (size_t)ca * (size_t)A + (size_t)cb;
-            if (elat[k1] < 0) { elat[k1] = g.elat[(size_t)e]; eloss[k1] = g.eloss[(size_t)e]; }
-            if (!g.directed) {
-                size_t k2 = (size_t)cb * (size_t)A + (size_t)ca;
-                if (elat[k2] < 0) { elat[k2] = g.elat[(size_t)e]; eloss[k2] = g.eloss[(size_t)e]; }
+        // dense A x A direct-edge matrices (lowest edge id wins, as orc_get_eid), resident in HBM
+        // while the columns stay: rebuilt only when the attached set changed
+        if (top->aaCols != top->attached || !top->d_elatAA.p || !top->d_vlossA.p) {
+            std::vector<double> elat((size_t)(A * A), -1.0), eloss((size_t)(A * A), 0.0), vl((size_t)A);
+            const HostGraph& g = top->g;
+            for (int64_t e = 0; e < g.E; e++) {
+                int32_t ca = top->colOf[(size_t)g.eu[(size_t)e]], cb = top->colOf[(size_t)g.ev[(size_t)e]];
+                if (ca < 0 || cb < 0) continue;
+                size_t k1 = (size_t)ca * (size_t)A + (size_t)cb;
+                if (elat[k1] < 0) { elat[k1] = g.elat[(size_t)e]; eloss[k1] = g.eloss[(size_t)e]; }
+                if (!g.directed) {
+                    size_t k2 = (size_t)cb * (size_t)A + (size_t)ca;
+                    if (elat[k2] < 0) { elat[k2] = g.elat[(size_t)e]; eloss[k2] = g.eloss[(size_t)e]; }
+                }
             }
+            for (int64_t i = 0; i < A; i++) vl[(size_t)i] = g.vloss[(size_t)top->attached[(size_t)i]];
+            HIPCHK(top->d_elatAA.ensure((size_t)(A * A)));
+            HIPCHK(top->d_elossAA.ensure((size_t)(A * A)));
+            HIPCHK(top->d_vlossA.ensure((size_t)A));
+            HIPCHK(hipMemcpyAsync(top->d_elatAA.p, elat.data(), sizeof(double) * (size_t)(A * A), hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(top->d_elossAA.p, eloss.data(), sizeof(double) * (size_t)(A * A), hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(top->d_vlossA.p, vl.data(), sizeof(double) * (size_t)A, hipMemcpyHostToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));  // the host vectors must outlive the async copies
+            top->aaCols = top->attached;
+            top->stats.pair_matrix_builds++;
         }
-        for (int64_t i = 0; i < A; i++) vl[(size_t)i] = g.vloss[(size_t)top->attached[(size_t)i]];
-        HIPCHK(top->d_elatAA.ensure((size_t)(A * A)));
-        HIPCHK(top->d_elossAA.ensure((size_t)(A * A)));
-        HIPCHK(top->d_vlossA.ensure((size_t)A));
-        HIPCHK(hipMemcpyAsync(top->d_elatAA.p, elat.data(), sizeof(double) * (size_t)(A * A), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(top->d_elossAA.p, eloss.data(), sizeof(double) * (size_t)(A * A), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(top->d_vlossA.p, vl.data(), sizeof(double) * (size_t)A, hipMemcpyHostToDevice, st));
+        // one launch: records, hops, row minima and the global minimum
         HIPCHK(hipEventRecord(top->ev0, st));
         HIPCHK(launch_pair_table_complete((int)A, row0, rows, top->d_elatAA.p, top->d_elossAA.p,
                                           top->d_vlossA.p, out_lr, out_hops, out_rowmin,
                                           top->d_stats.p, st));
         HIPCHK(hipEventRecord(top->ev1, st));
-        // the host vectors must outlive the async copies
-        HIPCHK(hipStreamSynchronize(st));
     } else {
         int r = upload_csr(top);
         if (r) return r;
@@ -1227,6 +1331,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     const SsspLdsPlan bp = sssp_batch_lds_plan(
                         K, top->hubLimit, (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 20)),
                         top->g.V);
+                    r = hub_rows_ready(top, bp.H, st);
+                    if (r) return r;
                     HIPCHK(launch_sssp_batch(K, dev_csr(top), pws, top->d_probeSrc.p, top->d_probeSh.p,
                                              (int)P, K, top->d_targets.p, (int)A, delta, bp,
                                              top->iterGuard, out_lr, out_hops, out_rowmin,
@@ -1419,6 +1525,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     K, top->hubLimit, (uint32_t)std::max<int64_t>(0, std::min<int64_t>(top->parHubs, 1 << 20)),
                     top->g.V);
                 top->stats.lds_hubs = bp.H;
+                r = hub_rows_ready(top, bp.H, st);
+                if (r) return r;
                 // diagnostic: SHD_BATCH_TRACE=<file> appends per batch {start tick, end tick,
                 // slot, near iterations, sweeps, expansions, relaxations, sources}, then per
                 // batch position {source vertex, pi bits}
@@ -1660,9 +1768,10 @@ Topology* make_peer(Topology* top, int phys) {
     p->isComplete = top->isComplete;
     p->isDirected = top->isDirected;
     p->hasMultiEdges = top->hasMultiEdges;
-    p->abortOnError = top->abortOnError;
+    p->abortOnError = top->abortOnError.load();
     p->lazy = false;
     p->device = phys;
+    p->isPeer = true;
     return p;
 }
 
@@ -1823,10 +1932,12 @@ int build_multi(Topology* top) {
     }
     // 1) rows, one host thread per device
     std::vector<int> rc(N, 0);
+    std::vector<double> dwall((size_t)N, 0.0);
     std::vector<std::thread> th;
     for (int d = 0; d < N; d++)
         th.emplace_back([&, d]() {
             Topology* T = slot_engine(top, d);
+            const auto tw = std::chrono::steady_clock::now();
             auto run = [&]() -> int {
                 HIPCHK(hipSetDevice(phys[(size_t)d]));
                 int r = dev_init(T);
@@ -1849,6 +1960,8 @@ int build_multi(Topology* top) {
                 return 0;
             };
             rc[(size_t)d] = run();
+            dwall[(size_t)d] = std::chrono::duration<double, std::milli>(
+                std::chrono::steady_clock::now() - tw).count();
         });
     for (auto& x : th) x.join();
     for (int d = 0; d < N; d++)
@@ -1926,6 +2039,16 @@ int build_multi(Topology* top) {
     memcpy(&g, &gm, 8);
     top->eagerMin = std::isinf(g) ? -1.0 : g;
     // whole-job statistics: the slowest device's kernels, every device's counts
+    for (int d = 0; d < 8; d++) {
+        top->stats.device_kernel_ms[d] = top->stats.device_build_ms[d] = 0.0;
+        top->stats.device_rows[d] = 0;
+    }
+    for (int d = 0; d < std::min(N, 8); d++) {
+        const int64_t r0 = std::min(A, d * R), r1 = std::min(A, r0 + R);
+        top->stats.device_kernel_ms[d] = r1 > r0 ? slot_engine(top, d)->stats.build_ms : 0.0;
+        top->stats.device_build_ms[d] = dwall[(size_t)d];
+        top->stats.device_rows[d] = r1 - r0;
+    }
     top->stats.devices = N;
     top->stats.sources = A;
     for (int d = 1; d < N; d++) {
@@ -2006,6 +2129,8 @@ int ensure_table(Topology* top) {
     top->stats.csr_host_runs_total = runs1;
     top->stats.build_wall_ms = std::chrono::duration<double, std::milli>(
         std::chrono::steady_clock::now() - tb0).count();
+    top->spTotalSec += top->stats.build_wall_ms / 1e3;
+    top->spCount += (uint64_t)A;
     top->tableGen.store(sg, std::memory_order_release);
     top->tableSerial.fetch_add(1);
     top->tableValid.store(true, std::memory_order_release);
@@ -2122,6 +2247,43 @@ void lazy_materialise(Topology* top, int32_t s, double rowmin) {
     if (rowmin > 0 && !std::isinf(rowmin)) lazy_store_min(top, rowmin);
 }
 
+const double2* tab_lr(const Topology* top);
+
+// The minimum of row s over the vertices attached NOW (shd-topology.c:690-744 take the targets
+// attached at the moment the row is computed).  The table's row minimum also covers the columns a
+// window adapter keeps for vertices that lost their last host (deferredOff, until the flush): while
+// such a column exists, the row is read (host snapshot, or one row from the device table -- the
+// caller holds buildMu there) and those columns are left out.
+double lazy_row_min(Topology* top, const HostTable& h, int32_t s) {
+    const int64_t cs = h.colOf[(size_t)s];
+    std::vector<int32_t> gone;
+    {
+        std::shared_lock<std::shared_mutex> lk(top->ipMu);
+        for (int32_t v : top->deferredOff)
+            if (top->hostsOn[(size_t)v] == 0) gone.push_back(v);
+    }
+    if (gone.empty()) return h.rowmin[(size_t)cs];
+    const int64_t A = h.A;
+    std::vector<double> lat((size_t)A);
+    if (h.full) {
+        for (int64_t c = 0; c < A; c++) lat[(size_t)c] = h.lat[(size_t)(cs * A + c)];
+    } else {
+        std::vector<double2> lr((size_t)A);
+        if (hipMemcpy(lr.data(), tab_lr(top) + cs * A, sizeof(double2) * (size_t)A,
+                      hipMemcpyDeviceToHost) != hipSuccess)
+            return h.rowmin[(size_t)cs];
+        for (int64_t c = 0; c < A; c++) lat[(size_t)c] = lr[(size_t)c].x;
+    }
+    for (int32_t v : gone) {
+        const int32_t c = h.colOf[(size_t)v];
+        if (c >= 0 && c < A) lat[(size_t)c] = -1.0;
+    }
+    double m = INFINITY;
+    for (double x : lat)
+        if (x >= 0 && x < m) m = x;
+    return m;
+}
+
 // First-rooted-wins orientation of the SSSP branch (shd-topology.c:894-915):
 // (s,d) is answered from row s if the cache holds (s,d), else from row d if it holds (d,s) and
 // the graph is undirected, else s's row is computed now.  Returns true when the answer comes
@@ -2129,7 +2291,7 @@ void lazy_materialise(Topology* top, int32_t s, double rowmin) {
 bool lazy_orient_row(Topology* top, const HostTable& h, int32_t s, int32_t d) {
     if (lazy_covered(top, s, d)) return false;
     if (!top->isDirected && lazy_covered(top, d, s)) return true;
-    lazy_materialise(top, s, h.rowmin[(size_t)h.colOf[(size_t)s]]);
+    lazy_materialise(top, s, lazy_row_min(top, h, s));
     return false;
 }
 
@@ -2373,13 +2535,13 @@ int shdtopo_version(void) { return 10000; }
 
 Topology* topology_new(const char* graphPath) {
     if (!graphPath) return nullptr;
-    Topology* top = new Topology();
+    Topology* top = new_topology(true);  // the device initialises while the file is parsed
     std::string err;
     MESSAGE("reading graphml topology graph at '%s'...", graphPath);
     const auto t0 = std::chrono::steady_clock::now();
     if (!graphml_load_file(graphPath, top->g, err)) {
         CRITICAL("reading graphml topology '%s' failed: %s", graphPath, err.c_str());
-        delete top;
+        topology_free(top);
         return nullptr;
     }
     const auto t1 = std::chrono::steady_clock::now();
@@ -2392,11 +2554,11 @@ Topology* topology_new(const char* graphPath) {
 
 Topology* shdtopo_new_from_buffer(const char* graphml, size_t len) {
     if (!graphml) return nullptr;
-    Topology* top = new Topology();
+    Topology* top = new_topology(true);
     std::string err;
     if (!graphml_parse(graphml, len, top->g, err)) {
         CRITICAL("parsing graphml buffer failed: %s", err.c_str());
-        delete top;
+        topology_free(top);
         return nullptr;
     }
     return finish_new(top);
@@ -2404,13 +2566,13 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len) {
 
 Topology* shdtopo_new_synthetic(const ShdSynthParams* p) {
     if (!p) return nullptr;
-    Topology* top = new Topology();
+    Topology* top = new_topology(false);  // a generator (tools): no device until it is used
     SynthParams sp{p->seed, p->n_routers, p->n_poi, p->n_edges, p->integer_latency,
                    p->alpha > 0 ? p->alpha : 1.0 / 1.1};
     std::string err;
     if (!synth_graph(sp, top->g, err)) {
         CRITICAL("synthetic topology: %s", err.c_str());
-        delete top;
+        topology_free(top);
         return nullptr;
     }
     return finish_new(top);
@@ -2418,7 +2580,12 @@ Topology* shdtopo_new_synthetic(const ShdSynthParams* p) {
 
 void topology_free(Topology* top) {
     if (!top) return;
+    if (top->initThread.joinable()) top->initThread.join();
     if (top->prepThread.joinable()) top->prepThread.join();
+    // _topology_clearCache (shd-topology.c:434-447): the reference reports its Dijkstra total here
+    if (top->g.V > 0 && !top->isPeer)
+        MESSAGE("path cache cleared, spent %f seconds computing %u shortest paths",
+                top->spTotalSec, (unsigned)top->spCount);
     for (Topology* p : top->peers) topology_free(p);
     top->peers.clear();
     if (!top->comms.empty() && rccl().ok)
@@ -2440,16 +2607,25 @@ void topology_free(Topology* top) {
 int shdtopo_set_option(Topology* top, const char* key, double value) {
     if (!top || !key) return -1;
     std::string k(key);
-    // the attach-time preparation thread and the builders read the options under buildMu
+    // flags the getters read on worker threads (atomics): no lock, so they never wait for the
+    // attach-time preparation or a build
+    if (k == "abort_on_error") { top->abortOnError = value != 0; return 0; }
+    if (k == "lazy") { top->lazy = value != 0; return 0; }
+    // the device-init and attach-time preparation threads and the builders read the rest under
+    // buildMu
     std::lock_guard<std::mutex> lk(top->buildMu);
-    if (k == "abort_on_error") top->abortOnError = value != 0;
-    else if (k == "lazy") top->lazy = value != 0;
-    else if (k == "delta") top->delta = value;
+    if (k == "delta") top->delta = value;
     else if (k == "slots") top->slotsOpt = (int)value;
     else if (k == "device") {
-        // the device is fixed once the attach-time preparation (or a build) initialised it
-        if ((top->prepStarted.load() || top->devInit) && (int)value != top->device) return -1;
-        top->device = (int)value;
+        const int d = (int)value;
+        if (d < 0) return -1;
+        if (d != top->device) {
+            // fixed once the attach-time preparation (or a build) uses it; before that, a device
+            // bound by topology_new's background init is released and the next use binds d
+            if (top->prepStarted.load() || top->csrUploaded || top->tableValid.load()) return -1;
+            dev_release(top);
+            top->device = d;
+        }
     }
     else if (k == "prepare_on_attach") top->prepOnAttach = value != 0;
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
@@ -2632,10 +2808,16 @@ int shdtopo_build_rows(Topology* top, int64_t row0, int64_t row1, void* d_lr, vo
             top->extHops = nullptr;
         }
     }
+    const auto tr0 = std::chrono::steady_clock::now();
     r = enqueue_rows(top, row0, row1, (double2*)d_lr, (uint16_t*)d_hops, (double*)d_rowmin, st);
     if (r) return r;
     top->stats.csr_host_runs = top->csrHostRuns - runs0;
-    return collect_row_stats(top);
+    r = collect_row_stats(top);
+    top->stats.build_wall_ms = std::chrono::duration<double, std::milli>(
+        std::chrono::steady_clock::now() - tr0).count();
+    top->spTotalSec += top->stats.build_wall_ms / 1e3;
+    top->spCount += (uint64_t)(row1 - row0);
+    return r;
 }
 
 int shdtopo_bind_table(Topology* top, const void* d_lr, const void* d_hops, double globalMin,
@@ -2910,6 +3092,10 @@ int shdtopo_get_stats(Topology* top, ShdStats* out) {
         top->stats.route_bad_packets = (int64_t)nb;
         top->routePending = false;
     }
+    top->stats.dev_inits = top->devInits;
+    top->stats.init_bg_ms = top->initBgMs;
+    top->stats.path_seconds_total = top->spTotalSec;
+    top->stats.paths_computed = (int64_t)top->spCount;
     *out = top->stats;
     return 0;
 }
@@ -3048,10 +3234,12 @@ int shdtopo_synth_packets(Topology* top, uint64_t seed, int64_t n_hosts, int64_t
     // takes no build lock, so any wait for the attach-time preparation shows in the build
     std::vector<int32_t> cols;
     {
+        // as compute_geometry: the attached vertices plus the columns a window adapter keeps
         std::shared_lock<std::shared_mutex> lk(top->ipMu);
-        cols.reserve(top->virtualIP.size());
+        cols.reserve(top->virtualIP.size() + top->deferredOff.size());
         for (auto& kv : top->virtualIP)
             if (kv.second >= 0) cols.push_back(kv.second);
+        cols.insert(cols.end(), top->deferredOff.begin(), top->deferredOff.end());
     }
     std::sort(cols.begin(), cols.end());
     cols.erase(std::unique(cols.begin(), cols.end()), cols.end());

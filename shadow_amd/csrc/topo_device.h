@@ -275,6 +275,9 @@ hipError_t launch_row_min(int64_t rows, int64_t A, const double2* lr, double* ou
 
 hipError_t launch_fill_u64(unsigned long long* p, unsigned long long v, int64_t n,
                            hipStream_t stream);
+// p[b * stride + i] = v for b < nb, i < n
+hipError_t launch_fill_u64_strided(unsigned long long* p, unsigned long long v, int64_t nb,
+                                   int64_t stride, int64_t n, hipStream_t stream);
 
 // ---- graph preparation on the GPU (topo_prep.hip), once per topology: DESIGN.md 3.1 ----
 // Input arrays are the parsed graph in HBM (document order: eu / ev int32[E], elat / eloss f64[E],

@@ -22,50 +22,67 @@ namespace shdtopo {
 using namespace dev;
 
 // ------------------------------------------------------------------------------------------
-// complete graphs: _topology_lookupPath (shd-topology.c:835-873) for every attached pair.
-// 34 B of HBM traffic per pair (8 B lat + 8 B loss read, 16 B record + 2 B hops written).
+// complete graphs: _topology_lookupPath (shd-topology.c:835-873) for every attached pair, and the
+// row minima (the runahead bookkeeping, shd-topology.c:500-511) in the same launch: one workgroup
+// per row (grid-stride over rows), the row's records written coalesced, its minimum reduced in
+// LDS.  34 B of HBM traffic per pair (8 B lat + 8 B loss read, 16 B record + 2 B hops written).
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
 pair_table_complete_kernel(int A, int64_t row0, int64_t rows, const double* __restrict__ elatAA,
                            const double* __restrict__ elossAA, const double* __restrict__ vlossA,
                            double2* __restrict__ out_lr, uint16_t* __restrict__ out_hops,
                            double* __restrict__ out_rowmin, unsigned long long* __restrict__ stats) {
-    const int64_t total = rows * (int64_t)A;
-    unsigned long long m = kInfBits;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
-         k += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = k / A;
-        const int64_t c = k - r * A;
+    __shared__ unsigned long long sm[4];
+    unsigned long long gm = kInfBits;
+    uint32_t nerr = 0;
+    for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
         const int64_t i = row0 + r;
-        const double el = elatAA[i * A + c];
-        double lat, rel;
-        if (el < 0.0) {  // no edge between the pair: igraph_get_eid fails (shd-topology.c:857)
-            atomicAdd(&stats[ST_ERRORS], 1ull);
-            lat = -1.0;
-            rel = -1.0;
-        } else {
-            rel = 1.0;
-            rel *= (1.0 - vlossA[i]);
-            rel *= (1.0 - vlossA[c]);
-            lat = 0.0;
-            lat += el;
-            rel *= (1.0 - elossAA[i * A + c]);
-            unsigned long long b = d2bits(lat);
-            m = b < m ? b : m;
+        const double vi = vlossA[i];
+        unsigned long long m = kInfBits;
+        for (int c = (int)threadIdx.x; c < A; c += 256) {
+            const double el = elatAA[i * A + c];
+            double lat, rel;
+            if (el < 0.0) {  // no edge between the pair: igraph_get_eid fails (shd-topology.c:857)
+                nerr++;
+                lat = -1.0;
+                rel = -1.0;
+            } else {
+                rel = 1.0;
+                rel *= (1.0 - vi);
+                rel *= (1.0 - vlossA[c]);
+                lat = 0.0;
+                lat += el;
+                rel *= (1.0 - elossAA[i * A + c]);
+                const unsigned long long b = d2bits(lat);
+                m = b < m ? b : m;
+            }
+            const int64_t k = r * (int64_t)A + c;
+            out_lr[k] = make_double2(lat, rel);
+            out_hops[k] = 1;
         }
-        out_lr[k] = make_double2(lat, rel);
-        out_hops[k] = 1;
-    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long y = __shfl_xor(m, o, 64);
-        m = y < m ? y : m;
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long y = __shfl_xor(m, o, 64);
+            m = y < m ? y : m;
+        }
+        if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long x = sm[0];
+#pragma unroll
+            for (int w = 1; w < 4; w++) x = sm[w] < x ? sm[w] : x;
+            if (out_rowmin) out_rowmin[r] = bits2d(x);
+            gm = x < gm ? x : gm;
+        }
+        __syncthreads();
     }
-    if ((threadIdx.x & 63) == 0 && m != kInfBits) atomicMin(&stats[ST_GLOBAL_MIN], m);
-    (void)out_rowmin;
+    if (threadIdx.x == 0 && gm != kInfBits) atomicMin(&stats[ST_GLOBAL_MIN], gm);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nerr += __shfl_xor(nerr, o, 64);
+    if ((threadIdx.x & 63) == 0 && nerr) atomicAdd(&stats[ST_ERRORS], (unsigned long long)nerr);
 }
 
-// per-row minimum for the complete table (lazy-runahead bookkeeping)
+// per-row minimum of an installed table (shdtopo_bind_table*: the lazy-runahead bookkeeping)
 __global__ void row_min_kernel(int64_t rows, int64_t A, const double2* __restrict__ lr,
                                double* __restrict__ out_rowmin) {
     const int64_t r = blockIdx.x;
@@ -171,6 +188,17 @@ __global__ void fill_u64_kernel(unsigned long long* p, unsigned long long v, int
         p[k] = v;
 }
 
+// p[b * stride + i] = v for b < nb, i < n (the same window of every slot's block)
+__global__ void fill_u64_strided_kernel(unsigned long long* p, unsigned long long v, int64_t nb,
+                                        int64_t stride, int64_t n) {
+    const int64_t tot = nb * n;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = k / n;
+        p[b * stride + (k - b * n)] = v;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
@@ -186,13 +214,11 @@ hipError_t launch_pair_table_complete(int A, int64_t row0, int64_t rows, const d
                                       uint16_t* out_hops, double* out_rowmin,
                                       unsigned long long* d_stats, hipStream_t stream) {
     if (rows <= 0 || A <= 0) return hipSuccess;
-    hipLaunchKernelGGL(pair_table_complete_kernel, dim3(grid_for(rows * A, 256)), dim3(256), 0,
-                       stream, A, row0, rows, elatAA, elossAA, vlossA, out_lr, out_hops,
-                       out_rowmin, d_stats);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !out_rowmin) return e;
-    hipLaunchKernelGGL(row_min_kernel, dim3((unsigned)rows), dim3(256), 0, stream, rows,
-                       (int64_t)A, out_lr, out_rowmin);
+    // one workgroup per row (a single launch: records, hops, row minima, global minimum)
+    const int64_t g = rows < 256 * 16 ? rows : 256 * 16;
+    hipLaunchKernelGGL(pair_table_complete_kernel, dim3((unsigned)g), dim3(256), 0, stream, A,
+                       row0, rows, elatAA, elossAA, vlossA, out_lr, out_hops, out_rowmin,
+                       d_stats);
     return hipGetLastError();
 }
 
@@ -222,6 +248,14 @@ hipError_t launch_fill_u64(unsigned long long* p, unsigned long long v, int64_t 
                            hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(fill_u64_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, p, v, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_u64_strided(unsigned long long* p, unsigned long long v, int64_t nb,
+                                   int64_t stride, int64_t n, hipStream_t stream) {
+    if (nb <= 0 || n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(fill_u64_strided_kernel, dim3(grid_for(nb * n, 256)), dim3(256), 0, stream,
+                       p, v, nb, stride, n);
     return hipGetLastError();
 }
 

@@ -192,3 +192,25 @@ def test_synth_packets_seed_chain_and_host_streams():
     assert np.all(pk["src_ip"] != pk["dst_ip"])
     assert 0.75 < (pk["payload"] > 0).mean() < 0.85
     assert np.all((pk["now"] >= 10**9) & (pk["now"] < 10**9 + 5_000_000))
+
+
+def test_device_option_fixed_once_the_attach_time_preparation_starts():
+    """The "device" option (shdtopo_set_option): before the first attach it may move the topology
+    to another device (topology_new's background init is released); once the first attach started
+    the attach-time preparation on a device, another device is refused (-1 -> KeyError) and the
+    same device is accepted.  "abort_on_error" / "lazy" are lock-free flags."""
+    top = sa.Topology.from_buffer(bundled_topology("topology.plab"))
+    top.set_option("device", 3)
+    top.set_option("device", 0)
+    top.set_option("lazy", 1)
+    top.set_option("abort_on_error", 0)
+    # plab is complete: no attach-time preparation, so attach a synthetic (SSSP) topology instead
+    syn = sa.Topology.synthetic(seed=3, n_routers=200, n_poi=20, n_edges=2000)
+    syn.set_option("device", 2)
+    syn.attach_ip(1, 5, typeHint="client")
+    with pytest.raises(KeyError):
+        syn.set_option("device", 1)
+    syn.set_option("device", 2)
+    syn.set_option("lazy", 0)
+    with pytest.raises(KeyError):
+        syn.set_option("device", -1)

@@ -512,3 +512,59 @@ def test_sssp_batch_peripheral_landmark(hubs):
     assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(hops, ohops.astype(np.uint16))
     assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+
+
+def test_lds_hubs_lowered_between_builds():
+    """a launch copies its hub distances into rows [0, H) of every slot's [V][K] block
+    (the epilogue).  A later launch with fewer LDS hubs treats vertices [H', H) as tail vertices,
+    whose lines must start at +inf: the library refills them before such a launch.  Build with
+    every hub in LDS, lower lds_hubs (two steps), rebuild: every table equals the oracle's."""
+    top, g = synthetic_pair(seed=13, n_routers=3000, n_poi=150, n_edges=30000)
+    top.set_option("batch_fill", 8)
+    top.set_option("slots", 4)  # few slots: every slot's block serves several batches
+    otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay", "server"])
+    oa, olat, orel, ohops = g.table(verts)
+    seen = []
+    for hubs in (-1, 600, 0):
+        top.set_option("lds_hubs", hubs)
+        top.rebuild()
+        a, lat, rel, hops = top.table()
+        st = top.stats()
+        seen.append(st["lds_hubs"])
+        assert st["errors"] == 0
+        assert np.array_equal(a, oa)
+        assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+        assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+        assert np.array_equal(hops, ohops.astype(np.uint16))
+    assert seen[0] > seen[1] > seen[2] == 0
+
+
+def test_device_option_after_topology_new_builds_on_that_device(tmp_path):
+    """topology_new initialises the default device in the background while it parses (the HIP
+    context, queues and code objects: ~150 ms off the first build).  Setting "device" before the
+    first attach releases that init and the next use initialises the chosen device (on the
+    one-GPU test box every ordinal maps to device 0, so the move is observed by the second
+    initialisation); the table built there equals the oracle's."""
+    import time
+    import torch
+    syn = sa.Topology.synthetic(seed=19, n_routers=2000, n_poi=100, n_edges=20000)
+    path = str(tmp_path / "t.graphml.xml")
+    syn.write_graphml(path)
+    syn.free()
+    top = sa.Topology.new(path)
+    g = oracle.OGraph.from_graphml(path)
+    t0 = time.time()
+    while top.stats()["dev_inits"] < 1 and time.time() - t0 < 60:
+        time.sleep(0.05)
+    assert top.stats()["dev_inits"] == 1 and top.stats()["init_bg_ms"] > 0
+    top.set_option("device", torch.cuda.device_count())  # another ordinal (maps to 0 here)
+    otop, ips, verts = attach_hosts(top, g, 200, type_hints=["client", "relay"])
+    with pytest.raises(KeyError):
+        top.set_option("device", 0 if torch.cuda.device_count() > 1 else 1 + torch.cuda.device_count())
+    a, lat, rel, hops = top.table()
+    assert top.stats()["dev_inits"] == 2
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(a, oa)
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))

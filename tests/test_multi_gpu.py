@@ -166,3 +166,44 @@ def test_multi_device_default_attach_prep_prepares_once(devices):
     assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
     assert np.array_equal(hops, ohops.astype(np.uint16))
     assert top.getMinimumLatency() == olat.min()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["topology", "topology.plab"])
+@pytest.mark.parametrize("devices", [8])
+def test_complete_branch_devices8_equals_oracle(name, devices):
+    """BASELINE config 3 ("all-pairs table on 8 MI355X") through the library's multi-device build:
+    the complete branch's rows sharded over 8 engines (C3: 183 rows -> 23 per engine, the last one
+    short), each engine's pair_table_complete_kernel, the row exchange and the all-reduce of the
+    minimum (device copies: the test box's engines share one GPU).  One host per vertex by its
+    unique geocode; every pair bit-exact against _topology_lookupPath's
+    restatement, the runahead minimum too (shd-master.c:113-124 consumes it)."""
+    from helpers import bundled_pair
+    top, g = bundled_pair(name)
+    assert top.is_complete
+    top.set_option("devices", devices)
+    geos = list(g.vattrs["geocode"])
+    assert len(set(geos)) == len(geos)
+    otop, ips, verts = attach_hosts(top, g, g.V, geo_hints=geos)
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    A = len(a)
+    assert st["devices"] == devices and st["errors"] == 0 and A == g.V
+    R = -(-A // devices)
+    assert st["device_rows"][:devices] == [max(0, min(A, (d + 1) * R) - min(A, d * R))
+                                           for d in range(devices)]
+    assert all(st["device_kernel_ms"][d] > 0 for d in range(devices) if st["device_rows"][d])
+    assert st["exchange_bytes"] == (devices - 1) * R * (A * 18 + 8)
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(a, oa)
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.all(hops == 1)
+    assert top.getMinimumLatency() == olat.min()
+    # a rebuild reuses the resident edge matrices of every engine (same attached set)
+    nb = st["pair_matrix_builds"]
+    top.rebuild()
+    assert top.stats()["pair_matrix_builds"] == nb
+    a2, lat2, rel2, _ = top.table()
+    assert np.array_equal(lat2.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel2.view(np.uint64), orel.view(np.uint64))

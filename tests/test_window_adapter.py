@@ -142,3 +142,92 @@ def test_window_routes_packets_of_a_host_detached_before_the_flush():
     # after the flush the vertex is no longer a column
     assert len(top.attached_vertices()) == A0 - 1
     lib.topowindow_free(w)
+
+
+def _near_pair_graphml():
+    """A ring of 16 routers (10 ms links) and 12 poi with distinct geocodes: poi 2j and 2j + 1
+    share router j (1 ms uplinks, so they are 2 ms apart) and have 100-ms self loops, so a poi's
+    nearest attached vertex is its twin, not itself."""
+    keys = ('<key attr.name="packetloss" attr.type="double" for="edge" id="d9" />'
+            '<key attr.name="latency" attr.type="double" for="edge" id="d7" />'
+            '<key attr.name="type" attr.type="string" for="node" id="d5" />'
+            '<key attr.name="geocode" attr.type="string" for="node" id="d2" />'
+            '<key attr.name="ip" attr.type="string" for="node" id="d1" />'
+            '<key attr.name="packetloss" attr.type="double" for="node" id="d0" />')
+    out = ['<?xml version="1.0" encoding="utf-8"?><graphml '
+           'xmlns="http://graphml.graphdrawing.org/xmlns">', keys,
+           '<graph edgedefault="undirected">']
+    for i in range(16):
+        out.append('<node id="r%d"><data key="d0">0.0</data><data key="d1">0.0.0.0</data>'
+                   '<data key="d2">XX</data><data key="d5">pop</data></node>' % i)
+    for k in range(12):
+        out.append('<node id="poi-%d"><data key="d0">0.001</data><data key="d1">0.0.0.0</data>'
+                   '<data key="d2">G%d</data><data key="d5">client</data></node>' % (k, k))
+    for i in range(16):
+        out.append('<edge source="r%d" target="r%d"><data key="d7">10.0</data>'
+                   '<data key="d9">0.0</data></edge>' % (i, (i + 1) % 16))
+    for k in range(12):
+        out.append('<edge source="poi-%d" target="r%d"><data key="d7">%r</data>'
+                   '<data key="d9">0.001</data></edge>' % (k, k // 2, 1.0 + 0.01 * k))
+        out.append('<edge source="poi-%d" target="poi-%d"><data key="d7">100.0</data>'
+                   '<data key="d9">0.0</data></edge>' % (k, k))
+    out.append("</graph></graphml>")
+    return "".join(out).encode()
+
+
+def test_window_lazy_minimum_excludes_a_column_detached_in_the_window():
+    """a vertex that loses its last host inside a window keeps its table column until
+    the flush, but a source row first computed after the detach must take its minimum over the
+    vertices attached at that moment (shd-topology.c:690-744), as the reference's row does.  Here
+    the detached poi is the twin (2.01 ms away) of the later source, whose other entries are >= 20
+    ms, and the only other computed row's minimum is 2.13 ms (X's twin): the running minimum must
+    stay the reference's 2.13, not drop to 2.01."""
+    data = _near_pair_graphml()
+    top = sa.Topology.from_buffer(data)
+    g = oracle.OGraph.from_graphml(data)
+    lib, shim = _lib.load()
+    otop = oracle.OracleTopology(g)
+    hosts = []
+    st = 3
+    for k in range(12):  # one host per poi (geocode hint)
+        st = (st * 1103515245 + 12345) & 0xFFFFFFFF
+        ip = host_ip(k + 1)
+        v1, s1 = top.attach_ip(ip, st, geocodeHint="G%d" % k)
+        v2, s2 = otop.attach(ip, st, geocode_hint="G%d" % k)
+        assert v1 == v2 and s1 == s2
+        hosts.append((ip, sa.Address(ip), sa.Random(s1)))
+    L, S, X, D = 0, 1, 6, 8  # L and S are twins; X, D elsewhere on the ring
+    w = lib.topowindow_new(top._h)
+    jump = lib.topowindow_jump_ns(top._h, 0)
+    got = {}
+
+    @_lib.WINDOW_DELIVER
+    def deliver(ctx, packet, delivered, time):
+        got[int(packet)] = (delivered, time)
+
+    ref_state = [h[2].state for h in hosts]
+    ref = []
+    t0 = 10**9
+
+    def emit(k, s, d):
+        now = t0 + 1000 * k
+        rel = otop.get_reliability(hosts[s][0], hosts[d][0])
+        r, ref_state[s] = oracle.next_double(ref_state[s])
+        dl = r <= rel
+        t = max(now + int(math.ceil(otop.get_latency(hosts[s][0], hosts[d][0]) * 1e6)),
+                now + jump) if dl else 0
+        ref.append((int(dl), t))
+        assert lib.topowindow_emit(w, hosts[s][1]._p, hosts[d][1]._p, 1448, hosts[s][2]._p, now,
+                                   k + 1) == k
+
+    emit(0, X, L)  # row X (all 12 columns, L's included) enters the cache
+    emit(1, L, X)  # answered from row X: row L is never computed
+    top.detach_ip(hosts[L][0])
+    otop.detach(hosts[L][0])
+    emit(2, S, D)  # row S computed now, over the 11 vertices still attached
+    assert lib.topowindow_flush(w, jump, 1, deliver, None) == 0
+    assert [got[k + 1] for k in range(len(ref))] == ref
+    # the reference's running minimum: row X's and row S's (without L's twin column)
+    assert otop.minimum_path_latency > 2.1
+    assert top.lazyMinimumLatency() == otop.minimum_path_latency
+    lib.topowindow_free(w)
