@@ -122,7 +122,9 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * in the same rounds of the slots), "source_order" / "batch_order" (row grouping and batch
  * dequeue order), "target_skip" (1: the batch relaxation drops pairs into
  * non-target vertices that would relax nothing reaching a target), "target_kappa" (iterations of
- * the target-aware kappa fixpoint behind that test, 0 = the row's smallest kappa; default 6).
+ * the target-aware kappa fixpoint behind that test, 0 = the row's smallest kappa; default 6),
+ * "share" (1: a batched launch's workgroups that run out of batches take part in the running
+ * batches' parent walks and epilogues -- the help board; 0: each batch stays in its workgroup).
  * Returns 0 or -1 for an unknown key / bad value. */
 int shdtopo_set_option(Topology* top, const char* key, double value);
 
@@ -351,6 +353,11 @@ typedef struct {
                                    seconds of every table / row build so far */
     int64_t paths_computed;     /* shortestPathCount (shd-topology.c:793): source rows built so far;
                                    both are logged at topology_free (:445-446) */
+    double help_ms;             /* the last batched launch (option "share"): wall time summed over
+                                   the workgroups that, out of batches, took part in other slots'
+                                   jobs (parent walks, epilogues) */
+    int64_t help_items[2];      /*   the items they took: walk start pairs, epilogue items */
+    int64_t help_board_errors;  /*   help-board spin limits hit (cannot happen; the build fails) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -247,6 +247,11 @@ struct _Topology {
     DevBuf<uint4> d_prec;  // per (vertex, source) pair records of the parent pass
     DevBuf<double> d_pathbuf;
     DevBuf<uint32_t> d_cnt, d_bslot, d_counters;
+    // help board of the batched launches (SlotWs.board): kBoardWords per slot + 1, zeroed before
+    // every launch; option "share" (default on): idle workgroups take part in the running
+    // batches' parent walks and epilogues
+    DevBuf<uint32_t> d_board;
+    bool share = true;
     int slots = 0;
     DevBuf<double2> d_lr;
     DevBuf<uint16_t> d_hops;
@@ -876,7 +881,7 @@ int ensure_workspace(Topology* top, int nsrc) {
     const int64_t V = top->g.V;
     const int K = batch_k(top);
     hipDeviceProp_t prop;
-    HIPCHK(hipGetDeviceProperties(&prop, top->device));
+    HIPCHK(hipGetDeviceProperties(&prop, top->devId));
     // a short shard runs fewer sources per batch (auto batch_fill), so it can use a slot per
     // source up to the CUs' slots -- sized by sources, not by batches of K (an 8-GPU shard of
     // 1,250 rows got 157 slots for 250 batches of 5: 120 ms instead of 73)
@@ -965,7 +970,18 @@ SlotWs slot_ws(Topology* top) {
     w.q_stride = queue_stride(top, w.K);
     w.mask = top->d_mask.p;
     w.hpar = top->d_hpar.p;
+    w.board = top->share ? top->d_board.p : nullptr;
     return w;
+}
+
+// zeroes the help board before a batched launch (every polled word starts at 0: no job, no
+// finished batch)
+int board_ready(Topology* top, hipStream_t st) {
+    if (!top->share) return 0;
+    const size_t n = ((size_t)top->slots + 1) * kBoardWords;
+    HIPCHK(top->d_board.ensure(n));
+    HIPCHK(hipMemsetAsync(top->d_board.p, 0, sizeof(uint32_t) * n, st));
+    return 0;
 }
 
 // Incidence-order CSR of the heap replay (ReplayCSR in topo_device.h).  Row x (relabelled id)
@@ -1059,7 +1075,7 @@ int ensure_replay_ws(Topology* top, int nrows) {
     const ReplayLayout lay = replay_layout(ik ? 1 : 0, (uint32_t)V);
     const size_t per_slot = 16 * V + nodeB * lay.nodeCap + (size_t)kMaxHops * 64 * 4 + 64;
     hipDeviceProp_t prop;
-    HIPCHK(hipGetDeviceProperties(&prop, top->device));
+    HIPCHK(hipGetDeviceProperties(&prop, top->devId));
     // wavefronts per CU: replay_wpc (20), or as many as the CU's LDS holds (each its heap's top
     // levels)
     const int lds = (replay_lds_bytes(ik ? 1 : 0) + 255) & ~255;
@@ -1238,6 +1254,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         HIPCHK(hipEventRecord(top->ev0, st));
         if (!allReplay) {
             r = ensure_workspace(top, (int)rows);
+            if (r) return r;
+            r = board_ready(top, st);
             if (r) return r;
             HIPCHK(top->d_rowflag.ensure((size_t)rows));
             HIPCHK(hipMemsetAsync(top->d_rowflag.p, 0, (size_t)rows, st));
@@ -1527,6 +1545,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 top->stats.lds_hubs = bp.H;
                 r = hub_rows_ready(top, bp.H, st);
                 if (r) return r;
+                r = board_ready(top, st);  // (a tie probe launch used it)
+                if (r) return r;
                 // diagnostic: SHD_BATCH_TRACE=<file> appends per batch {start tick, end tick,
                 // slot, near iterations, sweeps, expansions, relaxations, sources}, then per
                 // batch position {source vertex, pi bits}
@@ -1630,7 +1650,7 @@ int collect_row_stats(Topology* top) {
     top->stats.errors = (int64_t)h[ST_ERRORS];
     {
         int khz = 0;
-        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->device) != hipSuccess || khz <= 0)
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->devId) != hipSuccess || khz <= 0)
             khz = 100000;
         for (int i = 0; i < 4; i++) top->stats.phase_ms[i] = (double)h[ST_T_INIT + i] / (double)khz;
         for (int i = 0; i < 4; i++) top->stats.parent_phase_ms[i] = (double)h[ST_PT0 + i] / (double)khz;
@@ -1650,6 +1670,10 @@ int collect_row_stats(Topology* top) {
     top->stats.replay_rows = (int64_t)h[ST_RP_ROWS];
     top->stats.touched_lines = (int64_t)h[ST_TOUCHED];
     top->stats.walk_steps = (int64_t)h[ST_WALK];
+    top->stats.help_items[0] = (int64_t)h[ST_HELP_ITEMS];
+    top->stats.help_items[1] = (int64_t)h[ST_HELP_ITEMS + 1];
+    top->stats.help_board_errors = (int64_t)h[ST_HB_ERR];
+    if (h[ST_HB_ERR]) CRITICAL("help board: %llu spin limits hit", h[ST_HB_ERR]);
     for (int i = 0; i < 4; i++) top->stats.walk_kinds[i] = (int64_t)h[ST_WK0 + i];
     top->stats.replay_pops = (int64_t)h[ST_RP_POPS];
     top->stats.replay_pushes = (int64_t)h[ST_RP_PUSH];
@@ -1657,7 +1681,7 @@ int collect_row_stats(Topology* top) {
     for (int i = 0; i < 6; i++) top->stats.replay_lines[i] = (int64_t)h[ST_RP_L0 + i];
     {
         int khz = 0;
-        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->device) != hipSuccess || khz <= 0)
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->devId) != hipSuccess || khz <= 0)
             khz = 100000;
         for (int i = 0; i < 4; i++) top->stats.replay_phase_ms[i] = (double)h[ST_RP_T0 + i] / (double)khz;
         top->stats.replay_sink_rounds = (int64_t)h[ST_RP_T0 + 4];
@@ -1676,9 +1700,10 @@ int collect_row_stats(Topology* top) {
     top->stats.replay_int_keys = top->stats.replay_rows && top->replayIntOpt && top->replayIntOk ? 1 : 0;
     {
         int khz = 0;
-        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->device) != hipSuccess || khz <= 0)
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->devId) != hipSuccess || khz <= 0)
             khz = 100000;
         top->stats.split_ms = (double)h[ST_T_SPLIT] / (double)khz;
+        top->stats.help_ms = (double)h[ST_T_HELP] / (double)khz;
     }
     if (h[ST_OVERFLOW]) CRITICAL("SSSP queue overflow / iteration guard (code %llu)", h[ST_OVERFLOW]);
     if (top->stats.ambiguous_pairs && !top->tieReplay)
@@ -1686,7 +1711,7 @@ int collect_row_stats(Topology* top) {
                 "in the reference; tie_replay is off, so the lowest adjacency slot is used here",
                 (long long)top->stats.ambiguous_pairs);
     top->rowsPending = false;
-    return (h[ST_OVERFLOW] ? -4 : 0);
+    return (h[ST_OVERFLOW] || h[ST_HB_ERR] ? -4 : 0);
 }
 
 void push_min_to_engine(double m) {
@@ -1800,6 +1825,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->targetSkip = top->targetSkip;
     p->targetKappa = top->targetKappa;
     p->targetResort = top->targetResort;
+    p->share = top->share;
     p->attached = top->attached;
     p->colOf = top->colOf;
     p->A = top->A;
@@ -2628,6 +2654,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
         }
     }
     else if (k == "prepare_on_attach") top->prepOnAttach = value != 0;
+    else if (k == "share") top->share = value != 0;
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
     else if (k == "par_hubs") top->parHubs = (int64_t)value;
     else if (k == "batch") {

@@ -91,7 +91,10 @@ enum StatIdx {
     ST_WL0 = 69,        // batch kernel (SHD_BATCH_WRCOUNT builds): 64-B lines written per
                         //   category (16 slots, topo_sssp_batch.hip WL_*)
     ST_RL0 = 85,        //   then 64-B lines read per category (8 slots, RL_*)
-    ST_COUNT = 93
+    ST_T_HELP = 93,     // batch kernel: wall ticks summed over workgroups helping other slots' jobs
+    ST_HELP_ITEMS = 94, //   items they took: walk start pairs / epilogue items (2 slots)
+    ST_HB_ERR = 96,     //   help-board spin limits hit (cannot happen; reported)
+    ST_COUNT = 97
 };
 
 struct DevCSR {
@@ -148,7 +151,12 @@ struct SlotWs {
     const uint32_t* rowmap = nullptr;
     // diagnostic (SHD_BATCH_TRACE): per batch {wall_clock64 at dequeue, at its end, slot}
     unsigned long long* btrace = nullptr;
+    // help board (work sharing, topo_sssp_batch.hip): kBoardWords u32 per slot + one word of
+    // finished batches, zeroed before every launch; nullptr = every batch's parent walks and
+    // epilogue stay in its own workgroup
+    uint32_t* board = nullptr;
 };
+constexpr int kBoardWords = 64;  // u32 words per slot entry of the help board (256 B)
 
 // Incidence-order CSR of the heap replay (topo_replay.hip), relabelled vertex ids: row x holds
 // x's neighbours in igraph_incident order (ascending ORIGINAL neighbour id; directed graphs:

@@ -163,6 +163,14 @@ struct LdsB {
     unsigned long long wl[16];  // SHD_BATCH_WRCOUNT builds: 64-B lines stored / atomically
                                 // written per category (WL_*), then read per category (RL_*)
     unsigned long long rl[16];
+    // jobs (help board): this slot's jobs published (seq), the cursor of a board-less launch, the
+    // items this workgroup took of the current job; a helper's chosen entry, its descriptor
+    // {seq, kind, items, tag, first position, sources, list, valid}, "every batch done"; items a
+    // helper took (walk start pairs, epilogue items)
+    uint32_t jseq, jcur, jtaken;
+    uint32_t hjob, hflag;
+    uint32_t hd[8];
+    unsigned long long hitems[2];
 };
 
 // Write categories of SHD_BATCH_WRCOUNT builds (ShdStats.write_lines): each store / atomic
@@ -953,6 +961,61 @@ __device__ __forceinline__ void expand_pairs(const uint32_t* Q, uint32_t nq, con
     }
 }
 
+// ---- help board: work sharing between the launch's workgroups --------
+// A batch's parent walks (each level's start list) and its per-target epilogue are JOBS of items
+// that any workgroup can take: the owner publishes a job on its board entry, takes chunks of it
+// itself, and waits until every taken item is done; a workgroup whose dequeue found no batch left
+// scans the board and takes chunks of the running jobs (the walks' pair records are
+// deterministic, so concurrent takers write identical values; the epilogue's items are
+// independent).  Entry words: the cursor (u64: seq 16 | items 24 | next 24, claimed by CAS, so a
+// stale taker never moves a newer job's cursor), items done, the job's descriptor (written before
+// the cursor), the S list counter of walk jobs, the batch's row minima (u64 atomicMin).
+// Hand-offs: the owner's stores -> release fence -> cursor store; a helper's relaxed cursor load
+// -> acquire fence -> plain loads; a helper's stores -> release fence -> done add; the owner's
+// done poll -> acquire fence (MI355X_MICROARCH.md "inter-workgroup visibility").  Every spin is
+// bounded (ST_HB_ERR).
+enum {
+    HB_CUR = 0,    // u64 cursor (words 0-1)
+    HB_DONE = 2,   // items completed
+    HB_SEQ = 3,    // descriptor: the job's seq (validated against the cursor's)
+    HB_KIND = 4,   //   kJob*
+    HB_EP = 5,     //   the batch tag
+    HB_R0 = 6,     //   the batch's first position
+    HB_NK = 7,     //   its sources
+    HB_LIST = 8,   //   walk jobs: 0 = start list in qa, 1 = in qb
+    HB_SCNT = 9,   // walk jobs: entries reserved in the slot's S list (blocks of 64)
+    HB_RMIN = 16   // u64[16]: epilogue row minima (words 16-47)
+};
+constexpr uint32_t kJobWalkSync = 1;  // first-level walks (groups of K lanes start together)
+constexpr uint32_t kJobWalk = 2;      // later levels
+constexpr uint32_t kJobEpi = 3;       // per-target epilogue
+constexpr uint32_t kJobChunk = 256;   // items a wave claims at a time (4 per lane)
+constexpr unsigned long long kHbSpinTicks = 2000000000ull;  // 20 s at 100 MHz: a bound, not a wait
+constexpr uint32_t kJobNone = 0xFFFFFFFFu;
+constexpr uint32_t kNoPairS = 0xFFFFFFFFu;
+
+__device__ __forceinline__ unsigned long long hb_cur(const uint32_t* e) {
+    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(e + HB_CUR),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// claim up to c items of job `seq` (16 bits) on entry e: the first item, and *cnt items; kJobNone
+// when the job is used up or no longer the entry's
+__device__ __forceinline__ uint32_t hb_grab(uint32_t* e, uint32_t seq, uint32_t c, uint32_t* cnt) {
+    unsigned long long* p = reinterpret_cast<unsigned long long*>(e + HB_CUR);
+    unsigned long long old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        if ((uint32_t)(old >> 48) != seq) return kJobNone;
+        const uint32_t n = (uint32_t)(old >> 24) & 0xFFFFFFu, x = (uint32_t)old & 0xFFFFFFu;
+        if (x >= n) return kJobNone;
+        const uint32_t t = min(c, n - x);
+        if (__hip_atomic_compare_exchange_strong(p, &old, old + t, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            *cnt = t;
+            return x;
+        }
+    }
+}
+
 }  // namespace
 
 template <int K>
@@ -1036,6 +1099,309 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             L.tm[i] += t - L.tk;
             L.tk = t;
         }
+    };
+
+    if (tid == 0) {
+        L.jseq = 0;
+        L.jcur = 0;
+        L.jtaken = 0;
+        L.hitems[0] = L.hitems[1] = 0;
+        L.fover = 0;
+    }
+    const uint32_t lane = tid & 63u;
+    constexpr uint32_t kNoPair = 0xFFFFFFFFu;
+    // Walk hop inputs at vertex v for source j: the h0-tree record {parent, slot, f64 w, f64 loss of
+    // that edge} (32 B, one line) of a tail and d_j(v) -- independent loads, one round trip.  Hubs
+    // read their distance from their row of the [V][K] block (copied there at the SSSP's end).
+    struct Hop {
+        uint4 sp;
+        double sl;
+        unsigned long long d;
+    };
+
+    // One job of slot o: walks of a level's start list (kJobWalkSync /
+    // kJobWalk) or the per-target epilogue (kJobEpi) of the batch {tag epv, positions r0v..,
+    // nkv sources}; every wave claims kJobChunk items at a time until the job is used up.  The
+    // owner and helping workgroups run the same code; L.src holds the job's sources.  Adds this
+    // workgroup's claimed items to L.jtaken.
+    auto run_job = [&](uint32_t o, uint32_t seq, uint32_t kind, uint32_t n, uint32_t epv,
+                       uint32_t r0v, uint32_t nkv, uint32_t list) {
+        const bool shared = ws.board != nullptr;
+        uint32_t* const eo = shared ? ws.board + (size_t)o * kBoardWords : nullptr;
+        unsigned long long* const distO = ws.dist + (size_t)o * (size_t)V * K;
+        uint4* const precO = ws.prec + (size_t)o * (size_t)V * K;
+        uint32_t* const precwO = reinterpret_cast<uint32_t*>(precO);
+        const uint32_t eptv = epv | kTagClaim;
+        uint32_t taken = 0;
+        // the wave's next chunk of the job: its first item (kJobNone: used up) and *cnt items
+        auto grab = [&](uint32_t* cnt) -> uint32_t {
+            uint32_t b = kJobNone, c = 0;
+            if (lane == 0) {
+                if (shared) {
+                    b = hb_grab(eo, seq, kJobChunk, &c);
+                } else {
+                    const uint32_t x = atomicAdd(&L.jcur, kJobChunk);
+                    if (x < n) {
+                        b = x;
+                        c = min(kJobChunk, n - x);
+                    }
+                }
+            }
+            *cnt = __shfl(c, 0, 64);
+            return __shfl(b, 0, 64);
+        };
+        if (kind != kJobEpi) {
+            // Walks: chains are followed towards the source while the h0-tree guess certifies
+            // parents (no level barriers); a chain stops at the source, at a pair another walk
+            // claimed first (tag), or at a pair whose guess fails (-> the slot's S list, claimed:
+            // the owner's hint pass resolves it).  One round trip per hop: the tag word of q (claim,
+            // tie) goes out with the loads of q's tree parent pu (d_j(pu) certifies the guess, pu's
+            // own hop inputs serve the next hop).  Flattened: a lane takes its next start pair as
+            // soon as its chain ends.  The first level keeps a target's K lanes together (a group
+            // takes its next start pairs when the whole group is idle).
+            const uint32_t* P = reinterpret_cast<const uint32_t*>((list ? ws.qb : ws.qa) +
+                                                                  (size_t)o * ws.q_stride);
+            uint32_t* const S = reinterpret_cast<uint32_t*>(ws.ring) + (size_t)o * ws.ring_entries;
+            const uint32_t pcapS = (uint32_t)(V * K);
+            const bool gs = kind == kJobWalkSync;
+            auto put = [&](uint32_t q, uint32_t u, double loss) {
+                const unsigned long long lb = d2bits(loss);
+                wl_count(L, WL_PREC, true, precO + q);
+                precO[q] = make_uint4(u, eptv, (uint32_t)lb, (uint32_t)(lb >> 32));
+            };
+            auto load_hop = [&](uint32_t v, uint32_t j) -> Hop {
+                Hop hh;
+                const uint32_t q = v * K + j;
+                rl_count(L, RL_WALK, v >= H, reinterpret_cast<const uint4*>(g.spt) + 2 * (size_t)v);
+                rl_count(L, RL_WALK, true, distO + (size_t)q);
+                if (v >= H) {
+                    const uint4* sp = reinterpret_cast<const uint4*>(g.spt) + 2 * (size_t)v;
+                    hh.sp = sp[0];
+                    const uint2 l = *reinterpret_cast<const uint2*>(sp + 1);
+                    hh.sl = __hiloint2double((int)l.y, (int)l.x);
+                } else {
+                    hh.sp = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+                    hh.sl = 0.0;
+                }
+                hh.d = ld_l2_u64(&distO[(size_t)q]);
+                return hh;
+            };
+            uint32_t i = 0, iend = 0, q = 0, j = 0;
+            uint32_t nw = 0, nw0 = 0;   // walk steps, of which certified by the tree guess
+            uint32_t sb = 0, se = 0;    // the wave's reserved block of the S list (help board)
+            bool act = false, fresh = false, more = true;
+            Hop h;
+            h.sp = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+            h.sl = 0.0;
+            h.d = 0ull;
+            for (;;) {
+                if (more && !__any(i < iend)) {
+                    uint32_t c;
+                    const uint32_t b = grab(&c);
+                    if (b == kJobNone) {
+                        more = false;
+                    } else {
+                        i = b + lane;
+                        iend = b + c;
+                        taken += c;
+                    }
+                }
+                bool take = !act && i < iend;
+                if (gs) {  // the lane's group of K (one target) takes its starts together
+                    const unsigned long long am = __ballot(act);
+                    take = take && ((am >> (lane & ~(uint32_t)(K - 1))) & ((1ull << K) - 1ull)) == 0ull;
+                }
+                rl_count(L, RL_WALK, take, P + (take ? i : 0u));
+                if (take) {
+                    q = P[i];
+                    i += 64;
+                    j = q % K;
+                    act = q != kNoPair;
+                    fresh = act;
+                }
+                if (!more && !__any(act || i < iend)) break;
+                bool sp = false;  // q goes to the S list
+                if (act && fresh) {
+                    h = load_hop(q / K, j);
+                    fresh = false;
+                } else if (act) {
+                    const uint32_t v = q / K;
+                    const uint32_t pu = h.sp.x;
+                    const bool tree = v >= H && pu < (uint32_t)V;
+                    Hop hn = h;
+                    if (tree) hn = load_hop(pu, j);
+                    // The claim is a plain tag read issued with those loads; the pair's record
+                    // (put) or, for a pair left to the hint pass, a tag store marks it as this
+                    // batch's.  Two walks that reach an unclaimed pair in the same round trip both
+                    // walk on: they write identical records (the parent rule is deterministic), and
+                    // a pair listed twice in S is resolved twice the same way.
+                    rl_count(L, RL_WALK, true, precwO + 4 * (size_t)q);
+                    const uint32_t tw = ld_l2_u32(&precwO[4 * (size_t)q + 1]);
+                    if (tag_claimed(tw, epv)) {  // another walk's
+                        act = false;
+                    } else {
+                        nw++;
+                        const bool tied = tag_tied(tw, epv);
+                        if (tree && !tied &&
+                            __dadd_rn(bits2d(hn.d), __hiloint2double((int)h.sp.w, (int)h.sp.z)) ==
+                                bits2d(h.d)) {
+                            put(q, pu, h.sl);
+                            nw0++;
+                            if (pu == L.src[j]) {
+                                act = false;
+                            } else {
+                                q = pu * K + j;
+                                h = hn;
+                            }
+                        } else {
+                            wl_count(L, WL_PREC, true, precwO + 4 * (size_t)q);
+                            precwO[4 * (size_t)q + 1] = eptv | (tied ? kTagTie : 0u);
+                            sp = true;
+                            act = false;
+                        }
+                    }
+                }
+                // this round's S pairs, wave-aggregated: board launches reserve blocks of 64
+                // entries of the slot's S list (a block's unused entries are holes, kNoPairS)
+                const unsigned long long m = __ballot(sp);
+                if (m) {
+                    const uint32_t need = (uint32_t)__popcll(m);
+                    uint32_t base;
+                    if (shared) {
+                        if (se - sb < need) {
+                            if (lane < se - sb && sb + lane < pcapS) S[sb + lane] = kNoPairS;
+                            uint32_t nb = 0;
+                            if (lane == 0) nb = atomicAdd(eo + HB_SCNT, 64u);
+                            nb = __shfl(nb, 0, 64);
+                            sb = nb;
+                            se = nb + 64u;
+                        }
+                        base = sb;
+                        sb += need;
+                    } else {
+                        uint32_t x = 0;
+                        if (lane == 0) x = atomicAdd(&L.qtail, need);
+                        base = __shfl(x, 0, 64);
+                    }
+                    if (sp) {
+                        const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                        wl_count(L, WL_QUEUE, pos < pcapS, S + pos);
+                        if (pos < pcapS) S[pos] = q;
+                        else atomicOr(&L.fover, 128u);
+                    }
+                }
+            }
+            if (shared && lane < se - sb && sb + lane < pcapS) S[sb + lane] = kNoPairS;
+            const unsigned long long s0 = wave_sum_u64(nw), s1 = wave_sum_u64(nw0);
+            if (lane == 0) {
+                atomicAdd(&L.wk[0], s0);
+                atomicAdd(&L.wk[1], s1);
+            }
+        } else {
+            // Per-target latency / reliability / hops (shd-topology.c:561-671), items (target,
+            // source) target-major (the group's chains coincide up to the core, so each lockstep
+            // hop reads one target's pair records); each lane walks its item's chain backwards into
+            // its path buffer (the first nl levels in this workgroup's hub LDS, whose distances are
+            // in HBM by now; deeper ones in its HBM buffer) and multiplies in path order.
+            double* lpb = reinterpret_cast<double*>(smem + lay.hd);
+            const uint32_t nl = H * K / kSsspBlock;  // LDS levels of the path buffer
+            auto pb_at = [&](uint32_t x) -> double* {
+                return x < nl ? lpb + (size_t)x * kSsspBlock + tid : pbuf + (size_t)x * kSsspBlock + tid;
+            };
+            unsigned long long* const rminP =
+                shared ? reinterpret_cast<unsigned long long*>(eo + HB_RMIN) : L.rmin;
+            for (;;) {
+                uint32_t c;
+                const uint32_t b = grab(&c);
+                if (b == kJobNone) break;
+                taken += c;
+                for (uint32_t i = b + lane; i < b + c; i += 64) {
+                    const uint32_t jj = SHD_TGT_MAJOR ? i % nkv : i / (uint32_t)A;
+                    const uint32_t k = SHD_TGT_MAJOR ? i / nkv : i - jj * (uint32_t)A;
+                    rl_count(L, RL_EPI, true, targets + k);
+                    const uint32_t t = targets[k];
+                    const uint32_t src = L.src[jj];
+                    double lat, rel;
+                    uint32_t hcnt = 0;
+                    if (t == src) {
+                        // path [src]: the self loop (n == 1 branch), no destination loss
+                        const double sl = g.selfLat[src];
+                        if (isnan(sl)) {
+                            atomicAdd(&stats[ST_ERRORS], 1ull);
+                            lat = -1.0;
+                            rel = -1.0;
+                        } else {
+                            lat = 0.0 + sl;
+                            rel = 1.0;
+                            rel *= (1.0 - g.vloss[src]);
+                            rel *= (1.0 - g.selfLoss[src]);
+                            hcnt = 1;
+                        }
+                    } else {
+                        rl_count(L, RL_EPI, true, distO + (size_t)t * K + jj);
+                        rl_count(L, RL_EPI, true, g.vloss + t);
+                        lat = bits2d(ld_l2_u64(&distO[(size_t)t * K + jj]));
+                        bool amb = false, bad = false;
+                        uint32_t v = t;
+                        while (v != src) {
+                            // the pair record, L1-bypassing (written by other waves / workgroups)
+                            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                            rl_count(L, RL_EPI, true, reinterpret_cast<const u32x4*>(precO) + (size_t)v * K + jj);
+                            const u32x4 rv = __builtin_nontemporal_load(
+                                reinterpret_cast<const u32x4*>(precO) + (size_t)v * K + jj);
+                            if (rv.y != eptv || (rv.x & 0x40000000u)) {
+                                bad = true;
+                                break;
+                            }
+                            amb |= (rv.x >> 31) != 0u;
+                            wl_count(L, WL_OTHER, hcnt < kMaxHops && hcnt >= nl, pb_at(hcnt));
+                            if (hcnt < kMaxHops) *pb_at(hcnt) = __hiloint2double((int)rv.w, (int)rv.z);
+                            hcnt++;
+                            v = rv.x & 0x3FFFFFFFu;
+                            if (hcnt > (uint32_t)V) { bad = true; break; }
+                        }
+                        rel = 1.0;
+                        rel *= (1.0 - g.vloss[src]);
+                        rel *= (1.0 - g.vloss[t]);
+                        if (bad) {
+                            atomicAdd(&stats[ST_ERRORS], 1ull);
+                            lat = -1.0;
+                            rel = -1.0;
+                        } else if (hcnt <= (uint32_t)kMaxHops) {
+                            for (int x = (int)hcnt - 1; x >= 0; --x) rel *= (1.0 - *pb_at((uint32_t)x));
+                        } else {
+                            atomicAdd(&stats[ST_LONGPATH], 1ull);
+                            for (int x = (int)hcnt - 1; x >= 0; --x) {  // edge at depth x from t
+                                uint32_t y = t;
+                                for (int z = 0; z < x; ++z) y = precO[(size_t)y * K + jj].x & 0x3FFFFFFFu;
+                                const uint4 r = precO[(size_t)y * K + jj];
+                                rel *= (1.0 - __hiloint2double((int)r.w, (int)r.z));
+                            }
+                        }
+                        if (amb) {
+                            atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
+                            if (ws.rowflag) ws.rowflag[ws.rowmap ? ws.rowmap[r0v + jj] : r0v + jj] = 1;  // tie replay (topo_replay.hip)
+                        }
+                        if (lat == 0.0) lat = 1.0;
+                    }
+                    const size_t ob = (size_t)(ws.rowmap ? (int)ws.rowmap[r0v + jj] : (int)(r0v + jj)) * (size_t)A + k;
+                    const uint16_t hh = (uint16_t)(hcnt > 65535u ? 65535u : hcnt);
+                    wl_count(L, WL_OUT, true, out_lr + ob);
+                    wl_count(L, WL_OUT, true, out_hops + ob);
+                    if (SHD_OUT_NT) {  // the table (1.8 GB per launch) is not re-read by the kernel
+                        typedef double f64x2 __attribute__((ext_vector_type(2)));
+                        const f64x2 r2 = {lat, rel};
+                        __builtin_nontemporal_store(r2, reinterpret_cast<f64x2*>(out_lr) + ob);
+                        __builtin_nontemporal_store(hh, out_hops + ob);
+                    } else {
+                        out_lr[ob] = make_double2(lat, rel);
+                        out_hops[ob] = hh;
+                    }
+                    if (lat >= 0.0) atomicMin(&rminP[jj], d2bits(lat));  // row minimum (runahead)
+                }
+            }
+        }
+        if (lane == 0 && taken) atomicAdd(&L.jtaken, taken);
     };
 
     for (;;) {
@@ -1395,16 +1761,80 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
 
         // ---------------- parents for the target chains of every source of the batch ---------
         // One level-synchronous pass over (vertex, source) pairs p = v * K + j (SURVEY.md A.3:
-        // parent(v) = argmin d_j[u] over the candidates fl(d_j[u] + w) == d_j[v]).  A level finds
-        // the min d_j[u] over the candidates of each pair with one adjacency pass and counts them;
-        // pairs with several candidates get a recount at the minimum.  All K sources' chains run
-        // in the same levels, so the pass has K times the parallelism of one source's.
+        // parent(v) = argmin d_j[u] over the candidates fl(d_j[u] + w) == d_j[v]).  A level's walks
+        // certify most parents without scanning (h0-tree guess); the rest get the hint pass and a
+        // merged row scan; their parents start the next level.  Each level's walks and the
+        // epilogue are jobs of the slot's help-board entry (run_job): idle workgroups join them.
         if ((int)tid < nk) L.src[tid] = sources[r0 + tid];
         const uint32_t ept = ep | kTagClaim;  // tag word of a resolved / claimed pair record
+        const bool shared = ws.board != nullptr;
+        uint32_t* const my_e = shared ? ws.board + (size_t)slot * kBoardWords : nullptr;
+        // Publish a job on this slot's entry (every wave's earlier stores drained first: the hub
+        // rows, the start list, the pair records), and after taking part, wait until every
+        // claimed item is done (helpers add theirs after a release fence), then acquire.
+        auto job_publish = [&](uint32_t kind, uint32_t n, uint32_t list) -> uint32_t {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                L.jseq = (L.jseq + 1u) & 0xFFFFu;
+                if (L.jseq == 0u) L.jseq = 1u;
+                L.jtaken = 0;
+                L.jcur = 0;
+                L.qtail = 0;
+                if (shared) {
+                    __hip_atomic_store(my_e + HB_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(my_e + HB_SEQ, L.jseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(my_e + HB_KIND, kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(my_e + HB_EP, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(my_e + HB_R0, (uint32_t)r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(my_e + HB_NK, (uint32_t)nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(my_e + HB_LIST, list, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(my_e + HB_SCNT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (kind == kJobEpi)
+                        for (int jj = 0; jj < K; jj++)
+                            __hip_atomic_store(reinterpret_cast<unsigned long long*>(my_e + HB_RMIN) + jj,
+                                               kInfBits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(reinterpret_cast<unsigned long long*>(my_e + HB_CUR),
+                                       ((unsigned long long)L.jseq << 48) | ((unsigned long long)n << 24),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else if (kind == kJobEpi) {
+                    for (int jj = 0; jj < K; jj++) L.rmin[jj] = kInfBits;
+                }
+            }
+            __syncthreads();
+            return L.jseq;
+        };
+        auto job_finish = [&](uint32_t n) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (shared && tid == 0) {
+                atomicAdd(my_e + HB_DONE, L.jtaken);
+                const unsigned long long t0 = wall_clock64();
+                while (ld_l2_u32(my_e + HB_DONE) < n) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (wall_clock64() - t0 > kHbSpinTicks) {
+                        atomicAdd(&stats[ST_HB_ERR], 1ull);
+                        break;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+        };
+        // the hub distances move to their (otherwise unused) rows of the [V][K] block: the walks
+        // and the epilogue of every workgroup taking part in this batch's jobs read them there
+        for (uint32_t i = tid; i < H * K; i += kSsspBlock) {
+            wl_count(L, WL_HUB, true, D.dist + i);
+            D.dist[i] = D.hd[i];
+        }
         if (tid == 0) L.qtail = 0;
         __syncthreads();
         uint32_t* pcur = qa;
         uint32_t* pnxt = qb;
+        uint32_t plist = 0;  // pcur is qa (0) or qb (1)
 #if SHD_TGT_MAJOR
         // Target-major start list, K entries per target (kNoPair for the sources past nk and a
         // target that is the source): a target's chains for the K sources share their tail part
@@ -1412,7 +1842,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // same vertices in the same round trip and one line serves the group's tree records,
         // distances and pair records.  The first level's walks keep the groups together (a lane
         // takes its next start pair when its whole group is idle).
-        constexpr uint32_t kNoPair = 0xFFFFFFFFu;
         for (uint32_t i = tid; i < (uint32_t)A * K; i += kSsspBlock) {
             const uint32_t j = i % K;
             const uint32_t t = targets[i / K];
@@ -1420,10 +1849,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             wl_count(L, WL_QUEUE, true, pcur + i);
             pcur[i] = p ? t * K + j : kNoPair;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
         uint32_t nF = (uint32_t)A * K;
-        bool gsync = true;
+        uint32_t wkind = kJobWalkSync;
 #else
         for (uint32_t ib = 0; ib < (uint32_t)A * (uint32_t)nk; ib += kSsspBlock) {
             const uint32_t i = ib + tid;
@@ -1439,9 +1866,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         }
         __syncthreads();
         uint32_t nF = min(L.qtail, pcap);
-        __syncthreads();
-        constexpr uint32_t kNoPair = 0xFFFFFFFFu;
-        constexpr bool gsync = false;
+        uint32_t wkind = kJobWalk;
 #endif
         // A pair's record: its parent, the batch's tag, the loss of the parent edge (one store)
         auto put = [&](uint32_t q, uint32_t u, double loss) {
@@ -1466,9 +1891,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
 #pragma unroll
             for (int h = 0; h < kHP; h++) {
                 const uint32_t i = ib + (uint32_t)h * kSsspBlock + tid;
-                has[h] = i < nS;
-                q[h] = has[h] ? S[i] : 0u;
+                q[h] = i < nS ? S[i] : kNoPairS;
+                has[h] = q[h] != kNoPairS;  // a hole of the S list (board launches)
                 qo[h] = q[h];
+                if (!has[h]) q[h] = 0u;
                 const uint32_t v = q[h] / K, j = q[h] % K;
                 dv[h] = has[h] ? D.get(v, j) : 0ull;
                 rw[h] = make_uint2(0u, 0u);
@@ -1541,124 +1967,16 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 scan[h] = false;
             }
         };
-        // A walk hop's inputs at tail vertex v for source j: its h0-tree record {parent, slot,
-        // f64 w, f64 loss of that edge} (32 B, one line) and d_j(v) -- independent loads, in one
-        // round trip.  Hubs: d_j(v) only (LDS).
-        struct Hop {
-            uint4 sp;
-            double sl;
-            unsigned long long d;
-        };
-        auto load_hop = [&](uint32_t v, uint32_t j) -> Hop {
-            Hop h;
-            const uint32_t q = v * K + j;
-            rl_count(L, RL_WALK, v >= H, reinterpret_cast<const uint4*>(g.spt) + 2 * (size_t)v);
-            rl_count(L, RL_WALK, v >= H, D.dist + (size_t)q);
-            if (v >= H) {
-                const uint4* s = reinterpret_cast<const uint4*>(g.spt) + 2 * (size_t)v;
-                h.sp = s[0];
-                const uint2 l = *reinterpret_cast<const uint2*>(s + 1);
-                h.sl = __hiloint2double((int)l.y, (int)l.x);
-                h.d = ld_l2_u64(&D.dist[(size_t)q]);
-            } else {
-                h.sp = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
-                h.sl = 0.0;
-                h.d = D.hd[(size_t)q];
-            }
-            return h;
-        };
         while (nF > 0) {
             if (tid == 0) L.ev[3] += nF;
             unsigned long long tp0 = wall_clock64();
-            // Walks: chains are followed towards the source while the h0-tree guess certifies
-            // parents (no level barriers); a chain stops at the source, at a pair another walk
-            // claimed first (tag), or at a pair whose guess fails (-> S = fscr, claimed: the hint
-            // pass below resolves it).  One round trip per hop: the tag word of q (claim, tie)
-            // goes out with the loads of q's tree parent pu (d_j(pu) certifies the guess, pu's
-            // own hop inputs serve the next hop).  Flattened: a lane takes its next start pair as
-            // soon as its chain ends, so a wave runs for its busiest lane's total of hops, not
-            // for the sum over start pairs of the longest chain among its 64 lanes; the slower
-            // guesses (binary searches) are deferred so they do not stall the wave's other chains.
-            if (tid == 0) L.qtail = 0;
-            __syncthreads();
             {
-                uint32_t i = tid, q = 0, j = 0;
-                uint32_t nw = 0, nw0 = 0;  // walk steps, of which certified by the tree guess
-                bool act = false, fresh = false;
-                Hop h;
-                h.sp = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
-                h.sl = 0.0;
-                h.d = 0ull;
-                for (;;) {
-                    bool take = !act && i < nF;
-                    if (gsync) {  // the lane's group of K (one target) takes its starts together
-                        const unsigned long long am = __ballot(act);
-                        take = take && ((am >> ((tid & 63u) & ~(uint32_t)(K - 1))) & ((1ull << K) - 1ull)) == 0ull;
-                    }
-                    rl_count(L, RL_WALK, take, pcur + (take ? i : 0u));
-                    if (take) {
-                        q = pcur[i];
-                        i += kSsspBlock;
-                        j = q % K;
-                        act = q != kNoPair;
-                        fresh = act;
-                    }
-                    if (!__any(act || i < nF)) break;
-                    if (!act) continue;
-                    if (act && fresh) {
-                        h = load_hop(q / K, j);
-                        fresh = false;
-                    } else if (act) {
-                        const uint32_t v = q / K;
-                        const uint32_t pu = h.sp.x;
-                        const bool tree = v >= H && pu < (uint32_t)V;
-                        Hop hn = h;
-                        if (tree) hn = load_hop(pu, j);
-                        // The claim is a plain tag read issued with those loads; the pair's
-                        // record (put) or, for a pair left to the hint pass, a tag store marks
-                        // it as this batch's.  Two walks that reach an unclaimed pair in the same
-                        // round trip both walk on: they write identical records (the parent rule
-                        // is deterministic), and a pair listed twice in S is resolved twice the
-                        // same way -- cheaper than a returning atomic per hop (kernel -3.5 %).
-                        rl_count(L, RL_WALK, true, precw + 4 * (size_t)q);
-                        const uint32_t tw = ld_l2_u32(&precw[4 * (size_t)q + 1]);
-                        if (tag_claimed(tw, ep)) {  // another walk's
-                            act = false;
-                        } else {
-                            nw++;
-                            const bool tied = tag_tied(tw, ep);
-                            if (tree && !tied &&
-                                __dadd_rn(bits2d(hn.d), __hiloint2double((int)h.sp.w, (int)h.sp.z)) ==
-                                    bits2d(h.d)) {
-                                put(q, pu, h.sl);
-                                nw0++;
-                                if (pu == L.src[j]) {
-                                    act = false;
-                                } else {
-                                    q = pu * K + j;
-                                    h = hn;
-                                }
-                            } else {
-                                wl_count(L, WL_PREC, true, precw + 4 * (size_t)q);
-                                precw[4 * (size_t)q + 1] = ept | (tied ? kTagTie : 0u);
-                                const uint32_t pos = atomicAdd(&L.qtail, 1u);
-                                wl_count(L, WL_QUEUE, pos < pcap, fscr + pos);
-                                if (pos < pcap) fscr[pos] = q;
-                                else atomicOr(&L.fover, 128u);
-                                act = false;
-                            }
-                        }
-                    }
-                }
-                const unsigned long long s0 = wave_sum_u64(nw), s1 = wave_sum_u64(nw0);
-                if ((tid & 63) == 0) {
-                    atomicAdd(&L.wk[0], s0);
-                    atomicAdd(&L.wk[1], s1);
-                }
+                const uint32_t seq = job_publish(wkind, nF, plist);
+                run_job((uint32_t)slot, seq, wkind, nF, ep, (uint32_t)r0, (uint32_t)nk, plist);
+                job_finish(nF);
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            const uint32_t nS = min(L.qtail, pcap);
+            // the S list (pairs whose guess failed), with holes (kNoPairS) on a board launch
+            const uint32_t nS = min(shared ? ld_l2_u32(my_e + HB_SCNT) : L.qtail, pcap);
             __syncthreads();
             if (tid == 0) L.pt[1] += wall_clock64() - tp0;  // walks
             if (nS == 0) break;
@@ -1675,7 +1993,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
 #pragma unroll
                 for (int h = 0; h < kHP; h++) {
                     const uint32_t q = qs[h];
-                    const bool in = ib + (uint32_t)h * kSsspBlock + tid < nS;
+                    const bool in = ib + (uint32_t)h * kSsspBlock + tid < nS && q != kNoPairS;
                     // counters (walk kinds): tail hint, hub hint, row scan -- one LDS atomic per wave
                     const unsigned long long bt = __ballot(in && !scan[h] && q / K >= H);
                     const unsigned long long bh = __ballot(in && !scan[h] && q / K < H);
@@ -1833,8 +2151,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 const uint32_t i = ib + tid;
                 bool p = false;
                 uint32_t q = 0;
-                if (i < nS) {
-                    const uint32_t qc = fscr[i];
+                const uint32_t qc = i < nS ? fscr[i] : kNoPairS;
+                if (qc != kNoPairS) {
                     const uint32_t j = qc % K;
                     // the parent (hint pass or row scan: R's records come from other threads)
                     const uint32_t u = ld_l2_u32(&precw[4 * (size_t)qc]) & 0x3FFFFFFFu;
@@ -1846,125 +2164,35 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             __syncthreads();
             nF = min(L.qtail, pcap);
             { uint32_t* t = pcur; pcur = pnxt; pnxt = t; }
-#if SHD_TGT_MAJOR
-            gsync = false;  // later levels start at the scanned pairs' parents (compacted)
-#endif
+            plist ^= 1u;
+            wkind = kJobWalk;  // later levels start at the scanned pairs' parents (compacted)
             __syncthreads();
             if (tid == 0) L.pt[4] += wall_clock64() - tp0;  // next level
         }
         tick(2);
 
         // ---------------- per-target latency / reliability / hops (shd-topology.c:561-671) ----
-        // items (source j, target k) of the whole batch; each thread walks its pairs' chains.
-        // The hub distances move to their (otherwise unused) rows of the [V][K] block, so the
-        // hub LDS holds the first nl levels of the per-thread path buffer (the chain's edge
-        // losses, multiplied in path order after the walk); deeper levels go to HBM (pbuf).
-        if ((int)tid < K) L.rmin[tid] = kInfBits;
-        for (uint32_t i = tid; i < H * K; i += kSsspBlock) {
-            wl_count(L, WL_HUB, true, D.dist + i);
-            D.dist[i] = D.hd[i];
+        // items (source j, target k) of the whole batch: a job (run_job), so idle workgroups take
+        // part; the row minima come back through the board entry (or L.rmin)
+        {
+            const uint32_t ni = (uint32_t)A * (uint32_t)nk;
+            const uint32_t seq = job_publish(kJobEpi, ni, 0u);
+            run_job((uint32_t)slot, seq, kJobEpi, ni, ep, (uint32_t)r0, (uint32_t)nk, 0u);
+            job_finish(ni);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        double* lpb = reinterpret_cast<double*>(D.hd);
-        const uint32_t nl = H * K / kSsspBlock;  // LDS levels of the path buffer
-        auto pb_at = [&](uint32_t x) -> double* {
-            return x < nl ? lpb + (size_t)x * kSsspBlock + tid : pbuf + (size_t)x * kSsspBlock + tid;
-        };
-        for (uint32_t i = tid; i < (uint32_t)A * (uint32_t)nk; i += kSsspBlock) {
-            // target-major (as the walks): the group's chains coincide up to the core, so each
-            // lockstep hop reads one target's K pair records (two lines), not K lines
-            const uint32_t j = SHD_TGT_MAJOR ? i % (uint32_t)nk : i / (uint32_t)A;
-            const uint32_t k = SHD_TGT_MAJOR ? i / (uint32_t)nk : i - j * (uint32_t)A;
-            rl_count(L, RL_EPI, true, targets + k);
-            const uint32_t t = targets[k];
-            const uint32_t src = L.src[j];
-            double lat, rel;
-            uint32_t h = 0;
-            if (t == src) {
-                // path [src]: the self loop (n == 1 branch), no destination loss
-                const double sl = g.selfLat[src];
-                if (isnan(sl)) {
-                    atomicAdd(&stats[ST_ERRORS], 1ull);
-                    lat = -1.0;
-                    rel = -1.0;
-                } else {
-                    lat = 0.0 + sl;
-                    rel = 1.0;
-                    rel *= (1.0 - g.vloss[src]);
-                    rel *= (1.0 - g.selfLoss[src]);
-                    h = 1;
-                }
-            } else {
-                rl_count(L, RL_EPI, true, D.dist + (size_t)t * K + j);
-                rl_count(L, RL_EPI, true, g.vloss + t);
-                lat = bits2d(ld_l2_u64(&D.dist[(size_t)t * K + j]));
-                bool amb = false, bad = false;
-                uint32_t v = t;
-                while (v != src) {
-                    // the pair record, L1-bypassing (written by other waves of the workgroup)
-                    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                    rl_count(L, RL_EPI, true, reinterpret_cast<const u32x4*>(prec) + (size_t)v * K + j);
-                    const u32x4 rv = __builtin_nontemporal_load(
-                        reinterpret_cast<const u32x4*>(prec) + (size_t)v * K + j);
-                    const uint4 r = make_uint4(rv.x, rv.y, rv.z, rv.w);
-                    if (r.y != ept || (r.x & 0x40000000u)) {
-                        bad = true;
-                        break;
-                    }
-                    amb |= (r.x >> 31) != 0u;
-                    wl_count(L, WL_OTHER, h < kMaxHops && h >= nl, pb_at(h));
-                    if (h < kMaxHops) *pb_at(h) = __hiloint2double((int)r.w, (int)r.z);
-                    h++;
-                    v = r.x & 0x3FFFFFFFu;
-                    if (h > (uint32_t)V) { bad = true; break; }
-                }
-                rel = 1.0;
-                rel *= (1.0 - g.vloss[src]);
-                rel *= (1.0 - g.vloss[t]);
-                if (bad) {
-                    atomicAdd(&stats[ST_ERRORS], 1ull);
-                    lat = -1.0;
-                    rel = -1.0;
-                } else if (h <= (uint32_t)kMaxHops) {
-                    for (int x = (int)h - 1; x >= 0; --x) rel *= (1.0 - *pb_at((uint32_t)x));
-                } else {
-                    atomicAdd(&stats[ST_LONGPATH], 1ull);
-                    for (int x = (int)h - 1; x >= 0; --x) {  // edge at depth x from t
-                        uint32_t y = t;
-                        for (int z = 0; z < x; ++z) y = prec[(size_t)y * K + j].x & 0x3FFFFFFFu;
-                        const uint4 r = prec[(size_t)y * K + j];
-                        rel *= (1.0 - __hiloint2double((int)r.w, (int)r.z));
-                    }
-                }
-                if (amb) {
-                    atomicAdd(&stats[ST_AMBIGUOUS], 1ull);
-                    if (ws.rowflag) ws.rowflag[ws.rowmap ? ws.rowmap[r0 + (int)j] : r0 + (int)j] = 1;  // tie replay (topo_replay.hip)
-                }
-                if (lat == 0.0) lat = 1.0;
-            }
-            const size_t o = (size_t)(ws.rowmap ? (int)ws.rowmap[r0 + (int)j] : r0 + (int)j) * (size_t)A + k;
-            const uint16_t hh = (uint16_t)(h > 65535u ? 65535u : h);
-            wl_count(L, WL_OUT, true, out_lr + o);
-            wl_count(L, WL_OUT, true, out_hops + o);
-            if (SHD_OUT_NT) {  // the table (1.8 GB per launch) is not re-read by the kernel
-                typedef double f64x2 __attribute__((ext_vector_type(2)));
-                const f64x2 r2 = {lat, rel};
-                __builtin_nontemporal_store(r2, reinterpret_cast<f64x2*>(out_lr) + o);
-                __builtin_nontemporal_store(hh, out_hops + o);
-            } else {
-                out_lr[o] = make_double2(lat, rel);
-                out_hops[o] = hh;
-            }
-            if (lat >= 0.0) atomicMin(&L.rmin[j], d2bits(lat));  // row minimum (runahead)
-        }
-        __syncthreads();
         if ((int)tid < nk) {
-            if (out_rowmin) out_rowmin[ws.rowmap ? (int)ws.rowmap[r0 + tid] : r0 + (int)tid] = bits2d(L.rmin[tid]);
-            atomicMin(&stats[ST_GLOBAL_MIN], L.rmin[tid]);  // shd-topology.c:500-511
+            const unsigned long long rm =
+                shared ? __hip_atomic_load(reinterpret_cast<const unsigned long long*>(my_e + HB_RMIN) + tid,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : L.rmin[tid];
+            if (out_rowmin) out_rowmin[ws.rowmap ? (int)ws.rowmap[r0 + tid] : r0 + (int)tid] = bits2d(rm);
+            atomicMin(&stats[ST_GLOBAL_MIN], rm);  // shd-topology.c:500-511
         }
         __syncthreads();
         tick(3);
+        // the batch's rows are complete (every job's items done): one more finished batch for the
+        // helpers' exit condition
+        if (shared && tid == 0) atomicAdd(ws.board + (size_t)gridDim.x * kBoardWords, 1u);
         {
             // the distance lines this batch lowered from +inf back to +inf: only touched tail
             // vertices (their touched bit in D.pt), not the whole [V][K] block (64 MB at K = 8 per
@@ -2020,6 +2248,112 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             b[5] = L.ev[2] - b[5];
             b[6] = L.cnt[0] - b[6];
             b[7] = (unsigned long long)nk;
+        }
+    }
+    // ---------------- no batch left for this slot: help the running batches' jobs -------------
+    // A workgroup scans the board for the job with the most unclaimed items, acquires the owner's
+    // data, takes chunks of it (run_job), releases its own stores and adds its items to the job's
+    // done count; it stops when every batch of the launch is finished.  The scan is one wave's
+    // relaxed loads; an idle scan sleeps.
+    if (ws.board) {
+        const unsigned long long th0 = wall_clock64();
+        const uint32_t nbat = (uint32_t)((nsrc + kf - 1) / kf);
+        const uint32_t* const bdone = ws.board + (size_t)gridDim.x * kBoardWords;
+        unsigned long long tprog = th0;
+        uint32_t lastDone = 0;
+        for (;;) {
+            if (tid < 64) {
+                uint32_t bo = kJobNone, brem = 0;
+                unsigned long long bc = 0;
+                for (uint32_t o = tid; o < gridDim.x; o += 64) {
+                    if (o == (uint32_t)slot) continue;
+                    const unsigned long long c = hb_cur(ws.board + (size_t)o * kBoardWords);
+                    const uint32_t n = (uint32_t)(c >> 24) & 0xFFFFFFu, x = (uint32_t)c & 0xFFFFFFu;
+                    const uint32_t rem = (c >> 48) != 0ull && x < n ? n - x : 0u;
+                    if (rem > brem) {
+                        brem = rem;
+                        bo = o;
+                        bc = c;
+                    }
+                }
+                // the wave's largest (lowest lane on ties)
+#pragma unroll
+                for (int d = 32; d > 0; d >>= 1) {
+                    const uint32_t r2 = __shfl_xor(brem, d, 64), o2 = __shfl_xor(bo, d, 64);
+                    const unsigned long long c2 = __shfl_xor(bc, d, 64);
+                    if (r2 > brem || (r2 == brem && o2 < bo)) {
+                        brem = r2;
+                        bo = o2;
+                        bc = c2;
+                    }
+                }
+                if (tid == 0) {
+                    L.hjob = brem ? bo : kJobNone;
+                    L.hd[0] = (uint32_t)(bc >> 48);
+                    L.hd[2] = (uint32_t)(bc >> 24) & 0xFFFFFFu;
+                    L.hflag = ld_l2_u32(bdone) >= nbat ? 1u : 0u;
+                }
+            }
+            __syncthreads();
+            const uint32_t o = L.hjob;
+            if (L.hflag) break;
+            if (o == kJobNone) {
+                if (tid == 0) {
+                    const uint32_t dn = ld_l2_u32(bdone);
+                    const unsigned long long t = wall_clock64();
+                    if (dn != lastDone) {
+                        lastDone = dn;
+                        tprog = t;
+                    } else if (t - tprog > kHbSpinTicks) {
+                        atomicAdd(&stats[ST_HB_ERR], 1ull);
+                        L.hflag = 1u;
+                    }
+                    __builtin_amdgcn_s_sleep(32);
+                }
+                __syncthreads();
+                if (L.hflag) break;
+                continue;
+            }
+            // acquire the owner's data (its stores precede the cursor store we read), then its
+            // descriptor; a descriptor of another job than the cursor's: scan again
+            uint32_t* const eo = ws.board + (size_t)o * kBoardWords;
+            if (tid == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const uint32_t sq = ld_l2_u32(eo + HB_SEQ);
+                L.hd[1] = ld_l2_u32(eo + HB_KIND);
+                L.hd[3] = ld_l2_u32(eo + HB_EP);
+                L.hd[4] = ld_l2_u32(eo + HB_R0);
+                L.hd[5] = ld_l2_u32(eo + HB_NK);
+                L.hd[6] = ld_l2_u32(eo + HB_LIST);
+                L.hd[7] = sq == L.hd[0] && L.hd[5] >= 1u && L.hd[5] <= (uint32_t)K ? 1u : 0u;
+                L.jtaken = 0;
+            }
+            __syncthreads();
+            if (!L.hd[7]) continue;
+            const uint32_t hseq = L.hd[0], hkind = L.hd[1], hn = L.hd[2], hep = L.hd[3];
+            const uint32_t hr0 = L.hd[4], hnk = L.hd[5], hlist = L.hd[6];
+            if (tid < hnk) L.src[tid] = sources[hr0 + tid];
+            __syncthreads();
+            run_job(o, hseq, hkind, hn, hep, hr0, hnk, hlist);
+            // release this workgroup's stores (records, S entries, table rows), then count them
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                if (L.jtaken) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    atomicAdd(eo + HB_DONE, L.jtaken);
+                    L.hitems[hkind == kJobEpi ? 1 : 0] += L.jtaken;
+                }
+                tprog = wall_clock64();
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            atomicAdd(&stats[ST_T_HELP], wall_clock64() - th0);
+            atomicAdd(&stats[ST_HELP_ITEMS], L.hitems[0]);
+            atomicAdd(&stats[ST_HELP_ITEMS + 1], L.hitems[1]);
         }
     }
     __syncthreads();
@@ -2366,7 +2700,8 @@ static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32
                                  unsigned long long* d_stats, hipStream_t stream) {
     if (kf < 1 || kf > K) return hipErrorInvalidValue;
     const int nb = (nsrc + kf - 1) / kf;
-    const int grid = ws.slots < nb ? ws.slots : nb;
+    // with the help board every slot runs: the ones without a batch help the others' jobs
+    const int grid = ws.board ? ws.slots : (ws.slots < nb ? ws.slots : nb);
     if (grid < 1) return hipSuccess;
     if ((int64_t)plan.H > g.V || plan.P > plan.H || plan.bytes > kBMaxLds ||
         blayout<K>(plan.H, plan.P).bytes != plan.bytes || ws.K != K)
