@@ -168,6 +168,10 @@ struct LdsB {
     // {seq, kind, items, tag, first position, sources, list, valid}, "every batch done"; items a
     // helper took (walk start pairs, epilogue items)
     uint32_t jseq, jcur, jtaken;
+    // the workgroup's lease of the current job (board launches): {next item, end} packed, one
+    // wave refilling it from the board at a time, the job used up
+    unsigned long long lease;
+    uint32_t lrefill, ljdone;
     uint32_t hjob, hflag;
     uint32_t hd[8];
     unsigned long long hitems[2];
@@ -984,12 +988,18 @@ enum {
     HB_NK = 7,     //   its sources
     HB_LIST = 8,   //   walk jobs: 0 = start list in qa, 1 = in qb
     HB_SCNT = 9,   // walk jobs: entries reserved in the slot's S list (blocks of 64)
+    HB_HELP = 10,  // helping workgroups on this entry now (any job; at most kMaxHelpers)
     HB_RMIN = 16   // u64[16]: epilogue row minima (words 16-47)
 };
+// global words after the entries: batches finished, jobs published (idle helpers poll these two
+// words and scan the entries only when a job was published)
+enum { HBG_DONE = 0, HBG_PUB = 1 };
 constexpr uint32_t kJobWalkSync = 1;  // first-level walks (groups of K lanes start together)
 constexpr uint32_t kJobWalk = 2;      // later levels
 constexpr uint32_t kJobEpi = 3;       // per-target epilogue
-constexpr uint32_t kJobChunk = 256;   // items a wave claims at a time (4 per lane)
+constexpr uint32_t kJobChunk = 256;   // items a wave takes at a time from its workgroup's lease
+constexpr uint32_t kLeaseChunk = 4096; // items a workgroup claims on the board at a time
+constexpr uint32_t kMaxHelpers = 6;   // helping workgroups per entry (CAS traffic, S-list holes)
 constexpr unsigned long long kHbSpinTicks = 2000000000ull;  // 20 s at 100 MHz: a bound, not a wait
 constexpr uint32_t kJobNone = 0xFFFFFFFFu;
 constexpr uint32_t kNoPairS = 0xFFFFFFFFu;
@@ -1133,12 +1143,40 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         uint32_t* const precwO = reinterpret_cast<uint32_t*>(precO);
         const uint32_t eptv = epv | kTagClaim;
         uint32_t taken = 0;
-        // the wave's next chunk of the job: its first item (kJobNone: used up) and *cnt items
+        // The wave's next chunk of the job: its first item (kJobNone: used up) and *cnt items.
+        // Board launches: waves take kJobChunk items from the workgroup's lease (LDS); the wave
+        // that finds it used up refills it by one CAS on the board (kLeaseChunk items, counted
+        // in L.jtaken: the workgroup processes every leased item) while the others wait.
         auto grab = [&](uint32_t* cnt) -> uint32_t {
             uint32_t b = kJobNone, c = 0;
             if (lane == 0) {
                 if (shared) {
-                    b = hb_grab(eo, seq, kJobChunk, &c);
+                    for (;;) {
+                        const unsigned long long x = atomicAdd(&L.lease, (unsigned long long)kJobChunk);
+                        const uint32_t nx = (uint32_t)x, en = (uint32_t)(x >> 32);
+                        if (nx < en) {
+                            b = nx;
+                            c = min(kJobChunk, en - nx);
+                            break;
+                        }
+                        if (__hip_atomic_load(&L.ljdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                        if (atomicCAS(&L.lrefill, 0u, 1u) == 0u) {
+                            uint32_t gc = 0;
+                            const uint32_t gb = hb_grab(eo, seq, kLeaseChunk, &gc);
+                            if (gb == kJobNone) {
+                                __hip_atomic_store(&L.ljdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            } else {
+                                atomicAdd(&L.jtaken, gc);
+                                b = gb;
+                                c = min(kJobChunk, gc);
+                                atomicExch(&L.lease, ((unsigned long long)(gb + gc) << 32) | (gb + c));
+                            }
+                            __hip_atomic_store(&L.lrefill, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            break;
+                        }
+                        while (__hip_atomic_load(&L.lrefill, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))
+                            __builtin_amdgcn_s_sleep(1);
+                    }
                 } else {
                     const uint32_t x = atomicAdd(&L.jcur, kJobChunk);
                     if (x < n) {
@@ -1401,7 +1439,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 }
             }
         }
-        if (lane == 0 && taken) atomicAdd(&L.jtaken, taken);
+        if (!shared && lane == 0 && taken) atomicAdd(&L.jtaken, taken);
     };
 
     for (;;) {
@@ -1781,6 +1819,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 L.jtaken = 0;
                 L.jcur = 0;
                 L.qtail = 0;
+                L.lease = 0ull;
+                L.lrefill = 0;
+                L.ljdone = 0;
                 if (shared) {
                     __hip_atomic_store(my_e + HB_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(my_e + HB_SEQ, L.jseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1799,6 +1840,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     __hip_atomic_store(reinterpret_cast<unsigned long long*>(my_e + HB_CUR),
                                        ((unsigned long long)L.jseq << 48) | ((unsigned long long)n << 24),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    atomicAdd(ws.board + (size_t)gridDim.x * kBoardWords + HBG_PUB, 1u);
                 } else if (kind == kJobEpi) {
                     for (int jj = 0; jj < K; jj++) L.rmin[jj] = kInfBits;
                 }
@@ -1813,7 +1855,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 atomicAdd(my_e + HB_DONE, L.jtaken);
                 const unsigned long long t0 = wall_clock64();
                 while (ld_l2_u32(my_e + HB_DONE) < n) {
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(4);
                     if (wall_clock64() - t0 > kHbSpinTicks) {
                         atomicAdd(&stats[ST_HB_ERR], 1ull);
                         break;
@@ -2192,7 +2234,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         tick(3);
         // the batch's rows are complete (every job's items done): one more finished batch for the
         // helpers' exit condition
-        if (shared && tid == 0) atomicAdd(ws.board + (size_t)gridDim.x * kBoardWords, 1u);
+        if (shared && tid == 0) atomicAdd(ws.board + (size_t)gridDim.x * kBoardWords + HBG_DONE, 1u);
         {
             // the distance lines this batch lowered from +inf back to +inf: only touched tail
             // vertices (their touched bit in D.pt), not the whole [V][K] block (64 MB at K = 8 per
@@ -2258,25 +2300,48 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     if (ws.board) {
         const unsigned long long th0 = wall_clock64();
         const uint32_t nbat = (uint32_t)((nsrc + kf - 1) / kf);
-        const uint32_t* const bdone = ws.board + (size_t)gridDim.x * kBoardWords;
-        unsigned long long tprog = th0;
-        uint32_t lastDone = 0;
+        const uint32_t* const gw = ws.board + (size_t)gridDim.x * kBoardWords;
+        unsigned long long tprog = th0;  // (thread 0) the last progress seen
+        uint32_t lastDone = 0, lastPub = 0xFFFFFFFFu;
+        bool rescan = true;  // (thread 0) scan the entries in the next round
         for (;;) {
-            if (tid < 64) {
+            // thread 0: finished batches and published jobs (two words); the entries only when a
+            // job was published since the last scan, or after a scan found a job to join
+            if (tid == 0) {
+                L.hjob = kJobNone;
+                const uint32_t dn = ld_l2_u32(gw + HBG_DONE), pb = ld_l2_u32(gw + HBG_PUB);
+                L.hflag = dn >= nbat ? 1u : 0u;
+                if (pb != lastPub) rescan = true;
+                lastPub = pb;
+                const unsigned long long t = wall_clock64();
+                if (dn != lastDone) {
+                    lastDone = dn;
+                    tprog = t;
+                } else if (t - tprog > kHbSpinTicks) {
+                    atomicAdd(&stats[ST_HB_ERR], 1ull);
+                    L.hflag = 1u;
+                }
+                L.hd[7] = rescan ? 1u : 0u;
+            }
+            __syncthreads();
+            if (L.hflag) break;
+            if (L.hd[7] && tid < 64) {
+                // the entry with the most unclaimed items among those with room for a helper
                 uint32_t bo = kJobNone, brem = 0;
                 unsigned long long bc = 0;
                 for (uint32_t o = tid; o < gridDim.x; o += 64) {
                     if (o == (uint32_t)slot) continue;
-                    const unsigned long long c = hb_cur(ws.board + (size_t)o * kBoardWords);
+                    const uint32_t* e = ws.board + (size_t)o * kBoardWords;
+                    const unsigned long long c = hb_cur(e);
                     const uint32_t n = (uint32_t)(c >> 24) & 0xFFFFFFu, x = (uint32_t)c & 0xFFFFFFu;
-                    const uint32_t rem = (c >> 48) != 0ull && x < n ? n - x : 0u;
+                    uint32_t rem = (c >> 48) != 0ull && x < n ? n - x : 0u;
+                    if (rem && ld_l2_u32(e + HB_HELP) >= kMaxHelpers) rem = 0;
                     if (rem > brem) {
                         brem = rem;
                         bo = o;
                         bc = c;
                     }
                 }
-                // the wave's largest (lowest lane on ties)
 #pragma unroll
                 for (int d = 32; d > 0; d >>= 1) {
                     const uint32_t r2 = __shfl_xor(brem, d, 64), o2 = __shfl_xor(bo, d, 64);
@@ -2288,31 +2353,28 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     }
                 }
                 if (tid == 0) {
-                    L.hjob = brem ? bo : kJobNone;
-                    L.hd[0] = (uint32_t)(bc >> 48);
-                    L.hd[2] = (uint32_t)(bc >> 24) & 0xFFFFFFu;
-                    L.hflag = ld_l2_u32(bdone) >= nbat ? 1u : 0u;
+                    if (brem) {
+                        // join it unless the helpers' cap was reached meanwhile
+                        uint32_t* e = ws.board + (size_t)bo * kBoardWords;
+                        if (atomicAdd(e + HB_HELP, 1u) < kMaxHelpers) {
+                            L.hjob = bo;
+                            L.hd[0] = (uint32_t)(bc >> 48);
+                            L.hd[2] = (uint32_t)(bc >> 24) & 0xFFFFFFu;
+                        } else {
+                            atomicSub(e + HB_HELP, 1u);
+                        }
+                    }
+                    rescan = brem != 0;  // found one: look again right after it
                 }
             }
             __syncthreads();
             const uint32_t o = L.hjob;
-            if (L.hflag) break;
             if (o == kJobNone) {
                 if (tid == 0) {
-                    const uint32_t dn = ld_l2_u32(bdone);
-                    const unsigned long long t = wall_clock64();
-                    if (dn != lastDone) {
-                        lastDone = dn;
-                        tprog = t;
-                    } else if (t - tprog > kHbSpinTicks) {
-                        atomicAdd(&stats[ST_HB_ERR], 1ull);
-                        L.hflag = 1u;
-                    }
-                    __builtin_amdgcn_s_sleep(32);
+                    __builtin_amdgcn_s_sleep(127);
+                    __builtin_amdgcn_s_sleep(127);
                 }
-                __syncthreads();
-                if (L.hflag) break;
-                continue;
+                continue;  // (the loop head's barrier)
             }
             // acquire the owner's data (its stores precede the cursor store we read), then its
             // descriptor; a descriptor of another job than the cursor's: scan again
@@ -2328,14 +2390,18 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 L.hd[6] = ld_l2_u32(eo + HB_LIST);
                 L.hd[7] = sq == L.hd[0] && L.hd[5] >= 1u && L.hd[5] <= (uint32_t)K ? 1u : 0u;
                 L.jtaken = 0;
+                L.lease = 0ull;
+                L.lrefill = 0;
+                L.ljdone = 0;
             }
             __syncthreads();
-            if (!L.hd[7]) continue;
             const uint32_t hseq = L.hd[0], hkind = L.hd[1], hn = L.hd[2], hep = L.hd[3];
             const uint32_t hr0 = L.hd[4], hnk = L.hd[5], hlist = L.hd[6];
-            if (tid < hnk) L.src[tid] = sources[hr0 + tid];
-            __syncthreads();
-            run_job(o, hseq, hkind, hn, hep, hr0, hnk, hlist);
+            if (L.hd[7]) {
+                if (tid < hnk) L.src[tid] = sources[hr0 + tid];
+                __syncthreads();
+                run_job(o, hseq, hkind, hn, hep, hr0, hnk, hlist);
+            }
             // release this workgroup's stores (records, S entries, table rows), then count them
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -2346,6 +2412,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     atomicAdd(eo + HB_DONE, L.jtaken);
                     L.hitems[hkind == kJobEpi ? 1 : 0] += L.jtaken;
                 }
+                atomicSub(eo + HB_HELP, 1u);
                 tprog = wall_clock64();
             }
             __syncthreads();
