@@ -1161,6 +1161,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         }
                         if (__hip_atomic_load(&L.ljdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                         if (atomicCAS(&L.lrefill, 0u, 1u) == 0u) {
+                            // another wave may have installed a fresh lease between our look
+                            // and the lock: refill only a lease still used up
+                            const unsigned long long y = __hip_atomic_load(
+                                &L.lease, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if ((uint32_t)y < (uint32_t)(y >> 32)) {
+                                __hip_atomic_store(&L.lrefill, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                continue;
+                            }
                             uint32_t gc = 0;
                             const uint32_t gb = hb_grab(eo, seq, kLeaseChunk, &gc);
                             if (gb == kJobNone) {

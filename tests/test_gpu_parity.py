@@ -568,3 +568,33 @@ def test_device_option_after_topology_new_builds_on_that_device(tmp_path):
     assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
     assert np.array_equal(hops, ohops.astype(np.uint16))
+
+
+@pytest.mark.parametrize("integer", [False, True])
+def test_help_board_tables_equal_unshared(integer):
+    """The help board (option share, default on): workgroups out of batches take part in the
+    running batches' parent walks and epilogues (cross-workgroup jobs: leases claimed by CAS,
+    release / acquire fences around every hand-off).  Repeated builds with helpers active must
+    equal the unshared build and the oracle bit for bit, with no board error and no failed pair."""
+    top, g = synthetic_pair(seed=43, n_routers=20000, n_poi=400, n_edges=200000, integer=integer)
+    top.set_option("tie_dense", 0)
+    otop, ips, verts = attach_hosts(top, g, 1200, type_hints=["client", "relay", "server"])
+    top.set_option("share", 0)
+    a0, lat0, rel0, hops0 = top.table()
+    helped = 0
+    top.set_option("share", 1)
+    for rep in range(4):
+        top.rebuild()
+        a, lat, rel, hops = top.table()
+        st = top.stats()
+        assert st["errors"] == 0 and st["help_board_errors"] == 0
+        helped += st["help_items"][0] + st["help_items"][1]
+        assert np.array_equal(a, a0)
+        assert np.array_equal(lat.view(np.uint64), lat0.view(np.uint64))
+        assert np.array_equal(rel.view(np.uint64), rel0.view(np.uint64))
+        assert np.array_equal(hops, hops0)
+    assert helped > 0  # the launches had idle workgroups that took items
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(lat0.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel0.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops0, ohops.astype(np.uint16))
