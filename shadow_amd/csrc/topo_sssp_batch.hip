@@ -1143,6 +1143,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         uint32_t* const precwO = reinterpret_cast<uint32_t*>(precO);
         const uint32_t eptv = epv | kTagClaim;
         uint32_t taken = 0;
+        // a lease leaves room for helpers on a small job: an eighth of it, 256 .. kLeaseChunk
+        const uint32_t lease_chunk = min(kLeaseChunk, max(kJobChunk, (n / 8u + kJobChunk - 1u) / kJobChunk * kJobChunk));
         // The wave's next chunk of the job: its first item (kJobNone: used up) and *cnt items.
         // Board launches: waves take kJobChunk items from the workgroup's lease (LDS); the wave
         // that finds it used up refills it by one CAS on the board (kLeaseChunk items, counted
@@ -1170,7 +1172,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                 continue;
                             }
                             uint32_t gc = 0;
-                            const uint32_t gb = hb_grab(eo, seq, kLeaseChunk, &gc);
+                            const uint32_t gb = hb_grab(eo, seq, lease_chunk, &gc);
                             if (gb == kJobNone) {
                                 __hip_atomic_store(&L.ljdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             } else {
