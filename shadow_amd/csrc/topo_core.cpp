@@ -349,6 +349,8 @@ struct _Topology {
     // rows [d*R, (d+1)*R) with its own stream / workspace (a peer Topology on that device),
     // RCCL all-gathers the rows into every device's table and all-reduces the minimum
     int devicesOpt = 1;        // option "devices"
+    int memShareDiv = 1;       // engines of this build sharing this engine's physical device: its
+                               // workspaces take that share of the device's free memory
     bool forceRccl = false;    // option "rccl": the RCCL exchange even with one device (tests)
     std::vector<Topology*> peers;      // devices 1..N-1
     std::vector<ncclComm_t> comms;     // one per device, ncclCommInitAll
@@ -900,7 +902,10 @@ int ensure_workspace(Topology* top, int nsrc) {
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     // memory already held by this workspace counts as available
     const size_t held = top->slots > 0 ? (size_t)top->slots * per_slot : 0;
-    int memcap = (int)std::max<size_t>(1, ((freeb + held) * 3 / 5) / per_slot);
+    // engines sharing one device (a multi-engine test configuration) size their workspaces at the
+    // same time: each takes its share
+    int memcap = (int)std::max<size_t>(
+        1, ((freeb + held) * 3 / 5) / (size_t)std::max(1, top->memShareDiv) / per_slot);
     want = std::min(want, memcap);
     want = std::max(1, std::min(want, std::max(1, units)));
     // hparN follows par_hubs: the kernel indexes the hints at slot * P * K with the current P
@@ -1909,6 +1914,11 @@ int build_multi(Topology* top) {
     for (int d = 0; d < N; d++) {
         phys[(size_t)d] = slot_engine(top, d)->device % ndev;
         for (int e = 0; e < d; e++) distinct = distinct && phys[(size_t)e] != phys[(size_t)d];
+    }
+    for (int d = 0; d < N; d++) {
+        int k = 0;
+        for (int e = 0; e < N; e++) k += phys[(size_t)e] == phys[(size_t)d];
+        slot_engine(top, d)->memShareDiv = k;
     }
     // 0) the graph is prepared once, on this engine's device, and copied to the peers
     {
