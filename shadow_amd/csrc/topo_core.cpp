@@ -1557,7 +1557,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 // batch position {source vertex, pi bits}
                 const char* btf = getenv("SHD_BATCH_TRACE");
                 const int64_t nbt = (rows + kf - 1) / kf;
-                if (btf && *btf) HIPCHK(hipMalloc((void**)&ws.btrace, 64 * (size_t)nbt));
+                if (btf && *btf) HIPCHK(hipMalloc((void**)&ws.btrace, 8 * kBTraceWords * (size_t)nbt));
                 bstep_mark(top, 2);
                 HIPCHK(launch_sssp_batch(K, dev_csr(top), ws, top->d_bsrc.p,
                                          top->d_srcsh.p, (int)rows, kf, top->d_targets.p, (int)A,
@@ -1567,8 +1567,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 HIPCHK(hipStreamSynchronize(st));  // the kernel's wall time goes to step 3
                 bstep_mark(top, 3);
                 if (ws.btrace) {
-                    std::vector<unsigned long long> bt((size_t)nbt * 8);
-                    HIPCHK(hipMemcpy(bt.data(), ws.btrace, 64 * (size_t)nbt, hipMemcpyDeviceToHost));
+                    std::vector<unsigned long long> bt((size_t)nbt * kBTraceWords);
+                    HIPCHK(hipMemcpy(bt.data(), ws.btrace, 8 * kBTraceWords * (size_t)nbt, hipMemcpyDeviceToHost));
                     HIPCHK(hipFree(ws.btrace));
                     ws.btrace = nullptr;
                     if (FILE* f = fopen(btf, "ab")) {

@@ -149,14 +149,17 @@ struct SlotWs {
     // output row of batch position p (sources are taken in a locality order, the table keeps
     // row order); nullptr = identity
     const uint32_t* rowmap = nullptr;
-    // diagnostic (SHD_BATCH_TRACE): per batch {wall_clock64 at dequeue, at its end, slot}
+    // diagnostic (SHD_BATCH_TRACE): per batch kBTraceWords u64 {wall_clock64 at dequeue, at its
+    // end, slot, near iterations, sweeps, expansions, relaxations, sources, ticks at the SSSP's,
+    // the parent pass' and the epilogue's end, 0}
     unsigned long long* btrace = nullptr;
     // help board (work sharing, topo_sssp_batch.hip): kBoardWords u32 per slot + one word of
     // finished batches, zeroed before every launch; nullptr = every batch's parent walks and
     // epilogue stay in its own workgroup
     uint32_t* board = nullptr;
 };
-constexpr int kBoardWords = 64;  // u32 words per slot entry of the help board (256 B)
+constexpr int kBoardWords = 64;
+constexpr int kBTraceWords = 12;  // u32 words per slot entry of the help board (256 B)
 
 // Incidence-order CSR of the heap replay (topo_replay.hip), relabelled vertex ids: row x holds
 // x's neighbours in igraph_incident order (ascending ORIGINAL neighbour id; directed graphs:

@@ -1464,12 +1464,12 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         const int nk = min(kf, nsrc - r0);
         if (tid == 0) L.tk = wall_clock64();
         if (ws.btrace && tid == 0) {
-            ws.btrace[8 * (size_t)bidx] = L.tk;
-            ws.btrace[8 * (size_t)bidx + 3] = L.ev[0];
-            ws.btrace[8 * (size_t)bidx + 4] = L.ev[1];
-            ws.btrace[8 * (size_t)bidx + 5] = L.ev[2];
-            ws.btrace[8 * (size_t)bidx + 6] = L.cnt[0];
-            ws.btrace[8 * (size_t)bidx + 2] = (unsigned long long)slot;
+            ws.btrace[kBTraceWords * (size_t)bidx] = L.tk;
+            ws.btrace[kBTraceWords * (size_t)bidx + 3] = L.ev[0];
+            ws.btrace[kBTraceWords * (size_t)bidx + 4] = L.ev[1];
+            ws.btrace[kBTraceWords * (size_t)bidx + 5] = L.ev[2];
+            ws.btrace[kBTraceWords * (size_t)bidx + 6] = L.cnt[0];
+            ws.btrace[kBTraceWords * (size_t)bidx + 2] = (unsigned long long)slot;
         }
 
         // ---------------- init: hubs in LDS, the tail's K-wide rows in HBM --------------------
@@ -1806,6 +1806,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             atomicOr(&stats[ST_OVERSITE], (unsigned long long)L.fover);
         }
         tick(1);
+        if (ws.btrace && tid == 0) ws.btrace[kBTraceWords * (size_t)bidx + 8] = L.tk;
 
         // ---------------- parents for the target chains of every source of the batch ---------
         // One level-synchronous pass over (vertex, source) pairs p = v * K + j (SURVEY.md A.3:
@@ -2222,6 +2223,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             if (tid == 0) L.pt[4] += wall_clock64() - tp0;  // next level
         }
         tick(2);
+        if (ws.btrace && tid == 0) ws.btrace[kBTraceWords * (size_t)bidx + 9] = L.tk;
 
         // ---------------- per-target latency / reliability / hops (shd-topology.c:561-671) ----
         // items (source j, target k) of the whole batch: a job (run_job), so idle workgroups take
@@ -2242,6 +2244,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         }
         __syncthreads();
         tick(3);
+        if (ws.btrace && tid == 0) ws.btrace[kBTraceWords * (size_t)bidx + 10] = L.tk;
         // the batch's rows are complete (every job's items done): one more finished batch for the
         // helpers' exit condition
         if (shared && tid == 0) atomicAdd(ws.board + (size_t)gridDim.x * kBoardWords + HBG_DONE, 1u);
@@ -2293,7 +2296,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         }
         tick(0);
         if (ws.btrace && tid == 0) {
-            unsigned long long* b = ws.btrace + 8 * (size_t)bidx;
+            unsigned long long* b = ws.btrace + kBTraceWords * (size_t)bidx;
             b[1] = L.tk;
             b[3] = L.ev[0] - b[3];
             b[4] = L.ev[1] - b[4];

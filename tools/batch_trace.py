@@ -17,8 +17,9 @@ i = 0
 launch = 0
 while i < len(raw):
     nb, kf, slots, rows = (int(x) for x in raw[i:i + 4])
-    bt = raw[i + 4:i + 4 + 8 * nb].reshape(nb, 8).astype(np.float64)
-    i += 4 + 8 * nb
+    W = 12  # kBTraceWords
+    bt = raw[i + 4:i + 4 + W * nb].reshape(nb, W).astype(np.float64)
+    i += 4 + W * nb
     sp = raw[i:i + 2 * rows].reshape(rows, 2)
     i += 2 * rows
     src = sp[:, 0]
@@ -27,6 +28,8 @@ while i < len(raw):
     t0, t1 = st.min(), en.max()
     span = (t1 - t0) * TICK_MS
     dur = (en - st) * TICK_MS
+    ph = np.stack([bt[:, 8] - st, bt[:, 9] - bt[:, 8], bt[:, 10] - bt[:, 9], en - bt[:, 10]],
+                  axis=1) * TICK_MS  # SSSP, parents, epilogue, reset
     used = np.unique(sl)
     last = np.array([en[sl == s].max() for s in used])
     first = np.array([st[sl == s].min() for s in used])
@@ -36,6 +39,10 @@ while i < len(raw):
     print("launch %d: %d batches of %d, %d slots used of %d, span %.2f ms" %
           (launch, nb, kf, len(used), slots, span))
     q = np.percentile(dur, [0, 10, 50, 90, 100])
+    slow = np.argsort(dur)[-max(1, nb // 20):]
+    print("  phases ms (SSSP, parents, epilogue, reset): mean %s; slowest 5 %% of batches %s" % (
+        " ".join("%.2f" % x for x in ph.mean(axis=0)),
+        " ".join("%.2f" % x for x in ph[slow].mean(axis=0))))
     print("  batch ms: min %.2f p10 %.2f median %.2f p90 %.2f max %.2f  mean %.2f" %
           (*q, dur.mean()))
     print("  busy %.1f %% of slots x span; idle tail mean %.2f ms max %.2f; idle head max %.2f ms" %
