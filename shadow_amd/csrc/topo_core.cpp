@@ -859,7 +859,8 @@ int batch_k(Topology* top) { return top->batchK; }  // 2, 4, 8 or 16 (shdtopo_se
 int64_t bitmap_words(int64_t n) { return (n + 31) / 32 + 64; }
 int64_t ring_entries(Topology* top, int K) {
     const int64_t V = top->g.V;
-    return V * (K + 1) + bitmap_words(V) + bitmap_words(V);
+    // + the two pending-vertex lists of the sweeps (V entries each) and alignment slack
+    return V * (K + 1) + bitmap_words(V) + bitmap_words(V) + 2 * V + 64;
 }
 int64_t queue_stride(Topology* top, int K) {  // u64 per slot of each near queue / pair list
     const int64_t V = top->g.V;

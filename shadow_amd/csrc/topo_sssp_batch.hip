@@ -76,6 +76,9 @@ using namespace dev;
 #else
 #define BT_TICK(i) do { } while (0)
 #endif
+#ifndef SHD_SWEEP_LIST
+#define SHD_SWEEP_LIST 1  // tail sweeps over a list of the pending vertices (not the whole bitmap)
+#endif
 #ifndef SHD_PB_SPLIT
 #define SHD_PB_SPLIT 1  // phase-B rounds of tail-target pairs first, then rounds of LDS-hub pairs
 #endif
@@ -167,6 +170,8 @@ struct LdsB {
     // items this workgroup took of the current job; a helper's chosen entry, its descriptor
     // {seq, kind, items, tag, first position, sources, list, valid}, "every batch done"; items a
     // helper took (walk start pairs, epilogue items)
+    // pending-vertex list (SHD_SWEEP_LIST): entries, entries of the next list, which buffer
+    uint32_t plen, plen2, plsel;
     uint32_t jseq, jcur, jtaken;
     // the workgroup's lease of the current job (board launches): {next item, end} packed, one
     // wave refilling it from the board at a time, the job used up
@@ -606,7 +611,8 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                                               typename MaskOps<K>::M* mcur,
                                               typename MaskOps<K>::M* hdef,
                                               typename MaskOps<K>::M* mnxt, uint32_t* qout,
-                                              uint32_t qcap, uint32_t* hq, const BBuckets& B) {
+                                              uint32_t qcap, uint32_t* hq, const BBuckets& B,
+                                              uint32_t* plst) {
     using MO = MaskOps<K>;
     static_assert(64 % K == 0, "a wave holds whole edge groups");
     static_assert(UA >= 1 && (UA & (UA - 1)) == 0, "the phase-B edge search halves UA * 64");
@@ -831,6 +837,9 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             unsigned long long old[RB];
             uint32_t pm[RB];  // the mask word's previous bits (first: push), or ~0: no mask op
             bool hfv[RB];     // a hub's first deferral
+            uint32_t pold[RB];  // SHD_SWEEP_LIST: the pending word's bits before a first reach past
+                                // cb set its pending bit (not set before: the vertex joins the
+                                // pending list), or 0x55555555 (no such reach)
 #pragma unroll
             for (int rr = 0; rr < RB; rr++) {
                 const bool on = ab[rr] != ~0ull;
@@ -879,7 +888,13 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 // first reach: touched (bit 1), and pending when past cb (bit 0): one atomic
                 wl_count(L, WL_RELAX_TOUCH, head && gf, &D.pt[n[rr] >> 4]);
                 wl_count(L, WL_RELAX_MASK, head && gm && !hub, mnxt + n[rr]);
-                if (head && gf) (void)atomicOr(&D.pt[n[rr] >> 4], gf << (2u * (n[rr] & 15u)));
+                pold[rr] = 0x55555555u;
+                if (head && gf) {
+                    if (SHD_SWEEP_LIST && (gf & 1u))
+                        pold[rr] = atomicOr(&D.pt[n[rr] >> 4], gf << (2u * (n[rr] & 15u)));
+                    else
+                        (void)atomicOr(&D.pt[n[rr] >> 4], gf << (2u * (n[rr] & 15u)));
+                }
                 pm[rr] = ~0u;
                 hfv[rr] = false;
                 if (head && gm) {
@@ -908,6 +923,9 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 }
                 wpush<K>(L, pm[rr] == 0u, n[rr], qout, &L.qtail, qcap, &L.fover, 1u);
                 wpush<K>(L, hfv[rr], n[rr], hq, &L.htail, D.H, &L.fover, 1u);
+                if (SHD_SWEEP_LIST)
+                    wpush<K>(L, !((pold[rr] >> (2u * (n[rr] & 15u))) & 1u), n[rr], plst, &L.plen,
+                             qcap, &L.fover, 2u);
             }
             }
             if (__ballot(fm != kNoBucket)) {
@@ -1087,6 +1105,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     const uint32_t pw = (uint32_t)((V + 31) / 32);  // word pairs of the pending / touched bits
     unsigned long long* const pt2 = reinterpret_cast<unsigned long long*>(D.pt);
     constexpr unsigned long long kPendBits = 0x5555555555555555ull;
+    // the pending-vertex lists (SHD_SWEEP_LIST), V entries each, after the two bitmaps' words
+    uint32_t* const plist0 = D.pt + 2 * (size_t)((V + 31) / 32 + 64);
+    uint32_t* const plist1 = plist0 + V;
     const uint32_t pcap = (uint32_t)(V * K);
 
     uint32_t iter = ctr[0];
@@ -1492,6 +1513,9 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         if (tid == 0) {
             L.fminb = kNoBucket;
             L.fover = 0;
+            L.plen = 0;
+            L.plen2 = 0;
+            L.plsel = 0;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1502,6 +1526,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             else {
                 D.dist[(size_t)s * K + tid] = 0ull;
                 atomicOr(&D.pt[s >> 4], 3u << (2u * (s & 15u)));
+                if (SHD_SWEEP_LIST) plist0[atomicAdd(&L.plen, 1u)] = s;  // distinct sources
             }
             atomicMin(&L.fminb, bkt(0.0, L.sh[tid], B.inv_delta));
         }
@@ -1546,11 +1571,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
 #ifndef SHD_BATCH_NOWAVE
                 if (!hubs)
                     relax_batch_t<K, SHD_BATCH_U, true>(src, ns, g, L, D, mcur, hdef, mnxt, qout,
-                                                        cap, hfill, B);
+                                                        cap, hfill, B, L.plsel ? plist1 : plist0);
                 else
 #endif
                     relax_batch_t<K, SHD_BATCH_U>(src, ns, g, L, D, mcur, hdef, mnxt, qout, cap,
-                                                  hfill, B);
+                                                  hfill, B, L.plsel ? plist1 : plist0);
                 nq = min(L.qtail, cap);
                 if (tid == 0 && first_it) {
                     L.dg[2] += L.cnt[2] - e0;
@@ -1626,6 +1651,110 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     km = wave_min_u32(km);
                     if ((tid & 63) == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
                 }
+#if SHD_SWEEP_LIST
+                // tail: the pending-vertex list (every tail vertex whose pending bit is set, once:
+                // a relaxation appends a vertex when its first reach past cb sets the bit).  Each
+                // wave takes chunks of the list into its LDS slice (the chunk buffers are idle
+                // here), classifies their lines (LPV lanes x 16 B per vertex), appends the
+                // vertices that still hold a pair past nb to the next list and clears the others'
+                // pending bits.  Round 5: the bitmap version below read all V / 16 bitmap words
+                // per sweep, one round trip per 128 word pairs per wave.
+                {
+                    constexpr uint32_t NW = kSsspBlock / 64;
+                    constexpr uint32_t VPW = 64 / LPV;  // vertices per wave instruction
+                    constexpr uint32_t kKeep = 0x80000000u;  // slice entry: the vertex stays pending
+                    constexpr uint32_t kSweepU32 =
+                        (uint32_t)((offsetof(LdsB<K>, val) + sizeof(L.val) - offsetof(LdsB<K>, off)) / 4);
+                    constexpr uint32_t kClW = kSweepU32 / NW;
+                    constexpr uint32_t kCh = kClW / 64u * 64u;  // list entries per wave chunk
+                    static_assert(kCh >= 64, "sweep slice");
+                    const uint32_t wv = tid >> 6, lane = tid & 63u;
+                    uint32_t* clw = L.off + wv * kClW;
+                    const uint32_t np = min(L.plen, cap);
+                    const uint32_t* psrc = L.plsel ? plist1 : plist0;
+                    uint32_t* pdst = L.plsel ? plist0 : plist1;
+                    for (uint32_t base = wv * kCh; base < np; base += NW * kCh) {
+                        const uint32_t n = min(kCh, np - base);
+                        for (uint32_t i = lane; i < n; i += 64) {
+                            rl_count(L, RL_SWEEP, true, psrc + base + i);
+                            clw[i] = ld_l2_u32(psrc + base + i);
+                        }
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        __builtin_amdgcn_wave_barrier();
+                        for (uint32_t vb = 0; vb < n; vb += VPW * SU) {
+                            unsigned long long d[SU][2];
+                            uint32_t vv[SU];
+                            float k0[SU];
+#pragma unroll
+                            for (int u = 0; u < SU; u++) {
+                                const uint32_t e = vb + (uint32_t)u * VPW + lane / LPV;
+                                vv[u] = e < n ? clw[e] : 0xFFFFFFFFu;
+                                rl_count(L, RL_SWEEP, e < n, reinterpret_cast<const char*>(D.dist) + ((size_t)(e < n ? vv[u] : 0u) * LPV + lane % LPV) * 16);
+                                rl_count(L, RL_SWEEP, e < n, g.kap0 + (e < n ? vv[u] : 0u));
+                                k0[u] = g.kap0[e < n ? vv[u] : 0u];
+                                d[u][0] = d[u][1] = kInfBits;
+                                if (e < n) {
+                                    typedef unsigned long long u64x2
+                                        __attribute__((ext_vector_type(2)));
+                                    const u64x2 x = __builtin_nontemporal_load(
+                                        reinterpret_cast<const u64x2*>(D.dist) +
+                                        (size_t)vv[u] * LPV + lane % LPV);
+                                    d[u][0] = x.x;
+                                    d[u][1] = x.y;
+                                }
+                            }
+                            uint32_t km = kNoBucket;
+#pragma unroll
+                            for (int u = 0; u < SU; u++) {
+                                const uint32_t jl = 2 * (lane % LPV);
+                                uint32_t m = 0, keep = 0;
+#pragma unroll
+                                for (int h = 0; h < 2; h++) {
+                                    if (d[u][h] == kInfBits) continue;
+                                    const uint32_t b = bkt(bits2d(d[u][h]), L.sh[jl + h], B.inv_delta);
+                                    if (b == nb) {
+                                        if (kappa_useful(k0[u], L.dh0[jl + h], bits2d(d[u][h]), g.piMax))
+                                            m |= 1u << (jl + h);
+                                    } else if (b > nb) {
+                                        keep = 1u;
+                                        if (b < km) km = b;
+                                    }
+                                }
+#pragma unroll
+                                for (uint32_t o = 1; o < LPV; o <<= 1) {
+                                    m |= __shfl_xor(m, (int)o, 64);
+                                    keep |= __shfl_xor(keep, (int)o, 64);
+                                }
+                                const uint32_t v = vv[u];
+                                const uint32_t e = vb + (uint32_t)u * VPW + lane / LPV;
+                                const bool ok = (lane % LPV) == 0 && v != 0xFFFFFFFFu;
+                                const bool lead = ok && m != 0u;
+                                wl_count(L, WL_MASK_ST, lead, mcur + (lead ? v : 0u));
+                                if (lead) mcur[v] = (M)m;
+                                if (ok && keep) clw[e] = v | kKeep;
+                                wpush<K>(L, lead, v, qin, &L.qtail, cap, &L.fover, 32u);
+                            }
+                            km = wave_min_u32(km);
+                            if (lane == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
+                        }
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        __builtin_amdgcn_wave_barrier();
+                        // survivors to the next list; the others leave the pending set
+                        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+                            const uint32_t i = i0 + lane;
+                            const uint32_t x = i < n ? clw[i] : 0u;
+                            const bool keep = i < n && (x & kKeep);
+                            const uint32_t v = x & ~kKeep;
+                            wpush<K>(L, keep, v, pdst, &L.plen2, cap, &L.fover, 64u);
+                            wl_count(L, WL_PEND_ST, i < n && !keep, D.pt + (v >> 4));
+                            if (i < n && !keep) atomicAnd(&D.pt[v >> 4], ~(1u << (2u * (v & 15u))));
+                        }
+                        // the slice is refilled by the next chunk
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+#else
                 // tail: only the vertices whose pending bit is set (~9 % of them per sweep on
                 // C4, instead of streaming all [V][K] rows).  A round takes one bitmap word per
                 // thread, compacts the set bits' vertices into LDS (the chunk buffers are idle
@@ -1781,11 +1910,17 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         }
                     }
                 }
+#endif
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             nq = min(L.qtail, cap);
             if (tid == 0) L.cnt[1] += nq;
+            if (SHD_SWEEP_LIST && tid == 0) {  // the survivors' list is the current one
+                L.plen = min(L.plen2, cap);
+                L.plen2 = 0;
+                L.plsel ^= 1u;
+            }
             B.cb = nb;
             just_swept = true;
             if (tid == 0) {
