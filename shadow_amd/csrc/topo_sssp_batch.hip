@@ -77,7 +77,9 @@ using namespace dev;
 #define BT_TICK(i) do { } while (0)
 #endif
 #ifndef SHD_SWEEP_LIST
-#define SHD_SWEEP_LIST 1  // tail sweeps over a list of the pending vertices (not the whole bitmap)
+#define SHD_SWEEP_LIST 0  // 1: tail sweeps over a list of the pending vertices instead of the bitmap
+                          // (r05: full table 66.7 -> 74.7 ms -- the returning pending atomic in
+                          // phase B costs more than the bitmap scan it saves; kept off)
 #endif
 #ifndef SHD_PB_SPLIT
 #define SHD_PB_SPLIT 1  // phase-B rounds of tail-target pairs first, then rounds of LDS-hub pairs
