@@ -392,6 +392,9 @@ typedef struct {
     int64_t n_edges;     /* 10000000 undirected edges in total, incl. poi uplinks + self loops */
     int integer_latency; /* 1: latency ~ U{1..100} (heavy ties) */
     double alpha;        /* Chung-Lu endpoint weight ~ rank^(-alpha); 1/1.1 */
+    int directed;        /* 1: a directed topology -- every non-loop edge becomes two arcs, the
+                            reverse one with its own latency and loss draw (uplinks 5.0 both
+                            ways), so E = 2 x n_edges - n_poi (tools: directed-path probes) */
 } ShdSynthParams;
 Topology* shdtopo_new_synthetic(const ShdSynthParams* p);
 

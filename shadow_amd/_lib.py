@@ -64,7 +64,7 @@ class ShdStats(ctypes.Structure):
 
 class ShdSynthParams(ctypes.Structure):
     _fields_ = [("seed", u64), ("n_routers", i64), ("n_poi", i64), ("n_edges", i64),
-                ("integer_latency", ctypes.c_int), ("alpha", dbl)]
+                ("integer_latency", ctypes.c_int), ("alpha", dbl), ("directed", ctypes.c_int)]
 
 
 # every symbol include/shd_topology_abi.h declares: name -> (restype, argtypes)

@@ -237,6 +237,10 @@ struct _Topology {
     int64_t wsRing = 0;
     size_t wsHpar = 0;          // hub-hint entries per slot the workspace was sized for
     DevBuf<uint32_t> d_rowptr, d_adj;
+    // directed topologies: d_rowptr / d_adjo are the out-rows (relaxation, kappa copy, target
+    // fixpoint), d_rowptrIn / d_adj / d_aloss the in-rows (parent pass); undirected ones use
+    // d_rowptr / d_adj for both (d_adjo, d_rowptrIn empty) -- adj_out(), rowptr_in()
+    DevBuf<uint32_t> d_adjo, d_rowptrIn;
     DevBuf<uint32_t> d_adjk;  // rows re-sorted by kappa = w - pi(col) (batch relaxation copy)
     DevBuf<float> d_kap, d_ksum, d_kap0;  // kappa of d_adjk (f32, rounded down), per-vertex probes
     double meanLat = -1.0;
@@ -633,6 +637,36 @@ HubSegs hub_segs(Topology* top) {
     return h;
 }
 
+// out-rows (relaxation, kappa copy, target fixpoint) and in-rows (parent pass) of the prepared
+// graph: one adjacency serves both when undirected
+const uint32_t* adj_out(Topology* top) { return top->isDirected ? top->d_adjo.p : top->d_adj.p; }
+const uint32_t* rowptr_in(Topology* top) {
+    return top->isDirected ? top->d_rowptrIn.p : top->d_rowptr.p;
+}
+
+// segment tables of rows [0, H) of a device rowptr (host copy of its head)
+int make_hub_segs(const uint32_t* d_rowptr, uint32_t H, DevBuf<uint2>& dseg,
+                  DevBuf<uint4>& dmulti, uint32_t* nseg, uint32_t* nmulti, hipStream_t st) {
+    std::vector<uint32_t> head((size_t)H + 1);
+    HIPCHK(hipMemcpyAsync(head.data(), d_rowptr, 4 * ((size_t)H + 1), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<uint2> seg;
+    std::vector<uint4> multi;
+    hub_segments(head.data(), H, seg, multi);
+    dseg.release();
+    dmulti.release();
+    HIPCHK(dseg.ensure(seg.size()));
+    HIPCHK(hipMemcpyAsync(dseg.p, seg.data(), sizeof(uint2) * seg.size(), hipMemcpyHostToDevice, st));
+    if (!multi.empty()) {
+        HIPCHK(dmulti.ensure(multi.size()));
+        HIPCHK(hipMemcpyAsync(dmulti.p, multi.data(), sizeof(uint4) * multi.size(), hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    *nseg = (uint32_t)seg.size();
+    *nmulti = (uint32_t)multi.size();
+    return 0;
+}
+
 int upload_csr_impl(Topology* top);
 int upload_csr(Topology* top) {
     if (top->csrUploaded) return 0;
@@ -649,8 +683,7 @@ constexpr int64_t kGroupHubs = 16565;
 // sample rows of the tie probe (enqueue_rows): 8 batches of 8, one short launch
 constexpr int64_t kTieProbeRows = 64;
 
-// Graph preparation.  Directed topologies only run the heap replay (its out-edge
-// rows, upload_replay) and keep their labels.  Undirected ones are prepared on the GPU
+// Graph preparation.  Topologies are prepared on the GPU
 // (topo_prep.hip): the parsed edge arrays are copied to HBM once, and the relabel, the CSR, the
 // h0 distances and tree and the kappa-sorted relaxation copy are built there; the host keeps only
 // perm / inv / pi / the h0-tree parents (source ordering of the batched builds, the replay CSR).
@@ -664,44 +697,6 @@ int upload_csr_impl(Topology* top) {
     double host_ms = 0.0, copy_ms = 0.0;
     top->hp = std::make_shared<HostPrep>();
     top->csrHostRuns++;
-    if (top->isDirected) {
-        const auto th = clk::now();
-        top->hp->perm.resize((size_t)V);
-        std::iota(top->hp->perm.begin(), top->hp->perm.end(), 0);
-        top->hp->inv = top->hp->perm;
-        std::vector<double> selfLat((size_t)V, NAN), selfLoss((size_t)V, 0.0);
-        for (int64_t e = 0; e < g.E; e++) {
-            const int32_t a = g.eu[(size_t)e];
-            if (a == g.ev[(size_t)e] && std::isnan(selfLat[(size_t)a])) {
-                selfLat[(size_t)a] = g.elat[(size_t)e];
-                selfLoss[(size_t)a] = g.eloss[(size_t)e];
-            }
-        }
-        host_ms += ms_since(th);
-        const auto tc = clk::now();
-        const size_t E = (size_t)g.E;
-        HIPCHK(top->d_eu.ensure(E));
-        HIPCHK(top->d_ev.ensure(E));
-        HIPCHK(top->d_elat.ensure(E));
-        HIPCHK(top->d_eloss.ensure(E));
-        HIPCHK(top->d_inv.ensure((size_t)V));
-        HIPCHK(hipMemcpy(top->d_eu.p, g.eu.data(), 4 * E, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_ev.p, g.ev.data(), 4 * E, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_elat.p, g.elat.data(), 8 * E, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_eloss.p, g.eloss.data(), 8 * E, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_inv.p, top->hp->inv.data(), 4 * (size_t)V, hipMemcpyHostToDevice));
-        HIPCHK(top->d_vloss.ensure((size_t)V));
-        HIPCHK(top->d_selfLat.ensure((size_t)V));
-        HIPCHK(top->d_selfLoss.ensure((size_t)V));
-        HIPCHK(hipMemcpy(top->d_vloss.p, g.vloss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_selfLat.p, selfLat.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(top->d_selfLoss.p, selfLoss.data(), sizeof(double) * (size_t)V, hipMemcpyHostToDevice));
-        copy_ms += ms_since(tc);
-        top->stats.csr_host_ms = host_ms;
-        top->stats.csr_copy_ms = copy_ms;
-        top->csrUploaded = true;
-        return 0;
-    }
     const int64_t E = g.E;
     auto tstep = clk::now();
     for (double& x : top->stats.csr_step_ms) x = 0.0;
@@ -745,6 +740,9 @@ int upload_csr_impl(Topology* top) {
     HIPCHK(selfE.ensure((size_t)V));
     int64_t nadj = 0;
     HIPCHK(prep_degrees(V, E, eu.p, ev.p, deg.p, selfE.p, &nadj, st));
+    // a directed edge is one entry of its tail's out-row and one of its head's in-row
+    const bool dir = top->isDirected;
+    if (dir) nadj /= 2;
     const uint32_t H = (uint32_t)std::min<int64_t>(kGroupHubs, V);
     HIPCHK(dperm.ensure((size_t)V));
     HIPCHK(dinv.ensure((size_t)V));
@@ -758,50 +756,72 @@ int upload_csr_impl(Topology* top) {
     deg.release();
     selfE.release();
     vl0.release();
-    {
-        // the hub rows' segment tables (HubSegs) from the head of the rowptr
-        std::vector<uint32_t> head((size_t)H + 1);
-        HIPCHK(hipMemcpyAsync(head.data(), top->d_rowptr.p, 4 * ((size_t)H + 1), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        std::vector<uint2> seg;
-        std::vector<uint4> multi;
-        hub_segments(head.data(), H, seg, multi);
-        top->d_hseg.release();
-        top->d_hmulti.release();
-        HIPCHK(top->d_hseg.ensure(seg.size()));
-        HIPCHK(hipMemcpyAsync(top->d_hseg.p, seg.data(), sizeof(uint2) * seg.size(), hipMemcpyHostToDevice, st));
-        if (!multi.empty()) {
-            HIPCHK(top->d_hmulti.ensure(multi.size()));
-            HIPCHK(hipMemcpyAsync(top->d_hmulti.p, multi.data(), sizeof(uint4) * multi.size(), hipMemcpyHostToDevice, st));
-        }
-        HIPCHK(hipStreamSynchronize(st));
-        top->hsegRows = H;
-        top->hsegN = (uint32_t)seg.size();
-        top->hmultiN = (uint32_t)multi.size();
-    }
     step_done(1);
-    HIPCHK(top->d_adj.ensure(4 * (size_t)nadj));
-    HIPCHK(top->d_aloss.ensure((size_t)nadj));
-    HIPCHK(prep_adjacency(V, E, nadj, eu.p, ev.p, dinv.p, elat.p, eloss.p, top->d_adj.p,
-                          top->d_aloss.p, st));
+    if (!dir) {
+        HIPCHK(top->d_adj.ensure(4 * (size_t)nadj));
+        HIPCHK(top->d_aloss.ensure((size_t)nadj));
+        HIPCHK(prep_adjacency(V, E, nadj, eu.p, ev.p, dinv.p, elat.p, eloss.p, top->d_adj.p,
+                              top->d_aloss.p, st));
+    } else {
+        // out-rows (d_rowptr counted from them, replacing prep_relabel's in + out degrees) and
+        // in-rows with their losses
+        HIPCHK(top->d_adjo.ensure(4 * (size_t)std::max<int64_t>(1, nadj)));
+        HIPCHK(prep_adjacency(V, E, nadj, eu.p, ev.p, dinv.p, elat.p, eloss.p, top->d_adjo.p,
+                              nullptr, st, kAdjOut, top->d_rowptr.p));
+        HIPCHK(top->d_rowptrIn.ensure((size_t)V + 1));
+        HIPCHK(top->d_adj.ensure(4 * (size_t)std::max<int64_t>(1, nadj)));
+        HIPCHK(top->d_aloss.ensure((size_t)std::max<int64_t>(1, nadj)));
+        HIPCHK(prep_adjacency(V, E, nadj, eu.p, ev.p, dinv.p, elat.p, eloss.p, top->d_adj.p,
+                              top->d_aloss.p, st, kAdjIn, top->d_rowptrIn.p));
+    }
+    // the hub rows' segment tables (HubSegs) from the head of the (out-)rowptr
+    {
+        uint32_t ns = 0, nm = 0;
+        const int r = make_hub_segs(top->d_rowptr.p, H, top->d_hseg, top->d_hmulti, &ns, &nm, st);
+        if (r) return r;
+        top->hsegRows = H;
+        top->hsegN = ns;
+        top->hmultiN = nm;
+    }
     step_done(2);
-    // 3) pi = d(h0, .), the h0 tree, the records' landmark fields
+    // 3) pi = d(h0, .) over the out-rows, the h0 tree, the records' landmark fields
     HIPCHK(top->d_pot.ensure((size_t)V));
     int iters = 0;
-    HIPCHK(prep_h0_distances(V, top->d_rowptr.p, top->d_adj.p, top->d_pot.p, &iters, st));
+    HIPCHK(prep_h0_distances(V, top->d_rowptr.p, adj_out(top), top->d_pot.p, &iters, st));
     top->stats.csr_h0_rounds = iters;
     step_done(3);
     HIPCHK(top->d_sptPar.ensure((size_t)V));
     HIPCHK(top->d_spt.ensure(8 * (size_t)V));
-    HIPCHK(prep_tree(V, nadj, hub_segs(top), top->d_rowptr.p, top->d_adj.p, top->d_aloss.p, top->d_pot.p,
-                     top->d_sptPar.p, top->d_spt.p, &top->hp->piMax, st));
+    if (!dir) {
+        HIPCHK(prep_tree(V, nadj, hub_segs(top), top->d_rowptr.p, top->d_adj.p, top->d_aloss.p, top->d_pot.p,
+                         top->d_sptPar.p, top->d_spt.p, &top->hp->piMax, st));
+    } else {
+        // kappa0 and the records' field from the out-rows; the tree (a vertex's parent is an
+        // in-neighbour, its spt slot an in-row slot) from the in-rows, by their own segments
+        HIPCHK(prep_tree(V, nadj, hub_segs(top), top->d_rowptr.p, top->d_adjo.p, nullptr, top->d_pot.p,
+                         top->d_sptPar.p, top->d_spt.p, &top->hp->piMax, st, kTreeKappa));
+        DevBuf<uint2> iseg;
+        DevBuf<uint4> imulti;
+        uint32_t ns = 0, nm = 0;
+        const int r = make_hub_segs(top->d_rowptrIn.p, H, iseg, imulti, &ns, &nm, st);
+        if (r) return r;
+        HubSegs hin;
+        hin.rows = H;
+        hin.seg = iseg.p;
+        hin.nseg = ns;
+        hin.multi = imulti.p;
+        hin.nmulti = nm;
+        double pm = 0.0;
+        HIPCHK(prep_tree(V, nadj, hin, top->d_rowptrIn.p, top->d_adj.p, top->d_aloss.p, top->d_pot.p,
+                         top->d_sptPar.p, top->d_spt.p, &pm, st, kTreeParents));
+    }
     step_done(4);
-    // 4) the kappa-sorted relaxation copy
-    HIPCHK(top->d_adjk.ensure(4 * (size_t)nadj));
-    HIPCHK(top->d_kap.ensure((size_t)nadj));
+    // 4) the kappa-sorted relaxation copy (of the out-rows)
+    HIPCHK(top->d_adjk.ensure(4 * (size_t)std::max<int64_t>(1, nadj)));
+    HIPCHK(top->d_kap.ensure((size_t)std::max<int64_t>(1, nadj)));
     HIPCHK(top->d_ksum.ensure(kKProbes * (size_t)V));
     HIPCHK(top->d_kap0.ensure((size_t)V));
-    HIPCHK(launch_kappa_copy(V, nadj, hub_segs(top), top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
+    HIPCHK(launch_kappa_copy(V, nadj, hub_segs(top), top->d_rowptr.p, adj_out(top), top->d_pot.p,
                              top->d_sptPar.p, top->d_adjk.p, top->d_kap.p, top->d_ksum.p,
                              top->d_kap0.p, st));
     top->adjkPlain = true;
@@ -840,6 +860,8 @@ DevCSR dev_csr(Topology* top) {
     c.V = top->g.V;
     c.nadj = (int64_t)(top->d_adj.n / 4);
     c.rowptr = top->d_rowptr.p;
+    c.rowptr_in = rowptr_in(top);
+    c.directed = top->isDirected ? 1 : 0;
     c.adj = top->d_adj.p;
     c.adjk = top->d_adjk.p;
     c.kap = top->d_kap.p;
@@ -1049,7 +1071,7 @@ int upload_replay_impl(Topology* top) {
     HIPCHK(top->d_rhop.ensure(cap));
     int64_t nr = 0;
     HIPCHK(prep_replay_csr(V, E, dir ? 1 : 0, top->d_eu.p, top->d_ev.p, top->d_elat.p,
-                           top->d_eloss.p, top->d_inv.p, dir ? nullptr : top->d_pot.p,
+                           top->d_eloss.p, top->d_inv.p, top->d_pot.p,
                            top->d_rrow.p, top->d_rrec.p, top->d_rown.p, top->d_rhop.p, &nr,
                            top->stream));
     top->rnadj = nr;
@@ -1064,8 +1086,8 @@ ReplayCSR replay_csr(Topology* top) {
     c.rowptr = top->d_rrow.p;
     c.rec = top->d_rrec.p;
     c.own = top->d_rown.p;
-    // pi values exist for undirected topologies (upload_csr: d(h0, .) from relabelled vertex 0)
-    c.landmark = (!top->isDirected && top->replayLandmark && top->hp && !top->hp->pot.empty()) ? 0 : -1;
+    // pi = d(h0 -> .) from relabelled vertex 0 (upload_csr; over the out-rows when directed)
+    c.landmark = (top->replayLandmark && top->hp && !top->hp->pot.empty()) ? 0 : -1;
     c.intKeys = (top->replayIntOpt && top->replayIntOk) ? 1 : 0;
     c.hop = top->d_rhop.p;
     c.vloss = top->d_vloss.p;
@@ -1247,13 +1269,14 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
     } else {
         int r = upload_csr(top);
         if (r) return r;
-        // directed topologies (and the "replay_all" test hook) run every row through the exact
-        // heap replay; otherwise the batch kernel runs and flags the rows that need it
+        // the "replay_all" test hook runs every row through the exact heap replay; otherwise
+        // the batch kernel runs (directed topologies too: out-rows relaxed, parents from the
+        // in-rows) and flags the rows that need it
         // multigraphs too: the reference sums the igraph_get_eid edge of each hop, which the batch
         // epilogue (latency = distance) does not reproduce when parallel edges differ
         const bool dense = top->tieReplay && (top->tieDenseOpt == 1 ||
                                               (top->tieDenseOpt < 0 && top->tieDense));
-        const bool allReplay = top->isDirected || top->replayAll || top->hasMultiEdges || dense;
+        const bool allReplay = top->replayAll || top->hasMultiEdges || dense;
         bool probeDense = false;  // the tie probe below found the topology tie-dense
         std::vector<uint32_t> src((size_t)rows), tgt((size_t)A);
         for (int64_t i = 0; i < rows; i++) src[(size_t)i] = (uint32_t)top->hp->inv[(size_t)top->attached[(size_t)(row0 + i)]];
@@ -1280,7 +1303,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             // target skip is on.
             const int64_t nadjk = (int64_t)(top->d_adjk.n / 4);
             if (!top->adjkPlain && top->adjkTargets != tgt) {
-                HIPCHK(launch_kappa_copy(top->g.V, nadjk, hub_segs(top), top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
+                HIPCHK(launch_kappa_copy(top->g.V, nadjk, hub_segs(top), top->d_rowptr.p, adj_out(top), top->d_pot.p,
                                          top->d_sptPar.p, top->d_adjk.p, top->d_kap.p,
                                          top->d_ksum.p, top->d_kap0.p, st));
                 top->adjkPlain = true;
@@ -1301,7 +1324,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 HIPCHK(top->d_kfB.ensure((size_t)V));
                 HIPCHK(top->d_kfPart.ensure(std::max<size_t>(1, hs.nseg)));
                 HIPCHK(top->d_kfChanged.ensure(1));
-                HIPCHK(launch_kfix_step(top->d_rowptr.p, top->d_adj.p, top->d_pot.p, top->d_tbits.p,
+                HIPCHK(launch_kfix_step(top->d_rowptr.p, adj_out(top), top->d_pot.p, top->d_tbits.p,
                                         nullptr, top->d_kfA.p, V, hs, top->d_kfPart.p,
                                         top->d_kfChanged.p, st));
                 double* kin = top->d_kfA.p;
@@ -1309,7 +1332,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 int it = 0;
                 for (; it < top->targetKappa; it++) {
                     HIPCHK(hipMemsetAsync(top->d_kfChanged.p, 0, sizeof(unsigned int), st));
-                    HIPCHK(launch_kfix_step(top->d_rowptr.p, top->d_adj.p, top->d_pot.p,
+                    HIPCHK(launch_kfix_step(top->d_rowptr.p, adj_out(top), top->d_pot.p,
                                             top->d_tbits.p, kin, kout, V, hs, top->d_kfPart.p,
                                             top->d_kfChanged.p, st));
                     unsigned int ch = 0;
@@ -1864,6 +1887,8 @@ int copy_csr_from(Topology* p, int pdev, Topology* o, int odev) {
     }
     HIPCHK(peer_copy(p->d_rowptr, pdev, o->d_rowptr, odev, st));
     HIPCHK(peer_copy(p->d_adj, pdev, o->d_adj, odev, st));
+    HIPCHK(peer_copy(p->d_adjo, pdev, o->d_adjo, odev, st));
+    HIPCHK(peer_copy(p->d_rowptrIn, pdev, o->d_rowptrIn, odev, st));
     HIPCHK(peer_copy(p->d_adjk, pdev, o->d_adjk, odev, st));
     HIPCHK(peer_copy(p->d_kap, pdev, o->d_kap, odev, st));
     HIPCHK(peer_copy(p->d_ksum, pdev, o->d_ksum, odev, st));
@@ -2495,10 +2520,10 @@ int ensure_workspace(Topology* top, int nsrc);
 
 // The attach-time preparation (Topology::prepOnAttach): device init + graph preparation in a
 // background thread holding buildMu; a build (or any other buildMu holder) that comes first does
-// the work itself and the thread then finds nothing left to do.  Complete and directed topologies
-// have no batched-SSSP graph to prepare.
+// the work itself and the thread then finds nothing left to do.  Complete topologies have no
+// batched-SSSP graph to prepare.
 void start_attach_prep(Topology* top) {
-    if (!top->prepOnAttach || top->isComplete || top->isDirected) return;
+    if (!top->prepOnAttach || top->isComplete) return;
     if (top->prepStarted.exchange(true)) return;
     top->prepThread = std::thread([top]() {
         std::lock_guard<std::mutex> lk(top->buildMu);
@@ -2611,7 +2636,7 @@ Topology* shdtopo_new_synthetic(const ShdSynthParams* p) {
     if (!p) return nullptr;
     Topology* top = new_topology(false);  // a generator (tools): no device until it is used
     SynthParams sp{p->seed, p->n_routers, p->n_poi, p->n_edges, p->integer_latency,
-                   p->alpha > 0 ? p->alpha : 1.0 / 1.1};
+                   p->alpha > 0 ? p->alpha : 1.0 / 1.1, p->directed ? 1 : 0};
     std::string err;
     if (!synth_graph(sp, top->g, err)) {
         CRITICAL("synthetic topology: %s", err.c_str());

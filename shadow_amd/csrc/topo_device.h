@@ -97,12 +97,17 @@ enum StatIdx {
     ST_COUNT = 97
 };
 
+// A directed topology (igraph mode OUT, shd-topology.c:762-763) relaxes out-edges but finds a
+// vertex's parent among its in-edges: rowptr / adjk / kap / ksum / kap0 are the OUT rows,
+// rowptr_in / adj / aloss the IN rows (the parent pass).  Undirected: rowptr_in == rowptr.
 struct DevCSR {
     int32_t V = 0;
     int64_t nadj = 0;
-    const uint32_t* rowptr = nullptr;
+    const uint32_t* rowptr = nullptr;     // rows of adjk (relaxation)
+    const uint32_t* rowptr_in = nullptr;  // rows of adj / aloss (parent pass)
+    int directed = 0;
     const uint32_t* adj = nullptr;  // 16-B AdjRec {u32 col, f32 pi(col) rounded up, f64 wt}
-    const uint32_t* adjk = nullptr; // the same records, each row sorted by kappa = w - pi(col)
+    const uint32_t* adjk = nullptr; // the relaxation records, each row sorted by kappa = w - pi(col)
     const float* kap = nullptr;     // kappa of adjk (f32 rounded down; -inf: pi unknown)
     const float4* ksum = nullptr;   // per vertex: kappa at row positions 0, 1, 3, 7[, 15, 31, 63,
                                     // 127] (kKProbes floats, +inf past the row)
@@ -293,8 +298,8 @@ hipError_t launch_fill_u64_strided(unsigned long long* p, unsigned long long v, 
 // ---- graph preparation on the GPU (topo_prep.hip), once per topology: DESIGN.md 3.1 ----
 // Input arrays are the parsed graph in HBM (document order: eu / ev int32[E], elat / eloss f64[E],
 // vloss f64[V]); outputs are in the relabelled vertex order.  Each call synchronises `st`.
-// degrees of the non-loop graph (deg u32[V]), the lowest-id self loop (selfE, ~0 = none) and
-// the adjacency size *nadj = 2 x non-loop edges
+// degrees of the non-loop graph (deg u32[V], in + out when directed), the lowest-id self loop
+// (selfE, ~0 = none) and *nadj = 2 x non-loop edges
 hipError_t prep_degrees(int64_t V, int64_t E, const int32_t* eu, const int32_t* ev, uint32_t* deg,
                         uint32_t* selfE, int64_t* nadj, hipStream_t st);
 // relabel (degree descending, the tail grouped by its primary hub among the first H): perm
@@ -305,17 +310,26 @@ hipError_t prep_relabel(int64_t V, int64_t E, uint32_t H, const int32_t* eu, con
                         uint32_t* inv, uint32_t* rowptr, double* vloss, double* selfLat,
                         double* selfLoss, hipStream_t st);
 // 16-B adjacency records {col, 0, f64 w} rows ascending by (neighbour, edge id), and aloss
+// (nullable).  mode 0: every non-loop edge in both rows (undirected, nadj = 2E'); 1: out-rows
+// only, 2: in-rows only (directed, nadj = E'); for modes 1 and 2 rowptr (u32[V+1]) is counted
+// from the entries
+enum { kAdjBoth = 0, kAdjOut = 1, kAdjIn = 2 };
 hipError_t prep_adjacency(int64_t V, int64_t E, int64_t nadj, const int32_t* eu, const int32_t* ev,
                           const uint32_t* inv, const double* elat, const double* eloss,
-                          uint32_t* adj, double* aloss, hipStream_t st);
+                          uint32_t* adj, double* aloss, hipStream_t st, int mode = kAdjBoth,
+                          uint32_t* rowptr = nullptr);
 // pi = d(h0, .) from vertex 0 (f64[V], +inf = unreached); *iterations = frontier rounds
 hipError_t prep_h0_distances(int64_t V, const uint32_t* rowptr, const uint32_t* adj, double* pot,
                              int* iterations, hipStream_t st);
 // h0 tree (sptPar u32[V], spt {parent, slot in v's row, f64 w, f64 loss, pad} 32 B [V]), the
-// records' pi / kappa0 field, *piMax = the largest finite pi; hub rows by segments (hs)
+// records' pi / kappa0 field, *piMax = the largest finite pi; hub rows by segments (hs).
+// what: kTreeParents (the tree, from rows of candidate parents: in-rows when directed) |
+// kTreeKappa (kappa0 and the records' field, from relaxation rows: out-rows when directed)
+enum { kTreeParents = 1, kTreeKappa = 2 };
 hipError_t prep_tree(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t* rowptr,
                      uint32_t* adj, const double* aloss, const double* pot, uint32_t* sptPar,
-                     uint32_t* spt, double* piMax, hipStream_t st);
+                     uint32_t* spt, double* piMax, hipStream_t st,
+                     int what = kTreeParents | kTreeKappa);
 // the plain kappa-sorted relaxation copy (adjk, kap, ksum, kap0) of adj: also restores it after
 // a target-aware re-sort when the target-aware order no longer applies
 hipError_t launch_kappa_copy(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t* rowptr,

@@ -841,6 +841,20 @@ bool synth_graph(const SynthParams& p, HostGraph& g, std::string& err) {
         g.elat.push_back(p.integer_latency ? (double)(1 + rng.below(10)) : 1.0 + 9.0 * rng.uniform());
         g.eloss.push_back(0.01 * rng.uniform());
     }
+    if (p.directed) {
+        // every non-loop edge also the other way, with its own draws (uplinks stay 5.0): the
+        // spanning path in both directions keeps the graph strongly connected
+        g.directed = true;
+        const size_t n = g.eu.size();
+        for (size_t e = 0; e < n; e++) {
+            if (g.eu[e] == g.ev[e]) continue;
+            const bool uplink = g.eu[e] >= (int32_t)R;
+            g.eu.push_back(g.ev[e]);
+            g.ev.push_back(g.eu[e]);
+            g.elat.push_back(uplink ? 5.0 : draw_lat());
+            g.eloss.push_back(uplink ? 0.0 : 0.01 * rng.uniform());
+        }
+    }
     g.E = (int64_t)g.eu.size();
     g.ejitter.assign((size_t)g.E, 0.0);
     return true;

@@ -62,6 +62,7 @@ struct SynthParams {
     int64_t n_routers, n_poi, n_edges;
     int integer_latency;
     double alpha;
+    int directed = 0;
 };
 bool synth_graph(const SynthParams& p, HostGraph& g, std::string& err);
 

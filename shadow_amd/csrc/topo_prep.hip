@@ -197,19 +197,37 @@ __global__ void prep_relabel_kernel(int64_t V, const uint32_t* __restrict__ perm
 __global__ void prep_entry_kernel(int64_t E, int64_t V, const int32_t* __restrict__ eu,
                                   const int32_t* __restrict__ ev, const uint32_t* __restrict__ inv,
                                   unsigned long long* __restrict__ key,
-                                  uint32_t* __restrict__ val) {
+                                  uint32_t* __restrict__ val, int mode) {
     const unsigned long long sentinel = (unsigned long long)V << 32;  // self loops sort last
     for (int64_t e = gtid(); e < E; e += gstride()) {
         const int32_t a = eu[e], b = ev[e];
         unsigned long long k0 = sentinel, k1 = sentinel;
         if (a != b) {
             const unsigned long long na = inv[a], nb = inv[b];
-            k0 = (na << 32) | nb;
-            k1 = (nb << 32) | na;
+            k0 = (na << 32) | nb;  // a's row (out-entry of a directed edge a -> b)
+            k1 = (nb << 32) | na;  // b's row (in-entry)
         }
-        key[2 * e] = k0;
-        key[2 * e + 1] = k1;
-        val[2 * e] = val[2 * e + 1] = (uint32_t)e;
+        if (mode == kAdjBoth) {
+            key[2 * e] = k0;
+            key[2 * e + 1] = k1;
+            val[2 * e] = val[2 * e + 1] = (uint32_t)e;
+        } else {
+            key[e] = mode == kAdjOut ? k0 : k1;
+            val[e] = (uint32_t)e;
+        }
+    }
+}
+
+// rowptr[v] = the first sorted entry of row >= v (rows 0..V; self loops sort as row V)
+__global__ void prep_rowptr_kernel(int64_t V, int64_t n, const unsigned long long* __restrict__ key,
+                                   uint32_t* __restrict__ rowptr) {
+    for (int64_t v = gtid(); v <= V; v += gstride()) {
+        int64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)(key[mid] >> 32) < v) lo = mid + 1; else hi = mid;
+        }
+        rowptr[v] = (uint32_t)lo;
     }
 }
 
@@ -227,7 +245,7 @@ __global__ void prep_fill_adj_kernel(int64_t nadj, const unsigned long long* __r
         r.z = (uint32_t)wb;
         r.w = (uint32_t)(wb >> 32);
         reinterpret_cast<uint4*>(adj)[k] = r;
-        aloss[k] = eloss[e];
+        if (aloss) aloss[k] = eloss[e];
     }
 }
 
@@ -336,7 +354,9 @@ __device__ __forceinline__ void tree_scan(const uint32_t* adj, const double* pot
 
 __device__ __forceinline__ void tree_store(uint32_t v, const TreeBest& best, const uint32_t* adj,
                                            const double* aloss, uint32_t* sptPar, uint32_t* spt,
-                                           double kmin, double* kap0d) {
+                                           double kmin, double* kap0d, int what) {
+    if (what & kTreeKappa) kap0d[v] = kmin;
+    if (!(what & kTreeParents)) return;
     const bool ok = best.u != 0xFFFFFFFFu;
     sptPar[v] = ok ? best.u : 0xFFFFFFFFu;
     // 32-B record {parent, slot, f64 w, f64 loss, pad}: a walk hop reads it as one line
@@ -345,7 +365,6 @@ __device__ __forceinline__ void tree_store(uint32_t v, const TreeBest& best, con
     if (ok) r = make_uint4(best.u, best.k, adj[kAdjWords * best.k + 2], adj[kAdjWords * best.k + 3]);
     reinterpret_cast<uint4*>(spt)[2 * (size_t)v] = r;
     reinterpret_cast<uint4*>(spt)[2 * (size_t)v + 1] = make_uint4((uint32_t)lb, (uint32_t)(lb >> 32), 0u, 0u);
-    kap0d[v] = kmin;
 }
 
 __device__ __forceinline__ void tb_wave_min(TreeBest& best, double& kmin) {
@@ -366,7 +385,7 @@ prep_tree_kernel(int64_t V, HubSegs hs, const uint32_t* __restrict__ rowptr,
                  const uint32_t* __restrict__ adj, const double* __restrict__ aloss,
                  const double* __restrict__ pot, uint32_t* __restrict__ sptPar,
                  uint32_t* __restrict__ spt, double* __restrict__ kap0d, unsigned long long* __restrict__ pimax,
-                 TreeBest* __restrict__ pbest, double* __restrict__ pkmin) {
+                 TreeBest* __restrict__ pbest, double* __restrict__ pkmin, int what) {
     const uint32_t lane = threadIdx.x & 63u;
     const int64_t nw = gstride() >> 6;
     const TreeBest none{~0ull, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -382,7 +401,7 @@ prep_tree_kernel(int64_t V, HubSegs hs, const uint32_t* __restrict__ rowptr,
         tb_wave_min(best, kmin);
         if (lane == 0) {
             if (sg.y == r0 && e == r1) {
-                tree_store(v, best, adj, aloss, sptPar, spt, kmin, kap0d);
+                tree_store(v, best, adj, aloss, sptPar, spt, kmin, kap0d, what);
             } else {
                 pbest[s] = best;
                 pkmin[s] = kmin;
@@ -398,7 +417,7 @@ prep_tree_kernel(int64_t V, HubSegs hs, const uint32_t* __restrict__ rowptr,
         TreeBest best = none;
         double kmin = INFINITY;
         tree_scan(adj, pot, (uint32_t)v, dv, rowptr[v], rowptr[v + 1], 1u, best, kmin);
-        tree_store((uint32_t)v, best, adj, aloss, sptPar, spt, kmin, kap0d);
+        tree_store((uint32_t)v, best, adj, aloss, sptPar, spt, kmin, kap0d, what);
     }
     pm = wave_min_u64(~pm);
     if (lane == 0 && pm != ~0ull) atomicMax(pimax, ~pm);
@@ -409,7 +428,7 @@ __global__ void __launch_bounds__(kPB)
 prep_tree_multi_kernel(HubSegs hs, const uint32_t* __restrict__ adj,
                        const double* __restrict__ aloss, uint32_t* __restrict__ sptPar,
                        uint32_t* __restrict__ spt, double* __restrict__ kap0d, const TreeBest* __restrict__ pbest,
-                       const double* __restrict__ pkmin) {
+                       const double* __restrict__ pkmin, int what) {
     const uint32_t lane = threadIdx.x & 63u;
     for (int64_t m = gtid() >> 6; m < (int64_t)hs.nmulti; m += gstride() >> 6) {
         const uint4 mr = hs.multi[m];
@@ -422,7 +441,7 @@ prep_tree_multi_kernel(HubSegs hs, const uint32_t* __restrict__ adj,
             kmin = km < kmin ? km : kmin;
         }
         tb_wave_min(best, kmin);
-        if (lane == 0) tree_store(mr.x, best, adj, aloss, sptPar, spt, kmin, kap0d);
+        if (lane == 0) tree_store(mr.x, best, adj, aloss, sptPar, spt, kmin, kap0d, what);
     }
 }
 
@@ -552,7 +571,7 @@ __global__ void rp_fill_kernel(int64_t n, const unsigned long long* __restrict__
         const uint32_t y = inv[(uint32_t)k];
         // pi(y) = d(h0, y) rounded up to f32: the replay's landmark skip (topo_replay.hip)
         float pf = INFINITY;
-        if (!directed && pot) {
+        if (pot) {  // directed: pi = d(h0 -> y) over the out-rows, the same bound
             const double p = pot[y];
             if (isfinite(p)) pf = f32_up(p);
         }
@@ -651,28 +670,39 @@ hipError_t prep_relabel(int64_t V, int64_t E, uint32_t H, const int32_t* eu, con
 
 hipError_t prep_adjacency(int64_t V, int64_t E, int64_t nadj, const int32_t* eu, const int32_t* ev,
                           const uint32_t* inv, const double* elat, const double* eloss,
-                          uint32_t* adj, double* aloss, hipStream_t st) {
-    if (nadj <= 0) return hipSuccess;
+                          uint32_t* adj, double* aloss, hipStream_t st, int mode,
+                          uint32_t* rowptr) {
+    const int64_t n = mode == kAdjBoth ? 2 * E : E;  // entries incl. the self loops' sentinels
+    if (nadj <= 0 && !(mode != kAdjBoth && rowptr)) return hipSuccess;
     Tmp<unsigned long long> k0, k1;
     Tmp<uint32_t> v0, v1;
     Tmp<unsigned char> tmp;
-    PCHK(k0.alloc(2 * E));
-    PCHK(k1.alloc(2 * E));
-    PCHK(v0.alloc(2 * E));
-    PCHK(v1.alloc(2 * E));
-    hipLaunchKernelGGL(prep_entry_kernel, dim3(grid_for(E)), dim3(kPB), 0, st, E, V, eu, ev, inv,
-                       k0.p, v0.p);
-    PCHK(hipGetLastError());
-    const int endbit = 32 + bitlen((uint64_t)V);
-    size_t tb = 0;
-    PCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0.p, k1.p, v0.p, v1.p, (int)(2 * E), 0,
-                                            endbit, st));
-    PCHK(tmp.alloc(tb));
-    PCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k0.p, k1.p, v0.p, v1.p, (int)(2 * E), 0,
-                                            endbit, st));
-    hipLaunchKernelGGL(prep_fill_adj_kernel, dim3(grid_for(nadj)), dim3(kPB), 0, st, nadj, k1.p,
-                       v1.p, elat, eloss, adj, aloss);
-    PCHK(hipGetLastError());
+    PCHK(k0.alloc(std::max<int64_t>(1, n)));
+    PCHK(k1.alloc(std::max<int64_t>(1, n)));
+    PCHK(v0.alloc(std::max<int64_t>(1, n)));
+    PCHK(v1.alloc(std::max<int64_t>(1, n)));
+    if (E > 0) {
+        hipLaunchKernelGGL(prep_entry_kernel, dim3(grid_for(E)), dim3(kPB), 0, st, E, V, eu, ev,
+                           inv, k0.p, v0.p, mode);
+        PCHK(hipGetLastError());
+        const int endbit = 32 + bitlen((uint64_t)V);
+        size_t tb = 0;
+        PCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0.p, k1.p, v0.p, v1.p, (int)n, 0,
+                                                endbit, st));
+        PCHK(tmp.alloc(tb));
+        PCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k0.p, k1.p, v0.p, v1.p, (int)n, 0,
+                                                endbit, st));
+    }
+    if (nadj > 0) {
+        hipLaunchKernelGGL(prep_fill_adj_kernel, dim3(grid_for(nadj)), dim3(kPB), 0, st, nadj,
+                           k1.p, v1.p, elat, eloss, adj, aloss);
+        PCHK(hipGetLastError());
+    }
+    if (mode != kAdjBoth && rowptr) {
+        hipLaunchKernelGGL(prep_rowptr_kernel, dim3(grid_for(V + 1)), dim3(kPB), 0, st, V,
+                           E > 0 ? n : 0, k1.p, rowptr);
+        PCHK(hipGetLastError());
+    }
     return hipStreamSynchronize(st);
 }
 
@@ -736,7 +766,7 @@ void hub_segments(const uint32_t* rowptr_head, uint32_t rows, std::vector<uint2>
 
 hipError_t prep_tree(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t* rowptr,
                      uint32_t* adj, const double* aloss, const double* pot, uint32_t* sptPar,
-                     uint32_t* spt, double* piMax, hipStream_t st) {
+                     uint32_t* spt, double* piMax, hipStream_t st, int what) {
     Tmp<double> kap0d, pkmin;
     Tmp<unsigned long long> pm;
     Tmp<TreeBest> pbest;
@@ -747,14 +777,14 @@ hipError_t prep_tree(int64_t V, int64_t nadj, const HubSegs& hs, const uint32_t*
     PCHK(hipMemsetAsync(pm.p, 0, 8, st));
     const unsigned g = std::max(grid_for(V), (unsigned)std::min<int64_t>((hs.nseg + 3) / 4, 256 * 64));
     hipLaunchKernelGGL(prep_tree_kernel, dim3(g), dim3(kPB), 0, st, V, hs, rowptr, adj, aloss,
-                       pot, sptPar, spt, kap0d.p, pm.p, pbest.p, pkmin.p);
+                       pot, sptPar, spt, kap0d.p, pm.p, pbest.p, pkmin.p, what);
     PCHK(hipGetLastError());
     if (hs.nmulti > 0) {
         hipLaunchKernelGGL(prep_tree_multi_kernel, dim3((hs.nmulti + 3) / 4), dim3(kPB), 0, st, hs,
-                           adj, aloss, sptPar, spt, kap0d.p, pbest.p, pkmin.p);
+                           adj, aloss, sptPar, spt, kap0d.p, pbest.p, pkmin.p, what);
         PCHK(hipGetLastError());
     }
-    if (nadj > 0)
+    if (nadj > 0 && (what & kTreeKappa))
         hipLaunchKernelGGL(prep_recfield_kernel, dim3(grid_for(nadj)), dim3(kPB), 0, st, nadj, adj,
                            pot, kap0d.p);
     PCHK(hipGetLastError());

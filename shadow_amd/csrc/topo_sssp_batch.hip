@@ -403,7 +403,9 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
             mcur[v] = 0;
 #endif
         }
-        const uint32_t r0 = g.rowptr[v], r1 = g.rowptr[v + 1];
+        // relaxation: the out-rows (kappa copy); parent pass: the rows of candidate parents
+        const uint32_t* rp = CUT ? g.rowptr : g.rowptr_in;
+        const uint32_t r0 = rp[v], r1 = rp[v + 1];
         deg = m ? r1 - r0 : 0u;
         if (CUT && deg) {
             const float4 ks0 = g.ksum[kKProbes / 4 * (size_t)v];
@@ -966,7 +968,7 @@ __device__ __forceinline__ void expand_pairs(const uint32_t* Q, uint32_t nq, con
             const uint32_t q = Q[base + tid];
             double val = 0.0;
             vf(q, val);
-            const uint32_t r0 = g.rowptr[q / K], r1 = g.rowptr[q / K + 1];
+            const uint32_t r0 = g.rowptr_in[q / K], r1 = g.rowptr_in[q / K + 1];
             deg = r1 - r0;
             L.rs[tid] = r0;
             L.vx[tid] = q;
@@ -2116,14 +2118,16 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                             row = v;
                         }
                     } else if (v < P && !tbit[h] && hp[h] < (uint32_t)V) {
+                        // the edge hint -> hub: found in the hint's row (undirected: usually
+                        // far shorter than the hub's), in the hub's in-row when directed
                         live[h] = true;
                         uu[h] = hp[h];
-                        key[h] = v;
-                        row = hp[h];
+                        key[h] = g.directed ? hp[h] : v;
+                        row = g.directed ? v : hp[h];
                     }
                 }
-                lo[h] = live[h] ? g.rowptr[row] : 0u;
-                hi[h] = live[h] ? g.rowptr[row + 1] : 0u;
+                lo[h] = live[h] ? g.rowptr_in[row] : 0u;
+                hi[h] = live[h] ? g.rowptr_in[row + 1] : 0u;
                 du[h] = live[h] ? D.get(uu[h], j) : 0ull;
                 end[h] = hi[h];
             }

@@ -105,9 +105,10 @@ class Topology:
 
     @classmethod
     def synthetic(cls, seed=20261015, n_routers=990_000, n_poi=10_000, n_edges=10_000_000,
-                  integer_latency=False, alpha=1.0 / 1.1):
+                  integer_latency=False, alpha=1.0 / 1.1, directed=False):
         lib, _ = L.load()
-        p = L.ShdSynthParams(seed, n_routers, n_poi, n_edges, int(integer_latency), alpha)
+        p = L.ShdSynthParams(seed, n_routers, n_poi, n_edges, int(integer_latency), alpha,
+                             int(directed))
         h = lib.shdtopo_new_synthetic(ctypes.byref(p))
         return cls(h) if h else None
 

@@ -16,7 +16,7 @@ import pytest
 import oracle
 import shadow_amd as sa
 from shadow_amd import sharding
-from helpers import attach_hosts, synthetic_pair
+from helpers import attach_hosts, random_topology_graphml, synthetic_pair
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 8])
@@ -65,6 +65,29 @@ def test_multi_device_table_equals_single_and_oracle(devices, rccl, integer):
     assert np.array_equal(relN.view(np.uint64), orel.view(np.uint64))
     assert np.array_equal(hopsN, ohops.astype(np.uint16))
     assert topN.getMinimumLatency() == olat.min()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [2, 3])
+def test_directed_multi_device_table_equals_oracle(devices):
+    """A directed topology on devices = N engines: the peers copy the owner's out-rows and in-rows
+    (d_adjo, d_rowptrIn) with the rest of the prepared graph; every pair bit-exact against the
+    oracle."""
+    data = random_topology_graphml(n_routers=4000, n_poi=60, extra=20000, seed=13, directed=True)
+    top = sa.Topology.from_buffer(data)
+    g = oracle.OGraph.from_graphml(data)
+    top.set_option("devices", devices)
+    top.set_option("rccl", 0)
+    otop, ips, verts = attach_hosts(top, g, 150, type_hints=["client", "relay", "server"])
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    assert st["devices"] == devices and st["errors"] == 0 and st["replay_rows"] == 0
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(a, oa)
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+    assert top.getMinimumLatency() == olat.min()
 
 
 @pytest.mark.gpu

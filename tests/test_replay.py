@@ -129,22 +129,39 @@ def test_replay_int_key_bound(scale, int_keys):
     assert st["replay_int_keys"] == int_keys
 
 
-@pytest.mark.parametrize("integer", [False, True])
-def test_directed_topology_table(integer):
-    """Directed non-complete topology (igraph mode OUT, shd-topology.c:153,762-763): the table
-    is built by the replay over out-edge rows, bit-exact against the oracle; getters answer
-    forward rows only (no reverse lookup for directed graphs, shd-topology.c:896-898)."""
-    data = random_topology_graphml(n_routers=500, n_poi=50, extra=2500, seed=7, integer=integer,
-                                   directed=True)
+@pytest.mark.parametrize("integer,n_routers,extra,mode", [
+    (False, 500, 2500, "batch"), (True, 500, 2500, "batch"),
+    (False, 6000, 30000, "batch"), (True, 6000, 30000, "batch"),
+    (False, 500, 2500, "replay_all"), (True, 500, 2500, "replay_all")])
+def test_directed_topology_table(integer, n_routers, extra, mode):
+    """Directed non-complete topology (igraph mode OUT, shd-topology.c:153,762-763): the batch
+    kernel relaxes the out-rows and finds each vertex's parent among its in-rows (DevCSR
+    rowptr_in), rows crossing a tie go through the replay (mode "batch"); or the replay alone
+    builds every row ("replay_all").  Bit-exact against the oracle either way.  6,000 routers put
+    most vertices past the LDS hubs, so the tail paths (in-row scans, improver hints, tree walks)
+    run too.  Getters answer forward rows only (no reverse lookup for directed graphs,
+    shd-topology.c:896-898)."""
+    data = random_topology_graphml(n_routers=n_routers, n_poi=50, extra=extra, seed=7,
+                                   integer=integer, directed=True)
     top = sa.Topology.from_buffer(data)
     g = oracle.OGraph.from_graphml(data)
     assert top.is_directed and g.directed and not top.is_complete
+    if mode == "replay_all":
+        top.set_option("replay_all", 1)
+    else:
+        top.set_option("tie_dense", 0)  # the batch kernel + flagged-row replay (no tie probe)
     otop, ips, verts = attach_hosts(top, g, 120, type_hints=["client", "relay", "server"])
     a, lat, rel, hops = top.table()
     st = top.stats()
     oa, olat, orel, ohops = g.table(verts)
     assert np.array_equal(a, oa)
-    assert st["errors"] == 0 and st["replay_rows"] == len(a)
+    assert st["errors"] == 0
+    if mode == "replay_all":
+        assert st["replay_rows"] == len(a)
+    else:
+        assert st["sssp_kernel_ms"] > 0  # the batch kernel ran
+        if not integer:
+            assert st["replay_rows"] == 0  # no ties: every row is the batch kernel's
     assert not np.array_equal(lat, lat.T)  # really directed
     assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(hops, ohops.astype(np.uint16))
