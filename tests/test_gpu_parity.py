@@ -442,6 +442,35 @@ def test_sssp_full_size_c4_int_rows():
     assert np.array_equal(hp.cpu().numpy().view(np.uint16), ohops.astype(np.uint16))
 
 
+def test_sssp_full_size_c4_dir_rows():
+    """C4-dir at full size: the C4 generator with every non-loop edge as two arcs of independent
+    latency (1M vertices / 19.99M arcs, igraph mode OUT).  64 rows through the batch kernel --
+    out-rows relaxed, parents found in the in-rows -- every pair bit-exact against the oracle's
+    directed Dijkstra + helper (latency, reliability, hops); continuous latencies, so nothing is
+    replayed."""
+    import torch
+    top = sa.Topology.synthetic(seed=20261015, directed=True)
+    assert top.is_directed and top.num_edges == 2 * 10_000_000 - 10_000
+    top.synth_packets(20261015, 100_000, 1000, 10**9, 10**7)
+    att = top.attached_vertices()
+    A = len(att)
+    r0, r1 = 2000, 2064
+    lr = torch.empty((r1 - r0, A, 2), dtype=torch.float64, device="cuda")
+    hp = torch.empty((r1 - r0, A), dtype=torch.int16, device="cuda")
+    top.build_rows_into(r0, r1, lr, hp)
+    torch.cuda.synchronize()
+    st = top.stats()
+    assert st["errors"] == 0 and st["ambiguous_pairs"] == 0 and st["replay_rows"] == 0
+    V, eu, ev, elat, eloss, vloss = top.export_graph()
+    g = oracle.OGraph(V, eu, ev, elat, eloss, vloss, directed=True)
+    olat, orel, ohops = g.source_rows(att[r0:r1], att, nthreads=_oracle_threads())
+    glr = lr.cpu().numpy()
+    assert not np.array_equal(glr[:, r0:r1, 0], glr[:, r0:r1, 0].T)  # really directed
+    assert np.array_equal(glr[..., 0].view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(glr[..., 1].view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hp.cpu().numpy().view(np.uint16), ohops.astype(np.uint16))
+
+
 def _grid_graphml(n=30, n_poi=60, seed=5):
     """A 2-D grid of routers (random latencies) whose highest-degree vertex -- the batch kernel's
     landmark h0 -- sits in a corner with long extra edges, so the landmark bound is loose and
