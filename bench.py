@@ -122,6 +122,39 @@ def parallel_calls(fn, n, nthreads):
         return list(ex.map(lambda c: fn(*c), _chunks(n, nthreads)))
 
 
+def directed_line(hosts, steps=3):
+    """C4-dir: the C4 generator with every non-loop edge as two arcs of independent latency
+    (1M vertices, 19.99M arcs; igraph mode OUT, shd-topology.c:153,762-763), its whole attached
+    table built through the batch kernel (out-rows relaxed, parents from the in-rows).  Not a
+    BASELINE config: it shows the directed path at the bench's size (round 4 sent every directed
+    row through the heap replay: ~22.9 s for this table, profiles/r05k_directed_probe.log)."""
+    t0 = time.time()
+    dtop = sa.Topology.synthetic(seed=SEED, directed=True)
+    gen_s = time.time() - t0
+    dtop.synth_packets(SEED, hosts, 0, 10**9, 10**7)
+    A, E = len(dtop.attached_vertices()), dtop.num_edges
+    ms, kms = [], []
+    for i in range(1 + steps):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        dtop.rebuild()
+        torch.cuda.synchronize()
+        if i > 0:  # the first build prepares the graph (cold)
+            ms.append((time.perf_counter() - t1) * 1e3)
+            kms.append(dtop.stats()["sssp_kernel_ms"])
+    st = dtop.stats()
+    t = float(np.mean(ms)) / 1e3
+    out = dict(workload="C4-dir: C4 with every non-loop edge as two arcs of independent latency "
+                        "(directed, mode OUT), all %d x %d attached pairs" % (A, A),
+               vertices=dtop.num_vertices, arcs=E, generate_s=round(gen_s, 2), steps=steps,
+               ms_per_build=round(t * 1e3, 2), kernel_ms=round(float(np.mean(kms)), 3),
+               gteps=round(A * E / t / 1e9, 3), replay_rows=st["replay_rows"],
+               ambiguous_pairs=st["ambiguous_pairs"], errors=st["errors"],
+               min_latency_ms=dtop.getMinimumLatency())
+    dtop.free()
+    return out
+
+
 def complete_table_lines(repeats=20, nthreads=1, devices=1, cpu=True):
     """BASELINE configs 2 (plab, 303 x 303, "on 1 MI355X") and 3 (full Internet, 183 x 183, "on 8
     MI355X"): the complete-graph pair table (_topology_lookupPath for every attached pair,
@@ -263,6 +296,7 @@ def main():
     ap.add_argument("--no-graphml", action="store_true",
                     help="skip the GraphML write + topology_new load of the generated topology")
     ap.add_argument("--no-complete", action="store_true", help="skip the C2/C3 table lines")
+    ap.add_argument("--no-directed", action="store_true", help="skip the C4-dir line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--delta", type=float, default=0.0)
     ap.add_argument("--integer", action="store_true",
@@ -594,6 +628,13 @@ def main():
             # N-engine path on one GPU, the engines then sharing it)
             ndev = int(float(dict(kv.split("=") for kv in args.opt).get("devices", ngpu)))
             complete = complete_table_lines(nthreads=cpu_share(), devices=ndev, cpu=ngpu == 1)
+        directed = None
+        if library and ngpu == 1 and not args.no_directed and not args.integer:
+            # after the main topology's buffers are gone (its workspace holds ~110 GB)
+            top.free()
+            torch.cuda.empty_cache()
+            log(rank, "C4-dir line...")
+            directed = directed_line(args.hosts)
         out = {
             "metric": "routing-table build GTEPS + packet-routes/sec at 1/2/4/8 MI355X "
                       "(%HBM roofline)",
@@ -630,6 +671,7 @@ def main():
             "runahead_min_latency_ms": gmin,
             "graphml": graphml,
             "complete_tables": complete,
+            "directed": directed,
             "ambiguous_pairs": st["ambiguous_pairs"],
             "exchange": dict(kind={0: "none", 1: "rccl", 2: "peer copies"}.get(
                 int(st["exchange_kind"]), "?") if library else "torch.distributed",
