@@ -104,8 +104,6 @@ struct DevCSR {
     int32_t V = 0;
     int64_t nadj = 0;
     const uint32_t* rowptr = nullptr;     // rows of adjk (relaxation)
-    const uint32_t* rowptr_in = nullptr;  // rows of adj / aloss (parent pass)
-    int directed = 0;
     const uint32_t* adj = nullptr;  // 16-B AdjRec {u32 col, f32 pi(col) rounded up, f64 wt}
     const uint32_t* adjk = nullptr; // the relaxation records, each row sorted by kappa = w - pi(col)
     const float* kap = nullptr;     // kappa of adjk (f32 rounded down; -inf: pi unknown)
@@ -124,6 +122,9 @@ struct DevCSR {
     // bit 30 of adjk's column word marks an attached vertex (a table target); the batch
     // relaxation then skips pairs into non-target tail vertices that would expand nothing
     int tflags = 0;
+    // (last: the undirected kernel's argument layout stays that of the fields above)
+    int directed = 0;
+    const uint32_t* rowptr_in = nullptr;  // rows of adj / aloss (parent pass)
 };
 
 // per-slot workspace of the batched SSSP (sssp_batch_kernel, K sources per slot), slot-major:

@@ -364,7 +364,7 @@ __device__ __forceinline__ uint32_t kappa_cut(const DevCSR& g, float4 ks0, float
 // landmark filter for some source of the mask is taken (kappa <= max_j d_j(h0) - d_j(v) plus a
 // margin wider than the filter's); its K distances are read by the vertex's thread with the row
 // bounds.  Without CUT (parent pass) whole rows of the id-sorted adjacency.
-template <int K, bool CUT = false>
+template <int K, bool CUT = false, bool DIR = false>
 __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, const DevCSR& g,
                                                LdsB<K>& L, const BView<K>& D,
                                                typename MaskOps<K>::M* mcur,
@@ -403,8 +403,9 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
             mcur[v] = 0;
 #endif
         }
-        // relaxation: the out-rows (kappa copy); parent pass: the rows of candidate parents
-        const uint32_t* rp = CUT ? g.rowptr : g.rowptr_in;
+        // relaxation: the out-rows (kappa copy); parent pass: the rows of candidate parents (the
+        // in-rows of a directed topology)
+        const uint32_t* rp = (CUT || !DIR) ? g.rowptr : g.rowptr_in;
         const uint32_t r0 = rp[v], r1 = rp[v + 1];
         deg = m ? r1 - r0 : 0u;
         if (CUT && deg) {
@@ -957,7 +958,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
 
 // Load-balanced expansion of a list of (vertex, source) pairs q = v * K + j (parent pass):
 // VF(q, val) gives the pair's value, EF(q, val, adjacency slot) handles one edge of v's row.
-template <int K, class VF, class EF>
+template <int K, bool DIR, class VF, class EF>
 __device__ __forceinline__ void expand_pairs(const uint32_t* Q, uint32_t nq, const DevCSR& g,
                                              LdsB<K>& L, VF&& vf, EF&& ef) {
     const uint32_t tid = threadIdx.x;
@@ -968,7 +969,8 @@ __device__ __forceinline__ void expand_pairs(const uint32_t* Q, uint32_t nq, con
             const uint32_t q = Q[base + tid];
             double val = 0.0;
             vf(q, val);
-            const uint32_t r0 = g.rowptr_in[q / K], r1 = g.rowptr_in[q / K + 1];
+            const uint32_t* rp = DIR ? g.rowptr_in : g.rowptr;  // rows of candidate parents
+            const uint32_t r0 = rp[q / K], r1 = rp[q / K + 1];
             deg = r1 - r0;
             L.rs[tid] = r0;
             L.vx[tid] = q;
@@ -1050,7 +1052,9 @@ __device__ __forceinline__ uint32_t hb_grab(uint32_t* e, uint32_t seq, uint32_t 
 
 }  // namespace
 
-template <int K>
+// DIR: a directed topology (parents from the in-rows, DevCSR::rowptr_in); a separate
+// instantiation, so the undirected kernel's code and registers are those of round 5 before it
+template <int K, bool DIR>
 __global__ void __launch_bounds__(kSsspBlock, kBatchWgPerCu)
 sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                   const double* __restrict__ srcsh, int nsrc, int kf,
@@ -2122,12 +2126,13 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         // far shorter than the hub's), in the hub's in-row when directed
                         live[h] = true;
                         uu[h] = hp[h];
-                        key[h] = g.directed ? hp[h] : v;
-                        row = g.directed ? v : hp[h];
+                        key[h] = DIR ? hp[h] : v;
+                        row = DIR ? v : hp[h];
                     }
                 }
-                lo[h] = live[h] ? g.rowptr_in[row] : 0u;
-                hi[h] = live[h] ? g.rowptr_in[row + 1] : 0u;
+                const uint32_t* rp = DIR ? g.rowptr_in : g.rowptr;
+                lo[h] = live[h] ? rp[row] : 0u;
+                hi[h] = live[h] ? rp[row + 1] : 0u;
                 du[h] = live[h] ? D.get(uu[h], j) : 0ull;
                 end[h] = hi[h];
             }
@@ -2238,7 +2243,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 // (one line) and tests every source of the row's mask
                 for (uint32_t base = 0; base < nVs; base += kBChunk) {
                     const uint32_t cnt = min((uint32_t)kBChunk, nVs - base);
-                    const uint32_t total = load_chunk<K>(vscr + base, cnt, g, L, D, mA, hdef, false);
+                    const uint32_t total = load_chunk<K, false, DIR>(vscr + base, cnt, g, L, D, mA, hdef, false);
                     for (uint32_t e = tid; e < total; e += kSsspBlock) {
                         const int lo = chunk_slot<K>(L, cnt, e);
                         const uint32_t jr = L.rs[lo] + (e - L.off[lo]);
@@ -2302,7 +2307,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 const uint32_t nM = min(L.qtail, pcap);
                 __syncthreads();
                 if (nM > 0) {
-                    expand_pairs<K>(
+                    expand_pairs<K, DIR>(
                         pnxt, nM, g, L,
                         [&](uint32_t q, double& val) { val = bits2d(D.get(q / K, q % K)); },
                         [&](uint32_t q, double dv, uint32_t jr) {
@@ -2927,13 +2932,14 @@ static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32
     if ((int64_t)plan.H > g.V || plan.P > plan.H || plan.bytes > kBMaxLds ||
         blayout<K>(plan.H, plan.P).bytes != plan.bytes || ws.K != K)
         return hipErrorInvalidValue;
+    auto* kern = g.directed ? sssp_batch_kernel<K, true> : sssp_batch_kernel<K, false>;
     {  // per device (multi-GPU builds launch on several): set before every launch
-        hipError_t e = hipFuncSetAttribute((const void*)sssp_batch_kernel<K>,
+        hipError_t e = hipFuncSetAttribute((const void*)kern,
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)kBMaxLds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(sssp_batch_kernel<K>, dim3(grid), dim3(kSsspBlock), plan.bytes, stream, g,
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kSsspBlock), plan.bytes, stream, g,
                        ws, d_sources, d_srcsh, nsrc, kf, d_targets, A, delta, plan.H, plan.P, iter_guard,
                        out_lr, out_hops, out_rowmin, d_stats);
     return hipGetLastError();
@@ -2955,7 +2961,7 @@ hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uin
 
 hipError_t preload_batch_module() {
     hipFuncAttributes a;
-    return hipFuncGetAttributes(&a, (const void*)sssp_batch_kernel<8>);
+    return hipFuncGetAttributes(&a, (const void*)sssp_batch_kernel<8, false>);
 }
 
 }  // namespace shdtopo
