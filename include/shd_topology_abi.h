@@ -124,7 +124,9 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * non-target vertices that would relax nothing reaching a target), "target_kappa" (iterations of
  * the target-aware kappa fixpoint behind that test, 0 = the row's smallest kappa; default 6),
  * "share" (1: a batched launch's workgroups that run out of batches take part in the running
- * batches' parent walks and epilogues -- the help board; 0: each batch stays in its workgroup).
+ * batches' parent walks and epilogues -- the help board; 0, the default: each batch stays in its
+ * workgroup and the board-less kernel runs; -1: the board for a launch whose batches fit one
+ * round of the slots).
  * Returns 0 or -1 for an unknown key / bad value. */
 int shdtopo_set_option(Topology* top, const char* key, double value);
 

@@ -252,10 +252,10 @@ struct _Topology {
     DevBuf<double> d_pathbuf;
     DevBuf<uint32_t> d_cnt, d_bslot, d_counters;
     // help board of the batched launches (SlotWs.board): kBoardWords per slot + 1, zeroed before
-    // every launch; option "share" (default on): idle workgroups take part in the running
-    // batches' parent walks and epilogues
+    // every launch; option "share" (default 0: off; 1 on; -1 one-round launches): idle
+    // workgroups take part in the running batches' parent walks and epilogues
     DevBuf<uint32_t> d_board;
-    bool share = true;
+    int share = 0;  // 0 off (default); 1 on; -1 auto: the board on a one-round launch only
     int slots = 0;
     DevBuf<double2> d_lr;
     DevBuf<uint16_t> d_hops;
@@ -1004,14 +1004,14 @@ SlotWs slot_ws(Topology* top) {
     w.q_stride = queue_stride(top, w.K);
     w.mask = top->d_mask.p;
     w.hpar = top->d_hpar.p;
-    w.board = top->share ? top->d_board.p : nullptr;
+    w.board = top->share != 0 ? top->d_board.p : nullptr;  // (enqueue_rows decides per launch)
     return w;
 }
 
 // zeroes the help board before a batched launch (every polled word starts at 0: no job, no
 // finished batch)
 int board_ready(Topology* top, hipStream_t st) {
-    if (!top->share) return 0;
+    if (top->share == 0) return 0;
     const size_t n = ((size_t)top->slots + 1) * kBoardWords;
     HIPCHK(top->d_board.ensure(n));
     HIPCHK(hipMemsetAsync(top->d_board.p, 0, sizeof(uint32_t) * n, st));
@@ -1570,6 +1570,11 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 top->ordDelta = delta;
                 }
                 ws.rowmap = top->d_rowmap.p;
+                // the help board (option share; auto: a one-round launch, whose idle slots help
+                // its last batches -- in a launch of several rounds its code costs more than the
+                // help returns)
+                if (!(top->share > 0 || (top->share < 0 && nbat <= (int64_t)ws.slots)))
+                    ws.board = nullptr;
                 const std::vector<uint32_t>& psrc = top->ordPsrc;
                 top->stats.order_ms = std::chrono::duration<double, std::milli>(
                     std::chrono::steady_clock::now() - to0).count();
@@ -2696,7 +2701,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
         }
     }
     else if (k == "prepare_on_attach") top->prepOnAttach = value != 0;
-    else if (k == "share") top->share = value != 0;
+    else if (k == "share") top->share = value < 0 ? -1 : (value != 0 ? 1 : 0);
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
     else if (k == "par_hubs") top->parHubs = (int64_t)value;
     else if (k == "batch") {

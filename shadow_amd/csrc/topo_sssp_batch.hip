@@ -1053,8 +1053,13 @@ __device__ __forceinline__ uint32_t hb_grab(uint32_t* e, uint32_t seq, uint32_t 
 }  // namespace
 
 // DIR: a directed topology (parents from the in-rows, DevCSR::rowptr_in); a separate
-// instantiation, so the undirected kernel's code and registers are those of round 5 before it
-template <int K, bool DIR>
+// instantiation, so the undirected kernel's code and registers are those of round 5 before it.
+// BOARD: the help board compiled in (item 10).  Its code costs every batch registers: full table
+// 65.6-66.5 ms without, 67.0-67.6 with (same box); a one-round launch's idle slots helping its
+// last batches do not win that back (1,250 rows: 16.2-16.5 ms without, 16.5-16.7 with), so the
+// default launch is board-less (option share 0) and launch_batch_k picks the instantiation by
+// SlotWs.board.
+template <int K, bool DIR, bool BOARD>
 __global__ void __launch_bounds__(kSsspBlock, kBatchWgPerCu)
 sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                   const double* __restrict__ srcsh, int nsrc, int kf,
@@ -1165,7 +1170,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     // workgroup's claimed items to L.jtaken.
     auto run_job = [&](uint32_t o, uint32_t seq, uint32_t kind, uint32_t n, uint32_t epv,
                        uint32_t r0v, uint32_t nkv, uint32_t list) {
-        const bool shared = ws.board != nullptr;
+        const bool shared = BOARD && ws.board != nullptr;
         uint32_t* const eo = shared ? ws.board + (size_t)o * kBoardWords : nullptr;
         unsigned long long* const distO = ws.dist + (size_t)o * (size_t)V * K;
         uint4* const precO = ws.prec + (size_t)o * (size_t)V * K;
@@ -1959,7 +1964,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // epilogue are jobs of the slot's help-board entry (run_job): idle workgroups join them.
         if ((int)tid < nk) L.src[tid] = sources[r0 + tid];
         const uint32_t ept = ep | kTagClaim;  // tag word of a resolved / claimed pair record
-        const bool shared = ws.board != nullptr;
+        const bool shared = BOARD && ws.board != nullptr;
         uint32_t* const my_e = shared ? ws.board + (size_t)slot * kBoardWords : nullptr;
         // Publish a job on this slot's entry (every wave's earlier stores drained first: the hub
         // rows, the start list, the pair records), and after taking part, wait until every
@@ -2456,7 +2461,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     // data, takes chunks of it (run_job), releases its own stores and adds its items to the job's
     // done count; it stops when every batch of the launch is finished.  The scan is one wave's
     // relaxed loads; an idle scan sleeps.
-    if (ws.board) {
+    if (BOARD && ws.board) {
         const unsigned long long th0 = wall_clock64();
         const uint32_t nbat = (uint32_t)((nsrc + kf - 1) / kf);
         const uint32_t* const gw = ws.board + (size_t)gridDim.x * kBoardWords;
@@ -2932,7 +2937,12 @@ static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32
     if ((int64_t)plan.H > g.V || plan.P > plan.H || plan.bytes > kBMaxLds ||
         blayout<K>(plan.H, plan.P).bytes != plan.bytes || ws.K != K)
         return hipErrorInvalidValue;
-    auto* kern = g.directed ? sssp_batch_kernel<K, true> : sssp_batch_kernel<K, false>;
+    // the board-less instantiation exists for the default width only (K != 8: the board code is
+    // compiled in and off at run time when ws.board is null)
+    auto* kern = g.directed ? (ws.board || K != 8 ? sssp_batch_kernel<K, true, true>
+                                                  : sssp_batch_kernel<K, true, K != 8>)
+                            : (ws.board || K != 8 ? sssp_batch_kernel<K, false, true>
+                                                  : sssp_batch_kernel<K, false, K != 8>);
     {  // per device (multi-GPU builds launch on several): set before every launch
         hipError_t e = hipFuncSetAttribute((const void*)kern,
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2961,7 +2971,7 @@ hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uin
 
 hipError_t preload_batch_module() {
     hipFuncAttributes a;
-    return hipFuncGetAttributes(&a, (const void*)sssp_batch_kernel<8, false>);
+    return hipFuncGetAttributes(&a, (const void*)sssp_batch_kernel<8, false, false>);
 }
 
 }  // namespace shdtopo

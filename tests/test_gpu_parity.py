@@ -601,10 +601,12 @@ def test_device_option_after_topology_new_builds_on_that_device(tmp_path):
 
 @pytest.mark.parametrize("integer", [False, True])
 def test_help_board_tables_equal_unshared(integer):
-    """The help board (option share, default on): workgroups out of batches take part in the
-    running batches' parent walks and epilogues (cross-workgroup jobs: leases claimed by CAS,
-    release / acquire fences around every hand-off).  Repeated builds with helpers active must
-    equal the unshared build and the oracle bit for bit, with no board error and no failed pair."""
+    """The help board (option share: 1 on, 0 off -- the default, the board-less kernel
+    instantiation -- and -1, on for a one-round launch such as this one): workgroups out of batches take part
+    in the running batches' parent walks and epilogues (cross-workgroup jobs: leases claimed by
+    CAS, release / acquire fences around every hand-off).  Repeated builds with helpers active
+    must equal the unshared build and the oracle bit for bit, with no board error and no failed
+    pair."""
     top, g = synthetic_pair(seed=43, n_routers=20000, n_poi=400, n_edges=200000, integer=integer)
     top.set_option("tie_dense", 0)
     otop, ips, verts = attach_hosts(top, g, 1200, type_hints=["client", "relay", "server"])
@@ -623,6 +625,13 @@ def test_help_board_tables_equal_unshared(integer):
         assert np.array_equal(rel.view(np.uint64), rel0.view(np.uint64))
         assert np.array_equal(hops, hops0)
     assert helped > 0  # the launches had idle workgroups that took items
+    top.set_option("share", -1)
+    top.rebuild()
+    a, lat, rel, hops = top.table()
+    assert top.stats()["help_board_errors"] == 0
+    assert np.array_equal(lat.view(np.uint64), lat0.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), rel0.view(np.uint64))
+    assert np.array_equal(hops, hops0)
     oa, olat, orel, ohops = g.table(verts)
     assert np.array_equal(lat0.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(rel0.view(np.uint64), orel.view(np.uint64))
