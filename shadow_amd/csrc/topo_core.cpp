@@ -334,6 +334,13 @@ struct _Topology {
     const HostPrep* ordHp = nullptr;
     int ordKf = -1, ordSO = -1, ordBO = -1;
     double ordDelta = -1.0;
+    double ordPhase = -2.0;
+    // option "h0_phase": where the landmark h0 sits in its bucket (the fraction of the bucket
+    // below its shifted distance, which is the same for every source); default 0.98: h0 closes
+    // its bucket, so the hub core around it is expanded in the next bucket with d(h0) final and
+    // the landmark bound tight.  < 0: the round-4 shifts (sh = piMax - pi(s)
+    // + 2 delta, h0's phase whatever piMax / delta gives)
+    double h0Phase = 0.98;
     bool replayUploaded = false;
     int64_t rnadj = 0;  // entries of the replay CSR
     DevBuf<uint32_t> d_rrow;
@@ -814,6 +821,19 @@ int upload_csr_impl(Topology* top) {
         double pm = 0.0;
         HIPCHK(prep_tree(V, nadj, hin, top->d_rowptrIn.p, top->d_adj.p, top->d_aloss.p, top->d_pot.p,
                          top->d_sptPar.p, top->d_spt.p, &pm, st, kTreeParents));
+        // d(v, h0) over the in-rows: the bucket shifts align every source's h0 with it
+        // (undirected: d(v, h0) = pi(v))
+        DevBuf<double> prev;
+        HIPCHK(prev.ensure((size_t)V));
+        int it2 = 0;
+        HIPCHK(prep_h0_distances(V, top->d_rowptrIn.p, top->d_adj.p, prev.p, &it2, st));
+        top->hp->potSrc.resize((size_t)V);
+        HIPCHK(hipMemcpyAsync(top->hp->potSrc.data(), prev.p, 8 * (size_t)V, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        double mx = 0.0;
+        for (double x : top->hp->potSrc)
+            if (std::isfinite(x) && x > mx) mx = x;
+        top->hp->srcMax = mx;
     }
     step_done(4);
     // 4) the kappa-sorted relaxation copy (of the out-rows)
@@ -1197,13 +1217,27 @@ uint64_t compute_geometry(Topology* top) {
     return sg;
 }
 
+// The shifted distance C of the landmark h0 for every source (undirected: d_s(h0) = pi(s), so
+// sh_s = C - pi(s) puts h0 at C): the round-4 rule C = piMax + 2 delta, or, with option h0_phase
+// p in [0, 1), the smallest C >= piMax + 2 delta whose phase in its bucket is p (bkt(C) = floor(C
+// / delta); every shift stays >= 2 delta).
+double h0_shift(Topology* top, double delta) {
+    const double base = top->hp->to_h0_max() + 2.0 * delta;
+    if (!(top->h0Phase >= 0.0) || !(top->h0Phase < 1.0)) return base;
+    const double x = base / delta;
+    double b = std::floor(x - top->h0Phase) + top->h0Phase;
+    if (b < x) b += 1.0;
+    return b * delta;
+}
+
 double default_delta(Topology* top) {
     if (top->delta > 0) return top->delta;
     edge_scan(top);
     const double mean = top->meanLat;
-    // tuned on C4: the batch kernel gains from wide buckets (the sources of a batch
-    // share more expansions) up to 0.2 x mean (~10 ms)
-    return std::max(1e-9, 0.2 * mean);
+    // tuned on C4: with h0 closing its bucket (h0_phase 0.98) the kernel
+    // gains from wide buckets (the sources of a batch share more expansions) up to ~0.4 x mean
+    // and is flat to 0.8 x mean; 0.5 x mean (~25 ms) sits in the middle of the plateau
+    return std::max(1e-9, 0.5 * mean);
 }
 
 // wall checkpoints of a whole-table build (ShdStats.build_step_ms): the time since the previous
@@ -1369,11 +1403,12 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     const auto tq0 = std::chrono::steady_clock::now();
                     const int64_t P = kTieProbeRows;
                     const double delta = default_delta(top);
-                    const double pmax = top->hp->piMax;
+                    const double pmax = top->hp->to_h0_max();
+                    const double C = h0_shift(top, delta);
                     std::vector<double> sh((size_t)P);
                     for (int64_t i = 0; i < P; i++) {
-                        const double pp = top->hp->pot[(size_t)src[(size_t)i]];
-                        sh[(size_t)i] = (pmax - (std::isfinite(pp) ? pp : pmax)) + 2.0 * delta;
+                        const double pp = top->hp->to_h0(src[(size_t)i]);
+                        sh[(size_t)i] = C - (std::isfinite(pp) ? pp : pmax);
                     }
                     HIPCHK(top->d_probeSrc.ensure((size_t)P));
                     HIPCHK(top->d_probeSh.ensure((size_t)P));
@@ -1439,7 +1474,8 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                                    : nbat > 3 * (int64_t)std::max(1, ws.slots) ? 4 : 2;
                 const bool cached = top->ordHp == top->hp.get() && top->ordKf == kf &&
                                     top->ordSO == top->sourceOrder && top->ordBO == border &&
-                                    top->ordDelta == delta && top->ordSrc == src;
+                                    top->ordDelta == delta && top->ordPhase == top->h0Phase &&
+                                    top->ordSrc == src;
                 if (!cached) {
                 // Batches of K sources settle in lock-step and share an expansion when their
                 // shifted distances to a vertex fall in one bucket: sources whose shortest paths
@@ -1550,12 +1586,14 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 HIPCHK(top->d_bsrc.ensure((size_t)rows));
                 HIPCHK(hipMemcpyAsync(top->d_rowmap.p, perm.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
                 HIPCHK(hipMemcpyAsync(top->d_bsrc.p, psrc.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
-                // bucket shift per row: sh = C - pi(src) >= 2 delta (topo_sssp_batch.hip)
-                const double pmax = top->hp->piMax;  // largest finite pi (upload_csr)
+                // bucket shift per row: sh = C - d(src, h0) >= 2 delta, every source's h0 at C
+                // (h0_shift; topo_sssp_batch.hip)
+                const double pmax = top->hp->to_h0_max();  // largest finite d(., h0) (upload_csr)
+                const double C = h0_shift(top, delta);
                 std::vector<double> sh((size_t)rows);
                 for (int64_t i = 0; i < rows; i++) {
-                    const double p = top->hp->pot[(size_t)psrc[(size_t)i]];
-                    sh[(size_t)i] = (pmax - (std::isfinite(p) ? p : pmax)) + 2.0 * delta;
+                    const double p = top->hp->to_h0(psrc[(size_t)i]);
+                    sh[(size_t)i] = C - (std::isfinite(p) ? p : pmax);
                 }
                 HIPCHK(top->d_srcsh.ensure((size_t)rows));
                 HIPCHK(hipMemcpyAsync(top->d_srcsh.p, sh.data(), sizeof(double) * (size_t)rows,
@@ -1568,6 +1606,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 top->ordSO = top->sourceOrder;
                 top->ordBO = border;
                 top->ordDelta = delta;
+                top->ordPhase = top->h0Phase;
                 }
                 ws.rowmap = top->d_rowmap.p;
                 // the help board (option share; auto: a one-round launch, whose idle slots help
@@ -1862,6 +1901,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->sourceOrder = top->sourceOrder;
     p->batchOrder = top->batchOrder;
     p->batchFill = top->batchFill;
+    p->h0Phase = top->h0Phase;
     p->targetSkip = top->targetSkip;
     p->targetKappa = top->targetKappa;
     p->targetResort = top->targetResort;
@@ -2720,6 +2760,10 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "source_order") top->sourceOrder = (int)value;
     else if (k == "batch_order") top->batchOrder = (int)value;
     else if (k == "batch_fill") top->batchFill = (int)value;
+    else if (k == "h0_phase") {
+        if (!(value < 1.0)) return -1;
+        top->h0Phase = value;
+    }
     else if (k == "target_skip") top->targetSkip = value != 0;
     else if (k == "target_kappa") top->targetKappa = (int)value;
     else if (k == "target_resort") top->targetResort = value != 0;

@@ -104,6 +104,12 @@ struct HostPrep {
     std::vector<double> pot;        // pi = d(h0, v) from the top hub: bucket shifts, batch order
     std::vector<uint32_t> sptPar;   // h0 shortest-path tree parent (source ordering)
     double piMax = 0.0;             // largest finite pi
+    // directed topologies: d(v, h0) over the in-rows (undirected: empty, pot serves), the bucket
+    // shifts' value of d_s(h0), and its largest finite value
+    std::vector<double> potSrc;
+    double srcMax = 0.0;
+    double to_h0(uint32_t v) const { return potSrc.empty() ? pot[v] : potSrc[v]; }
+    double to_h0_max() const { return potSrc.empty() ? piMax : srcMax; }
 };
 
 uint32_t string_to_ip(const char* s);  // inet_pton(AF_INET) as shd-address.c:137-144

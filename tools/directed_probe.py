@@ -29,6 +29,7 @@ ap.add_argument("--routers", type=int, default=990_000)
 ap.add_argument("--poi", type=int, default=10_000)
 ap.add_argument("--edges", type=int, default=10_000_000)
 ap.add_argument("--integer", type=int, default=0)
+ap.add_argument("--opt", action="append", default=[], help="key=value library option")
 args = ap.parse_args()
 
 
@@ -37,6 +38,9 @@ def make():
     top = sa.Topology.synthetic(n_routers=args.routers, n_poi=args.poi, n_edges=args.edges,
                                 integer_latency=bool(args.integer), directed=True)
     assert top.is_directed
+    for kv in args.opt:
+        k, v = kv.split("=")
+        top.set_option(k, float(v))
     top.synth_packets(20261015, 100_000, 0, 10**9, 10**7)  # attaches the hosts
     print("graph + attach %.1fs V=%d E=%d A=%d" % (time.time() - t, top.num_vertices,
                                                     top.num_edges, len(top.attached_vertices())),
