@@ -52,7 +52,11 @@ using namespace dev;
 #define SHD_BATCH_RB 2  // phase-B rounds whose loads are in flight together (pair rounds: 2 < 3 < 4 by 1-4 %, 8 spills)
 #endif
 #ifndef SHD_BATCH_SPEC
-#define SHD_BATCH_SPEC 1  // buckets past cb whose hub sources join a hub expansion speculatively
+// buckets past cb whose hub sources join a hub expansion speculatively (-1: none).  Round 5,
+// with 25-ms buckets and h0 closing its bucket: 0 (only the current bucket's sources) 55.4-55.6
+// ms full table, 13.1 ms at 1,250 rows against 56.9-57.1 / 13.6-13.7 with 1 (relaxations per
+// source 222 k -> 174 k); with the round-4 10-ms buckets 1 was 4 % ahead of 0
+#define SHD_BATCH_SPEC 0
 #endif
 #ifndef SHD_BATCH_U
 #define SHD_BATCH_U 2  // phase-A edges per lane
@@ -656,7 +660,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             if (base >= nq) break;
             cnt = min((uint32_t)kBChunk, nq - base);
             total = load_chunk<K, true>(Q + base, cnt, g, L, D, mcur, hdef, true,
-                                        B.cb + (uint32_t)SHD_BATCH_SPEC);
+                                        SHD_BATCH_SPEC < 0 ? 0u : B.cb + (uint32_t)SHD_BATCH_SPEC);
         }
         BT_TICK(0);
         constexpr uint32_t kStep = WAVE ? 64u : (uint32_t)kSsspBlock;  // lanes per phase-A slot
