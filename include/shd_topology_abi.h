@@ -101,7 +101,7 @@ int shdtopo_version(void);
 Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
 
 /* options: "abort_on_error" (1), "lazy" (1 = K3 first-rooted-wins emulation, 0 = eager
- * forward rows), "delta" (delta-stepping bucket width, ms; default 0.5 x the mean edge latency),
+ * forward rows), "delta" (delta-stepping bucket width, ms; default the mean edge latency),
  * "h0_phase" (where the landmark h0 sits in its bucket, [0, 1); default 0.98; < 0: the round-4
  * bucket shifts), "slots" (concurrent SSSP
  * workgroups), "device" (HIP device ordinal), "lds_hubs" (cap on LDS-resident hub distances,

@@ -1234,10 +1234,11 @@ double default_delta(Topology* top) {
     if (top->delta > 0) return top->delta;
     edge_scan(top);
     const double mean = top->meanLat;
-    // tuned on C4: with h0 closing its bucket (h0_phase 0.98) the kernel
-    // gains from wide buckets (the sources of a batch share more expansions) up to ~0.4 x mean
-    // and is flat to 0.8 x mean; 0.5 x mean (~25 ms) sits in the middle of the plateau
-    return std::max(1e-9, 0.5 * mean);
+    // tuned on C4: with h0 closing its bucket (h0_phase 0.98) and no hub
+    // speculation the kernel gains from wide buckets (fewer sweeps and near iterations; the
+    // landmark filter keeps the relaxations flat) up to ~0.8 x mean and is flat to ~1.3 x mean;
+    // 1.0 x mean (~50 ms) sits in the middle of the plateau
+    return std::max(1e-9, 1.0 * mean);
 }
 
 // wall checkpoints of a whole-table build (ShdStats.build_step_ms): the time since the previous
