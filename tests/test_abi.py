@@ -214,3 +214,23 @@ def test_device_option_fixed_once_the_attach_time_preparation_starts():
     syn.set_option("lazy", 0)
     with pytest.raises(KeyError):
         syn.set_option("device", -1)
+
+
+def test_synthetic_directed_shape_and_bucket_options():
+    """The synthetic generator's directed variant (ShdSynthParams.directed, tools' C4-dir): every
+    non-loop edge becomes two arcs, the reverse one with its own draws, so E = 2 x n_edges -
+    n_poi and the graph stays strongly connected; and the batched SSSP's bucket options: "delta"
+    and "h0_phase" in [0, 1) (< 0: the round-4 shifts) are accepted, a phase >= 1 is refused."""
+    top = sa.Topology.synthetic(seed=3, n_routers=500, n_poi=40, n_edges=5000, directed=True)
+    assert top.is_directed and not top.is_complete
+    assert top.num_vertices == 540 and top.num_edges == 2 * 5000 - 40
+    V, eu, ev, el, lo, vl = top.export_graph()
+    nl = eu != ev
+    fwd = set(zip(eu[nl].tolist(), ev[nl].tolist()))
+    assert all((b, a) in fwd for a, b in fwd)  # every arc has its reverse
+    und = sa.Topology.synthetic(seed=3, n_routers=500, n_poi=40, n_edges=5000)
+    assert not und.is_directed and und.num_edges == 5000
+    for k, v in (("delta", 25.0), ("h0_phase", 0.5), ("h0_phase", 0.0), ("h0_phase", -1)):
+        top.set_option(k, v)
+    with pytest.raises(KeyError):
+        top.set_option("h0_phase", 1.0)

@@ -636,3 +636,29 @@ def test_help_board_tables_equal_unshared(integer):
     assert np.array_equal(lat0.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(rel0.view(np.uint64), orel.view(np.uint64))
     assert np.array_equal(hops0, ohops.astype(np.uint16))
+
+
+@pytest.mark.parametrize("integer", [False, True])
+def test_bucket_width_and_landmark_phase_do_not_change_the_table(integer):
+    """Option delta (bucket width) and h0_phase (where the landmark h0 sits in its bucket; < 0 the
+    round-4 shifts) change only the order of the label-correcting work, not the fixpoint: tables
+    built with several settings on one topology are bit-identical, and equal the oracle's."""
+    top, g = synthetic_pair(seed=47, n_routers=20000, n_poi=300, n_edges=200000, integer=integer)
+    top.set_option("tie_dense", 0)
+    otop, ips, verts = attach_hosts(top, g, 900, type_hints=["client", "relay", "server"])
+    a0, lat0, rel0, hops0 = top.table()
+    assert top.stats()["errors"] == 0
+    for delta, phase in ((10.1, -1.0), (25.0, 0.3), (80.0, 0.98), (5.0, 0.5)):
+        top.set_option("delta", delta)
+        top.set_option("h0_phase", phase)
+        top.rebuild()
+        a, lat, rel, hops = top.table()
+        assert top.stats()["errors"] == 0
+        assert np.array_equal(a, a0)
+        assert np.array_equal(lat.view(np.uint64), lat0.view(np.uint64)), (delta, phase)
+        assert np.array_equal(rel.view(np.uint64), rel0.view(np.uint64)), (delta, phase)
+        assert np.array_equal(hops, hops0), (delta, phase)
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(lat0.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel0.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops0, ohops.astype(np.uint16))
