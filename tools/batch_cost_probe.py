@@ -34,8 +34,9 @@ torch.cuda.synchronize()
 csr = top.export_csr()
 raw = np.fromfile(trace, dtype=np.int64)
 nb, kf, slots, nr = (int(x) for x in raw[:4])
-bt = raw[4:4 + 8 * nb].reshape(nb, 8).astype(np.float64)
-sp = raw[4 + 8 * nb:4 + 8 * nb + 2 * nr].reshape(nr, 2)
+W = 12  # kBTraceWords
+bt = raw[4:4 + W * nb].reshape(nb, W).astype(np.float64)
+sp = raw[4 + W * nb:4 + W * nb + 2 * nr].reshape(nr, 2)
 src = sp[:, 0].astype(np.int64)
 dur = (bt[:, 1] - bt[:, 0]) * 1e-5
 rel, exp = bt[:, 6], bt[:, 5]
