@@ -102,8 +102,9 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
 
 /* options: "abort_on_error" (1), "lazy" (1 = K3 first-rooted-wins emulation, 0 = eager
  * forward rows), "delta" (delta-stepping bucket width, ms; default the mean edge latency),
- * "h0_phase" (where the landmark h0 sits in its bucket, [0, 1); default 0.98; < 0: the round-4
- * bucket shifts), "slots" (concurrent SSSP
+ * "h0_phase" (where the landmark h0 sits in its bucket, [0, 1); default: at its bucket's end, a
+ * gap of min(1 % of delta, half the smallest edge latency) below it; < 0: the round-4 bucket
+ * shifts), "slots" (concurrent SSSP
  * workgroups), "device" (HIP device ordinal), "lds_hubs" (cap on LDS-resident hub distances,
  * -1 = fill), "par_hubs" (hubs with SSSP parent hints), "wg_per_cu" (SSSP workgroups sharing a
  * CU's LDS), "far_cap" / "near_cap" (entries per window bucket and overflow pile / per near

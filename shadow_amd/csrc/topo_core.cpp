@@ -244,6 +244,7 @@ struct _Topology {
     DevBuf<uint32_t> d_adjk;  // rows re-sorted by kappa = w - pi(col) (batch relaxation copy)
     DevBuf<float> d_kap, d_ksum, d_kap0;  // kappa of d_adjk (f32, rounded down), per-vertex probes
     double meanLat = -1.0;
+    double minLat = 0.0;  // smallest non-loop edge latency (edge_scan): the landmark's bucket gap
     uint64_t ipGen = 1, geomGen = 0;  // attach/detach generation; compute_geometry's copy  // mean non-loop edge latency (default delta), computed once
     DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
     DevBuf<unsigned long long> d_dist, d_best, d_qa, d_qb;
@@ -336,11 +337,13 @@ struct _Topology {
     double ordDelta = -1.0;
     double ordPhase = -2.0;
     // option "h0_phase": where the landmark h0 sits in its bucket (the fraction of the bucket
-    // below its shifted distance, which is the same for every source); default 0.98: h0 closes
-    // its bucket, so the hub core around it is expanded in the next bucket with d(h0) final and
-    // the landmark bound tight.  < 0: the round-4 shifts (sh = piMax - pi(s)
-    // + 2 delta, h0's phase whatever piMax / delta gives)
-    double h0Phase = 0.98;
+    // below its shifted distance, which is the same for every source).  Unset: h0 closes its
+    // bucket with a gap of min(0.01 delta, minLat / 2) to the bucket's end, so no neighbour of h0
+    // shares its bucket and the hub core around it is expanded in the next bucket with d(h0)
+    // final and the landmark bound tight.  < 0: the round-4 shifts (sh =
+    // piMax - pi(s) + 2 delta, h0's phase whatever piMax / delta gives)
+    double h0Phase = 0.99;
+    bool h0PhaseSet = false;
     bool replayUploaded = false;
     int64_t rnadj = 0;  // entries of the replay CSR
     DevBuf<uint32_t> d_rrow;
@@ -1055,7 +1058,7 @@ int board_ready(Topology* top, hipStream_t st) {
 void edge_scan(Topology* top) {
     if (top->meanLat >= 0) return;
     const HostGraph& g = top->g;
-    double s = 0.0, wmax = 0.0;
+    double s = 0.0, wmax = 0.0, wmin = INFINITY;
     int64_t n = 0;
     bool ints = true;
     for (int64_t e = 0; e < g.E; e++) {
@@ -1063,10 +1066,12 @@ void edge_scan(Topology* top) {
         const double w = g.elat[(size_t)e];
         s += w;
         n++;
+        wmin = std::min(wmin, w);
         if (!(w >= 0.0) || w != std::floor(w)) ints = false;
         else wmax = std::max(wmax, w);
     }
     top->replayIntOk = ints && (double)g.V * wmax < 4294967295.0;
+    top->minLat = n ? wmin : 0.0;
     top->meanLat = n ? s / (double)n : 1.0;
 }
 
@@ -1221,11 +1226,20 @@ uint64_t compute_geometry(Topology* top) {
 // sh_s = C - pi(s) puts h0 at C): the round-4 rule C = piMax + 2 delta, or, with option h0_phase
 // p in [0, 1), the smallest C >= piMax + 2 delta whose phase in its bucket is p (bkt(C) = floor(C
 // / delta); every shift stays >= 2 delta).
+// the phase h0_shift uses (-1: the round-4 shifts)
+double h0_phase(Topology* top, double delta) {
+    if (top->h0PhaseSet) return top->h0Phase >= 0.0 && top->h0Phase < 1.0 ? top->h0Phase : -1.0;
+    edge_scan(top);
+    const double gap = std::min(0.01 * delta, 0.5 * top->minLat);
+    return gap > 0.0 && gap < delta ? 1.0 - gap / delta : 0.99;
+}
+
 double h0_shift(Topology* top, double delta) {
     const double base = top->hp->to_h0_max() + 2.0 * delta;
-    if (!(top->h0Phase >= 0.0) || !(top->h0Phase < 1.0)) return base;
+    const double ph = h0_phase(top, delta);
+    if (ph < 0.0) return base;
     const double x = base / delta;
-    double b = std::floor(x - top->h0Phase) + top->h0Phase;
+    double b = std::floor(x - ph) + ph;
     if (b < x) b += 1.0;
     return b * delta;
 }
@@ -1475,7 +1489,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                                    : nbat > 3 * (int64_t)std::max(1, ws.slots) ? 4 : 2;
                 const bool cached = top->ordHp == top->hp.get() && top->ordKf == kf &&
                                     top->ordSO == top->sourceOrder && top->ordBO == border &&
-                                    top->ordDelta == delta && top->ordPhase == top->h0Phase &&
+                                    top->ordDelta == delta && top->ordPhase == h0_phase(top, delta) &&
                                     top->ordSrc == src;
                 if (!cached) {
                 // Batches of K sources settle in lock-step and share an expansion when their
@@ -1607,7 +1621,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 top->ordSO = top->sourceOrder;
                 top->ordBO = border;
                 top->ordDelta = delta;
-                top->ordPhase = top->h0Phase;
+                top->ordPhase = h0_phase(top, delta);
                 }
                 ws.rowmap = top->d_rowmap.p;
                 // the help board (option share; auto: a one-round launch, whose idle slots help
@@ -1896,6 +1910,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->replayLandmark = top->replayLandmark;
     p->replayIntOpt = top->replayIntOpt;
     if (top->meanLat >= 0 && !(p->meanLat >= 0)) {  // the owner's edge scan (same graph)
+        p->minLat = top->minLat;
         p->meanLat = top->meanLat;
         p->replayIntOk = top->replayIntOk;
     }
@@ -1903,6 +1918,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->batchOrder = top->batchOrder;
     p->batchFill = top->batchFill;
     p->h0Phase = top->h0Phase;
+    p->h0PhaseSet = top->h0PhaseSet;
     p->targetSkip = top->targetSkip;
     p->targetKappa = top->targetKappa;
     p->targetResort = top->targetResort;
@@ -2023,6 +2039,7 @@ int build_multi(Topology* top) {
                     HIPCHK(hipSetDevice(phys[(size_t)d]));
                     int rr = dev_init(T);
                     if (rr) return rr;
+                    T->minLat = top->minLat;
                     T->meanLat = top->meanLat;
                     T->replayIntOk = top->replayIntOk;  // the owner's edge scan (same graph)
                     if (!top->isComplete && !T->csrUploaded) {
@@ -2764,6 +2781,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "h0_phase") {
         if (!(value < 1.0)) return -1;
         top->h0Phase = value;
+        top->h0PhaseSet = true;
     }
     else if (k == "target_skip") top->targetSkip = value != 0;
     else if (k == "target_kappa") top->targetKappa = (int)value;
