@@ -129,7 +129,9 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * "share" (1: a batched launch's workgroups that run out of batches take part in the running
  * batches' parent walks and epilogues -- the help board; 0, the default: each batch stays in its
  * workgroup and the board-less kernel runs; -1: the board for a launch whose batches fit one
- * round of the slots).
+ * round of the slots), "balance" (1, the default: from the second batched build of a graph on,
+ * batches are sized (one round of the slots) or dequeued longest first (several rounds) by the
+ * sources' costs measured from the earlier builds' batch times; 0: the grouping order only).
  * Returns 0 or -1 for an unknown key / bad value. */
 int shdtopo_set_option(Topology* top, const char* key, double value);
 
@@ -363,6 +365,10 @@ typedef struct {
                                    jobs (parent walks, epilogues) */
     int64_t help_items[2];      /*   the items they took: walk start pairs, epilogue items */
     int64_t help_board_errors;  /*   help-board spin limits hit (cannot happen; the build fails) */
+    int64_t batch_layout_measured; /* 1: the last batched launch used the measured layout (option
+                                      "balance": batches sized / ordered by the sources' costs
+                                      from earlier builds' batch times), 0: the grouping order */
+    int64_t batches;            /*   batches of that launch */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -59,7 +59,8 @@ class ShdStats(ctypes.Structure):
                 ("device_kernel_ms", dbl * 8), ("device_build_ms", dbl * 8),
                 ("device_rows", i64 * 8), ("dev_inits", i64), ("init_bg_ms", dbl),
                 ("path_seconds_total", dbl), ("paths_computed", i64), ("help_ms", dbl),
-                ("help_items", i64 * 2), ("help_board_errors", i64)]
+                ("help_items", i64 * 2), ("help_board_errors", i64),
+                ("batch_layout_measured", i64), ("batches", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):

@@ -331,8 +331,22 @@ struct _Topology {
     DevBuf<unsigned int> d_kfChanged;
     DevBuf<uint32_t> d_rowmap, d_bsrc;  // batch order: output row and source of each position
     // cache of the last batch order (enqueue_rows): the rows' sources, batch fill and options
-    std::vector<uint32_t> ordSrc, ordPsrc;
+    std::vector<uint32_t> ordSrc;
+    std::vector<uint32_t> ordBase;  // positions in the grouping order (source_order)
+    std::vector<uint32_t> ordPerm;  // ... then batches in batch_order
+    bool ordUploaded = false;       // d_rowmap / d_bsrc / d_srcsh hold ordPerm's layout
     const HostPrep* ordHp = nullptr;
+    // measured batch layout (option "balance"): per vertex the cost of a
+    // source in its batch (wall-clock ticks, EMA over the builds; 0 = none yet), and a batch's
+    // fixed cost; the positions' sources and batch starts of the uploaded layout
+    int balance = 1;  // 2: costs frozen after the first build (diagnostic)
+    int64_t lastBatches = 0;
+    std::vector<float> srcCost;
+    const HostPrep* costHp = nullptr;
+    double costA = 0.0;
+    std::vector<uint32_t> layPsrc;
+    DevBuf<uint32_t> d_bstart;
+    DevBuf<unsigned long long> d_btrace;
     int ordKf = -1, ordSO = -1, ordBO = -1;
     double ordDelta = -1.0;
     double ordPhase = -2.0;
@@ -960,6 +974,11 @@ int ensure_workspace(Topology* top, int nsrc) {
         1, ((freeb + held) * 3 / 5) / (size_t)std::max(1, top->memShareDiv) / per_slot);
     want = std::min(want, memcap);
     want = std::max(1, std::min(want, std::max(1, units)));
+    // the batch times of the measured layout (option balance): a launch has at most nsrc batches;
+    // allocated here, with the workspace (a fresh allocation right before the launch made the
+    // first build's kernel 6-7 ms slower)
+    if (top->balance)
+        HIPCHK(top->d_btrace.ensure((size_t)std::max<int64_t>(1, std::min<int64_t>(nsrc, V)) * kBTraceWords));
     // hparN follows par_hubs: the kernel indexes the hints at slot * P * K with the current P
     if (top->slots >= want && top->wsK == K && top->wsRing == ringE && top->wsHpar >= hparN)
         return 0;
@@ -1255,6 +1274,168 @@ double default_delta(Topology* top) {
     return std::max(1e-9, 1.0 * mean);
 }
 
+// The batch layout of a launch goes to the device: output row (rowmap) and source of each
+// position, its bucket shift sh = C - d(src, h0) >= 2 delta (every source's h0 at C, h0_shift;
+// topo_sssp_batch.hip), and the batch starts of a measured layout.
+int upload_layout(Topology* top, const std::vector<uint32_t>& src, const std::vector<uint32_t>& perm,
+                  const std::vector<uint32_t>* bstart, double delta, hipStream_t st) {
+    const int64_t rows = (int64_t)src.size();
+    std::vector<uint32_t>& psrc = top->layPsrc;
+    psrc.resize((size_t)rows);
+    for (int64_t i = 0; i < rows; i++) psrc[(size_t)i] = src[(size_t)perm[(size_t)i]];
+    HIPCHK(top->d_rowmap.ensure((size_t)rows));
+    HIPCHK(top->d_bsrc.ensure((size_t)rows));
+    HIPCHK(hipMemcpyAsync(top->d_rowmap.p, perm.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(top->d_bsrc.p, psrc.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
+    const double pmax = top->hp->to_h0_max();  // largest finite d(., h0) (upload_csr)
+    const double C = h0_shift(top, delta);
+    std::vector<double> sh((size_t)rows);
+    for (int64_t i = 0; i < rows; i++) {
+        const double p = top->hp->to_h0(psrc[(size_t)i]);
+        sh[(size_t)i] = C - (std::isfinite(p) ? p : pmax);
+    }
+    HIPCHK(top->d_srcsh.ensure((size_t)rows));
+    HIPCHK(hipMemcpyAsync(top->d_srcsh.p, sh.data(), sizeof(double) * (size_t)rows,
+                          hipMemcpyHostToDevice, st));
+    if (bstart) {
+        HIPCHK(top->d_bstart.ensure(bstart->size()));
+        HIPCHK(hipMemcpyAsync(top->d_bstart.p, bstart->data(), 4 * bstart->size(),
+                              hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));  // perm / sh / bstart must outlive the copies
+    return 0;
+}
+
+// the kernel's contract (topo_sssp_batch.hip): runs of 1..K positions covering [0, rows)
+static bool check_runs(const std::vector<uint32_t>& lstart, int64_t rows, int K) {
+    if (lstart.size() < 2 || lstart.front() != 0u || lstart.back() != (uint32_t)rows) return false;
+    for (size_t b = 0; b + 1 < lstart.size(); b++)
+        if (lstart[b + 1] <= lstart[b] || lstart[b + 1] - lstart[b] > (uint32_t)K) return false;
+    return true;
+}
+
+// Measured batch layout (option balance).  A batch's wall time is modelled
+// as a fixed part a plus its sources' costs; both come from the batch times of earlier launches
+// on this graph (record_costs).  Once every source of the rows has a cost:
+//  * one round of the slots (an 8-GPU shard): the grouping order (source_order) is cut into at
+//    most `slots` runs of <= K consecutive positions minimising the largest predicted batch
+//    (greedy cuts under a bisected bound) -- batches stay runs of the grouping, so the sources
+//    that share expansions stay together, but a run of expensive sources gets fewer of them;
+//  * several rounds: batches of kf in the grouping order, dequeued longest predicted first (the
+//    dynamic dequeue is then list scheduling in LPT order), the ragged batch last.
+// The layout changes only which batch computes a row: every row is the same (bit-exact tests).
+// A re-cut from the updated costs each build beat refining the previous cut (moving edge sources
+// off the slowest batches): a batch's time repeats within ~0.3 ms for the same sources but is
+// predicted from other compositions only loosely (corr 0.4-0.7), and both end near 11 ms at 1,250
+// rows.
+bool measured_layout(Topology* top, const std::vector<uint32_t>& src, int kf, int slots,
+                     std::vector<uint32_t>& lperm, std::vector<uint32_t>& lstart) {
+    const int64_t rows = (int64_t)src.size();
+    const std::vector<uint32_t>& base = top->ordBase;
+    if (top->costHp != top->hp.get() || (int64_t)base.size() != rows || rows < 2 || kf < 1 ||
+        slots < 1)
+        return false;
+    const int K = batch_k(top);
+    std::vector<double> c((size_t)rows);
+    for (int64_t i = 0; i < rows; i++) {
+        const float x = top->srcCost[(size_t)src[(size_t)base[(size_t)i]]];
+        if (!(x > 0.0f)) return false;
+        c[(size_t)i] = (double)x;
+    }
+    const double a = top->costA;
+    const int64_t nplain = (rows + kf - 1) / kf;
+    lperm = base;
+    lstart.clear();
+    if (nplain <= (int64_t)slots) {
+        // the fewest runs whose predicted cost stays <= B (greedy is optimal for a bound)
+        auto cut = [&](double B, std::vector<uint32_t>* out) -> int64_t {
+            int64_t n = 0, i = 0;
+            if (out) out->push_back(0u);
+            while (i < rows) {
+                double s = a;
+                int m = 0;
+                while (i < rows && m < K && (m == 0 || s + c[(size_t)i] <= B)) {
+                    s += c[(size_t)i];
+                    i++;
+                    m++;
+                }
+                n++;
+                if (out) out->push_back((uint32_t)i);
+            }
+            return n;
+        };
+        double lo = a, hi = a;
+        for (int64_t b = 0; b < nplain; b++) {  // the plain layout's largest batch: feasible
+            double s = a;
+            for (int64_t i = b * kf; i < std::min(rows, (b + 1) * kf); i++) s += c[(size_t)i];
+            hi = std::max(hi, s);
+        }
+        for (int64_t i = 0; i < rows; i++) lo = std::max(lo, a + c[(size_t)i]);
+        if (cut(hi, nullptr) > (int64_t)slots) return false;
+        for (int it = 0; it < 40 && hi - lo > 1e-4 * hi; it++) {
+            const double mid = 0.5 * (lo + hi);
+            if (cut(mid, nullptr) <= (int64_t)slots) hi = mid;
+            else lo = mid;
+        }
+        cut(hi, &lstart);
+    } else {
+        std::vector<double> bc((size_t)nplain, a);
+        for (int64_t i = 0; i < rows; i++) bc[(size_t)(i / kf)] += c[(size_t)i];
+        std::vector<uint32_t> bo((size_t)nplain);
+        std::iota(bo.begin(), bo.end(), 0u);
+        const bool ragged = rows % kf != 0;
+        std::stable_sort(bo.begin(), bo.end() - (ragged ? 1 : 0),
+                         [&](uint32_t x, uint32_t y) { return bc[x] > bc[y]; });
+        lperm.clear();
+        lstart.push_back(0u);
+        for (uint32_t b : bo) {
+            for (int64_t i = (int64_t)b * kf; i < std::min(rows, ((int64_t)b + 1) * kf); i++)
+                lperm.push_back(base[(size_t)i]);
+            lstart.push_back((uint32_t)lperm.size());
+        }
+    }
+    return check_runs(lstart, rows, K);
+}
+
+// Costs from a launch's batch times (SlotWs::btrace: dequeue and end ticks per batch): the
+// fixed part a = 1/3 of the mean batch (C4: a lone source takes 4.3 ms, a batch of 5 8.9 ms,
+// of 8 10.2 ms), the rest shared equally by the batch's sources; both averaged with the earlier
+// builds' (weight 1/2), so a source that moves to another batch converges to its own share.
+void record_costs(Topology* top, const std::vector<uint32_t>& psrc, const std::vector<uint32_t>& lstart,
+                  const std::vector<unsigned long long>& bt) {
+    const int64_t nb = (int64_t)lstart.size() - 1;
+    if (nb < 1) return;
+    if (top->balance == 2 && top->costHp == top->hp.get()) return;  // frozen (diagnostic)
+    if (top->costHp != top->hp.get() || (int64_t)top->srcCost.size() != top->g.V) {
+        top->srcCost.assign((size_t)top->g.V, 0.0f);
+        top->costHp = top->hp.get();
+        top->costA = 0.0;
+    }
+    std::vector<double> T((size_t)nb, 0.0);
+    double sum = 0.0;
+    int64_t n = 0;
+    for (int64_t b = 0; b < nb; b++) {
+        const unsigned long long t0 = bt[(size_t)b * kBTraceWords], t1 = bt[(size_t)b * kBTraceWords + 1];
+        if (t1 > t0) {
+            T[(size_t)b] = (double)(t1 - t0);
+            sum += T[(size_t)b];
+            n++;
+        }
+    }
+    if (n == 0) return;
+    const double mean = sum / (double)n, a = mean / 3.0;
+    top->costA = top->costA > 0.0 ? 0.5 * (top->costA + a) : a;
+    for (int64_t b = 0; b < nb; b++) {
+        if (!(T[(size_t)b] > 0.0)) continue;
+        const uint32_t p0 = lstart[(size_t)b], p1 = lstart[(size_t)b + 1];
+        const double cs = std::max(0.01 * mean, (T[(size_t)b] - a) / (double)(p1 - p0));
+        for (uint32_t p = p0; p < p1 && p < psrc.size(); p++) {
+            float& x = top->srcCost[(size_t)psrc[p]];
+            x = x > 0.0f ? (float)(0.5 * ((double)x + cs)) : (float)cs;
+        }
+    }
+}
+
 // wall checkpoints of a whole-table build (ShdStats.build_step_ms): the time since the previous
 // mark goes to step i
 void bstep_mark(Topology* top, int i) {
@@ -1268,6 +1449,8 @@ void bstep_mark(Topology* top, int i) {
 void reset_build_stats(Topology* top) {
     top->stats.csr_ms = top->stats.csr_host_ms = top->stats.csr_copy_ms = 0.0;
     top->stats.order_ms = top->stats.replay_prep_ms = top->stats.target_prep_ms = 0.0;
+    top->stats.batch_layout_measured = 0;
+    top->lastBatches = 0;
     top->stats.workspace_ms = 0.0;
     top->stats.csr_host_runs = 0;
     top->stats.tie_probe_rows = top->stats.tie_probe_flagged = 0;
@@ -1540,6 +1723,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     std::stable_sort(perm.begin(), perm.end(),
                                      [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
                 }
+                top->ordBase = perm;  // the grouping order (the measured layout starts from it)
                 // order of the batches (groups of kf consecutive positions) in the dequeue: the
                 // kernel ends with the slowest slot, so the last batches decide its tail
                 // batch_order 5 (auto): by depth when the batches fill more than 3 rounds of the
@@ -1595,26 +1779,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                             p2.push_back(perm[(size_t)i]);
                     perm.swap(p2);
                 }
-                std::vector<uint32_t> psrc((size_t)rows);
-                for (int64_t i = 0; i < rows; i++) psrc[(size_t)i] = src[(size_t)perm[(size_t)i]];
-                HIPCHK(top->d_rowmap.ensure((size_t)rows));
-                HIPCHK(top->d_bsrc.ensure((size_t)rows));
-                HIPCHK(hipMemcpyAsync(top->d_rowmap.p, perm.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
-                HIPCHK(hipMemcpyAsync(top->d_bsrc.p, psrc.data(), 4 * (size_t)rows, hipMemcpyHostToDevice, st));
-                // bucket shift per row: sh = C - d(src, h0) >= 2 delta, every source's h0 at C
-                // (h0_shift; topo_sssp_batch.hip)
-                const double pmax = top->hp->to_h0_max();  // largest finite d(., h0) (upload_csr)
-                const double C = h0_shift(top, delta);
-                std::vector<double> sh((size_t)rows);
-                for (int64_t i = 0; i < rows; i++) {
-                    const double p = top->hp->to_h0(psrc[(size_t)i]);
-                    sh[(size_t)i] = C - (std::isfinite(p) ? p : pmax);
-                }
-                HIPCHK(top->d_srcsh.ensure((size_t)rows));
-                HIPCHK(hipMemcpyAsync(top->d_srcsh.p, sh.data(), sizeof(double) * (size_t)rows,
-                                      hipMemcpyHostToDevice, st));
-                HIPCHK(hipStreamSynchronize(st));  // perm / psrc / sh must outlive the copies
-                top->ordPsrc.swap(psrc);
+                top->ordPerm.swap(perm);
                 top->ordSrc = src;
                 top->ordHp = top->hp.get();
                 top->ordKf = kf;
@@ -1622,14 +1787,45 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 top->ordBO = border;
                 top->ordDelta = delta;
                 top->ordPhase = h0_phase(top, delta);
+                top->ordUploaded = false;
                 }
+                // the launch's layout: batches sized and ordered by the sources' measured costs
+                // (option balance, once every source has one), else the cached order
+                std::vector<uint32_t> lperm, lstart;
+                const bool measured =
+                    top->balance && measured_layout(top, src, kf, ws.slots, lperm, lstart);
+                if (measured || !top->ordUploaded) {
+                    const std::vector<uint32_t>& perm = measured ? lperm : top->ordPerm;
+                    r = upload_layout(top, src, perm, measured ? &lstart : nullptr, delta, st);
+                    if (r) return r;
+                    top->ordUploaded = !measured;
+                }
+                if (!measured) {
+                    lstart.resize((size_t)nbat + 1);
+                    for (int64_t b = 0; b <= nbat; b++) lstart[(size_t)b] = (uint32_t)std::min(rows, b * kf);
+                }
+                ws.bstart = measured ? top->d_bstart.p : nullptr;
+                ws.nbat = measured ? (int)(lstart.size() - 1) : 0;
+                const int64_t lnbat = (int64_t)lstart.size() - 1;
+                top->slotsUsed = (int)std::min<int64_t>(ws.slots, lnbat);
+                top->stats.batch_layout_measured = measured ? 1 : 0;
+                top->lastBatches = lnbat;
                 ws.rowmap = top->d_rowmap.p;
                 // the help board (option share; auto: a one-round launch, whose idle slots help
                 // its last batches -- in a launch of several rounds its code costs more than the
                 // help returns)
-                if (!(top->share > 0 || (top->share < 0 && nbat <= (int64_t)ws.slots)))
+                if (!(top->share > 0 || (top->share < 0 && lnbat <= (int64_t)ws.slots)))
                     ws.board = nullptr;
-                const std::vector<uint32_t>& psrc = top->ordPsrc;
+                const std::vector<uint32_t>& psrc = top->layPsrc;  // source of each position
+                // per batch {start tick, end tick, slot, near iterations, sweeps, expansions,
+                // relaxations, sources, ...} (kBTraceWords u64): the batch times give the sources'
+                // costs (option balance); SHD_BATCH_TRACE=<file> (diagnostic) appends them, then
+                // per batch position {source vertex, pi bits}
+                const char* btf = getenv("SHD_BATCH_TRACE");
+                if (top->balance || (btf && *btf)) {
+                    HIPCHK(top->d_btrace.ensure((size_t)lnbat * kBTraceWords));
+                    ws.btrace = top->d_btrace.p;
+                }
                 top->stats.order_ms = std::chrono::duration<double, std::milli>(
                     std::chrono::steady_clock::now() - to0).count();
                 HIPCHK(hipEventRecord(top->ev0, st));
@@ -1641,36 +1837,32 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 if (r) return r;
                 r = board_ready(top, st);  // (a tie probe launch used it)
                 if (r) return r;
-                // diagnostic: SHD_BATCH_TRACE=<file> appends per batch {start tick, end tick,
-                // slot, near iterations, sweeps, expansions, relaxations, sources}, then per
-                // batch position {source vertex, pi bits}
-                const char* btf = getenv("SHD_BATCH_TRACE");
-                const int64_t nbt = (rows + kf - 1) / kf;
-                if (btf && *btf) HIPCHK(hipMalloc((void**)&ws.btrace, 8 * kBTraceWords * (size_t)nbt));
                 bstep_mark(top, 2);
                 HIPCHK(launch_sssp_batch(K, dev_csr(top), ws, top->d_bsrc.p,
-                                         top->d_srcsh.p, (int)rows, kf, top->d_targets.p, (int)A,
-                                         delta, bp, top->iterGuard, out_lr, out_hops,
+                                         top->d_srcsh.p, (int)rows, measured ? K : kf, top->d_targets.p,
+                                         (int)A, delta, bp, top->iterGuard, out_lr, out_hops,
                                          out_rowmin, top->d_stats.p, st));
                 HIPCHK(hipEventRecord(top->ev1, st));
                 HIPCHK(hipStreamSynchronize(st));  // the kernel's wall time goes to step 3
                 bstep_mark(top, 3);
                 if (ws.btrace) {
-                    std::vector<unsigned long long> bt((size_t)nbt * kBTraceWords);
-                    HIPCHK(hipMemcpy(bt.data(), ws.btrace, 8 * kBTraceWords * (size_t)nbt, hipMemcpyDeviceToHost));
-                    HIPCHK(hipFree(ws.btrace));
+                    std::vector<unsigned long long> bt((size_t)lnbat * kBTraceWords);
+                    HIPCHK(hipMemcpy(bt.data(), ws.btrace, 8 * kBTraceWords * (size_t)lnbat, hipMemcpyDeviceToHost));
                     ws.btrace = nullptr;
-                    if (FILE* f = fopen(btf, "ab")) {
-                        const int64_t hdr[4] = {nbt, kf, (int64_t)ws.slots, rows};
-                        fwrite(hdr, 8, 4, f);
-                        fwrite(bt.data(), 8, bt.size(), f);
-                        for (int64_t i = 0; i < rows; i++) {
-                            const double p = top->hp->pot[(size_t)psrc[(size_t)i]];
-                            const int64_t rec[2] = {(int64_t)psrc[(size_t)i], 0};
-                            fwrite(rec, 8, 1, f);
-                            fwrite(&p, 8, 1, f);
+                    if (top->balance) record_costs(top, psrc, lstart, bt);
+                    if (btf && *btf) {
+                        if (FILE* f = fopen(btf, "ab")) {
+                            const int64_t hdr[4] = {lnbat, measured ? 0 : kf, (int64_t)ws.slots, rows};
+                            fwrite(hdr, 8, 4, f);
+                            fwrite(bt.data(), 8, bt.size(), f);
+                            for (int64_t i = 0; i < rows; i++) {
+                                const double p = top->hp->pot[(size_t)psrc[(size_t)i]];
+                                const int64_t rec[2] = {(int64_t)psrc[(size_t)i], 0};
+                                fwrite(rec, 8, 1, f);
+                                fwrite(&p, 8, 1, f);
+                            }
+                            fclose(f);
                         }
-                        fclose(f);
                     }
                 }
             }
@@ -1767,6 +1959,7 @@ int collect_row_stats(Topology* top) {
     top->stats.help_items[0] = (int64_t)h[ST_HELP_ITEMS];
     top->stats.help_items[1] = (int64_t)h[ST_HELP_ITEMS + 1];
     top->stats.help_board_errors = (int64_t)h[ST_HB_ERR];
+    top->stats.batches = top->lastBatches;
     if (h[ST_HB_ERR]) CRITICAL("help board: %llu spin limits hit", h[ST_HB_ERR]);
     for (int i = 0; i < 4; i++) top->stats.walk_kinds[i] = (int64_t)h[ST_WK0 + i];
     top->stats.replay_pops = (int64_t)h[ST_RP_POPS];
@@ -1915,6 +2108,7 @@ void sync_peer(Topology* top, Topology* p) {
         p->replayIntOk = top->replayIntOk;
     }
     p->sourceOrder = top->sourceOrder;
+    p->balance = top->balance;
     p->batchOrder = top->batchOrder;
     p->batchFill = top->batchFill;
     p->h0Phase = top->h0Phase;
@@ -2778,6 +2972,7 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "source_order") top->sourceOrder = (int)value;
     else if (k == "batch_order") top->batchOrder = (int)value;
     else if (k == "batch_fill") top->batchFill = (int)value;
+    else if (k == "balance") top->balance = (int)value;
     else if (k == "h0_phase") {
         if (!(value < 1.0)) return -1;
         top->h0Phase = value;

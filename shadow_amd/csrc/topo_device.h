@@ -163,6 +163,10 @@ struct SlotWs {
     // finished batches, zeroed before every launch; nullptr = every batch's parent walks and
     // epilogue stay in its own workgroup
     uint32_t* board = nullptr;
+    // batch layout (option balance, topo_core.cpp): batch b takes positions [bstart[b],
+    // bstart[b + 1]) (at most K), nbat batches; nullptr = batch b takes [b kf, b kf + kf)
+    const uint32_t* bstart = nullptr;
+    int nbat = 0;
 };
 constexpr int kBoardWords = 64;
 constexpr int kBTraceWords = 12;  // u32 words per slot entry of the help board (256 B)

@@ -1496,10 +1496,18 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         const uint32_t bidx = L.idx;
         __syncthreads();
         // batch bidx: sources [bidx kf, bidx kf + kf) in lanes 0..nk-1 (kf <= K: the host fills
-        // batches below K when that finishes the sources in fewer rounds of the slots)
-        if ((int64_t)bidx * kf >= nsrc) break;
-        const int r0 = (int)bidx * kf;
-        const int nk = min(kf, nsrc - r0);
+        // batches below K when that finishes the sources in fewer rounds of the slots), or the
+        // host's layout [bstart[bidx], bstart[bidx + 1]) sized by measured costs
+        int r0, nk;
+        if (ws.bstart) {
+            if (bidx >= (uint32_t)ws.nbat) break;
+            r0 = (int)ws.bstart[bidx];
+            nk = (int)ws.bstart[bidx + 1] - r0;
+        } else {
+            if ((int64_t)bidx * kf >= nsrc) break;
+            r0 = (int)bidx * kf;
+            nk = min(kf, nsrc - r0);
+        }
         if (tid == 0) L.tk = wall_clock64();
         if (ws.btrace && tid == 0) {
             ws.btrace[kBTraceWords * (size_t)bidx] = L.tk;
@@ -2467,7 +2475,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     // relaxed loads; an idle scan sleeps.
     if (BOARD && ws.board) {
         const unsigned long long th0 = wall_clock64();
-        const uint32_t nbat = (uint32_t)((nsrc + kf - 1) / kf);
+        const uint32_t nbat = ws.bstart ? (uint32_t)ws.nbat : (uint32_t)((nsrc + kf - 1) / kf);
         const uint32_t* const gw = ws.board + (size_t)gridDim.x * kBoardWords;
         unsigned long long tprog = th0;  // (thread 0) the last progress seen
         uint32_t lastDone = 0, lastPub = 0xFFFFFFFFu;
@@ -2934,7 +2942,8 @@ static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32
                                  double2* out_lr, uint16_t* out_hops, double* out_rowmin,
                                  unsigned long long* d_stats, hipStream_t stream) {
     if (kf < 1 || kf > K) return hipErrorInvalidValue;
-    const int nb = (nsrc + kf - 1) / kf;
+    // (a layout's batches are checked on the host: each within 1..K positions, covering [0, nsrc))
+    const int nb = ws.bstart ? ws.nbat : (nsrc + kf - 1) / kf;
     // with the help board every slot runs: the ones without a batch help the others' jobs
     const int grid = ws.board ? ws.slots : (ws.slots < nb ? ws.slots : nb);
     if (grid < 1) return hipSuccess;

@@ -230,7 +230,8 @@ def test_synthetic_directed_shape_and_bucket_options():
     assert all((b, a) in fwd for a, b in fwd)  # every arc has its reverse
     und = sa.Topology.synthetic(seed=3, n_routers=500, n_poi=40, n_edges=5000)
     assert not und.is_directed and und.num_edges == 5000
-    for k, v in (("delta", 25.0), ("h0_phase", 0.5), ("h0_phase", 0.0), ("h0_phase", -1)):
+    for k, v in (("delta", 25.0), ("h0_phase", 0.5), ("h0_phase", 0.0), ("h0_phase", -1),
+                 ("balance", 0), ("balance", 1)):
         top.set_option(k, v)
     with pytest.raises(KeyError):
         top.set_option("h0_phase", 1.0)

@@ -227,6 +227,39 @@ def test_sssp_batch_order_and_rounds(order, slots, fill):
     assert np.array_equal(hops, ohops.astype(np.uint16))
 
 
+@pytest.mark.parametrize("slots,integer", [(64, False), (64, True), (8, False)])
+def test_measured_batch_layout_rebuilds_equal_oracle(slots, integer):
+    """Option balance (default on): from the second build on, batches are cut and ordered by the
+    sources' costs measured from the previous builds' batch times -- 300 rows on 64 slots run one
+    round (runs of the grouping order sized to equal predicted time), on 8 slots several rounds
+    (batches dequeued longest predicted first).  Every rebuild equals the oracle bit for bit."""
+    top, g = synthetic_pair(seed=37, n_routers=3000, n_poi=150, n_edges=30000, integer=integer)
+    top.set_option("slots", slots)
+    top.set_option("tie_dense", 0)  # the batch kernel path (no tie probe)
+    otop, ips, verts = attach_hosts(top, g, 300, type_hints=["client", "relay", "server"])
+    oa, olat, orel, ohops = g.table(verts)
+    sizes = set()
+    for rep in range(4):
+        if rep:
+            top.rebuild()
+        a, lat, rel, hops = top.table()
+        st = top.stats()
+        assert st["errors"] == 0
+        assert st["batch_layout_measured"] == (1 if rep else 0)
+        assert 0 < st["batches"] and (slots == 8 or st["batches"] <= slots)
+        sizes.add(st["batches"])
+        assert np.array_equal(a, oa)
+        assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+        assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+        assert np.array_equal(hops, ohops.astype(np.uint16))
+    top.set_option("balance", 0)
+    top.rebuild()
+    a, lat, rel, hops = top.table()
+    assert top.stats()["batch_layout_measured"] == 0
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+
+
 def test_sssp_rows_shard_equals_full():
     """build_rows on a row range == the same rows of the full table (sharding correctness)."""
     import torch

@@ -50,6 +50,8 @@ for rep in range(args.reps):
           % (rep, rows, dt, st["sssp_kernel_ms"], rows * E / (st["sssp_kernel_ms"] / 1e3) / 1e9,
              st["relaxations"] / rows, st["ambiguous_pairs"], st["errors"], st["long_paths"]),
           flush=True)
+    print("   batches %d (measured layout %d), fill %d, order %.2f ms" % (
+        st["batches"], st["batch_layout_measured"], st["batch_fill"], st["order_ms"]), flush=True)
     ph = st["phase_ms"]
     print("   per-source ms: init %.2f sssp %.2f parents %.2f targets %.2f | near-it/src %.0f "
           "splits/src %.0f slots %d" % tuple([x / rows for x in ph] +
