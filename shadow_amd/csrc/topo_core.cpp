@@ -1510,6 +1510,13 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                                               (top->tieDenseOpt < 0 && top->tieDense));
         const bool allReplay = top->replayAll || top->hasMultiEdges || dense;
         bool probeDense = false;  // the tie probe below found the topology tie-dense
+        // the batched launch's per-batch times, read back after its closing event: its batch
+        // starts, fill (0: measured layout), slots and the SHD_BATCH_TRACE file
+        struct {
+            std::vector<uint32_t> start;
+            int kf = 0, slots = 0;
+            const char* file = nullptr;
+        } bt;
         std::vector<uint32_t> src((size_t)rows), tgt((size_t)A);
         for (int64_t i = 0; i < rows; i++) src[(size_t)i] = (uint32_t)top->hp->inv[(size_t)top->attached[(size_t)(row0 + i)]];
         for (int64_t i = 0; i < A; i++) tgt[(size_t)i] = (uint32_t)top->hp->inv[(size_t)top->attached[(size_t)i]];
@@ -1816,7 +1823,6 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 // help returns)
                 if (!(top->share > 0 || (top->share < 0 && lnbat <= (int64_t)ws.slots)))
                     ws.board = nullptr;
-                const std::vector<uint32_t>& psrc = top->layPsrc;  // source of each position
                 // per batch {start tick, end tick, slot, near iterations, sweeps, expansions,
                 // relaxations, sources, ...} (kBTraceWords u64): the batch times give the sources'
                 // costs (option balance); SHD_BATCH_TRACE=<file> (diagnostic) appends them, then
@@ -1845,30 +1851,39 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 HIPCHK(hipEventRecord(top->ev1, st));
                 HIPCHK(hipStreamSynchronize(st));  // the kernel's wall time goes to step 3
                 bstep_mark(top, 3);
-                if (ws.btrace) {
-                    std::vector<unsigned long long> bt((size_t)lnbat * kBTraceWords);
-                    HIPCHK(hipMemcpy(bt.data(), ws.btrace, 8 * kBTraceWords * (size_t)lnbat, hipMemcpyDeviceToHost));
-                    ws.btrace = nullptr;
-                    if (top->balance) record_costs(top, psrc, lstart, bt);
-                    if (btf && *btf) {
-                        if (FILE* f = fopen(btf, "ab")) {
-                            const int64_t hdr[4] = {lnbat, measured ? 0 : kf, (int64_t)ws.slots, rows};
-                            fwrite(hdr, 8, 4, f);
-                            fwrite(bt.data(), 8, bt.size(), f);
-                            for (int64_t i = 0; i < rows; i++) {
-                                const double p = top->hp->pot[(size_t)psrc[(size_t)i]];
-                                const int64_t rec[2] = {(int64_t)psrc[(size_t)i], 0};
-                                fwrite(rec, 8, 1, f);
-                                fwrite(&p, 8, 1, f);
-                            }
-                            fclose(f);
-                        }
-                    }
+                if (ws.btrace) {  // read back after the build's closing event (below)
+                    bt.kf = measured ? 0 : kf;
+                    bt.slots = ws.slots;
+                    bt.start.swap(lstart);
+                    bt.file = btf;
                 }
             }
         }
         HIPCHK(hipEventRecord(top->ev1, st));
         HIPCHK(hipStreamSynchronize(st));
+        // the batch times: the sources' costs (option balance) and the SHD_BATCH_TRACE file -- after
+        // ev1, so the copy and the host work stay out of the kernel's event time
+        if (!bt.start.empty()) {
+            const int64_t lnbat = (int64_t)bt.start.size() - 1;
+            const std::vector<uint32_t>& psrc = top->layPsrc;
+            std::vector<unsigned long long> bv((size_t)lnbat * kBTraceWords);
+            HIPCHK(hipMemcpy(bv.data(), top->d_btrace.p, 8 * kBTraceWords * (size_t)lnbat, hipMemcpyDeviceToHost));
+            if (top->balance) record_costs(top, psrc, bt.start, bv);
+            if (bt.file && *bt.file) {
+                if (FILE* f = fopen(bt.file, "ab")) {
+                    const int64_t hdr[4] = {lnbat, (int64_t)bt.kf, (int64_t)bt.slots, rows};
+                    fwrite(hdr, 8, 4, f);
+                    fwrite(bv.data(), 8, bv.size(), f);
+                    for (int64_t i = 0; i < rows; i++) {
+                        const double p = top->hp->pot[(size_t)psrc[(size_t)i]];
+                        const int64_t rec[2] = {(int64_t)psrc[(size_t)i], 0};
+                        fwrite(rec, 8, 1, f);
+                        fwrite(&p, 8, 1, f);
+                    }
+                    fclose(f);
+                }
+            }
+        }
         // rows that need igraph's heap pop order: replayed exactly on the GPU
         std::vector<uint32_t> rlist;
         top->stats.tie_dense = dense || probeDense ? 1 : 0;
