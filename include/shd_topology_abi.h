@@ -372,6 +372,16 @@ typedef struct {
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 
+/* Test hook: the measured batch layout (option "balance") for per-position
+ * costs cost[rows] (grouping order) with a batch's fixed part `fixed`, batch fill `fill`, `slots`
+ * workgroups and batch width `batch`.  order u32[rows] receives the grouping positions in launch
+ * order, starts u32[rows + 1] the batch starts (*nbatches + 1 entries): one round of the slots =
+ * runs of the grouping order minimising the largest predicted batch; several rounds = batches of
+ * `fill` consecutive positions, longest predicted first, the ragged one last.  Returns 0, or -1
+ * when no layout applies (the build then keeps the grouping order).  Host-only: no device use. */
+int shdtopo_test_batch_layout(const double* cost, int64_t rows, double fixed, int fill, int slots,
+                              int batch, uint32_t* order, uint32_t* starts, int64_t* nbatches);
+
 /* Test hook: run the exact heap replay (igraph_get_shortest_paths_dijkstra restated on the GPU)
  * from vertex `src` over the current attached set.  full = 1 runs to an empty heap instead of
  * stopping when every attached vertex is popped.  dist f64[V] (-1 = unreached) and parent int32[V]

@@ -1328,23 +1328,16 @@ static bool check_runs(const std::vector<uint32_t>& lstart, int64_t rows, int K)
 // off the slowest batches): a batch's time repeats within ~0.3 ms for the same sources but is
 // predicted from other compositions only loosely (corr 0.4-0.7), and both end near 11 ms at 1,250
 // rows.
-bool measured_layout(Topology* top, const std::vector<uint32_t>& src, int kf, int slots,
-                     std::vector<uint32_t>& lperm, std::vector<uint32_t>& lstart) {
-    const int64_t rows = (int64_t)src.size();
-    const std::vector<uint32_t>& base = top->ordBase;
-    if (top->costHp != top->hp.get() || (int64_t)base.size() != rows || rows < 2 || kf < 1 ||
-        slots < 1)
-        return false;
-    const int K = batch_k(top);
-    std::vector<double> c((size_t)rows);
-    for (int64_t i = 0; i < rows; i++) {
-        const float x = top->srcCost[(size_t)src[(size_t)base[(size_t)i]]];
-        if (!(x > 0.0f)) return false;
-        c[(size_t)i] = (double)x;
-    }
-    const double a = top->costA;
+// The layout from the costs c (per position of the grouping order) and the fixed part a: `order`
+// lists the grouping positions in launch order, `lstart` the batch starts (shdtopo_test_batch_layout
+// exposes it to the CPU tests).
+static bool layout_from_costs(const std::vector<double>& c, double a, int kf, int slots, int K,
+                              std::vector<uint32_t>& order, std::vector<uint32_t>& lstart) {
+    const int64_t rows = (int64_t)c.size();
+    if (rows < 1 || kf < 1 || kf > K || slots < 1) return false;
     const int64_t nplain = (rows + kf - 1) / kf;
-    lperm = base;
+    order.resize((size_t)rows);
+    std::iota(order.begin(), order.end(), 0u);
     lstart.clear();
     if (nplain <= (int64_t)slots) {
         // the fewest runs whose predicted cost stays <= B (greedy is optimal for a bound)
@@ -1386,15 +1379,33 @@ bool measured_layout(Topology* top, const std::vector<uint32_t>& src, int kf, in
         const bool ragged = rows % kf != 0;
         std::stable_sort(bo.begin(), bo.end() - (ragged ? 1 : 0),
                          [&](uint32_t x, uint32_t y) { return bc[x] > bc[y]; });
-        lperm.clear();
+        order.clear();
         lstart.push_back(0u);
         for (uint32_t b : bo) {
             for (int64_t i = (int64_t)b * kf; i < std::min(rows, ((int64_t)b + 1) * kf); i++)
-                lperm.push_back(base[(size_t)i]);
-            lstart.push_back((uint32_t)lperm.size());
+                order.push_back((uint32_t)i);
+            lstart.push_back((uint32_t)order.size());
         }
     }
     return check_runs(lstart, rows, K);
+}
+
+bool measured_layout(Topology* top, const std::vector<uint32_t>& src, int kf, int slots,
+                     std::vector<uint32_t>& lperm, std::vector<uint32_t>& lstart) {
+    const int64_t rows = (int64_t)src.size();
+    const std::vector<uint32_t>& base = top->ordBase;
+    if (top->costHp != top->hp.get() || (int64_t)base.size() != rows || rows < 2) return false;
+    std::vector<double> c((size_t)rows);
+    for (int64_t i = 0; i < rows; i++) {
+        const float x = top->srcCost[(size_t)src[(size_t)base[(size_t)i]]];
+        if (!(x > 0.0f)) return false;
+        c[(size_t)i] = (double)x;
+    }
+    std::vector<uint32_t> order;
+    if (!layout_from_costs(c, top->costA, kf, slots, batch_k(top), order, lstart)) return false;
+    lperm.resize((size_t)rows);
+    for (int64_t i = 0; i < rows; i++) lperm[(size_t)i] = base[(size_t)order[(size_t)i]];
+    return true;
 }
 
 // Costs from a launch's batch times (SlotWs::btrace: dequeue and end ticks per batch): the
@@ -3444,6 +3455,18 @@ int shdtopo_get_stats(Topology* top, ShdStats* out) {
     top->stats.path_seconds_total = top->spTotalSec;
     top->stats.paths_computed = (int64_t)top->spCount;
     *out = top->stats;
+    return 0;
+}
+
+int shdtopo_test_batch_layout(const double* cost, int64_t rows, double fixed, int fill, int slots,
+                              int batch, uint32_t* order, uint32_t* starts, int64_t* nbatches) {
+    if (!cost || !order || !starts || !nbatches || rows < 1 || rows > (1 << 30)) return -1;
+    std::vector<double> c(cost, cost + rows);
+    std::vector<uint32_t> ord, st;
+    if (!layout_from_costs(c, fixed, fill, slots, batch, ord, st)) return -1;
+    std::copy(ord.begin(), ord.end(), order);
+    std::copy(st.begin(), st.end(), starts);
+    *nbatches = (int64_t)st.size() - 1;
     return 0;
 }
 

@@ -235,3 +235,75 @@ def test_synthetic_directed_shape_and_bucket_options():
         top.set_option(k, v)
     with pytest.raises(KeyError):
         top.set_option("h0_phase", 1.0)
+
+
+def _layout(cost, fixed, fill, slots, batch):
+    lib, _ = _lib.load()
+    cost = np.ascontiguousarray(cost, dtype=np.float64)
+    n = len(cost)
+    order = np.zeros(n, np.uint32)
+    starts = np.zeros(n + 1, np.uint32)
+    nb = ctypes.c_int64(0)
+    r = lib.shdtopo_test_batch_layout(cost.ctypes.data, n, fixed, fill, slots, batch,
+                                      order.ctypes.data, starts.ctypes.data, ctypes.byref(nb))
+    return r, order, starts[:nb.value + 1]
+
+
+def _best_runs(cost, fixed, slots, batch):
+    """Brute force: the smallest largest-run cost over every cut into <= slots runs of <= batch."""
+    n = len(cost)
+    best = [[np.inf] * (slots + 1) for _ in range(n + 1)]  # best[i][k]: first i positions, k runs
+    best[0][0] = 0.0
+    for i in range(1, n + 1):
+        for k in range(1, slots + 1):
+            for m in range(1, min(batch, i) + 1):
+                prev = best[i - m][k - 1]
+                if prev < np.inf:
+                    best[i][k] = min(best[i][k], max(prev, fixed + cost[i - m:i].sum()))
+    return min(best[n][1:])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_measured_layout_one_round_is_min_max(seed):
+    """Option balance, one round of the slots: runs of the grouping order,
+    at most `slots` runs of 1..batch positions covering every row once, minimising the largest
+    predicted batch (fixed part + its sources' costs) -- checked against a brute-force cut."""
+    rng = np.random.default_rng(seed)
+    n, slots, batch = int(rng.integers(8, 20)), int(rng.integers(3, 6)), 4
+    fill = -(-n // slots)
+    if fill > batch:
+        n = slots * batch
+        fill = batch
+    cost = rng.uniform(0.5, 3.0, n) * (1 + 4 * (rng.random(n) < 0.15))  # a few heavy sources
+    fixed = 1.5
+    r, order, starts = _layout(cost, fixed, fill, slots, batch)
+    assert r == 0
+    assert np.array_equal(order, np.arange(n))  # runs keep the grouping order
+    sizes = np.diff(starts.astype(np.int64))
+    assert starts[0] == 0 and starts[-1] == n and len(sizes) <= slots
+    assert sizes.min() >= 1 and sizes.max() <= batch
+    got = max(fixed + cost[a:b].sum() for a, b in zip(starts[:-1], starts[1:]))
+    plain = max(fixed + cost[i:i + fill].sum() for i in range(0, n, fill))
+    assert got <= plain + 1e-9
+    assert got <= _best_runs(cost, fixed, slots, batch) * (1 + 2e-4)
+
+
+def test_measured_layout_several_rounds_longest_first():
+    """Several rounds: batches stay groups of `fill` consecutive grouping positions, dequeued by
+    predicted cost descending (list scheduling in LPT order), the ragged batch last."""
+    rng = np.random.default_rng(3)
+    n, fill, slots = 203, 8, 4
+    cost = rng.uniform(0.2, 2.0, n)
+    r, order, starts = _layout(cost, 1.0, fill, slots, 8)
+    assert r == 0
+    assert sorted(order.tolist()) == list(range(n))
+    groups = [order[a:b] for a, b in zip(starts[:-1], starts[1:])]
+    assert len(groups) == -(-n // fill)
+    for g in groups:  # whole groups of the grouping order
+        assert g[0] % fill == 0 and np.array_equal(g, np.arange(g[0], g[0] + len(g)))
+    assert len(groups[-1]) == n % fill  # the ragged batch last
+    pred = [1.0 + cost[g].sum() for g in groups[:-1]]
+    assert all(x >= y for x, y in zip(pred, pred[1:]))
+    # no layout for bad shapes: the build keeps the grouping order
+    assert _layout(cost, 1.0, 9, slots, 8)[0] == -1
+    assert _layout(cost[:1], 1.0, 1, 0, 8)[0] == -1
