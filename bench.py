@@ -240,6 +240,81 @@ def cpu_route_baseline(lat, rel, payload, state, now, jump, nthreads=1):
     return len(lat) / (time.perf_counter() - t0)
 
 
+def getters_block(top, pk, n_q, nthreads, cpu):
+    """The per-packet getter path as unchanged Shadow drives it: n_q queries of
+    the C5 window, each the getReliability + getLatency pair of shd-worker.c:352,360, issued by
+    worker threads through the C ABI (tests/c/libgetter_bench.so).  Pass 1 follows a rebuild: the
+    lazy emulation materialises rows and each row the queries touch is copied to the host on its
+    first read (16 A bytes).  Passes 2-3 are warm (1 thread, then every thread of the job's share).
+    Beside it, on N = 1, the reference's own cached path restated in C (oracle.c orc_cache_*:
+    virtualIP + two-level path cache behind RW locks, shd-topology.c:450-531,876-958), timed on
+    cache hits only."""
+    import ctypes
+    g = ctypes.CDLL(os.path.join(ROOT, "tests", "c", "libgetter_bench.so"))
+    P = ctypes.c_void_p
+    g.getbench_run.restype = ctypes.c_int64
+    g.getbench_run.argtypes = [P, ctypes.c_int64, P, P, ctypes.c_int, P, P]
+    pp = lambda a: a.ctypes.data_as(P)
+    sip = np.ascontiguousarray(pk["src_ip"][:n_q], np.uint32)
+    dip = np.ascontiguousarray(pk["dst_ip"][:n_q], np.uint32)
+    n = len(sip)
+    calls = 2 * n
+
+    def run(nt):
+        lat, rel = np.empty(n), np.empty(n)
+        ns = g.getbench_run(top._h, n, pp(sip), pp(dip), int(nt), pp(lat), pp(rel))
+        if ns <= 0:
+            raise RuntimeError("getter bench failed (%d)" % ns)
+        return ns / 1e9, lat, rel
+
+    s0 = top.stats()
+    t0, lat0, rel0 = run(nthreads)
+    s1 = top.stats()
+    t1, lat1, rel1 = run(1)
+    tn, latn, reln = run(nthreads)
+    u = lambda a: a.view(np.uint64)
+    # (the orientation of an answer depends on which rows the lazy emulation materialised first,
+    # shd-topology.c:894-915, so passes may differ in the last bits of asymmetric pairs; the
+    # getters' values are checked against the table by tests/test_getters_mt.py)
+    valid = bool(all(np.all(x > 0) for x in (lat0, lat1, latn)) and
+                 all(np.all((x >= 0) & (x <= 1)) for x in (rel0, rel1, reln)))
+    out = dict(queries=n, getter_calls=calls, threads=nthreads,
+               cold_pass=dict(threads=nthreads, ms=round(t0 * 1e3, 2),
+                              rows_copied=int(s1["rows_to_host"] - s0["rows_to_host"]),
+                              rows_copy_ms=round(s1["rows_to_host_ms"] - s0["rows_to_host_ms"], 2),
+                              bytes_per_row=16 * len(top.attached_vertices())),
+               ns_per_call_1_thread=round(t1 * 1e9 / calls, 1),
+               ns_per_call_per_thread=round(tn * 1e9 * nthreads / calls, 1),
+               calls_per_s_1_thread=round(calls / t1, 1),
+               calls_per_s_all_threads=round(calls / tn, 1),
+               answers_valid=valid,
+               note="getter call = one topology_getReliability or topology_getLatency (Shadow "
+                    "issues the pair per packet); the first pass after a rebuild copies each row "
+                    "it reads once (rows_copied x bytes_per_row), later calls read host rows "
+                    "without a lock")
+    if cpu:
+        import oracle
+        ips = np.unique(np.concatenate([sip, dip]))
+        verts = np.array([top.vertex_of_ip(int(x)) for x in ips], np.int32)
+        vmap = dict(zip(ips.tolist(), verts.tolist()))
+        sv = np.array([vmap[x] for x in sip.tolist()], np.int32)
+        dv = np.array([vmap[x] for x in dip.tolist()], np.int32)
+        oc = oracle.OracleCache(ips, verts, directed=top.is_directed)
+        oc.store(sv, dv, lat1, rel1)
+        r1, olat, orel = oc.bench(sip, dip, 1)
+        rn, _, _ = oc.bench(sip, dip, nthreads)
+        oc.free()
+        out["reference_cached"] = dict(
+            kind="port", ns_per_call_1_thread=round(r1 * 1e9 / calls, 1),
+            ns_per_call_per_thread=round(rn * 1e9 * nthreads / calls, 1),
+            calls_per_s_1_thread=round(calls / r1, 1),
+            calls_per_s_all_threads=round(calls / rn, 1),
+            answers_equal=bool(np.array_equal(u(olat), u(lat1)) and np.array_equal(u(orel), u(rel1))),
+            note="the reference's getPathEntry on cache hits (the pairs filled beforehand): 2 "
+                 "virtualIP lookups + 1-2 path-cache lookups, each under its RW lock")
+    return out
+
+
 def load_pmc(path, key):
     """A committed counter summary (tools/summarize_prof.py) if it was measured on this exact
     workload and code (key), else None."""
@@ -298,6 +373,8 @@ def main():
     ap.add_argument("--no-complete", action="store_true", help="skip the C2/C3 table lines")
     ap.add_argument("--no-directed", action="store_true", help="skip the C4-dir line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--getter-queries", type=int, default=1_000_000,
+                    help="queries of the getters block (0: skip it)")
     ap.add_argument("--delta", type=float, default=0.0)
     ap.add_argument("--integer", action="store_true",
                     help="C4-int variant (integer latencies U{1..100}: heavy parent ties)")
@@ -434,8 +511,15 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    # ---- cold build: the first table of the loaded topology, right after the attach phase ----
-    step()
+    # ---- cold build: the first table of the loaded topology, right after the attach phase.  In
+    # library mode it is what Shadow's first packet triggers: topology_getLatency of two hosts
+    # (shd-worker.c:360) builds the whole table and answers from its first copied row ----
+    first_lat = None
+    if library:
+        first_lat = top.latency_ip(sa.ip_to_network("11.0.0.1"), sa.ip_to_network("11.0.0.2"))
+        assert first_lat > 0, "the first getter failed"
+    else:
+        step()
     barrier()
     t1 = time.perf_counter()
     cold_s = max_over_ranks(t1 - t_att1)
@@ -501,6 +585,12 @@ def main():
     barrier()
     t_window = max_over_ranks(time.perf_counter() - tr0) / args.route_steps
     routes_per_s = args.packets / t_window
+
+    getters = None
+    if library and rank == 0 and args.getter_queries > 0:
+        log(rank, "getters block: %d queries..." % args.getter_queries)
+        getters = getters_block(top, pk, args.getter_queries, cpu_share(),
+                                cpu=ngpu == 1 and not args.no_cpu_baseline)
 
     if rank == 0:
         srch = source_hash()
@@ -576,13 +666,20 @@ def main():
                                           [round(x, 2) for x in cs["attach_prep_step_ms"]])),
             attach_phase_ms=round(attach_phase_s * 1e3, 2),
             first_attach_to_table_ms=round(attach_to_table_s * 1e3, 2),
+            trigger="first topology_getLatency (library mode)" if library else "shdtopo_build_rows",
+            first_getter_ms=round(attach_to_table_s * 1e3, 2) if library else None,
+            getter_beyond_build_ms=round(cold_s * 1e3 - cs["build_wall_ms"] - cold_wait_ms, 2)
+            if library else None,
             library_first_attach_to_table_ms=round(cs["first_attach_to_table_ms"], 2),
             serialised_ms=round(cs["attach_prep_ms"] + cold_s * 1e3 - cold_wait_ms, 2),
             tie_probe=dict(rows=int(cs["tie_probe_rows"]), flagged=int(cs["tie_probe_flagged"]),
                            ms=round(cs["tie_probe_ms"], 2)),
             host_ms=round(host_ms, 2), host_frac=round(host_ms / (cold_s * 1e3), 4),
             host_preparations=int(cs["csr_host_runs"]),
-            note="ms = the first build call, made right after the attach phase (attach_phase_ms: "
+            note="ms = the first getter (library mode: topology_getLatency of hosts 0 -> 1, which "
+                 "builds the whole table and answers from one copied row; first_getter_ms = first "
+                 "attach -> that answer; getter_beyond_build_ms = its time outside the build and "
+                 "the lock wait), made right after the attach phase (attach_phase_ms: "
                  "%d hosts, wall clock); device init, graph preparation and the workspace run "
                  "from the first attach on in a background thread (attach_prep_ms) that overlaps "
                  "the attaches, and the build waits build_wait_ms for the rest of it; "
@@ -666,6 +763,7 @@ def main():
             "ms_per_window": round(t_window * 1e3, 4),
             "roofline": roofline,
             "route_roofline": route_roof,
+            "getters": getters,
             "sssp": sssp,
             "cpu_baseline": cpu,
             "runahead_min_latency_ms": gmin,

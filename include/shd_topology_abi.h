@@ -214,6 +214,15 @@ int shdtopo_route_batch_device_slot(Topology* top, int slot, const int32_t* d_sr
 /* lazily tracked minimum (reference trajectory, shd-topology.c:500-511) */
 double shdtopo_get_lazy_minimum_latency(Topology* top);
 
+/* Test hook: the source rows the lazy emulation has materialised so far (the rows whose
+ * computeSourcePaths the reference would have run, shd-topology.c:900-915): up to cap vertices
+ * with, per vertex, the attach epoch of its latest materialisation (epochs grow; a row
+ * materialised again after a late attach gets a larger one) and the row minimum that
+ * materialisation offered to the running minimum (shd-topology.c:500-511).  Any array may be
+ * NULL.  Returns the number of materialised rows (may exceed cap), -1 on a NULL topology. */
+int64_t shdtopo_lazy_rows(Topology* top, int32_t* vertex, uint64_t* epoch, double* rowmin,
+                          int64_t cap);
+
 typedef struct {
     double build_ms;          /* wall time of the last table build (device, event timed) */
     double sssp_kernel_ms;    /* event-timed duration of the last SSSP / pair kernel launch */
@@ -369,6 +378,10 @@ typedef struct {
                                       "balance": batches sized / ordered by the sources' costs
                                       from earlier builds' batch times), 0: the grouping order */
     int64_t batches;            /*   batches of that launch */
+    int64_t rows_to_host;       /* getters (topology_getLatency & co.): table rows copied to the
+                                   host on their first read, cumulative (16 A bytes each; the
+                                   getters never copy the whole A x A table) */
+    double rows_to_host_ms;     /*   and the wall time of those copies */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -72,6 +72,12 @@ def lib():
         L.orc_parent_ties.argtypes = [i32, P, P, P, P, P, P, i32, P]
         L.orc_complete_pairs.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, P, P, i64, P, P]
         L.orc_route_packets.argtypes = [i64, P, P, P, P, P, ctypes.c_uint64, ctypes.c_int, P, P]
+        L.orc_cache_new.argtypes = [i64, P, P, ctypes.c_int]
+        L.orc_cache_new.restype = P
+        L.orc_cache_store.argtypes = [P, i64, P, P, P, P]
+        L.orc_cache_bench.argtypes = [P, i64, P, P, ctypes.c_int, P, P]
+        L.orc_cache_bench.restype = i64
+        L.orc_cache_free.argtypes = [P]
         _lib = L
     return _lib
 
@@ -471,3 +477,44 @@ def route_packets(lat, rel, payload, state, now, jump, clamp):
     lib().orc_route_packets(n, _p(lat), _p(rel), _p(payload), _p(st), _p(now),
                             ctypes.c_uint64(int(jump)), int(clamp), _p(t), _p(dl))
     return t, dl, st
+
+
+class OracleCache:
+    """The reference's cached getter path in C (oracle.c orc_cache_*: virtualIP hash + two-level
+    path cache behind their RW locks, shd-topology.c:450-531,876-958), filled with given pairs so
+    that only cache hits are timed -- the per-packet cost unchanged Shadow pays once a row is
+    materialised."""
+
+    def __init__(self, host_ip, host_vertex, directed=False):
+        L = lib()
+        self._ip = np.ascontiguousarray(host_ip, np.uint32)
+        self._v = np.ascontiguousarray(host_vertex, np.int32)
+        self._h = L.orc_cache_new(len(self._ip), _p(self._ip), _p(self._v), int(bool(directed)))
+
+    def store(self, s, d, lat, rel):
+        s, d = np.ascontiguousarray(s, np.int32), np.ascontiguousarray(d, np.int32)
+        lat, rel = np.ascontiguousarray(lat, np.float64), np.ascontiguousarray(rel, np.float64)
+        lib().orc_cache_store(self._h, len(s), _p(s), _p(d), _p(lat), _p(rel))
+
+    def bench(self, src_ip, dst_ip, nthreads=1):
+        """(wall seconds, lat, rel) of the getReliability + getLatency pair per query."""
+        sip = np.ascontiguousarray(src_ip, np.uint32)
+        dip = np.ascontiguousarray(dst_ip, np.uint32)
+        lat = np.empty(len(sip), np.float64)
+        rel = np.empty(len(sip), np.float64)
+        ns = lib().orc_cache_bench(self._h, len(sip), _p(sip), _p(dip), int(nthreads), _p(lat),
+                                   _p(rel))
+        if ns < 0:
+            raise RuntimeError("a queried pair is not in the cache")
+        return ns / 1e9, lat, rel
+
+    def free(self):
+        if self._h:
+            lib().orc_cache_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

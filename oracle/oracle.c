@@ -13,6 +13,8 @@
  *     src/engine/shd-worker.c:332-370       worker_schedulePacket               -> orc_route_packets()
  *     src/engine/shd-worker.c:310-324       inter-host clamp                    -> orc_route_packets()
  *     src/utility/shd-random.c:30-37        random_nextInt/nextDouble (rand_r)  -> orc_rand_r()
+ *     src/topology/shd-topology.c:450-531,876-958  cached getter path (locks + hashes, hits)
+ *                                                                          -> orc_cache_bench()
  *
  *   third-party dependency restated (NOT in /root/reference): igraph C library, version
  *   unpinned by the reference (cmake/FindIGRAPH.cmake:12-49); API usage pins it to 0.7.x,
@@ -36,6 +38,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #define ORC_RAND_MAX 2147483647.0
 
@@ -519,4 +522,225 @@ void orc_route_packets(int64_t n, const double* lat, const double* rel, const ui
             out_delivered[k] = 0;
         }
     }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* The reference's per-call getter path over a filled cache (bench.py's getters baseline):     */
+/*   src/topology/shd-topology.c:514-531  _topology_getConnectedVertexIndex (virtualIPLock read  */
+/*                                        lock + hash lookup IP -> vertex)                      */
+/*   src/topology/shd-topology.c:450-471  _topology_getPathFromCache (pathCacheLock read lock,   */
+/*                                        source hash -> destination hash -> Path*)             */
+/*   src/topology/shd-topology.c:876-938  _topology_getPathEntry (both vertices, (s,d) then     */
+/*                                        (d,s) when undirected), :940-958 the two getters      */
+/* GHashTable is restated as an open-addressing table (g_direct_hash keys), each Path a        */
+/* separate allocation (path_new, src/topology/shd-path.c:17-27).  Only cache HITS are timed:  */
+/* the cache is filled beforehand with the queried pairs (rows the run materialised).          */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    uint64_t* k; /* key + 1 (0 = empty) */
+    void** v;
+    uint64_t mask;
+    int64_t n;
+} orc_hmap;
+
+typedef struct {
+    double latency, reliability;
+} orc_path;
+
+static uint64_t orc_hmix(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    return x;
+}
+
+static void orc_hmap_init(orc_hmap* m, int64_t cap) {
+    uint64_t c = 8;
+    while (c < (uint64_t)(2 * cap)) c <<= 1;
+    m->k = (uint64_t*)calloc(c, sizeof(uint64_t));
+    m->v = (void**)calloc(c, sizeof(void*));
+    m->mask = c - 1;
+    m->n = 0;
+}
+
+static void orc_hmap_put(orc_hmap* m, uint64_t key, void* val);
+
+static void orc_hmap_grow(orc_hmap* m) {
+    orc_hmap o = *m;
+    orc_hmap_init(m, (int64_t)(o.mask + 1));
+    for (uint64_t i = 0; i <= o.mask; i++)
+        if (o.k[i]) orc_hmap_put(m, o.k[i] - 1, o.v[i]);
+    free(o.k);
+    free(o.v);
+}
+
+static void orc_hmap_put(orc_hmap* m, uint64_t key, void* val) {
+    if (2 * (m->n + 1) > (int64_t)(m->mask + 1)) orc_hmap_grow(m);
+    uint64_t i = orc_hmix(key) & m->mask;
+    while (m->k[i] && m->k[i] != key + 1) i = (i + 1) & m->mask;
+    if (!m->k[i]) m->n++;
+    m->k[i] = key + 1;
+    m->v[i] = val;
+}
+
+static void* orc_hmap_get(const orc_hmap* m, uint64_t key, int* found) {
+    uint64_t i = orc_hmix(key) & m->mask;
+    while (m->k[i]) {
+        if (m->k[i] == key + 1) {
+            *found = 1;
+            return m->v[i];
+        }
+        i = (i + 1) & m->mask;
+    }
+    *found = 0;
+    return NULL;
+}
+
+typedef struct {
+    pthread_rwlock_t ipLock, cacheLock; /* virtualIPLock, pathCacheLock (shd-topology.c:29-40) */
+    orc_hmap vip;                       /* network-order IP -> vertex */
+    orc_hmap cache;                     /* source vertex -> orc_hmap* (destination -> orc_path*) */
+    int directed;
+} orc_cache;
+
+orc_cache* orc_cache_new(int64_t nhost, const uint32_t* ip, const int32_t* vertex, int directed) {
+    orc_cache* c = (orc_cache*)calloc(1, sizeof(orc_cache));
+    pthread_rwlock_init(&c->ipLock, NULL);
+    pthread_rwlock_init(&c->cacheLock, NULL);
+    orc_hmap_init(&c->vip, nhost);
+    for (int64_t h = 0; h < nhost; h++)
+        orc_hmap_put(&c->vip, ip[h], (void*)(intptr_t)vertex[h]);
+    orc_hmap_init(&c->cache, 64);
+    c->directed = directed;
+    return c;
+}
+
+/* _topology_storePathInCache (shd-topology.c:473-512) for n pairs (vertex ids) */
+void orc_cache_store(orc_cache* c, int64_t n, const int32_t* s, const int32_t* d,
+                     const double* lat, const double* rel) {
+    for (int64_t i = 0; i < n; i++) {
+        int found = 0;
+        orc_hmap* src = (orc_hmap*)orc_hmap_get(&c->cache, (uint64_t)s[i], &found);
+        if (!found) {
+            src = (orc_hmap*)calloc(1, sizeof(orc_hmap));
+            orc_hmap_init(src, 16);
+            orc_hmap_put(&c->cache, (uint64_t)s[i], src);
+        }
+        orc_path* p = (orc_path*)orc_hmap_get(src, (uint64_t)d[i], &found);
+        if (!found) {
+            p = (orc_path*)malloc(sizeof(orc_path));
+            orc_hmap_put(src, (uint64_t)d[i], p);
+        }
+        p->latency = lat[i];
+        p->reliability = rel[i];
+    }
+}
+
+static int32_t orc_cache_vertex(orc_cache* c, uint32_t ip) {
+    int found = 0;
+    pthread_rwlock_rdlock(&c->ipLock);
+    void* v = orc_hmap_get(&c->vip, ip, &found);
+    pthread_rwlock_unlock(&c->ipLock);
+    return found ? (int32_t)(intptr_t)v : -1;
+}
+
+static orc_path* orc_cache_path(orc_cache* c, int32_t s, int32_t d) {
+    int found = 0;
+    orc_path* p = NULL;
+    pthread_rwlock_rdlock(&c->cacheLock);
+    orc_hmap* src = (orc_hmap*)orc_hmap_get(&c->cache, (uint64_t)s, &found);
+    if (found) p = (orc_path*)orc_hmap_get(src, (uint64_t)d, &found);
+    pthread_rwlock_unlock(&c->cacheLock);
+    return found ? p : NULL;
+}
+
+/* _topology_getPathEntry on a hit; -1 when the pair is not cached (a miss: not timed here) */
+static int orc_cache_entry(orc_cache* c, uint32_t sip, uint32_t dip, double* lat, double* rel) {
+    const int32_t s = orc_cache_vertex(c, sip), d = orc_cache_vertex(c, dip);
+    if (s < 0 || d < 0) return -1;
+    orc_path* p = orc_cache_path(c, s, d);
+    if (!p && !c->directed) p = orc_cache_path(c, d, s);
+    if (!p) return -1;
+    if (lat) *lat = p->latency;
+    if (rel) *rel = p->reliability;
+    return 0;
+}
+
+typedef struct {
+    orc_cache* c;
+    const uint32_t *sip, *dip;
+    double *lat, *rel;
+    int64_t lo, hi, misses;
+    struct timespec t0, t1;
+    pthread_barrier_t* bar;
+} orc_cb_arg;
+
+static void* orc_cache_worker(void* a_) {
+    orc_cb_arg* a = (orc_cb_arg*)a_;
+    pthread_barrier_wait(a->bar);
+    clock_gettime(CLOCK_MONOTONIC, &a->t0);
+    for (int64_t i = a->lo; i < a->hi; i++) {
+        /* shd-worker.c:352 getReliability, :360 getLatency: two full getPathEntry calls */
+        if (orc_cache_entry(a->c, a->sip[i], a->dip[i], NULL, &a->rel[i]) ||
+            orc_cache_entry(a->c, a->sip[i], a->dip[i], &a->lat[i], NULL))
+            a->misses++;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &a->t1);
+    return NULL;
+}
+
+/* n (srcIP, dstIP) queries, each the getReliability + getLatency pair, split over nthreads
+ * threads; lat / rel receive the answers.  Returns the wall nanoseconds of the query loop (first
+ * start to last end), or -1 if a pair was not cached. */
+int64_t orc_cache_bench(orc_cache* c, int64_t n, const uint32_t* sip, const uint32_t* dip,
+                        int nthreads, double* lat, double* rel) {
+    if (nthreads < 1) nthreads = 1;
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    orc_cb_arg* a = (orc_cb_arg*)calloc((size_t)nthreads, sizeof(orc_cb_arg));
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
+    for (int t = 0; t < nthreads; t++) {
+        a[t].c = c;
+        a[t].sip = sip;
+        a[t].dip = dip;
+        a[t].lat = lat;
+        a[t].rel = rel;
+        a[t].lo = n * t / nthreads;
+        a[t].hi = n * (t + 1) / nthreads;
+        a[t].bar = &bar;
+        pthread_create(&th[t], NULL, orc_cache_worker, &a[t]);
+    }
+    int64_t t0 = INT64_MAX, t1 = 0, miss = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        const int64_t s = (int64_t)a[t].t0.tv_sec * 1000000000 + a[t].t0.tv_nsec;
+        const int64_t e = (int64_t)a[t].t1.tv_sec * 1000000000 + a[t].t1.tv_nsec;
+        if (s < t0) t0 = s;
+        if (e > t1) t1 = e;
+        miss += a[t].misses;
+    }
+    pthread_barrier_destroy(&bar);
+    free(th);
+    free(a);
+    return miss ? -1 : t1 - t0;
+}
+
+void orc_cache_free(orc_cache* c) {
+    if (!c) return;
+    for (uint64_t i = 0; i <= c->cache.mask; i++) {
+        if (!c->cache.k[i]) continue;
+        orc_hmap* src = (orc_hmap*)c->cache.v[i];
+        for (uint64_t j = 0; j <= src->mask; j++)
+            if (src->k[j]) free(src->v[j]);
+        free(src->k);
+        free(src->v);
+        free(src);
+    }
+    free(c->cache.k);
+    free(c->cache.v);
+    free(c->vip.k);
+    free(c->vip.v);
+    pthread_rwlock_destroy(&c->ipLock);
+    pthread_rwlock_destroy(&c->cacheLock);
+    free(c);
 }

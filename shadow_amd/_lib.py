@@ -60,7 +60,8 @@ class ShdStats(ctypes.Structure):
                 ("device_rows", i64 * 8), ("dev_inits", i64), ("init_bg_ms", dbl),
                 ("path_seconds_total", dbl), ("paths_computed", i64), ("help_ms", dbl),
                 ("help_items", i64 * 2), ("help_board_errors", i64),
-                ("batch_layout_measured", i64), ("batches", i64)]
+                ("batch_layout_measured", i64), ("batches", i64), ("rows_to_host", i64),
+                ("rows_to_host_ms", dbl)]
 
 
 class ShdSynthParams(ctypes.Structure):
@@ -110,6 +111,7 @@ SIGNATURES = {
     "shdtopo_route_batch_vertices": (ctypes.c_int, [P, P, P, P, P, P, ctypes.c_size_t, u64,
                                                     ctypes.c_int, P]),
     "shdtopo_get_lazy_minimum_latency": (dbl, [P]),
+    "shdtopo_lazy_rows": (i64, [P, P, P, P, i64]),
     "shdtopo_get_stats": (ctypes.c_int, [P, P]),
     "shdtopo_write_graphml": (ctypes.c_int, [P, cstr]),
     "shdtopo_replay_source": (ctypes.c_int, [P, i32, ctypes.c_int, P, P]),
@@ -150,6 +152,7 @@ SHIM_SIGNATURES = {
     "shim_reset": (None, []),
     "logging_log": (None, [cstr, ctypes.c_int, cstr, cstr, ctypes.c_int, cstr]),
     "shim_log_count": (ctypes.c_int, []),
+    "shim_log_criticals": (ctypes.c_int, []),
     "shim_log_get": (ctypes.c_int, [ctypes.c_int, P, ctypes.c_char_p, ctypes.c_int,
                                     ctypes.c_char_p, ctypes.c_int]),
     "shim_log_reset": (None, []),

@@ -150,6 +150,44 @@ struct DevBuf {
     }
 };
 
+// Open-addressing IP -> vertex table read by the getters without a lock (Shadow calls them from
+// every worker thread, shd-worker.c:179-203; the reference takes virtualIPLock per lookup,
+// shd-topology.c:514-531).  A slot holds (ip << 32) | (vertex + 2); 0 = empty, low word kTomb =
+// detached.  An IP keeps its slot for the table's lifetime, so a lookup stops at its key or at an
+// empty slot.  Writers (attach / detach) are serialised by Topology::ipMu.
+struct IpTable {
+    static constexpr uint32_t kTomb = 0xFFFFFFFFu;
+    uint64_t mask = 0;
+    size_t used = 0;
+    std::unique_ptr<std::atomic<uint64_t>[]> slot;
+    explicit IpTable(uint64_t cap) : mask(cap - 1), slot(new std::atomic<uint64_t>[cap]) {
+        for (uint64_t i = 0; i < cap; i++) slot[i].store(0, std::memory_order_relaxed);
+    }
+    uint64_t home(uint32_t ip) const { return ((uint64_t)ip * 0x9E3779B97F4A7C15ull >> 17) & mask; }
+    int32_t find(uint32_t ip) const {
+        for (uint64_t i = home(ip);; i = (i + 1) & mask) {
+            const uint64_t w = slot[i].load(std::memory_order_acquire);
+            if (w == 0) return -1;
+            if ((uint32_t)(w >> 32) == ip) {
+                const uint32_t lo = (uint32_t)w;
+                return lo == kTomb ? -1 : (int32_t)(lo - 2);
+            }
+        }
+    }
+    // writer: the slot of ip (existing, else the first empty one)
+    uint64_t place(uint32_t ip) const {
+        for (uint64_t i = home(ip);; i = (i + 1) & mask) {
+            const uint64_t w = slot[i].load(std::memory_order_relaxed);
+            if (w == 0 || (uint32_t)(w >> 32) == ip) return i;
+        }
+    }
+};
+
+uint64_t next_topology_uid() {
+    static std::atomic<uint64_t> n{0};
+    return n.fetch_add(1) + 1;
+}
+
 }  // namespace
 
 struct _Topology {
@@ -180,16 +218,29 @@ struct _Topology {
     std::shared_mutex ipMu;
     std::unordered_map<uint32_t, int32_t> virtualIP;
     AttachIndex aidx;
+    // the getters' lock-free view of virtualIP (IpTable): written under ipMu (exclusive) next to
+    // the map, read with acquire loads and no lock; superseded tables stay allocated until free
+    std::atomic<IpTable*> ipTab{nullptr};
+    std::vector<std::unique_ptr<IpTable>> ipTabs;
+    const uint64_t uid = next_topology_uid();  // identifies this topology to thread-local caches
 
     // table geometry
     std::mutex buildMu;
+    // writers of the device table (builds, binds) hold it exclusively inside buildMu; the getters'
+    // row copies (snap_row) hold it shared, so they run in parallel and never see a half-built table
+    std::shared_mutex tabMu;
     std::atomic<bool> tableValid{false};
     std::vector<int32_t> attached;  // columns: distinct attached vertices, ascending
     std::vector<int32_t> colOf;     // vertex -> column
+    std::shared_ptr<const std::vector<int32_t>> colOfShared;  // colOf for the snapshots (lazily
+                                                              // made, reset with the geometry)
     int64_t A = 0;
 
     // device state
     bool devInit = false;
+    // any entry point asked this engine's device for work (every one goes through dev_init): the
+    // "device" option is fixed from then on (buffers, tables and matrices live on that device)
+    bool deviceUsed = false;
     int devId = 0;               // the device dev_init bound (every later entry re-binds it)
     int64_t devInits = 0;        // dev_init runs (a "device" change before the first attach
                                  // re-initialises on the new device)
@@ -388,6 +439,8 @@ struct _Topology {
     // host mirror of the table for the per-call getters: an immutable snapshot swapped atomically
     // (getters on worker threads never see a table being rebuilt)
     std::shared_ptr<const HostTable> snap;
+    std::atomic<int64_t> rowsToHost{0};      // ShdStats.rows_to_host
+    std::atomic<int64_t> rowsToHostNs{0};    // ShdStats.rows_to_host_ms
     double eagerMin = -1.0;
 
     // attached-set generations: setGen bumps whenever a vertex gains its first or loses its last
@@ -410,6 +463,7 @@ struct _Topology {
     std::atomic<uint64_t> lastNewEpoch{0};                     // latest interval start
     std::unique_ptr<std::atomic<uint64_t>[]> matGen;          // per vertex: latest epoch
     std::unordered_map<int32_t, std::vector<uint64_t>> matEpochs;  // all epochs (lazyMu)
+    std::unordered_map<int32_t, double> matMin;  // the row minimum its latest one offered (lazyMu)
     std::mutex lazyMu;
     std::unique_ptr<std::atomic<uint64_t>[]> matPair;  // per (column pair) bit (complete branch)
     size_t matPairWords = 0;
@@ -563,6 +617,7 @@ Topology* new_topology(bool earlyInit) {
 // device setup
 // ---------------------------------------------------------------------------------------------
 int dev_init(Topology* top) {
+    top->deviceUsed = true;  // (topology_new's background init restores it: start_device_init)
     if (top->devInit) {
         // HIP's current device is per thread: bind this engine's device for the caller
         HIPCHK(hipSetDevice(top->devId));
@@ -645,7 +700,9 @@ void start_device_init(Topology* top) {
             (void)hipGetLastError();
             return;
         }
+        const bool used = top->deviceUsed;
         if (dev_init(top) != 0) (void)hipGetLastError();
+        top->deviceUsed = used;  // binding the default device early is not a use of it
         top->initBgMs = std::chrono::duration<double, std::milli>(
             std::chrono::steady_clock::now() - t0).count();
     });
@@ -1231,6 +1288,7 @@ uint64_t compute_geometry(Topology* top) {
     top->A = (int64_t)vs.size();
     top->colOf.assign((size_t)top->g.V, -1);
     for (size_t i = 0; i < vs.size(); i++) top->colOf[(size_t)vs[i]] = (int32_t)i;
+    top->colOfShared.reset();
     top->tableValid.store(false);
     // complete-branch materialisation bits are per column pair: a new geometry starts them over
     // (a re-touched pair re-offers a latency >= the running minimum: a no-op, shd-topology.c:501)
@@ -2427,6 +2485,7 @@ int ensure_table(Topology* top) {
     const auto tw0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lk(top->buildMu);
     if (table_current(top)) return 0;
+    std::unique_lock<std::shared_mutex> tw(top->tabMu);  // no row copy while the table changes
     const auto tb0 = std::chrono::steady_clock::now();
     // (waiting for the attach-time preparation thread, or another builder)
     top->stats.build_wait_ms = std::chrono::duration<double, std::milli>(tb0 - tw0).count();
@@ -2494,48 +2553,38 @@ int ensure_table(Topology* top) {
     return 0;
 }
 
-// Host snapshot of the current device table: column map + row minima, and (full) the whole
-// A x A lat / rel / hops mirror.  Published atomically; readers keep the old one alive.
-int ensure_snapshot(Topology* top, bool full, std::shared_ptr<const HostTable>* out) {
+// Host snapshot of the current device table: column map + row minima; its rows are copied on
+// first use (snap_row).  Published atomically; readers keep the old one alive.
+int ensure_snapshot(Topology* top, std::shared_ptr<const HostTable>* out) {
     for (int attempt = 0; attempt < 4; attempt++) {
         int r = ensure_table(top);
         if (r) return r;
         std::shared_ptr<const HostTable> cur = std::atomic_load(&top->snap);
-        if (cur && cur->serial == top->tableSerial.load() && (cur->full || !full) &&
-            table_current(top)) {
+        if (cur && cur->serial == top->tableSerial.load() && table_current(top)) {
             *out = cur;
             return 0;
         }
         std::lock_guard<std::mutex> lk(top->buildMu);
         if (!table_current(top)) continue;  // an attach / detach raced: rebuild first
         cur = std::atomic_load(&top->snap);
-        if (cur && cur->serial == top->tableSerial.load() && (cur->full || !full)) {
+        if (cur && cur->serial == top->tableSerial.load()) {
             *out = cur;
             return 0;
         }
+        r = dev_init(top);  // this thread's HIP device = the table's
+        if (r) return r;
         auto h = std::make_shared<HostTable>();
         h->gen = top->tableGen.load(std::memory_order_acquire);
         h->serial = top->tableSerial.load();
+        h->epoch = top->geomGen;
         h->A = top->A;
-        h->colOf = top->colOf;
-        const size_t A = (size_t)top->A, n = A * A;
+        if (!top->colOfShared) top->colOfShared = std::make_shared<const std::vector<int32_t>>(top->colOf);
+        h->colOf = top->colOfShared;
+        const size_t A = (size_t)top->A;
         h->rowmin.resize(A);
         if (A) HIPCHK(hipMemcpy(h->rowmin.data(), top->d_rowmin.p, sizeof(double) * A, hipMemcpyDeviceToHost));
-        if (full) {
-            h->full = true;
-            std::vector<double2> lr(n);
-            h->hops.resize(n);
-            if (n) {
-                HIPCHK(hipMemcpy(lr.data(), tab_lr(top), sizeof(double2) * n, hipMemcpyDeviceToHost));
-                HIPCHK(hipMemcpy(h->hops.data(), tab_hops(top), sizeof(uint16_t) * n, hipMemcpyDeviceToHost));
-            }
-            h->lat.resize(n);
-            h->rel.resize(n);
-            for (size_t i = 0; i < n; i++) {
-                h->lat[i] = lr[i].x;
-                h->rel[i] = lr[i].y;
-            }
-        }
+        h->rows.reset(new std::atomic<const double2*>[A ? A : 1]);
+        for (size_t i = 0; i < std::max<size_t>(A, 1); i++) h->rows[i].store(nullptr, std::memory_order_relaxed);
         std::shared_ptr<const HostTable> hc = h;
         std::atomic_store(&top->snap, hc);
         *out = hc;
@@ -2545,10 +2594,96 @@ int ensure_snapshot(Topology* top, bool full, std::shared_ptr<const HostTable>* 
     return -5;
 }
 
+// The getters' snapshot of `top`: this thread's cached one while it is still the current table
+// (no lock, no reference count traffic: Shadow's workers query from many threads at once),
+// else refreshed through ensure_snapshot.  The pointer stays valid until this thread's next call.
+// A thread keeps its last snapshot alive until it queries again or exits.
+struct SnapCache {
+    uint64_t uid = 0;
+    std::shared_ptr<const HostTable> h;
+};
+thread_local SnapCache t_snap;
+
+int getter_snapshot(Topology* top, const HostTable** out) {
+    SnapCache& c = t_snap;
+    if (c.uid == top->uid && c.h && c.h->serial == top->tableSerial.load(std::memory_order_acquire) &&
+        table_current(top)) {
+        *out = c.h.get();
+        return 0;
+    }
+    std::shared_ptr<const HostTable> h;
+    const int r = ensure_snapshot(top, &h);
+    if (r) return r;
+    c.uid = top->uid;
+    c.h = std::move(h);
+    *out = c.h.get();
+    return 0;
+}
+
+// Row c of a snapshot's table ({latency, reliability} per column), copied from the device table
+// the first time a query reads it: one 16 A-byte copy (C4: 160 KB) instead of the whole table.
+// Copies run in parallel (per-thread HIP streams, tabMu shared); two threads racing for the same
+// row both copy it and the first to publish wins.  Returns 0 (*out set), 1 when the device table
+// is no longer the snapshot's (a rebuild ran in between: the caller takes a new snapshot), or a
+// negative error.  Rows already copied are read without a lock (acquire load).
+int snap_row(Topology* top, const HostTable& h, int64_t c, const double2** out) {
+    const double2* p = h.rows[(size_t)c].load(std::memory_order_acquire);
+    if (p) {
+        *out = p;
+        return 0;
+    }
+    std::shared_lock<std::shared_mutex> lk(top->tabMu);
+    if (!top->tableValid.load(std::memory_order_acquire) || top->tableSerial.load() != h.serial)
+        return 1;
+    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(hipSetDevice(top->devId));  // the table's device, for this (worker) thread
+    std::unique_ptr<double2[]> buf(new double2[(size_t)std::max<int64_t>(1, h.A)]);
+    HIPCHK(hipMemcpyAsync(buf.get(), tab_lr(top) + c * h.A, sizeof(double2) * (size_t)h.A,
+                          hipMemcpyDeviceToHost, hipStreamPerThread));
+    HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+    const double2* expect = nullptr;
+    if (h.rows[(size_t)c].compare_exchange_strong(expect, buf.get(), std::memory_order_acq_rel)) {
+        *out = buf.get();
+        std::lock_guard<std::mutex> g(h.storeMu);
+        h.rowStore.push_back(std::move(buf));
+    } else {
+        *out = expect;  // another thread published this row first
+    }
+    top->rowsToHost.fetch_add(1, std::memory_order_relaxed);
+    top->rowsToHostNs.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                    std::chrono::steady_clock::now() - t0).count(),
+                                std::memory_order_relaxed);
+    return 0;
+}
+
+// virtualIP[ip] = v (v < 0: not attached) in the getters' lock-free table.  Caller holds ipMu
+// exclusively.  The table doubles at half load; the old one stays readable (a reader that loaded
+// it sees the state before this write).
+void ip_tab_set(Topology* top, uint32_t ip, int32_t v) {
+    IpTable* t = top->ipTab.load(std::memory_order_relaxed);
+    if (!t || 2 * (t->used + 1) > t->mask + 1) {
+        auto n = std::make_unique<IpTable>(t ? 2 * (t->mask + 1) : 1024);
+        if (t)
+            for (uint64_t i = 0; i <= t->mask; i++) {
+                const uint64_t w = t->slot[i].load(std::memory_order_relaxed);
+                if (!w) continue;
+                n->slot[n->place((uint32_t)(w >> 32))].store(w, std::memory_order_relaxed);
+                n->used++;
+            }
+        t = n.get();
+        top->ipTabs.push_back(std::move(n));
+        top->ipTab.store(t, std::memory_order_release);
+    }
+    const uint64_t i = t->place(ip);
+    if (t->slot[i].load(std::memory_order_relaxed) == 0) t->used++;
+    const uint32_t lo = v < 0 ? IpTable::kTomb : (uint32_t)v + 2u;
+    t->slot[i].store(((uint64_t)ip << 32) | lo, std::memory_order_release);
+}
+
+// _topology_getConnectedVertexIndex (shd-topology.c:514-531) without the lock
 int32_t vertex_of_ip(Topology* top, uint32_t ip) {
-    std::shared_lock<std::shared_mutex> lk(top->ipMu);
-    auto it = top->virtualIP.find(ip);
-    return it == top->virtualIP.end() ? -1 : it->second;
+    const IpTable* t = top->ipTab.load(std::memory_order_acquire);
+    return t ? t->find(ip) : -1;
 }
 
 void lazy_store_min(Topology* top, double lat) {
@@ -2580,17 +2715,16 @@ bool lazy_covered(Topology* top, int32_t s, int32_t t) {
 }
 
 // computeSourcePaths(s) now: row s over the current targets enters the cache and its minimum the
-// running minimum (shd-topology.c:808-823, :500-511)
-void lazy_materialise(Topology* top, int32_t s, double rowmin) {
-    uint64_t e;
-    {
-        std::shared_lock<std::shared_mutex> lk(top->ipMu);
-        e = top->ipGen;
-    }
+// running minimum (shd-topology.c:808-823, :500-511).  e = the attach epoch of the table the row
+// is read from (HostTable::epoch): the row covers the vertices attached then -- a vertex attached
+// after that table was built is not in it, as if the query had run before that attach.
+void lazy_materialise(Topology* top, int32_t s, double rowmin, uint64_t e) {
     {
         std::lock_guard<std::mutex> lk(top->lazyMu);
-        auto& v = top->matEpochs[s];
-        if (v.empty() || v.back() != e) v.push_back(e);
+        auto& v = top->matEpochs[s];  // ascending (a query on an older snapshot may come late)
+        auto it = std::lower_bound(v.begin(), v.end(), e);
+        if (it == v.end() || *it != e) v.insert(it, e);
+        if (v.back() == e) top->matMin[s] = rowmin;
     }
     uint64_t old = top->matGen[(size_t)s].load();
     while (old < e && !top->matGen[(size_t)s].compare_exchange_weak(old, e)) {
@@ -2598,15 +2732,13 @@ void lazy_materialise(Topology* top, int32_t s, double rowmin) {
     if (rowmin > 0 && !std::isinf(rowmin)) lazy_store_min(top, rowmin);
 }
 
-const double2* tab_lr(const Topology* top);
-
 // The minimum of row s over the vertices attached NOW (shd-topology.c:690-744 take the targets
 // attached at the moment the row is computed).  The table's row minimum also covers the columns a
 // window adapter keeps for vertices that lost their last host (deferredOff, until the flush): while
-// such a column exists, the row is read (host snapshot, or one row from the device table -- the
-// caller holds buildMu there) and those columns are left out.
-double lazy_row_min(Topology* top, const HostTable& h, int32_t s) {
-    const int64_t cs = h.colOf[(size_t)s];
+// such a column exists, row s is read (rowS, or copied now) and those columns are left out
+// (ADVICE r04).
+double lazy_row_min(Topology* top, const HostTable& h, int32_t s, const double2* rowS) {
+    const int64_t cs = h.col(s);
     std::vector<int32_t> gone;
     {
         std::shared_lock<std::shared_mutex> lk(top->ipMu);
@@ -2614,41 +2746,38 @@ double lazy_row_min(Topology* top, const HostTable& h, int32_t s) {
             if (top->hostsOn[(size_t)v] == 0) gone.push_back(v);
     }
     if (gone.empty()) return h.rowmin[(size_t)cs];
-    const int64_t A = h.A;
-    std::vector<double> lat((size_t)A);
-    if (h.full) {
-        for (int64_t c = 0; c < A; c++) lat[(size_t)c] = h.lat[(size_t)(cs * A + c)];
-    } else {
-        std::vector<double2> lr((size_t)A);
-        if (hipMemcpy(lr.data(), tab_lr(top) + cs * A, sizeof(double2) * (size_t)A,
-                      hipMemcpyDeviceToHost) != hipSuccess)
-            return h.rowmin[(size_t)cs];
-        for (int64_t c = 0; c < A; c++) lat[(size_t)c] = lr[(size_t)c].x;
+    if (!rowS && snap_row(top, h, cs, &rowS) != 0) {
+        WARNING("row %lld of the routing table could not be read: the running minimum takes the "
+                "table's row minimum", (long long)cs);
+        return h.rowmin[(size_t)cs];
     }
+    std::vector<uint8_t> skip((size_t)h.A, 0);
     for (int32_t v : gone) {
-        const int32_t c = h.colOf[(size_t)v];
-        if (c >= 0 && c < A) lat[(size_t)c] = -1.0;
+        const int32_t c = h.col(v);
+        if (c >= 0 && c < h.A) skip[(size_t)c] = 1;
     }
     double m = INFINITY;
-    for (double x : lat)
-        if (x >= 0 && x < m) m = x;
+    for (int64_t c = 0; c < h.A; c++) {
+        const double x = rowS[c].x;
+        if (!skip[(size_t)c] && x >= 0 && x < m) m = x;
+    }
     return m;
 }
 
 // First-rooted-wins orientation of the SSSP branch (shd-topology.c:894-915):
-// (s,d) is answered from row s if the cache holds (s,d), else from row d if it holds (d,s) and
-// the graph is undirected, else s's row is computed now.  Returns true when the answer comes
-// from row d.
-bool lazy_orient_row(Topology* top, const HostTable& h, int32_t s, int32_t d) {
-    if (lazy_covered(top, s, d)) return false;
-    if (!top->isDirected && lazy_covered(top, d, s)) return true;
-    lazy_materialise(top, s, lazy_row_min(top, h, s));
-    return false;
+// (s,d) is answered from row s if the cache holds (s,d) (0), else from row d if it holds (d,s)
+// and the graph is undirected (1), else s's row is computed now (2: row s, materialised by the
+// caller once it has read the row).
+int lazy_orientation(Topology* top, int32_t s, int32_t d) {
+    if (lazy_covered(top, s, d)) return 0;
+    if (!top->isDirected && lazy_covered(top, d, s)) return 1;
+    return 2;
 }
 
 // Per-pair first touch of the complete branch (shd-topology.c:894-915 + :835-873): the pair's
-// values are symmetric bit for bit, only the running minimum depends on the order.
-void lazy_touch_pair(Topology* top, const HostTable& h, int64_t cs, int64_t cd) {
+// values are symmetric bit for bit, only the running minimum depends on the order.  lat = the
+// table's latency of (cs, cd).
+void lazy_touch_pair(Topology* top, const HostTable& h, int64_t cs, int64_t cd, double lat) {
     const int64_t A = h.A;
     const size_t b1 = (size_t)(cs * A + cd), b2 = (size_t)(cd * A + cs);
     if (top->matPairWords * 64 < (size_t)(A * A)) return;  // geometry moved on (raced)
@@ -2657,11 +2786,13 @@ void lazy_touch_pair(Topology* top, const HostTable& h, int64_t cs, int64_t cd) 
         have = (top->matPair[b2 >> 6].load(std::memory_order_relaxed) >> (b2 & 63)) & 1;
     if (!have) {
         uint64_t old = top->matPair[b1 >> 6].fetch_or(1ull << (b1 & 63));
-        if (!((old >> (b1 & 63)) & 1) && h.lat[b1] > 0) lazy_store_min(top, h.lat[b1]);
+        if (!((old >> (b1 & 63)) & 1) && lat > 0) lazy_store_min(top, lat);
     }
 }
 
-// _topology_getPathEntry (shd-topology.c:876-938) over the prebuilt table
+// _topology_getPathEntry (shd-topology.c:876-938) over the prebuilt table.  Called concurrently
+// from every worker thread (shd-worker.c:179-203,352-360): the snapshot is immutable, its rows
+// are published once, the lazy state is atomics + short locks.
 bool get_path_entry(Topology* top, uint32_t srcIP, uint32_t dstIP, double* lat, double* rel) {
     int32_t s = vertex_of_ip(top, srcIP);
     if (s < 0) {
@@ -2673,36 +2804,44 @@ bool get_path_entry(Topology* top, uint32_t srcIP, uint32_t dstIP, double* lat, 
         CRITICAL("invalid vertex %d, destination address is not connected to topology", d);
         return false;
     }
-    std::shared_ptr<const HostTable> h;
-    int r = ensure_snapshot(top, true, &h);
-    if (r) {
-        fatal_or_continue(top, "unable to build the routing table");
-        return false;
+    for (int attempt = 0; attempt < 8; attempt++) {
+        const HostTable* h = nullptr;
+        if (getter_snapshot(top, &h)) {
+            fatal_or_continue(top, "unable to build the routing table");
+            return false;
+        }
+        const int64_t cs = h->col(s), cd = h->col(d);
+        if (cs < 0 || cd < 0) {  // detached / re-attached while this call ran
+            CRITICAL("address is not connected to the current routing table");
+            return false;
+        }
+        const bool lz = top->lazy;
+        const int how = lz && !top->isComplete ? lazy_orientation(top, s, d) : 0;
+        const int64_t rr = how == 1 ? cd : cs, cc = how == 1 ? cs : cd;
+        const double2* row = nullptr;
+        const int rc = snap_row(top, *h, rr, &row);
+        if (rc > 0) continue;  // the table was rebuilt meanwhile: a new snapshot
+        if (rc < 0) {
+            fatal_or_continue(top, "unable to read the routing table");
+            return false;
+        }
+        const double L = row[cc].x, R = row[cc].y;
+        if (lz) {
+            if (top->isComplete) lazy_touch_pair(top, *h, cs, cd, L);
+            else if (how == 2)
+                lazy_materialise(top, s, lazy_row_min(top, *h, s, row), h->epoch);
+        }
+        if (L < 0) {
+            // the reference error()s: "unable to find path between node ..." (shd-topology.c:924)
+            fatal_or_continue(top, "unable to find path between attached vertices");
+            return false;
+        }
+        if (lat) *lat = L;
+        if (rel) *rel = R;
+        return true;
     }
-    const int64_t A = h->A;
-    const int64_t cs = h->colOf[(size_t)s], cd = h->colOf[(size_t)d];
-    if (cs < 0 || cd < 0) {  // detached / re-attached while this call ran
-        CRITICAL("address is not connected to the current routing table");
-        return false;
-    }
-    size_t k;
-    if (top->isComplete) {
-        k = (size_t)(cs * A + cd);
-        if (top->lazy) lazy_touch_pair(top, *h, cs, cd);
-    } else if (!top->lazy) {
-        k = (size_t)(cs * A + cd);
-    } else {
-        k = lazy_orient_row(top, *h, s, d) ? (size_t)(cd * A + cs) : (size_t)(cs * A + cd);
-    }
-    double L = h->lat[k], R = h->rel[k];
-    if (L < 0) {
-        // the reference error()s: "unable to find path between node ..." (shd-topology.c:924)
-        fatal_or_continue(top, "unable to find path between attached vertices");
-        return false;
-    }
-    if (lat) *lat = L;
-    if (rel) *rel = R;
-    return true;
+    CRITICAL("the routing table keeps changing under a query");
+    return false;
 }
 
 // _topology_findAttachmentVertex (shd-topology.c:1068-1152) over the candidate index.
@@ -2852,6 +2991,7 @@ void do_attach(Topology* top, uint32_t ip, int32_t v, uint64_t* bwDownOut, uint6
         auto it = top->virtualIP.find(ip);
         const int32_t old = it == top->virtualIP.end() ? -1 : it->second;
         top->virtualIP[ip] = v;
+        ip_tab_set(top, ip, v);
         top->ipGen++;
         if (old != v) {
             if (old >= 0) host_off(top, old);
@@ -2871,6 +3011,7 @@ void do_detach(Topology* top, uint32_t ip) {
     if (it == top->virtualIP.end()) return;
     const int32_t v = it->second;
     top->virtualIP.erase(it);
+    ip_tab_set(top, ip, -1);
     top->ipGen++;
     if (v >= 0) host_off(top, v);
 }
@@ -2973,7 +3114,9 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
         if (d != top->device) {
             // fixed once the attach-time preparation (or a build) uses it; before that, a device
             // bound by topology_new's background init is released and the next use binds d
-            if (top->prepStarted.load() || top->csrUploaded || top->tableValid.load()) return -1;
+            if (top->prepStarted.load() || top->csrUploaded || top->tableValid.load() ||
+                top->deviceUsed)
+                return -1;
             dev_release(top);
             top->device = d;
         }
@@ -3091,6 +3234,27 @@ double shdtopo_get_lazy_minimum_latency(Topology* top) {
     return top->lazyMin;
 }
 
+int64_t shdtopo_lazy_rows(Topology* top, int32_t* vertex, uint64_t* epoch, double* rowmin,
+                          int64_t cap) {
+    if (!top) return -1;
+    std::lock_guard<std::mutex> lk(top->lazyMu);
+    int64_t n = 0;
+    for (int32_t v = 0; v < top->g.V; v++) {
+        const uint64_t e = top->matGen[(size_t)v].load(std::memory_order_acquire);
+        if (e == 0) continue;
+        if (n < cap) {
+            if (vertex) vertex[n] = v;
+            if (epoch) epoch[n] = e;
+            if (rowmin) {
+                auto it = top->matMin.find(v);
+                rowmin[n] = it == top->matMin.end() ? -1.0 : it->second;
+            }
+        }
+        n++;
+    }
+    return n;
+}
+
 int64_t shdtopo_num_vertices(Topology* top) { return top ? top->g.V : -1; }
 int64_t shdtopo_num_edges(Topology* top) { return top ? top->g.E : -1; }
 int shdtopo_is_complete(Topology* top) { return top ? (int)top->isComplete : -1; }
@@ -3139,6 +3303,7 @@ int shdtopo_build_rows(Topology* top, int64_t row0, int64_t row1, void* d_lr, vo
                        void* d_rowmin, void* stream) {
     if (!top || !d_lr || !d_hops) return -1;
     std::lock_guard<std::mutex> lk(top->buildMu);
+    std::unique_lock<std::shared_mutex> tw(top->tabMu);
     int r = dev_init(top);
     if (r) return r;
     compute_geometry(top);
@@ -3182,6 +3347,7 @@ int shdtopo_bind_table(Topology* top, const void* d_lr, const void* d_hops, doub
                        void* stream) {
     if (!top || !d_lr || !d_hops) return -1;
     std::lock_guard<std::mutex> lk(top->buildMu);
+    std::unique_lock<std::shared_mutex> tw(top->tabMu);
     int r = dev_init(top);
     if (r) return r;
     const uint64_t sg = compute_geometry(top);
@@ -3207,6 +3373,7 @@ int shdtopo_bind_table_ref(Topology* top, const void* d_lr, const void* d_hops, 
                            void* stream) {
     if (!top || !d_lr || !d_hops) return -1;
     std::lock_guard<std::mutex> lk(top->buildMu);
+    std::unique_lock<std::shared_mutex> tw(top->tabMu);
     int r = dev_init(top);
     if (r) return r;
     const uint64_t sg = compute_geometry(top);
@@ -3234,14 +3401,31 @@ int shdtopo_rebuild(Topology* top) {
 
 int shdtopo_table_to_host(Topology* top, double* lat, double* rel, uint16_t* hops) {
     if (!top) return -1;
-    std::shared_ptr<const HostTable> h;
-    int r = ensure_snapshot(top, true, &h);
-    if (r) return r;
-    const size_t n = (size_t)(h->A * h->A);
-    if (lat) memcpy(lat, h->lat.data(), sizeof(double) * n);
-    if (rel) memcpy(rel, h->rel.data(), sizeof(double) * n);
-    if (hops) memcpy(hops, h->hops.data(), sizeof(uint16_t) * n);
-    return 0;
+    for (int attempt = 0; attempt < 4; attempt++) {
+        int r = ensure_table(top);
+        if (r) return r;
+        std::lock_guard<std::mutex> lk(top->buildMu);
+        if (!table_current(top)) continue;  // an attach / detach raced: rebuild first
+        r = dev_init(top);
+        if (r) return r;
+        const size_t n = (size_t)(top->A * top->A);
+        if (lat || rel) {  // {lat, rel} records split in 64 MB pieces
+            const size_t chunk = (size_t)1 << 22;
+            std::vector<double2> lr(std::min(n, chunk));
+            for (size_t o = 0; o < n; o += chunk) {
+                const size_t m = std::min(chunk, n - o);
+                HIPCHK(hipMemcpy(lr.data(), tab_lr(top) + o, sizeof(double2) * m, hipMemcpyDeviceToHost));
+                for (size_t i = 0; i < m; i++) {
+                    if (lat) lat[o + i] = lr[i].x;
+                    if (rel) rel[o + i] = lr[i].y;
+                }
+            }
+        }
+        if (hops && n) HIPCHK(hipMemcpy(hops, tab_hops(top), sizeof(uint16_t) * n, hipMemcpyDeviceToHost));
+        return 0;
+    }
+    CRITICAL("the attached set keeps changing while the routing table is built");
+    return -5;
 }
 
 }  // extern "C"
@@ -3296,7 +3480,7 @@ int64_t route_vertices(Topology* top, const int32_t* sv, const int32_t* dv, cons
     // the snapshot and the device table must be the same build: retry if a rebuild intervened
     for (int attempt = 0;; attempt++) {
         std::shared_ptr<const HostTable> h;
-        int r = ensure_snapshot(top, top->lazy && top->isComplete, &h);
+        int r = ensure_snapshot(top, &h);
         if (r) return r;
         std::unique_lock<std::mutex> lk(top->buildMu);
         if (!table_current(top) || h->serial != top->tableSerial.load()) {
@@ -3309,8 +3493,8 @@ int64_t route_vertices(Topology* top, const int32_t* sv, const int32_t* dv, cons
         // sequentially; the kernel reads the chosen row.
         bad = 0;
         for (size_t i = 0; i < n; i++) {
-            sc[i] = sv[i] >= 0 && sv[i] < top->g.V ? h->colOf[(size_t)sv[i]] : -1;
-            dc[i] = dv[i] >= 0 && dv[i] < top->g.V ? h->colOf[(size_t)dv[i]] : -1;
+            sc[i] = sv[i] >= 0 && sv[i] < top->g.V ? h->col(sv[i]) : -1;
+            dc[i] = dv[i] >= 0 && dv[i] < top->g.V ? h->col(dv[i]) : -1;
             if (sc[i] < 0 || dc[i] < 0 || sc[i] >= h->A || dc[i] >= h->A) {
                 sc[i] = dc[i] = -1;  // not routed (the kernel leaves it undelivered)
                 bad++;
@@ -3318,9 +3502,16 @@ int64_t route_vertices(Topology* top, const int32_t* sv, const int32_t* dv, cons
             }
             if (top->lazy) {
                 if (top->isComplete) {
-                    lazy_touch_pair(top, *h, sc[i], dc[i]);
-                } else if (lazy_orient_row(top, *h, sv[i], dv[i])) {
-                    std::swap(sc[i], dc[i]);
+                    const double2* row = nullptr;
+                    r = snap_row(top, *h, sc[i], &row);
+                    if (r) return r < 0 ? r : -5;  // (serial checked above: cannot be stale)
+                    lazy_touch_pair(top, *h, sc[i], dc[i], row[dc[i]].x);
+                } else {
+                    const int how = lazy_orientation(top, sv[i], dv[i]);
+                    if (how == 1) std::swap(sc[i], dc[i]);
+                    if (how == 2)
+                        lazy_materialise(top, sv[i], lazy_row_min(top, *h, sv[i], nullptr),
+                                         h->epoch);
                 }
             }
         }
@@ -3450,6 +3641,8 @@ int shdtopo_get_stats(Topology* top, ShdStats* out) {
         top->stats.route_bad_packets = (int64_t)nb;
         top->routePending = false;
     }
+    top->stats.rows_to_host = top->rowsToHost.load();
+    top->stats.rows_to_host_ms = (double)top->rowsToHostNs.load() / 1e6;
     top->stats.dev_inits = top->devInits;
     top->stats.init_bg_ms = top->initBgMs;
     top->stats.path_seconds_total = top->spTotalSec;

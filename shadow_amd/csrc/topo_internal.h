@@ -3,6 +3,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <shared_mutex>
@@ -114,17 +115,24 @@ struct HostPrep {
 
 uint32_t string_to_ip(const char* s);  // inet_pton(AF_INET) as shd-address.c:137-144
 
-// Immutable host mirror of one device routing table (the per-call getters' view): the column
-// map it was built for, row minima, and (full) the A x A latency / reliability / hop arrays.
+// Host view of one device routing table for the per-call getters: the column map it was built
+// for and the row minima (immutable), plus the rows the getters have read so far.  A row's
+// {latency, reliability} records are copied from the device table the first time a query needs
+// them (16 A bytes, C4: 160 KB) and published with a release store; readers never lock.  A full
+// A x A mirror is never made (round 5 copied all 1.8 GB at C4 before the first answer).
 struct HostTable {
     uint64_t gen = 0;     // attached-set generation (Topology::setGen) of the table
     uint64_t serial = 0;  // Topology::tableSerial of the table (every build / bind bumps it)
+    uint64_t epoch = 0;   // attach epoch (Topology::ipGen) of its columns: a row materialised
+                          // from this table covers the vertices attached at that epoch
     int64_t A = 0;
-    std::vector<int32_t> colOf;
+    std::shared_ptr<const std::vector<int32_t>> colOf;  // shared by snapshots of one geometry
     std::vector<double> rowmin;
-    bool full = false;
-    std::vector<double> lat, rel;
-    std::vector<uint16_t> hops;
+    // per column: its row, nullptr until first read (published once, compare-exchange)
+    std::unique_ptr<std::atomic<const double2*>[]> rows;
+    mutable std::vector<std::unique_ptr<double2[]>> rowStore;  // owner of the copied rows
+    mutable std::mutex storeMu;                                // (guards rowStore)
+    int32_t col(int32_t v) const { return (*colOf)[(size_t)v]; }
 };
 
 // Index of the attachment candidates (the "poi" vertices) so that attaching H hosts costs

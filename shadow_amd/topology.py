@@ -212,6 +212,19 @@ class Topology:
         self._lib.shdtopo_attached_vertices(self._h, _p(out), n)
         return out[:n]
 
+    def vertex_of_ip(self, ip):
+        return int(self._lib.shdtopo_vertex_of_ip(self._h, int(ip)))
+
+    def lazy_rows(self):
+        """Test hook (shdtopo_lazy_rows): the materialised source rows -- (vertices, epochs, the
+        row minimum each latest materialisation offered to the running minimum)."""
+        n = int(self._lib.shdtopo_lazy_rows(self._h, None, None, None, 0))
+        v = np.empty(max(n, 1), np.int32)
+        e = np.empty(max(n, 1), np.uint64)
+        m = np.empty(max(n, 1), np.float64)
+        n = int(self._lib.shdtopo_lazy_rows(self._h, _p(v), _p(e), _p(m), n))
+        return v[:n], e[:n], m[:n]
+
     def column_of_ip(self, ip):
         return int(self._lib.shdtopo_column_of_ip(self._h, int(ip)))
 

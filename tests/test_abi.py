@@ -216,6 +216,31 @@ def test_device_option_fixed_once_the_attach_time_preparation_starts():
         syn.set_option("device", -1)
 
 
+def test_device_option_fixed_after_a_complete_topology_build():
+    """a complete topology never starts the attach-time preparation, so a
+    build (or any other device use) must fix the "device" option too -- its table and resident
+    A x A edge matrices live on that device.  On a CPU-only box the build fails, but it asked the
+    device for work: another device is refused afterwards, the same one still accepted."""
+    top = sa.Topology.from_buffer(bundled_topology("topology.plab"))
+    top.set_option("abort_on_error", 0)
+    top.set_option("device", 1)                    # before any use: allowed
+    top.attach_ip(sa.ip_to_network("11.0.0.1"), 5)
+    top.attach_ip(sa.ip_to_network("11.0.0.2"), 6)
+    try:
+        top.build()
+    except RuntimeError:
+        pass                                       # no GPU here
+    with pytest.raises(KeyError):
+        top.set_option("device", 0)
+    top.set_option("device", 1)
+    try:
+        top.rebuild()                              # invalidates the table first
+    except RuntimeError:
+        pass
+    with pytest.raises(KeyError):                  # still fixed
+        top.set_option("device", 2)
+
+
 def test_synthetic_directed_shape_and_bucket_options():
     """The synthetic generator's directed variant (ShdSynthParams.directed, tools' C4-dir): every
     non-loop edge becomes two arcs, the reverse one with its own draws, so E = 2 x n_edges -
