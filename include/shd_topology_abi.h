@@ -382,6 +382,9 @@ typedef struct {
                                    host on their first read, cumulative (16 A bytes each; the
                                    getters never copy the whole A x A table) */
     double rows_to_host_ms;     /*   and the wall time of those copies */
+    int64_t prep_trigger;       /* what started the background graph preparation (attach_prep_ms):
+                                   0 none, 1 the first attach, 2 topology_new (right after the
+                                   parse; SHDTOPO_NO_LOAD_PREP=1 turns that off) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

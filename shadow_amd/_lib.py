@@ -61,7 +61,7 @@ class ShdStats(ctypes.Structure):
                 ("path_seconds_total", dbl), ("paths_computed", i64), ("help_ms", dbl),
                 ("help_items", i64 * 2), ("help_board_errors", i64),
                 ("batch_layout_measured", i64), ("batches", i64), ("rows_to_host", i64),
-                ("rows_to_host_ms", dbl)]
+                ("rows_to_host_ms", dbl), ("prep_trigger", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):

@@ -254,6 +254,11 @@ struct _Topology {
     // host attaches its hosts, so the first table build -- whose lock waits for the thread --
     // no longer pays them.  The device option must be set before the first attach.
     bool prepOnAttach = true;
+    // Preparation at topology_new: a non-complete topology loaded from
+    // GraphML starts the same thread right after the parse, so the attach phase and everything
+    // Shadow does before it hide it (C4: ~50 ms); a later "device" change re-prepares there.
+    // SHDTOPO_NO_LOAD_PREP=1 leaves it to the first attach.
+    bool prepOnLoad = false;  // the running / finished preparation was started by topology_new
     std::atomic<bool> prepStarted{false};
     std::thread prepThread;
     double prepBgMs = 0.0;       // the thread's wall time
@@ -2490,6 +2495,7 @@ int ensure_table(Topology* top) {
     // (waiting for the attach-time preparation thread, or another builder)
     top->stats.build_wait_ms = std::chrono::duration<double, std::milli>(tb0 - tw0).count();
     top->stats.attach_prep_ms = top->prepBgMs;
+    top->stats.prep_trigger = top->prepStarted.load() ? (top->prepOnLoad ? 2 : 1) : 0;
     for (int i = 0; i < 4; i++) top->stats.attach_prep_step_ms[i] = top->prepStepMs[i];
     for (double& x : top->stats.build_step_ms) x = 0.0;
     top->bstepT = tb0;
@@ -2944,11 +2950,14 @@ int ensure_workspace(Topology* top, int nsrc);
 // background thread holding buildMu; a build (or any other buildMu holder) that comes first does
 // the work itself and the thread then finds nothing left to do.  Complete topologies have no
 // batched-SSSP graph to prepare.
-void start_attach_prep(Topology* top) {
-    if (!top->prepOnAttach || top->isComplete) return;
+void start_graph_prep(Topology* top, bool onLoad) {
+    if (top->isComplete) return;
+    if (!onLoad && !top->prepOnAttach) return;
     if (top->prepStarted.exchange(true)) return;
-    top->prepThread = std::thread([top]() {
+    top->prepOnLoad = onLoad;
+    top->prepThread = std::thread([top, onLoad]() {
         std::lock_guard<std::mutex> lk(top->buildMu);
+        const bool used = top->deviceUsed;
         const auto t0 = std::chrono::steady_clock::now();
         int n = 0;
         if (!top->devInit && (hipGetDeviceCount(&n) != hipSuccess || n <= 0)) {
@@ -2974,7 +2983,34 @@ void start_attach_prep(Topology* top) {
         step(3);
         top->prepBgRc = r;
         top->prepBgMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        // preparing at topology_new is not a use of the device: the "device" option may still move
+        // the topology (set_option re-prepares on the new device)
+        if (onLoad) top->deviceUsed = used;
     });
+}
+
+// Everything the graph preparation and the SSSP workspace put on the device (a "device" change
+// after topology_new's preparation: the next preparation runs on the new device).  Caller holds
+// buildMu; no table, attach or build exists yet.
+void release_prepared(Topology* top) {
+    release_workspace(top);
+    for (auto* b : {&top->d_spt, &top->d_sptPar, &top->d_inv, &top->d_rowptr, &top->d_adj,
+                    &top->d_adjo, &top->d_rowptrIn, &top->d_adjk})
+        b->release();
+    for (auto* b : {&top->d_elat, &top->d_eloss, &top->d_aloss, &top->d_vloss, &top->d_selfLat,
+                    &top->d_selfLoss, &top->d_pot, &top->d_kfA, &top->d_kfB, &top->d_kfPart})
+        b->release();
+    top->d_eu.release(); top->d_ev.release();
+    top->d_kap.release(); top->d_ksum.release(); top->d_kap0.release();
+    top->d_hseg.release(); top->d_hmulti.release(); top->d_kfChanged.release();
+    top->d_board.release();
+    top->hsegRows = top->hsegN = top->hmultiN = 0;
+    top->csrUploaded = top->rowsSorted = false;
+    top->adjkPlain = top->adjkFlagged = top->adjkResorted = false;
+    top->adjkTargets.clear();
+    top->ordUploaded = false;
+    top->ordHp = nullptr;
+    top->hp.reset();
 }
 
 void do_attach(Topology* top, uint32_t ip, int32_t v, uint64_t* bwDownOut, uint64_t* bwUpOut) {
@@ -2985,7 +3021,7 @@ void do_attach(Topology* top, uint32_t ip, int32_t v, uint64_t* bwDownOut, uint6
             top->firstAttachSet.store(true);
         }
     }
-    start_attach_prep(top);
+    start_graph_prep(top, false);
     {
         std::unique_lock<std::shared_mutex> lk(top->ipMu);
         auto it = top->virtualIP.find(ip);
@@ -3038,6 +3074,7 @@ Topology* topology_new(const char* graphPath) {
     }
     const auto t1 = std::chrono::steady_clock::now();
     Topology* r = finish_new(top);
+    if (r && !getenv("SHDTOPO_NO_LOAD_PREP")) start_graph_prep(r, true);
     const auto t2 = std::chrono::steady_clock::now();
     MESSAGE("graphml parsed in %.3f s, checked in %.3f s",
             std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count());
@@ -3053,7 +3090,9 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len) {
         topology_free(top);
         return nullptr;
     }
-    return finish_new(top);
+    Topology* r = finish_new(top);
+    if (r && !getenv("SHDTOPO_NO_LOAD_PREP")) start_graph_prep(r, true);
+    return r;
 }
 
 Topology* shdtopo_new_synthetic(const ShdSynthParams* p) {
@@ -3112,13 +3151,24 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
         const int d = (int)value;
         if (d < 0) return -1;
         if (d != top->device) {
-            // fixed once the attach-time preparation (or a build) uses it; before that, a device
-            // bound by topology_new's background init is released and the next use binds d
-            if (top->prepStarted.load() || top->csrUploaded || top->tableValid.load() ||
-                top->deviceUsed)
+            // fixed once an attach or a build uses it; before that, topology_new's background
+            // init (and preparation) are released and redone on d
+            const bool loadPrep = top->prepStarted.load() && top->prepOnLoad;
+            if ((top->prepStarted.load() && !loadPrep) || top->firstAttachSet.load() ||
+                top->tableValid.load() || top->deviceUsed)
                 return -1;
+            if (loadPrep) {
+                if (top->prepThread.joinable()) top->prepThread.join();  // done: we hold buildMu
+                if (top->devInit) (void)hipSetDevice(top->devId);
+                (void)hipStreamSynchronize(top->stream);
+                release_prepared(top);
+            }
             dev_release(top);
             top->device = d;
+            if (loadPrep) {
+                top->prepStarted.store(false);
+                start_graph_prep(top, true);  // waits for buildMu: runs after this call
+            }
         }
     }
     else if (k == "prepare_on_attach") top->prepOnAttach = value != 0;
