@@ -315,6 +315,33 @@ def getters_block(top, pk, n_q, nthreads, cpu):
     return out
 
 
+def batched_model(st, pairs, k_ms, traffic):
+    """roofline.model_batched: the bytes the batched, target-pruned SSSP
+    moves per build as implemented, from the kernel's own counters of the measured build --
+      * adjacency: every expansion reads its row bounds (8 B) and its kappa-cut row of 16-B
+        relaxation records (events.expanded expansions, events.tail_relax records);
+      * distance lines: every [V][K] tail line a batch touches is written once and reset once for
+        the next batch (2 x 64 B per touched line; hub lines live in LDS);
+      * output: 18 B per pair (lat, rel, hops).
+    It assumes perfect reuse inside a batch (a line touched by many relaxations moves once), so it
+    is a lower bound for this algorithm; counter traffic / model is its waste ratio.  The
+    per-relaxation bound (one 64-B line per relaxation record) is reported beside it."""
+    ev = st["events"]
+    exp_, recs, touched = int(ev["expanded"]), int(ev["tail_relax"]), int(st["touched_lines"])
+    comp = dict(adjacency=8 * exp_ + 16 * recs, distance_lines=128 * touched, output=18 * pairs)
+    b = sum(comp.values())
+    k_s = k_ms / 1e3
+    out = dict(bytes=b, components=comp, expansions=exp_, relaxation_records=recs,
+               touched_lines=touched,
+               achieved=round(b / k_s / 1e9, 2) if k_s > 0 else None, unit="GB/s",
+               frac=round(b / k_s / 1e9 / HBM_PEAK_GBS, 5) if k_s > 0 else None,
+               traffic_over_model=round(traffic / b, 3) if (traffic and b) else None,
+               per_relaxation_line_bytes=64 * recs,
+               note="lower bound of the batched algorithm's bytes (perfect reuse within a batch); "
+                    "traffic_over_model = the PMC bytes per launch over it (its waste ratio)")
+    return out
+
+
 def load_pmc(path, key):
     """A committed counter summary (tools/summarize_prof.py) if it was measured on this exact
     workload and code (key), else None."""
@@ -623,6 +650,8 @@ def main():
                 "batch kernel touches a fraction of it, so this equivalent rate exceeds the HBM "
                 "peak and is not a bandwidth -- achieved / frac above are the measured bytes")
         roofline["pmc_key"] = key
+        if not tie_dense:
+            roofline["model_batched"] = batched_model(st, rows * A, k_ms, roofline.get("traffic"))
         sssp = dict(kernel=roofline["kernel"], batch=K, lds_hubs=int(st["lds_hubs"]),
                     sweeps=int(st["far_splits"]), slots=st["slots"],
                     batch_fill=int(st["batch_fill"]),
@@ -774,6 +803,9 @@ def main():
             "exchange": dict(kind={0: "none", 1: "rccl", 2: "peer copies"}.get(
                 int(st["exchange_kind"]), "?") if library else "torch.distributed",
                              ms=round(st["exchange_ms"], 2),
+                             ms_exposed=round(st["exchange_exposed_ms"], 2) if library else None,
+                             split=int(st["exchange_split"]) if library else None,
+                             part0_stream_ms=round(st["exchange_part_ms"][0], 3) if library else None,
                              devices=int(st["devices"]) if library else world,
                              device_kernel_ms=[round(x, 3) for x in
                                                st["device_kernel_ms"][:min(8, int(st["devices"]))]]

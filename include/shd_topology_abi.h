@@ -385,6 +385,13 @@ typedef struct {
     int64_t prep_trigger;       /* what started the background graph preparation (attach_prep_ms):
                                    0 none, 1 the first attach, 2 topology_new (right after the
                                    parse; SHDTOPO_NO_LOAD_PREP=1 turns that off) */
+    int64_t exchange_split;     /* parts of the last multi-device build (option "exchange_split"):
+                                   2 = the first part's exchange ran while the devices computed
+                                   the second, 1 = the exchange followed all the rows */
+    double exchange_exposed_ms; /*   wall time from the last part's rows to the end of the exchange
+                                     (the part of exchange_ms not hidden behind kernels) */
+    double exchange_part_ms[2]; /*   event time of part 0's exchange on device 0's exchange stream
+                                     (split builds; [1] unused) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -61,7 +61,8 @@ class ShdStats(ctypes.Structure):
                 ("path_seconds_total", dbl), ("paths_computed", i64), ("help_ms", dbl),
                 ("help_items", i64 * 2), ("help_board_errors", i64),
                 ("batch_layout_measured", i64), ("batches", i64), ("rows_to_host", i64),
-                ("rows_to_host_ms", dbl), ("prep_trigger", i64)]
+                ("rows_to_host_ms", dbl), ("prep_trigger", i64), ("exchange_split", i64),
+                ("exchange_exposed_ms", dbl), ("exchange_part_ms", dbl * 2)]
 
 
 class ShdSynthParams(ctypes.Structure):

@@ -230,3 +230,45 @@ def test_complete_branch_devices8_equals_oracle(name, devices):
     a2, lat2, rel2, _ = top.table()
     assert np.array_equal(lat2.view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(rel2.view(np.uint64), orel.view(np.uint64))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_full_size_c4_devices8_equals_devices1():
+    """BASELINE config 4 at full size (1M vertices / 10M edges, 10,000 x
+    10,000 table) built by 8 engines -- rows sharded in two parts per device, part 0 exchanged on
+    the exchange streams while part 1 computes (option exchange_split, default 2).  On the
+    one-GPU test box the engines share the device and exchange with device copies.  The table
+    must equal the devices = 1 table bit for bit (latency, reliability and hops hashed),
+    getMinimumLatency must be equal (the all-reduced minimum, shd-master.c:113-124), and 16 seeded
+    rows must equal the oracle's Dijkstra + helper."""
+    import hashlib
+    import os
+    top = sa.Topology.synthetic(seed=20261015)
+    top.synth_packets(20261015, 100_000, 0, 10**9, 10**7)
+    att = top.attached_vertices()
+    A = len(att)
+    top.set_option("devices", 8)
+    a8, lat8, rel8, hop8 = top.table()
+    st = top.stats()
+    assert st["devices"] == 8 and st["exchange_split"] == 2 and st["errors"] == 0
+    assert sum(st["device_rows"]) == A and st["exchange_exposed_ms"] <= st["exchange_ms"]
+    m8 = top.getMinimumLatency()
+    digest = lambda *xs: hashlib.sha256(b"".join(x.tobytes() for x in xs)).hexdigest()
+    h8 = digest(lat8, rel8, hop8)
+    rows = np.sort(np.random.default_rng(8).choice(A, 16, replace=False))
+    sl, sr, sh = lat8[rows].copy(), rel8[rows].copy(), hop8[rows].copy()
+    del lat8, rel8, hop8
+    top.set_option("devices", 1)
+    a1, lat1, rel1, hop1 = top.table()
+    assert top.stats()["devices"] == 1
+    assert np.array_equal(a1, a8)
+    assert digest(lat1, rel1, hop1) == h8
+    assert top.getMinimumLatency() == m8 == float(lat1.min())
+    del lat1, rel1, hop1
+    V, eu, ev, elat, eloss, vloss = top.export_graph()
+    g = oracle.OGraph(V, eu, ev, elat, eloss, vloss)
+    olat, orel, ohops = g.source_rows(att[rows], att, nthreads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(sl.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(sr.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(sh, ohops.astype(np.uint16))
