@@ -369,11 +369,6 @@ typedef struct {
                                    seconds of every table / row build so far */
     int64_t paths_computed;     /* shortestPathCount (shd-topology.c:793): source rows built so far;
                                    both are logged at topology_free (:445-446) */
-    double help_ms;             /* the last batched launch (option "share"): wall time summed over
-                                   the workgroups that, out of batches, took part in other slots'
-                                   jobs (parent walks, epilogues) */
-    int64_t help_items[2];      /*   the items they took: walk start pairs, epilogue items */
-    int64_t help_board_errors;  /*   help-board spin limits hit (cannot happen; the build fails) */
     int64_t batch_layout_measured; /* 1: the last batched launch used the measured layout (option
                                       "balance": batches sized / ordered by the sources' costs
                                       from earlier builds' batch times), 0: the grouping order */

@@ -58,8 +58,7 @@ class ShdStats(ctypes.Structure):
                 ("attach_prep_step_ms", dbl * 4), ("pair_matrix_builds", i64),
                 ("device_kernel_ms", dbl * 8), ("device_build_ms", dbl * 8),
                 ("device_rows", i64 * 8), ("dev_inits", i64), ("init_bg_ms", dbl),
-                ("path_seconds_total", dbl), ("paths_computed", i64), ("help_ms", dbl),
-                ("help_items", i64 * 2), ("help_board_errors", i64),
+                ("path_seconds_total", dbl), ("paths_computed", i64),
                 ("batch_layout_measured", i64), ("batches", i64), ("rows_to_host", i64),
                 ("rows_to_host_ms", dbl), ("prep_trigger", i64), ("exchange_split", i64),
                 ("exchange_exposed_ms", dbl), ("exchange_part_ms", dbl * 2)]

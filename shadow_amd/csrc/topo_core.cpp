@@ -309,11 +309,6 @@ struct _Topology {
     DevBuf<uint4> d_prec;  // per (vertex, source) pair records of the parent pass
     DevBuf<double> d_pathbuf;
     DevBuf<uint32_t> d_cnt, d_bslot, d_counters;
-    // help board of the batched launches (SlotWs.board): kBoardWords per slot + 1, zeroed before
-    // every launch; option "share" (default 0: off; 1 on; -1 one-round launches): idle
-    // workgroups take part in the running batches' parent walks and epilogues
-    DevBuf<uint32_t> d_board;
-    int share = 0;  // 0 off (default); 1 on; -1 auto: the board on a one-round launch only
     int slots = 0;
     DevBuf<double2> d_lr;
     DevBuf<uint16_t> d_hops;
@@ -993,8 +988,8 @@ int batch_k(Topology* top) { return top->batchK; }  // 2, 4, 8 or 16 (shdtopo_se
 int64_t bitmap_words(int64_t n) { return (n + 31) / 32 + 64; }
 int64_t ring_entries(Topology* top, int K) {
     const int64_t V = top->g.V;
-    // + the two pending-vertex lists of the sweeps (V entries each) and alignment slack
-    return V * (K + 1) + bitmap_words(V) + bitmap_words(V) + 2 * V + 64;
+    // + alignment slack
+    return V * (K + 1) + bitmap_words(V) + bitmap_words(V) + 64;
 }
 int64_t queue_stride(Topology* top, int K) {  // u64 per slot of each near queue / pair list
     const int64_t V = top->g.V;
@@ -1115,18 +1110,7 @@ SlotWs slot_ws(Topology* top) {
     w.q_stride = queue_stride(top, w.K);
     w.mask = top->d_mask.p;
     w.hpar = top->d_hpar.p;
-    w.board = top->share != 0 ? top->d_board.p : nullptr;  // (enqueue_rows decides per launch)
     return w;
-}
-
-// zeroes the help board before a batched launch (every polled word starts at 0: no job, no
-// finished batch)
-int board_ready(Topology* top, hipStream_t st) {
-    if (top->share == 0) return 0;
-    const size_t n = ((size_t)top->slots + 1) * kBoardWords;
-    HIPCHK(top->d_board.ensure(n));
-    HIPCHK(hipMemsetAsync(top->d_board.p, 0, sizeof(uint32_t) * n, st));
-    return 0;
 }
 
 // Incidence-order CSR of the heap replay (ReplayCSR in topo_device.h).  Row x (relabelled id)
@@ -1610,8 +1594,6 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         if (!allReplay) {
             r = ensure_workspace(top, (int)rows);
             if (r) return r;
-            r = board_ready(top, st);
-            if (r) return r;
             HIPCHK(top->d_rowflag.ensure((size_t)rows));
             HIPCHK(hipMemsetAsync(top->d_rowflag.p, 0, (size_t)rows, st));
             SlotWs ws = slot_ws(top);
@@ -1901,11 +1883,6 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 top->stats.batch_layout_measured = measured ? 1 : 0;
                 top->lastBatches = lnbat;
                 ws.rowmap = top->d_rowmap.p;
-                // the help board (option share; auto: a one-round launch, whose idle slots help
-                // its last batches -- in a launch of several rounds its code costs more than the
-                // help returns)
-                if (!(top->share > 0 || (top->share < 0 && lnbat <= (int64_t)ws.slots)))
-                    ws.board = nullptr;
                 // per batch {start tick, end tick, slot, near iterations, sweeps, expansions,
                 // relaxations, sources, ...} (kBTraceWords u64): the batch times give the sources'
                 // costs (option balance); SHD_BATCH_TRACE=<file> (diagnostic) appends them, then
@@ -1923,8 +1900,6 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                     top->g.V);
                 top->stats.lds_hubs = bp.H;
                 r = hub_rows_ready(top, bp.H, st);
-                if (r) return r;
-                r = board_ready(top, st);  // (a tie probe launch used it)
                 if (r) return r;
                 bstep_mark(top, 2);
                 HIPCHK(launch_sssp_batch(K, dev_csr(top), ws, top->d_bsrc.p,
@@ -2054,11 +2029,7 @@ int collect_row_stats(Topology* top) {
     top->stats.replay_rows = (int64_t)h[ST_RP_ROWS];
     top->stats.touched_lines = (int64_t)h[ST_TOUCHED];
     top->stats.walk_steps = (int64_t)h[ST_WALK];
-    top->stats.help_items[0] = (int64_t)h[ST_HELP_ITEMS];
-    top->stats.help_items[1] = (int64_t)h[ST_HELP_ITEMS + 1];
-    top->stats.help_board_errors = (int64_t)h[ST_HB_ERR];
     top->stats.batches = top->lastBatches;
-    if (h[ST_HB_ERR]) CRITICAL("help board: %llu spin limits hit", h[ST_HB_ERR]);
     for (int i = 0; i < 4; i++) top->stats.walk_kinds[i] = (int64_t)h[ST_WK0 + i];
     top->stats.replay_pops = (int64_t)h[ST_RP_POPS];
     top->stats.replay_pushes = (int64_t)h[ST_RP_PUSH];
@@ -2088,7 +2059,6 @@ int collect_row_stats(Topology* top) {
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, top->devId) != hipSuccess || khz <= 0)
             khz = 100000;
         top->stats.split_ms = (double)h[ST_T_SPLIT] / (double)khz;
-        top->stats.help_ms = (double)h[ST_T_HELP] / (double)khz;
     }
     if (h[ST_OVERFLOW]) CRITICAL("SSSP queue overflow / iteration guard (code %llu)", h[ST_OVERFLOW]);
     if (top->stats.ambiguous_pairs && !top->tieReplay)
@@ -2096,7 +2066,7 @@ int collect_row_stats(Topology* top) {
                 "in the reference; tie_replay is off, so the lowest adjacency slot is used here",
                 (long long)top->stats.ambiguous_pairs);
     top->rowsPending = false;
-    return (h[ST_OVERFLOW] || h[ST_HB_ERR] ? -4 : 0);
+    return h[ST_OVERFLOW] ? -4 : 0;
 }
 
 void push_min_to_engine(double m) {
@@ -2214,7 +2184,6 @@ void sync_peer(Topology* top, Topology* p) {
     p->targetSkip = top->targetSkip;
     p->targetKappa = top->targetKappa;
     p->targetResort = top->targetResort;
-    p->share = top->share;
     p->attached = top->attached;
     p->colOf = top->colOf;
     p->A = top->A;
@@ -3149,7 +3118,6 @@ void release_prepared(Topology* top) {
     top->d_eu.release(); top->d_ev.release();
     top->d_kap.release(); top->d_ksum.release(); top->d_kap0.release();
     top->d_hseg.release(); top->d_hmulti.release(); top->d_kfChanged.release();
-    top->d_board.release();
     top->hsegRows = top->hsegN = top->hmultiN = 0;
     top->csrUploaded = top->rowsSorted = false;
     top->adjkPlain = top->adjkFlagged = top->adjkResorted = false;
@@ -3319,7 +3287,6 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
         }
     }
     else if (k == "prepare_on_attach") top->prepOnAttach = value != 0;
-    else if (k == "share") top->share = value < 0 ? -1 : (value != 0 ? 1 : 0);
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
     else if (k == "par_hubs") top->parHubs = (int64_t)value;
     else if (k == "batch") {

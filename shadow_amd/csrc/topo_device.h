@@ -91,10 +91,7 @@ enum StatIdx {
     ST_WL0 = 69,        // batch kernel (SHD_BATCH_WRCOUNT builds): 64-B lines written per
                         //   category (16 slots, topo_sssp_batch.hip WL_*)
     ST_RL0 = 85,        //   then 64-B lines read per category (8 slots, RL_*)
-    ST_T_HELP = 93,     // batch kernel: wall ticks summed over workgroups helping other slots' jobs
-    ST_HELP_ITEMS = 94, //   items they took: walk start pairs / epilogue items (2 slots)
-    ST_HB_ERR = 96,     //   help-board spin limits hit (cannot happen; reported)
-    ST_COUNT = 97
+    ST_COUNT = 93
 };
 
 // A directed topology (igraph mode OUT, shd-topology.c:762-763) relaxes out-edges but finds a
@@ -159,17 +156,12 @@ struct SlotWs {
     // end, slot, near iterations, sweeps, expansions, relaxations, sources, ticks at the SSSP's,
     // the parent pass' and the epilogue's end, 0}
     unsigned long long* btrace = nullptr;
-    // help board (work sharing, topo_sssp_batch.hip): kBoardWords u32 per slot + one word of
-    // finished batches, zeroed before every launch; nullptr = every batch's parent walks and
-    // epilogue stay in its own workgroup
-    uint32_t* board = nullptr;
     // batch layout (option balance, topo_core.cpp): batch b takes positions [bstart[b],
     // bstart[b + 1]) (at most K), nbat batches; nullptr = batch b takes [b kf, b kf + kf)
     const uint32_t* bstart = nullptr;
     int nbat = 0;
 };
-constexpr int kBoardWords = 64;
-constexpr int kBTraceWords = 12;  // u32 words per slot entry of the help board (256 B)
+constexpr int kBTraceWords = 12;  // u64 words per batch of SlotWs::btrace (per-batch trace / costs)
 
 // Incidence-order CSR of the heap replay (topo_replay.hip), relabelled vertex ids: row x holds
 // x's neighbours in igraph_incident order (ascending ORIGINAL neighbour id; directed graphs:

@@ -80,22 +80,11 @@ using namespace dev;
 #else
 #define RP_STICK(i) do { } while (0)
 #endif
-#ifndef SHD_RP_PREF
-#define SHD_RP_PREF 1  // the next root's row bounds and target bit loaded right after the sink
-#endif
 constexpr int kRpLA = 5;  // LDS walk of the sink: heap levels per LDS round (62 nodes)
 #ifndef SHD_RP_HL
 #define SHD_RP_HL 5  // levels per HBM round of the path-first sink (6: two nodes per lane)
 #endif
 constexpr int kHL = SHD_RP_HL;
-#ifndef SHD_RP_BLOCKED
-#define SHD_RP_BLOCKED 0  // (1: slower) HBM heap levels stored as contiguous sink-round subtrees (RpHeap::phys)
-#endif
-// Blocks (of 2 << kHL nodes) in the bands before band b: band b' has one per node of its root
-// level L0 - 1 + kHL b'.
-__host__ __device__ __forceinline__ uint32_t rp_band_base(uint32_t L0, uint32_t b) {
-    return (1u << (L0 - 1u)) * (((1u << (kHL * b)) - 1u) / ((1u << kHL) - 1u));
-}
 constexpr int kHNodes = (2 << kHL) - 2;
 static_assert(kHL >= 1 && kHNodes <= 128, "at most two nodes per lane");
 
@@ -242,39 +231,10 @@ struct RpHeap {
     uint4* vr;
     unsigned long long* nl;
     uint32_t stdPos, stdBase;
-    // Physical node of HBM position p.  Positions below stdPos sit in bands of kHL levels: the
-    // 2^(kHL+1) - 2 descendants of a band root r (level L0 - 1 + kHL b) -- exactly the nodes one
-    // sink round loads below its path end -- are one contiguous block in the BFS order of
-    // rp_sub_pos, so a round reads 8 whole lines (u32 keys; 16 for f64) instead of ~12 (~21)
-    // across five position-major levels, and a path's moves inside the band share lines.
-    __device__ __forceinline__ uint32_t phys(uint32_t p) const {
-        if (p >= stdPos) return p - stdPos + stdBase;
-        const uint32_t l = 31u - (uint32_t)__clz(p + 1u);  // level of p (>= L0)
-        const uint32_t b = (l - (uint32_t)K::kLevels) / (uint32_t)kHL;
-        const uint32_t r = (uint32_t)K::kLevels - 1u + (uint32_t)kHL * b;  // band root level
-        const uint32_t dl = l - r;                                          // 1..kHL below it
-        const uint32_t a = ((p + 1u) >> dl) - 1u;                           // the band root
-        return (rp_band_base(K::kLevels, b) + (a + 1u - (1u << r))) * (2u << kHL) +
-               (p + 1u) - ((a + 1u) << dl) + (1u << dl) - 2u;
-    }
-    // Physical node of the first of the 2^(kHL+1) - 2 descendants of band root `cur` (uniform),
-    // when they all lie in the blocked bands (then descendant BFS index i + 1 is node base + i);
-    // ~0u otherwise.
-    __device__ __forceinline__ uint32_t sub_base(uint32_t cur) const {
-        if (((unsigned long long)(cur + 1u) << kHL) > stdPos) return 0xFFFFFFFFu;  // past the bands
-        const uint32_t r = 31u - (uint32_t)__clz(cur + 1u);
-        const uint32_t b = (r + 1u - (uint32_t)K::kLevels) / (uint32_t)kHL;
-        return (rp_band_base(K::kLevels, b) + (cur + 1u - (1u << r))) * (2u << kHL);
-    }
-    // the sink round's node load: physical node x (x != ~0u) or position p
-    __device__ __forceinline__ void node_at(uint32_t x, uint32_t p, T& k, uint32_t& v, int cat) const {
-        if (x == 0xFFFFFFFFu) {
-            node(p, k, v, cat);
-        } else {
-            rp_lines(nl, cat, true, gn + x);
-            K::unpack(gn[x], k, v);
-        }
-    }
+    // Physical node of HBM position p (positions below stdPos = kT live in LDS).  (Round 5 also
+    // had a banded layout -- a sink round's subtree in one contiguous block -- measured slower and
+    // removed in round 6: DESIGN.md 4.)
+    __device__ __forceinline__ uint32_t phys(uint32_t p) const { return p - stdPos + stdBase; }
     __device__ __forceinline__ void node(uint32_t p, T& k, uint32_t& v, int cat) const {
         if (p < kT) {
             k = lds_k<I>(p);
@@ -326,9 +286,6 @@ __device__ __forceinline__ uint32_t rp_lds_find(uint32_t t, uint32_t size, int l
     return found;
 }
 
-#ifndef SHD_RP_PARPATH
-#define SHD_RP_PARPATH 1  // a sink round's path of larger children found lane-parallel (ballots)
-#endif
 // One sink round's path of larger children, lane-parallel: lane i holds node rr = i + 2 of the
 // subtree below the round's head (BFS, head = 1; `valid`: the node exists, i.e. its position is
 // below the heap size).  igraph_2wheap_sink goes left when data[L] >= data[R] (or R does not
@@ -413,7 +370,6 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap<I>& H, uint32_t size, i
             k = lds_k<I>(p);
             v = lds_v<I>(p);
         }
-#if SHD_RP_PARPATH
         {
             const int m = rp_round_path<I>(cur, lane, valid, k, v, p, np, pp, pk, pv);
             np += m;
@@ -423,7 +379,6 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap<I>& H, uint32_t size, i
             }
             continue;
         }
-#endif
         uint32_t q = 0;
         for (int s = 0; s < la; ++s) {
             const uint32_t L = 2u * cur + 1u;
@@ -466,16 +421,14 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap<I>& H, uint32_t size, i
         H.nl[6]++;  // HBM sink rounds
 #endif
         const uint32_t p = rp_sub_pos(cur, lane);
-        // cur is a band root here (the LDS walk ends at level L0 - 1, rounds take kHL levels)
-        const uint32_t xb = SHD_RP_BLOCKED ? H.sub_base(cur) : 0xFFFFFFFFu;
         T k = K::lo(), k2 = K::lo();
         uint32_t v = 0, v2 = 0;
         if (lane < kHNodes && p < size)
-            H.node_at(xb == 0xFFFFFFFFu ? xb : xb + (uint32_t)lane, p, k, v, RPL_SINK_LD);
+            H.node(p, k, v, RPL_SINK_LD);
         if (kHNodes > 64) {  // BFS nodes 64.. in a second register
             const uint32_t p2 = rp_sub_pos(cur, lane + 64);
             if (lane + 64 < kHNodes && p2 < size)
-                H.node_at(xb == 0xFFFFFFFFu ? xb : xb + (uint32_t)lane + 64u, p2, k2, v2, RPL_SINK_LD);
+                H.node(p2, k2, v2, RPL_SINK_LD);
         }
         if (!havex) {
             xk = K::rl(kx, 63);
@@ -487,7 +440,6 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap<I>& H, uint32_t size, i
                 break;
             }
         }
-#if SHD_RP_PARPATH
         if (kHNodes <= 64) {
             // the round's path at once; x stops at the first of its nodes it is not smaller than
             const bool valid = lane < kHNodes && p < size;
@@ -502,7 +454,6 @@ __device__ __forceinline__ void rp_pop_sink(const RpHeap<I>& H, uint32_t size, i
             if (m < kHL) bottom = true;
             continue;
         }
-#endif
         uint32_t q = 0;
 #pragma unroll
         for (int s = 0; s < kHL; ++s) {
@@ -663,7 +614,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
             uint32_t v1 = 0;
             if (lane == 63) H.node(lastp, k1, v1, RPL_SINK_LD);
             uint32_t tb, rb, re;
-            if (SHD_RP_PREF && u == pf_u) {
+            if (u == pf_u) {
 #if SHD_RP_TIME
                 nl[13]++;
 #endif
@@ -685,7 +636,7 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
             if (size > 0) rp_pop_sink<I>(H, size, lane, k1, v1);
             n_pop++;
             RP_TICK(0);
-            if (SHD_RP_PREF && size > 0) {
+            if (size > 0) {
                 pf_u = uni_u32(lds_v<I>(0));
                 if (lane < 2) pf_r = g.rowptr[pf_u + (uint32_t)lane];
                 if (lane == 0) pf_t = g.tbits[pf_u >> 5];
@@ -897,13 +848,9 @@ heap_replay_kernel(ReplayCSR g, ReplayWs ws, const uint32_t* __restrict__ source
 
 ReplayLayout replay_layout(int int_keys, uint32_t V) {
     const uint32_t L0 = (uint32_t)replay_lds_levels(int_keys);
-    uint32_t lmax = 0;  // level of the deepest position a heap of V elements can use
-    while (V > 1 && ((2ull << lmax) - 1ull) < (unsigned long long)V) lmax++;
-    uint32_t nb = 0;    // bands whose levels all lie within [L0, lmax]
-    while (SHD_RP_BLOCKED && L0 + (uint32_t)kHL * (nb + 1) - 1 <= lmax && L0 + (uint32_t)kHL * (nb + 1) < 31) nb++;
     ReplayLayout r;
-    r.stdPos = (uint32_t)((1ull << (L0 + (uint32_t)kHL * nb)) - 1ull);
-    r.stdBase = rp_band_base(L0, nb) * (2u << kHL);  // positions < kT live in LDS only
+    r.stdPos = (uint32_t)((1ull << L0) - 1ull);  // positions < kT live in LDS only
+    r.stdBase = 0;
     const unsigned long long cap = (unsigned long long)r.stdBase + (V > r.stdPos ? V - r.stdPos : 0u);
     r.nodeCap = (uint32_t)((std::max<unsigned long long>(cap, 64) + 63ull) & ~63ull);  // blocks stay aligned per slot
     return r;

@@ -48,26 +48,15 @@ namespace {
 
 using namespace dev;
 
-#ifndef SHD_BATCH_RB
-#define SHD_BATCH_RB 2  // phase-B rounds whose loads are in flight together (pair rounds: 2 < 3 < 4 by 1-4 %, 8 spills)
-#endif
-#ifndef SHD_BATCH_SPEC
-// buckets past cb whose hub sources join a hub expansion speculatively (-1: none).  Round 5,
-// with 25-ms buckets and h0 closing its bucket: 0 (only the current bucket's sources) 55.4-55.6
-// ms full table, 13.1 ms at 1,250 rows against 56.9-57.1 / 13.6-13.7 with 1 (relaxations per
-// source 222 k -> 174 k); with the round-4 10-ms buckets 1 was 4 % ahead of 0
-#define SHD_BATCH_SPEC 0
-#endif
-#ifndef SHD_BATCH_U
-#define SHD_BATCH_U 2  // phase-A edges per lane
-#endif
-#ifndef SHD_TAIL_HINT
-#define SHD_TAIL_HINT 1  // record each tail pair's improver during the SSSP (parent-pass guess)
-#endif
-#ifndef SHD_MASK_TAKE
-#define SHD_MASK_TAKE 1  // a queued tail vertex's mask read and cleared by one returning atomic
-                         // (r04: 94.7 -> 92.3 ms, same box)
-#endif
+// Tuning constants (A/B measured): phase-B rounds whose loads are in flight together
+// (2 < 3 < 4 by 1-4 %, 8 spills), phase-A edges per lane, queue vertices per expansion chunk.
+// Round 6 removed the measured-slower variants that were compiled in behind SHD_* switches (the
+// help board, the pending-vertex sweep list, speculative hub buckets, the phase-B target skip,
+// node-major walks, temporal stores of the reset and the table, the mask read + store pair); their
+// A/B numbers stay in DESIGN.md 4 and the code in git history.
+constexpr int kBatchRB = 2;
+constexpr int kBatchU = 2;
+constexpr int kBChunk = 512;  // (<= kSsspBlock)
 #ifndef SHD_BATCH_WRCOUNT
 #define SHD_BATCH_WRCOUNT 0  // profiling build: 64-B lines written per category (ST_WL0)
 #endif
@@ -80,30 +69,6 @@ using namespace dev;
 #else
 #define BT_TICK(i) do { } while (0)
 #endif
-#ifndef SHD_SWEEP_LIST
-#define SHD_SWEEP_LIST 0  // 1: tail sweeps over a list of the pending vertices instead of the bitmap
-                          // (r05: full table 66.7 -> 74.7 ms -- the returning pending atomic in
-                          // phase B costs more than the bitmap scan it saves; kept off)
-#endif
-#ifndef SHD_PB_SPLIT
-#define SHD_PB_SPLIT 1  // phase-B rounds of tail-target pairs first, then rounds of LDS-hub pairs
-#endif
-#ifndef SHD_PA_SKIP
-#define SHD_PA_SKIP 1  // the target skip decided in phase A (dropped pairs take no phase-B lane)
-#endif
-#ifndef SHD_TGT_MAJOR
-#define SHD_TGT_MAJOR 1  // parent walks and epilogue items numbered target-major (a target's K sources in adjacent lanes)
-#endif
-#ifndef SHD_INIT_NT
-#define SHD_INIT_NT 1  // the batch's [V][K] distance reset with nontemporal stores
-#endif
-#ifndef SHD_OUT_NT
-#define SHD_OUT_NT 1  // table rows written with nontemporal stores
-#endif
-#ifndef SHD_BATCH_CHUNK
-#define SHD_BATCH_CHUNK 512
-#endif
-constexpr int kBChunk = SHD_BATCH_CHUNK;  // queue vertices per expansion chunk (<= kSsspBlock)
 constexpr uint32_t kNoBucket = 0xFFFFFFFFu;
 constexpr size_t kBMaxLds = 160 * 1024 / kBatchWgPerCu;  // a CU's LDS over its workgroups
 
@@ -172,20 +137,8 @@ struct LdsB {
     unsigned long long wl[16];  // SHD_BATCH_WRCOUNT builds: 64-B lines stored / atomically
                                 // written per category (WL_*), then read per category (RL_*)
     unsigned long long rl[16];
-    // jobs (help board): this slot's jobs published (seq), the cursor of a board-less launch, the
-    // items this workgroup took of the current job; a helper's chosen entry, its descriptor
-    // {seq, kind, items, tag, first position, sources, list, valid}, "every batch done"; items a
-    // helper took (walk start pairs, epilogue items)
-    // pending-vertex list (SHD_SWEEP_LIST): entries, entries of the next list, which buffer
-    uint32_t plen, plen2, plsel;
-    uint32_t jseq, jcur, jtaken;
-    // the workgroup's lease of the current job (board launches): {next item, end} packed, one
-    // wave refilling it from the board at a time, the job used up
-    unsigned long long lease;
-    uint32_t lrefill, ljdone;
-    uint32_t hjob, hflag;
-    uint32_t hd[8];
-    unsigned long long hitems[2];
+    // jobs (a level's walks, the epilogue): the cursor of the current job's items
+    uint32_t jcur;
 };
 
 // Write categories of SHD_BATCH_WRCOUNT builds (ShdStats.write_lines): each store / atomic
@@ -310,7 +263,7 @@ struct BView {
     // pending vertex is always touched, so one atomic sets both and the reset clears both.
     uint32_t* pt;
     uint32_t* tpar;            // HBM [V][K] pair records: word 0 = vertex whose relaxation last
-                               // lowered the tail pair (SHD_TAIL_HINT; the parent field before
+                               // lowered the tail pair (the parent field before
                                // the parent pass), word 1 = tag word (ties: kTagTie)
     uint32_t H, P;
     __device__ __forceinline__ unsigned long long get(uint32_t v, uint32_t j) const {
@@ -398,14 +351,8 @@ __device__ __forceinline__ uint32_t load_chunk(const uint32_t* Q, uint32_t cnt, 
                 if (m) atomicOr(&D.xb[(v * K) >> 5], m << ((v * K) & 31));
             }
         } else {
-#if SHD_MASK_TAKE
             wl_count(L, WL_MASK_ST, true, mcur + v);
             m = MO::take(mcur, v);  // read-and-clear: one returning atomic
-#else
-            m = MO::get_l2(mcur, v);
-            wl_count(L, WL_MASK_ST, true, mcur + v);
-            mcur[v] = 0;
-#endif
         }
         // relaxation: the out-rows (kappa copy); parent pass: the rows of candidate parents (the
         // in-rows of a directed topology)
@@ -541,12 +488,8 @@ __device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t
         const uint32_t v = qv;  // this lane's queue entry (loaded by the caller)
         // every load of the vertex in one round trip: its mask (a queued vertex's is almost
         // never empty), row bounds, kappa probes and K distances
-#if SHD_MASK_TAKE
         wl_count(L, WL_MASK_ST, true, mcur + v);
         const uint32_t m = MO::take(mcur, v);  // read-and-clear: one returning atomic
-#else
-        const uint32_t m = MO::get_l2(mcur, v);
-#endif
         rl_count(L, RL_CHUNK, true, mcur + v);
         rl_count(L, RL_CHUNK, true, g.rowptr + v);
         rl_count(L, RL_CHUNK, true, g.ksum + kKProbes / 4 * (size_t)v);
@@ -565,10 +508,6 @@ __device__ __forceinline__ uint32_t load_sub(uint32_t qv, uint32_t cnt, uint32_t
                 dv[2 * h + 1] = bits2d(x.y);
             }
         }
-#if !SHD_MASK_TAKE
-        wl_count(L, WL_MASK_ST, true, mcur + v);
-        mcur[v] = 0;
-#endif
         deg = m ? r1 - r0 : 0u;
         if (deg) {
             double T = -INFINITY;
@@ -620,12 +559,11 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                                               typename MaskOps<K>::M* mcur,
                                               typename MaskOps<K>::M* hdef,
                                               typename MaskOps<K>::M* mnxt, uint32_t* qout,
-                                              uint32_t qcap, uint32_t* hq, const BBuckets& B,
-                                              uint32_t* plst) {
+                                              uint32_t qcap, uint32_t* hq, const BBuckets& B) {
     using MO = MaskOps<K>;
     static_assert(64 % K == 0, "a wave holds whole edge groups");
     static_assert(UA >= 1 && (UA & (UA - 1)) == 0, "the phase-B edge search halves UA * 64");
-    constexpr int RB = SHD_BATCH_RB;     // phase-B rounds whose loads are in flight together
+    constexpr int RB = kBatchRB;     // phase-B rounds whose loads are in flight together
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     const uint32_t wv = tid >> 6;
@@ -660,7 +598,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             if (base >= nq) break;
             cnt = min((uint32_t)kBChunk, nq - base);
             total = load_chunk<K, true>(Q + base, cnt, g, L, D, mcur, hdef, true,
-                                        SHD_BATCH_SPEC < 0 ? 0u : B.cb + (uint32_t)SHD_BATCH_SPEC);
+                                        B.cb);
         }
         BT_TICK(0);
         constexpr uint32_t kStep = WAVE ? 64u : (uint32_t)kSsspBlock;  // lanes per phase-A slot
@@ -691,14 +629,20 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             // is dropped from the edge (91 % of the tail relaxations on C4).  Every relaxation
             // that sets or ties a final value is still performed: distances, parent hints and
             // tie bits are unchanged.
-            // The target skip (phase B's comment below) is decided here too, per (edge, source):
-            // a dropped pair takes no phase-B lane (C4: 21 % of the pairs).
+            // The target skip is decided here too, per (edge, source): a tail vertex that is no
+            // table target and would expand nothing at this candidate (kappa0 above the landmark
+            // threshold, the test that keeps it out of the near queue) needs no distance at all --
+            // only targets and the vertices of their parent chains are read after the SSSP, and a
+            // chain vertex is expanded at its final distance (its chain edge passes the filter),
+            // so every relaxation that sets or ties its final value passes this test (a larger,
+            // stale d_j(h0) only widens it).  A dropped pair takes no phase-B lane (C4: 21 % of
+            // the pairs).
 #pragma unroll
             for (int a = 0; a < UA; a++) {
                 uint32_t mk = amk[a];
                 const double w = __hiloint2double((int)awh[a], (int)awl[a]);
                 const double pv = rec_pi(apb[a]);
-                const bool skippable = SHD_PA_SKIP && kKapInRec && g.tflags &&
+                const bool skippable = kKapInRec && g.tflags &&
                                        (an[a] & 0x3FFFFFFFu) >= D.H && !((an[a] >> 30) & 1u);
                 const float kz0 = rec_kap0(apb[a]);
                 while (mk) {
@@ -728,11 +672,10 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
 #pragma unroll
             for (int a = 0; a < UA; a++) {
                 const uint32_t c = (uint32_t)__popc(amk[a]);
-                const bool tl = !SHD_PB_SPLIT ||
-                                (an[a] & (g.tflags ? 0x3FFFFFFFu : 0x7FFFFFFFu)) >= D.H;
+                const bool tl = (an[a] & (g.tflags ? 0x3FFFFFFFu : 0x7FFFFFFFu)) >= D.H;
                 uint32_t tt, th = 0;
                 po[a] = npt + wave_excl_scan(tl ? c : 0u, &tt);
-                ph[a] = SHD_PB_SPLIT ? nph + wave_excl_scan(tl ? 0u : c, &th) : 0u;
+                ph[a] = nph + wave_excl_scan(tl ? 0u : c, &th);
                 npt += tt;
                 nph += th;
             }
@@ -806,16 +749,6 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 const double w = __hiloint2double((int)xwh, (int)xwl);
                 const double abd = __dadd_rn(L.val[lo[rr] * K + jj], w);
                 if (kKapInRec) kz[rr] = rec_kap0(xpb);
-                // A tail vertex that is no table target and would expand nothing at this
-                // candidate (kappa0 above the landmark threshold, the test that keeps it out of
-                // the near queue) needs no distance at all: only targets and the vertices of
-                // their parent chains are read after the SSSP, and a chain vertex is expanded at
-                // its final distance (its chain edge passes the filter), so every relaxation that
-                // sets or ties its final value passes this test (a larger, stale d_j(h0) only
-                // widens it).  The pair is dropped before its pre-check load and atomics.
-                if (!SHD_PA_SKIP && kKapInRec && g.tflags && on && n[rr] >= D.H && !((xn >> 30) & 1u) &&
-                    !kappa_useful(kz[rr], L.dh0[jj], abd, g.piMax))
-                    on = false;
                 er[rr] = on ? e : 0x10000u + lane;  // segment key (no segment across empty lanes)
                 ab[rr] = on ? d2bits(abd) : ~0ull;
                 // pre-check: the edge's pairs read its target's line in one request
@@ -846,9 +779,6 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
             unsigned long long old[RB];
             uint32_t pm[RB];  // the mask word's previous bits (first: push), or ~0: no mask op
             bool hfv[RB];     // a hub's first deferral
-            uint32_t pold[RB];  // SHD_SWEEP_LIST: the pending word's bits before a first reach past
-                                // cb set its pending bit (not set before: the vertex joins the
-                                // pending list), or 0x55555555 (no such reach)
 #pragma unroll
             for (int rr = 0; rr < RB; rr++) {
                 const bool on = ab[rr] != ~0ull;
@@ -897,13 +827,7 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 // first reach: touched (bit 1), and pending when past cb (bit 0): one atomic
                 wl_count(L, WL_RELAX_TOUCH, head && gf, &D.pt[n[rr] >> 4]);
                 wl_count(L, WL_RELAX_MASK, head && gm && !hub, mnxt + n[rr]);
-                pold[rr] = 0x55555555u;
-                if (head && gf) {
-                    if (SHD_SWEEP_LIST && (gf & 1u))
-                        pold[rr] = atomicOr(&D.pt[n[rr] >> 4], gf << (2u * (n[rr] & 15u)));
-                    else
-                        (void)atomicOr(&D.pt[n[rr] >> 4], gf << (2u * (n[rr] & 15u)));
-                }
+                if (head && gf) (void)atomicOr(&D.pt[n[rr] >> 4], gf << (2u * (n[rr] & 15u)));
                 pm[rr] = ~0u;
                 hfv[rr] = false;
                 if (head && gm) {
@@ -923,8 +847,8 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                     if (ab[rr] == old[rr]) D.tpar[4 * wi + 1] = B.tie_tag;
                     // the improver: the parent pass' second guess (verified there; the h0-tree
                     // edge needs no record: it is the pass' first guess)
-                    wl_count(L, WL_RELAX_HINT, SHD_TAIL_HINT && im && !tree[rr], D.tpar + 4 * wi);
-                    if (SHD_TAIL_HINT && im && !tree[rr]) D.tpar[4 * wi] = L.vx[lo[rr]];
+                    wl_count(L, WL_RELAX_HINT, im && !tree[rr], D.tpar + 4 * wi);
+                    if (im && !tree[rr]) D.tpar[4 * wi] = L.vx[lo[rr]];
                     if (im) {
                         const uint32_t b = bkt(bits2d(ab[rr]), L.sh[jj], B.inv_delta);
                         if (b > B.cb) fm = b < fm ? b : fm;
@@ -932,9 +856,6 @@ __device__ __forceinline__ void relax_batch_t(const uint32_t* Q, uint32_t nq, co
                 }
                 wpush<K>(L, pm[rr] == 0u, n[rr], qout, &L.qtail, qcap, &L.fover, 1u);
                 wpush<K>(L, hfv[rr], n[rr], hq, &L.htail, D.H, &L.fover, 1u);
-                if (SHD_SWEEP_LIST)
-                    wpush<K>(L, !((pold[rr] >> (2u * (n[rr] & 15u))) & 1u), n[rr], plst, &L.plen,
-                             qcap, &L.fover, 2u);
             }
             }
             if (__ballot(fm != kNoBucket)) {
@@ -993,77 +914,21 @@ __device__ __forceinline__ void expand_pairs(const uint32_t* Q, uint32_t nq, con
     }
 }
 
-// ---- help board: work sharing between the launch's workgroups --------
-// A batch's parent walks (each level's start list) and its per-target epilogue are JOBS of items
-// that any workgroup can take: the owner publishes a job on its board entry, takes chunks of it
-// itself, and waits until every taken item is done; a workgroup whose dequeue found no batch left
-// scans the board and takes chunks of the running jobs (the walks' pair records are
-// deterministic, so concurrent takers write identical values; the epilogue's items are
-// independent).  Entry words: the cursor (u64: seq 16 | items 24 | next 24, claimed by CAS, so a
-// stale taker never moves a newer job's cursor), items done, the job's descriptor (written before
-// the cursor), the S list counter of walk jobs, the batch's row minima (u64 atomicMin).
-// Hand-offs: the owner's stores -> release fence -> cursor store; a helper's relaxed cursor load
-// -> acquire fence -> plain loads; a helper's stores -> release fence -> done add; the owner's
-// done poll -> acquire fence (MI355X_MICROARCH.md "inter-workgroup visibility").  Every spin is
-// bounded (ST_HB_ERR).
-enum {
-    HB_CUR = 0,    // u64 cursor (words 0-1)
-    HB_DONE = 2,   // items completed
-    HB_SEQ = 3,    // descriptor: the job's seq (validated against the cursor's)
-    HB_KIND = 4,   //   kJob*
-    HB_EP = 5,     //   the batch tag
-    HB_R0 = 6,     //   the batch's first position
-    HB_NK = 7,     //   its sources
-    HB_LIST = 8,   //   walk jobs: 0 = start list in qa, 1 = in qb
-    HB_SCNT = 9,   // walk jobs: entries reserved in the slot's S list (blocks of 64)
-    HB_HELP = 10,  // helping workgroups on this entry now (any job; at most kMaxHelpers)
-    HB_RMIN = 16   // u64[16]: epilogue row minima (words 16-47)
-};
-// global words after the entries: batches finished, jobs published (idle helpers poll these two
-// words and scan the entries only when a job was published)
-enum { HBG_DONE = 0, HBG_PUB = 1 };
+// ---- jobs: a level's parent walks (its start list) and the per-target epilogue are jobs of
+// items the workgroup's waves take kJobChunk at a time (round 5 also let idle workgroups join them
+// through a help board: measured slower, removed in round 6 -- DESIGN.md 4 item 10)
 constexpr uint32_t kJobWalkSync = 1;  // first-level walks (groups of K lanes start together)
 constexpr uint32_t kJobWalk = 2;      // later levels
 constexpr uint32_t kJobEpi = 3;       // per-target epilogue
-constexpr uint32_t kJobChunk = 256;   // items a wave takes at a time from its workgroup's lease
-constexpr uint32_t kLeaseChunk = 4096; // items a workgroup claims on the board at a time
-constexpr uint32_t kMaxHelpers = 6;   // helping workgroups per entry (CAS traffic, S-list holes)
-constexpr unsigned long long kHbSpinTicks = 2000000000ull;  // 20 s at 100 MHz: a bound, not a wait
+constexpr uint32_t kJobChunk = 256;   // items a wave takes at a time
 constexpr uint32_t kJobNone = 0xFFFFFFFFu;
 constexpr uint32_t kNoPairS = 0xFFFFFFFFu;
-
-__device__ __forceinline__ unsigned long long hb_cur(const uint32_t* e) {
-    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(e + HB_CUR),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// claim up to c items of job `seq` (16 bits) on entry e: the first item, and *cnt items; kJobNone
-// when the job is used up or no longer the entry's
-__device__ __forceinline__ uint32_t hb_grab(uint32_t* e, uint32_t seq, uint32_t c, uint32_t* cnt) {
-    unsigned long long* p = reinterpret_cast<unsigned long long*>(e + HB_CUR);
-    unsigned long long old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-        if ((uint32_t)(old >> 48) != seq) return kJobNone;
-        const uint32_t n = (uint32_t)(old >> 24) & 0xFFFFFFu, x = (uint32_t)old & 0xFFFFFFu;
-        if (x >= n) return kJobNone;
-        const uint32_t t = min(c, n - x);
-        if (__hip_atomic_compare_exchange_strong(p, &old, old + t, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            *cnt = t;
-            return x;
-        }
-    }
-}
 
 }  // namespace
 
 // DIR: a directed topology (parents from the in-rows, DevCSR::rowptr_in); a separate
 // instantiation, so the undirected kernel's code and registers are those of round 5 before it.
-// BOARD: the help board compiled in (item 10).  Its code costs every batch registers: full table
-// 65.6-66.5 ms without, 67.0-67.6 with (same box); a one-round launch's idle slots helping its
-// last batches do not win that back (1,250 rows: 16.2-16.5 ms without, 16.5-16.7 with), so the
-// default launch is board-less (option share 0) and launch_batch_k picks the instantiation by
-// SlotWs.board.
-template <int K, bool DIR, bool BOARD>
+template <int K, bool DIR>
 __global__ void __launch_bounds__(kSsspBlock, kBatchWgPerCu)
 sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                   const double* __restrict__ srcsh, int nsrc, int kf,
@@ -1122,9 +987,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     const uint32_t pw = (uint32_t)((V + 31) / 32);  // word pairs of the pending / touched bits
     unsigned long long* const pt2 = reinterpret_cast<unsigned long long*>(D.pt);
     constexpr unsigned long long kPendBits = 0x5555555555555555ull;
-    // the pending-vertex lists (SHD_SWEEP_LIST), V entries each, after the two bitmaps' words
-    uint32_t* const plist0 = D.pt + 2 * (size_t)((V + 31) / 32 + 64);
-    uint32_t* const plist1 = plist0 + V;
     const uint32_t pcap = (uint32_t)(V * K);
 
     uint32_t iter = ctr[0];
@@ -1150,10 +1012,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     };
 
     if (tid == 0) {
-        L.jseq = 0;
         L.jcur = 0;
-        L.jtaken = 0;
-        L.hitems[0] = L.hitems[1] = 0;
         L.fover = 0;
     }
     const uint32_t lane = tid & 63u;
@@ -1167,70 +1026,24 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         unsigned long long d;
     };
 
-    // One job of slot o: walks of a level's start list (kJobWalkSync /
-    // kJobWalk) or the per-target epilogue (kJobEpi) of the batch {tag epv, positions r0v..,
-    // nkv sources}; every wave claims kJobChunk items at a time until the job is used up.  The
-    // owner and helping workgroups run the same code; L.src holds the job's sources.  Adds this
-    // workgroup's claimed items to L.jtaken.
-    auto run_job = [&](uint32_t o, uint32_t seq, uint32_t kind, uint32_t n, uint32_t epv,
-                       uint32_t r0v, uint32_t nkv, uint32_t list) {
-        const bool shared = BOARD && ws.board != nullptr;
-        uint32_t* const eo = shared ? ws.board + (size_t)o * kBoardWords : nullptr;
-        unsigned long long* const distO = ws.dist + (size_t)o * (size_t)V * K;
-        uint4* const precO = ws.prec + (size_t)o * (size_t)V * K;
-        uint32_t* const precwO = reinterpret_cast<uint32_t*>(precO);
+    // One job of this slot: walks of a level's start list (kJobWalkSync / kJobWalk) or the
+    // per-target epilogue (kJobEpi) of the batch {tag epv, positions r0v.., nkv sources}; every
+    // wave claims kJobChunk items at a time until the job is used up (L.jcur, reset by the
+    // caller).  L.src holds the batch's sources.
+    auto run_job = [&](uint32_t kind, uint32_t n, uint32_t epv, uint32_t r0v, uint32_t nkv,
+                       uint32_t list) {
+        unsigned long long* const distO = D.dist;
+        uint4* const precO = prec;
+        uint32_t* const precwO = precw;
         const uint32_t eptv = epv | kTagClaim;
-        uint32_t taken = 0;
-        // a lease leaves room for helpers on a small job: an eighth of it, 256 .. kLeaseChunk
-        const uint32_t lease_chunk = min(kLeaseChunk, max(kJobChunk, (n / 8u + kJobChunk - 1u) / kJobChunk * kJobChunk));
-        // The wave's next chunk of the job: its first item (kJobNone: used up) and *cnt items.
-        // Board launches: waves take kJobChunk items from the workgroup's lease (LDS); the wave
-        // that finds it used up refills it by one CAS on the board (kLeaseChunk items, counted
-        // in L.jtaken: the workgroup processes every leased item) while the others wait.
+        // the wave's next chunk of the job: its first item (kJobNone: used up) and *cnt items
         auto grab = [&](uint32_t* cnt) -> uint32_t {
             uint32_t b = kJobNone, c = 0;
             if (lane == 0) {
-                if (shared) {
-                    for (;;) {
-                        const unsigned long long x = atomicAdd(&L.lease, (unsigned long long)kJobChunk);
-                        const uint32_t nx = (uint32_t)x, en = (uint32_t)(x >> 32);
-                        if (nx < en) {
-                            b = nx;
-                            c = min(kJobChunk, en - nx);
-                            break;
-                        }
-                        if (__hip_atomic_load(&L.ljdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-                        if (atomicCAS(&L.lrefill, 0u, 1u) == 0u) {
-                            // another wave may have installed a fresh lease between our look
-                            // and the lock: refill only a lease still used up
-                            const unsigned long long y = __hip_atomic_load(
-                                &L.lease, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            if ((uint32_t)y < (uint32_t)(y >> 32)) {
-                                __hip_atomic_store(&L.lrefill, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                continue;
-                            }
-                            uint32_t gc = 0;
-                            const uint32_t gb = hb_grab(eo, seq, lease_chunk, &gc);
-                            if (gb == kJobNone) {
-                                __hip_atomic_store(&L.ljdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            } else {
-                                atomicAdd(&L.jtaken, gc);
-                                b = gb;
-                                c = min(kJobChunk, gc);
-                                atomicExch(&L.lease, ((unsigned long long)(gb + gc) << 32) | (gb + c));
-                            }
-                            __hip_atomic_store(&L.lrefill, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            break;
-                        }
-                        while (__hip_atomic_load(&L.lrefill, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))
-                            __builtin_amdgcn_s_sleep(1);
-                    }
-                } else {
-                    const uint32_t x = atomicAdd(&L.jcur, kJobChunk);
-                    if (x < n) {
-                        b = x;
-                        c = min(kJobChunk, n - x);
-                    }
+                const uint32_t x = atomicAdd(&L.jcur, kJobChunk);
+                if (x < n) {
+                    b = x;
+                    c = min(kJobChunk, n - x);
                 }
             }
             *cnt = __shfl(c, 0, 64);
@@ -1245,9 +1058,8 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             // own hop inputs serve the next hop).  Flattened: a lane takes its next start pair as
             // soon as its chain ends.  The first level keeps a target's K lanes together (a group
             // takes its next start pairs when the whole group is idle).
-            const uint32_t* P = reinterpret_cast<const uint32_t*>((list ? ws.qb : ws.qa) +
-                                                                  (size_t)o * ws.q_stride);
-            uint32_t* const S = reinterpret_cast<uint32_t*>(ws.ring) + (size_t)o * ws.ring_entries;
+            const uint32_t* P = list ? qb : qa;
+            uint32_t* const S = fscr;
             const uint32_t pcapS = (uint32_t)(V * K);
             const bool gs = kind == kJobWalkSync;
             auto put = [&](uint32_t q, uint32_t u, double loss) {
@@ -1274,7 +1086,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             };
             uint32_t i = 0, iend = 0, q = 0, j = 0;
             uint32_t nw = 0, nw0 = 0;   // walk steps, of which certified by the tree guess
-            uint32_t sb = 0, se = 0;    // the wave's reserved block of the S list (help board)
             bool act = false, fresh = false, more = true;
             Hop h;
             h.sp = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
@@ -1289,7 +1100,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     } else {
                         i = b + lane;
                         iend = b + c;
-                        taken += c;
                     }
                 }
                 bool take = !act && i < iend;
@@ -1347,28 +1157,13 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         }
                     }
                 }
-                // this round's S pairs, wave-aggregated: board launches reserve blocks of 64
-                // entries of the slot's S list (a block's unused entries are holes, kNoPairS)
+                // this round's S pairs, wave-aggregated
                 const unsigned long long m = __ballot(sp);
                 if (m) {
                     const uint32_t need = (uint32_t)__popcll(m);
-                    uint32_t base;
-                    if (shared) {
-                        if (se - sb < need) {
-                            if (lane < se - sb && sb + lane < pcapS) S[sb + lane] = kNoPairS;
-                            uint32_t nb = 0;
-                            if (lane == 0) nb = atomicAdd(eo + HB_SCNT, 64u);
-                            nb = __shfl(nb, 0, 64);
-                            sb = nb;
-                            se = nb + 64u;
-                        }
-                        base = sb;
-                        sb += need;
-                    } else {
-                        uint32_t x = 0;
-                        if (lane == 0) x = atomicAdd(&L.qtail, need);
-                        base = __shfl(x, 0, 64);
-                    }
+                    uint32_t x = 0;
+                    if (lane == 0) x = atomicAdd(&L.qtail, need);
+                    const uint32_t base = __shfl(x, 0, 64);
                     if (sp) {
                         const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                         wl_count(L, WL_QUEUE, pos < pcapS, S + pos);
@@ -1377,7 +1172,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     }
                 }
             }
-            if (shared && lane < se - sb && sb + lane < pcapS) S[sb + lane] = kNoPairS;
             const unsigned long long s0 = wave_sum_u64(nw), s1 = wave_sum_u64(nw0);
             if (lane == 0) {
                 atomicAdd(&L.wk[0], s0);
@@ -1394,16 +1188,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             auto pb_at = [&](uint32_t x) -> double* {
                 return x < nl ? lpb + (size_t)x * kSsspBlock + tid : pbuf + (size_t)x * kSsspBlock + tid;
             };
-            unsigned long long* const rminP =
-                shared ? reinterpret_cast<unsigned long long*>(eo + HB_RMIN) : L.rmin;
+            unsigned long long* const rminP = L.rmin;
             for (;;) {
                 uint32_t c;
                 const uint32_t b = grab(&c);
                 if (b == kJobNone) break;
-                taken += c;
                 for (uint32_t i = b + lane; i < b + c; i += 64) {
-                    const uint32_t jj = SHD_TGT_MAJOR ? i % nkv : i / (uint32_t)A;
-                    const uint32_t k = SHD_TGT_MAJOR ? i / nkv : i - jj * (uint32_t)A;
+                    const uint32_t jj = i % nkv;  // target-major: a target's sources adjacent
+                    const uint32_t k = i / nkv;
                     rl_count(L, RL_EPI, true, targets + k);
                     const uint32_t t = targets[k];
                     const uint32_t src = L.src[jj];
@@ -1474,20 +1266,16 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     const uint16_t hh = (uint16_t)(hcnt > 65535u ? 65535u : hcnt);
                     wl_count(L, WL_OUT, true, out_lr + ob);
                     wl_count(L, WL_OUT, true, out_hops + ob);
-                    if (SHD_OUT_NT) {  // the table (1.8 GB per launch) is not re-read by the kernel
+                    {  // the table (1.8 GB per launch) is not re-read by the kernel: nontemporal
                         typedef double f64x2 __attribute__((ext_vector_type(2)));
                         const f64x2 r2 = {lat, rel};
                         __builtin_nontemporal_store(r2, reinterpret_cast<f64x2*>(out_lr) + ob);
                         __builtin_nontemporal_store(hh, out_hops + ob);
-                    } else {
-                        out_lr[ob] = make_double2(lat, rel);
-                        out_hops[ob] = hh;
                     }
                     if (lat >= 0.0) atomicMin(&rminP[jj], d2bits(lat));  // row minimum (runahead)
                 }
             }
         }
-        if (!shared && lane == 0 && taken) atomicAdd(&L.jtaken, taken);
     };
 
     for (;;) {
@@ -1538,9 +1326,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         if (tid == 0) {
             L.fminb = kNoBucket;
             L.fover = 0;
-            L.plen = 0;
-            L.plen2 = 0;
-            L.plsel = 0;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1551,7 +1336,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             else {
                 D.dist[(size_t)s * K + tid] = 0ull;
                 atomicOr(&D.pt[s >> 4], 3u << (2u * (s & 15u)));
-                if (SHD_SWEEP_LIST) plist0[atomicAdd(&L.plen, 1u)] = s;  // distinct sources
             }
             atomicMin(&L.fminb, bkt(0.0, L.sh[tid], B.inv_delta));
         }
@@ -1593,14 +1377,12 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 if (tid == 0) L.ev[2] += ns;
                 const unsigned long long e0 = L.cnt[2], a0 = L.cnt[0];
                 const bool first_it = guard == 0 || just_swept;
-#ifndef SHD_BATCH_NOWAVE
                 if (!hubs)
-                    relax_batch_t<K, SHD_BATCH_U, true>(src, ns, g, L, D, mcur, hdef, mnxt, qout,
-                                                        cap, hfill, B, L.plsel ? plist1 : plist0);
+                    relax_batch_t<K, kBatchU, true>(src, ns, g, L, D, mcur, hdef, mnxt, qout,
+                                                    cap, hfill, B);
                 else
-#endif
-                    relax_batch_t<K, SHD_BATCH_U>(src, ns, g, L, D, mcur, hdef, mnxt, qout, cap,
-                                                  hfill, B, L.plsel ? plist1 : plist0);
+                    relax_batch_t<K, kBatchU>(src, ns, g, L, D, mcur, hdef, mnxt, qout, cap,
+                                              hfill, B);
                 nq = min(L.qtail, cap);
                 if (tid == 0 && first_it) {
                     L.dg[2] += L.cnt[2] - e0;
@@ -1635,10 +1417,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 static_assert(K >= 2 && 64 % (K / 2) == 0, "lanes per vertex");
                 constexpr uint32_t LPV = K / 2;
                 const size_t hpair = (size_t)H * K / 2;
-#ifndef SHD_SWEEP_SU
-#define SHD_SWEEP_SU 8  // 8 > 4 by 0.3 % (sweeps 1.47 -> 1.44 ms/source), 2: +0.8 %
-#endif
-                constexpr int SU = SHD_SWEEP_SU;  // 16-B loads in flight per lane
+                constexpr int SU = 8;  // 16-B loads in flight per lane (8 > 4 by 0.3 %, 2: +0.8 %)
                 // hubs: every (hub, source) word of LDS
                 for (size_t ib = 0; ib < hpair; ib += (size_t)kSsspBlock * SU) {
                     unsigned long long d[SU][2];
@@ -1676,110 +1455,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     km = wave_min_u32(km);
                     if ((tid & 63) == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
                 }
-#if SHD_SWEEP_LIST
-                // tail: the pending-vertex list (every tail vertex whose pending bit is set, once:
-                // a relaxation appends a vertex when its first reach past cb sets the bit).  Each
-                // wave takes chunks of the list into its LDS slice (the chunk buffers are idle
-                // here), classifies their lines (LPV lanes x 16 B per vertex), appends the
-                // vertices that still hold a pair past nb to the next list and clears the others'
-                // pending bits.  Round 5: the bitmap version below read all V / 16 bitmap words
-                // per sweep, one round trip per 128 word pairs per wave.
-                {
-                    constexpr uint32_t NW = kSsspBlock / 64;
-                    constexpr uint32_t VPW = 64 / LPV;  // vertices per wave instruction
-                    constexpr uint32_t kKeep = 0x80000000u;  // slice entry: the vertex stays pending
-                    constexpr uint32_t kSweepU32 =
-                        (uint32_t)((offsetof(LdsB<K>, val) + sizeof(L.val) - offsetof(LdsB<K>, off)) / 4);
-                    constexpr uint32_t kClW = kSweepU32 / NW;
-                    constexpr uint32_t kCh = kClW / 64u * 64u;  // list entries per wave chunk
-                    static_assert(kCh >= 64, "sweep slice");
-                    const uint32_t wv = tid >> 6, lane = tid & 63u;
-                    uint32_t* clw = L.off + wv * kClW;
-                    const uint32_t np = min(L.plen, cap);
-                    const uint32_t* psrc = L.plsel ? plist1 : plist0;
-                    uint32_t* pdst = L.plsel ? plist0 : plist1;
-                    for (uint32_t base = wv * kCh; base < np; base += NW * kCh) {
-                        const uint32_t n = min(kCh, np - base);
-                        for (uint32_t i = lane; i < n; i += 64) {
-                            rl_count(L, RL_SWEEP, true, psrc + base + i);
-                            clw[i] = ld_l2_u32(psrc + base + i);
-                        }
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        __builtin_amdgcn_wave_barrier();
-                        for (uint32_t vb = 0; vb < n; vb += VPW * SU) {
-                            unsigned long long d[SU][2];
-                            uint32_t vv[SU];
-                            float k0[SU];
-#pragma unroll
-                            for (int u = 0; u < SU; u++) {
-                                const uint32_t e = vb + (uint32_t)u * VPW + lane / LPV;
-                                vv[u] = e < n ? clw[e] : 0xFFFFFFFFu;
-                                rl_count(L, RL_SWEEP, e < n, reinterpret_cast<const char*>(D.dist) + ((size_t)(e < n ? vv[u] : 0u) * LPV + lane % LPV) * 16);
-                                rl_count(L, RL_SWEEP, e < n, g.kap0 + (e < n ? vv[u] : 0u));
-                                k0[u] = g.kap0[e < n ? vv[u] : 0u];
-                                d[u][0] = d[u][1] = kInfBits;
-                                if (e < n) {
-                                    typedef unsigned long long u64x2
-                                        __attribute__((ext_vector_type(2)));
-                                    const u64x2 x = __builtin_nontemporal_load(
-                                        reinterpret_cast<const u64x2*>(D.dist) +
-                                        (size_t)vv[u] * LPV + lane % LPV);
-                                    d[u][0] = x.x;
-                                    d[u][1] = x.y;
-                                }
-                            }
-                            uint32_t km = kNoBucket;
-#pragma unroll
-                            for (int u = 0; u < SU; u++) {
-                                const uint32_t jl = 2 * (lane % LPV);
-                                uint32_t m = 0, keep = 0;
-#pragma unroll
-                                for (int h = 0; h < 2; h++) {
-                                    if (d[u][h] == kInfBits) continue;
-                                    const uint32_t b = bkt(bits2d(d[u][h]), L.sh[jl + h], B.inv_delta);
-                                    if (b == nb) {
-                                        if (kappa_useful(k0[u], L.dh0[jl + h], bits2d(d[u][h]), g.piMax))
-                                            m |= 1u << (jl + h);
-                                    } else if (b > nb) {
-                                        keep = 1u;
-                                        if (b < km) km = b;
-                                    }
-                                }
-#pragma unroll
-                                for (uint32_t o = 1; o < LPV; o <<= 1) {
-                                    m |= __shfl_xor(m, (int)o, 64);
-                                    keep |= __shfl_xor(keep, (int)o, 64);
-                                }
-                                const uint32_t v = vv[u];
-                                const uint32_t e = vb + (uint32_t)u * VPW + lane / LPV;
-                                const bool ok = (lane % LPV) == 0 && v != 0xFFFFFFFFu;
-                                const bool lead = ok && m != 0u;
-                                wl_count(L, WL_MASK_ST, lead, mcur + (lead ? v : 0u));
-                                if (lead) mcur[v] = (M)m;
-                                if (ok && keep) clw[e] = v | kKeep;
-                                wpush<K>(L, lead, v, qin, &L.qtail, cap, &L.fover, 32u);
-                            }
-                            km = wave_min_u32(km);
-                            if (lane == 0 && km != kNoBucket) atomicMin(&L.fminb, km);
-                        }
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        __builtin_amdgcn_wave_barrier();
-                        // survivors to the next list; the others leave the pending set
-                        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-                            const uint32_t i = i0 + lane;
-                            const uint32_t x = i < n ? clw[i] : 0u;
-                            const bool keep = i < n && (x & kKeep);
-                            const uint32_t v = x & ~kKeep;
-                            wpush<K>(L, keep, v, pdst, &L.plen2, cap, &L.fover, 64u);
-                            wl_count(L, WL_PEND_ST, i < n && !keep, D.pt + (v >> 4));
-                            if (i < n && !keep) atomicAnd(&D.pt[v >> 4], ~(1u << (2u * (v & 15u))));
-                        }
-                        // the slice is refilled by the next chunk
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                }
-#else
                 // tail: only the vertices whose pending bit is set (~9 % of them per sweep on
                 // C4, instead of streaming all [V][K] rows).  A round takes one bitmap word per
                 // thread, compacts the set bits' vertices into LDS (the chunk buffers are idle
@@ -1791,10 +1466,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 // sweep ends.  ~1.7 % of the vertices are pending per sweep, so a block of 64
                 // word pairs yields ~35 vertices; SG blocks share one round trip of line loads.
                 {
-#ifndef SHD_SWEEP_G
-#define SHD_SWEEP_G 2  // 2: -2.9 % full table; 4 spills (+4 %)
-#endif
-                    constexpr uint32_t SG = SHD_SWEEP_G;  // word pairs per lane and block
+                    constexpr uint32_t SG = 2;  // word pairs per lane and block (2: -2.9 %; 4 spills)
                     constexpr uint32_t NW = kSsspBlock / 64;
                     constexpr uint32_t VPW = 64 / LPV;  // vertices per wave instruction
                     constexpr uint32_t kKeep = 0x80000000u;  // slice entry: the vertex stays pending
@@ -1935,17 +1607,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         }
                     }
                 }
-#endif
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             nq = min(L.qtail, cap);
             if (tid == 0) L.cnt[1] += nq;
-            if (SHD_SWEEP_LIST && tid == 0) {  // the survivors' list is the current one
-                L.plen = min(L.plen2, cap);
-                L.plen2 = 0;
-                L.plsel ^= 1u;
-            }
             B.cb = nb;
             just_swept = true;
             if (tid == 0) {
@@ -1973,68 +1639,24 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         // parent(v) = argmin d_j[u] over the candidates fl(d_j[u] + w) == d_j[v]).  A level's walks
         // certify most parents without scanning (h0-tree guess); the rest get the hint pass and a
         // merged row scan; their parents start the next level.  Each level's walks and the
-        // epilogue are jobs of the slot's help-board entry (run_job): idle workgroups join them.
+        // epilogue are jobs (run_job) the workgroup's waves take in chunks.
         if ((int)tid < nk) L.src[tid] = sources[r0 + tid];
         const uint32_t ept = ep | kTagClaim;  // tag word of a resolved / claimed pair record
-        const bool shared = BOARD && ws.board != nullptr;
-        uint32_t* const my_e = shared ? ws.board + (size_t)slot * kBoardWords : nullptr;
-        // Publish a job on this slot's entry (every wave's earlier stores drained first: the hub
-        // rows, the start list, the pair records), and after taking part, wait until every
-        // claimed item is done (helpers add theirs after a release fence), then acquire.
-        auto job_publish = [&](uint32_t kind, uint32_t n, uint32_t list) -> uint32_t {
+        // A job starts once every wave's earlier stores are drained (the hub rows, the start
+        // list, the pair records), and ends when every wave's stores are.
+        auto job_start = [&](uint32_t kind) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) {
-                L.jseq = (L.jseq + 1u) & 0xFFFFu;
-                if (L.jseq == 0u) L.jseq = 1u;
-                L.jtaken = 0;
                 L.jcur = 0;
                 L.qtail = 0;
-                L.lease = 0ull;
-                L.lrefill = 0;
-                L.ljdone = 0;
-                if (shared) {
-                    __hip_atomic_store(my_e + HB_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(my_e + HB_SEQ, L.jseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(my_e + HB_KIND, kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(my_e + HB_EP, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(my_e + HB_R0, (uint32_t)r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(my_e + HB_NK, (uint32_t)nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(my_e + HB_LIST, list, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(my_e + HB_SCNT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (kind == kJobEpi)
-                        for (int jj = 0; jj < K; jj++)
-                            __hip_atomic_store(reinterpret_cast<unsigned long long*>(my_e + HB_RMIN) + jj,
-                                               kInfBits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_store(reinterpret_cast<unsigned long long*>(my_e + HB_CUR),
-                                       ((unsigned long long)L.jseq << 48) | ((unsigned long long)n << 24),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    atomicAdd(ws.board + (size_t)gridDim.x * kBoardWords + HBG_PUB, 1u);
-                } else if (kind == kJobEpi) {
+                if (kind == kJobEpi)
                     for (int jj = 0; jj < K; jj++) L.rmin[jj] = kInfBits;
-                }
             }
             __syncthreads();
-            return L.jseq;
         };
-        auto job_finish = [&](uint32_t n) {
+        auto job_end = [&]() {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (shared && tid == 0) {
-                atomicAdd(my_e + HB_DONE, L.jtaken);
-                const unsigned long long t0 = wall_clock64();
-                while (ld_l2_u32(my_e + HB_DONE) < n) {
-                    __builtin_amdgcn_s_sleep(4);
-                    if (wall_clock64() - t0 > kHbSpinTicks) {
-                        atomicAdd(&stats[ST_HB_ERR], 1ull);
-                        break;
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
             __syncthreads();
         };
         // the hub distances move to their (otherwise unused) rows of the [V][K] block: the walks
@@ -2048,7 +1670,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         uint32_t* pcur = qa;
         uint32_t* pnxt = qb;
         uint32_t plist = 0;  // pcur is qa (0) or qb (1)
-#if SHD_TGT_MAJOR
         // Target-major start list, K entries per target (kNoPair for the sources past nk and a
         // target that is the source): a target's chains for the K sources share their tail part
         // (the h0-tree guess is source-independent), so the K lanes of an aligned group walk the
@@ -2064,23 +1685,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         }
         uint32_t nF = (uint32_t)A * K;
         uint32_t wkind = kJobWalkSync;
-#else
-        for (uint32_t ib = 0; ib < (uint32_t)A * (uint32_t)nk; ib += kSsspBlock) {
-            const uint32_t i = ib + tid;
-            bool p = false;
-            uint32_t q = 0;
-            if (i < (uint32_t)A * (uint32_t)nk) {
-                const uint32_t j = i / (uint32_t)A;
-                const uint32_t t = targets[i - j * (uint32_t)A];
-                q = t * K + j;
-                p = t != L.src[j];
-            }
-            wpush<K>(L, p, q, pcur, &L.qtail, pcap, &L.fover, 128u);
-        }
-        __syncthreads();
-        uint32_t nF = min(L.qtail, pcap);
-        uint32_t wkind = kJobWalk;
-#endif
         // A pair's record: its parent, the batch's tag, the loss of the parent edge (one store)
         auto put = [&](uint32_t q, uint32_t u, double loss) {
             const unsigned long long lb = d2bits(loss);
@@ -2105,7 +1709,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             for (int h = 0; h < kHP; h++) {
                 const uint32_t i = ib + (uint32_t)h * kSsspBlock + tid;
                 q[h] = i < nS ? S[i] : kNoPairS;
-                has[h] = q[h] != kNoPairS;  // a hole of the S list (board launches)
+                has[h] = q[h] != kNoPairS;
                 qo[h] = q[h];
                 if (!has[h]) q[h] = 0u;
                 const uint32_t v = q[h] / K, j = q[h] % K;
@@ -2132,7 +1736,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 if (has[h] && g.rows_sorted) {
                     if (v >= H) {
                         const uint32_t u = rw[h].x & 0x3FFFFFFFu;
-                        if (SHD_TAIL_HINT && !tag_tied(rw[h].y, ep) && u < (uint32_t)V && u != v) {
+                        if (!tag_tied(rw[h].y, ep) && u < (uint32_t)V && u != v) {
                             live[h] = true;
                             uu[h] = u;
                             key[h] = u;
@@ -2186,13 +1790,11 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         while (nF > 0) {
             if (tid == 0) L.ev[3] += nF;
             unsigned long long tp0 = wall_clock64();
-            {
-                const uint32_t seq = job_publish(wkind, nF, plist);
-                run_job((uint32_t)slot, seq, wkind, nF, ep, (uint32_t)r0, (uint32_t)nk, plist);
-                job_finish(nF);
-            }
-            // the S list (pairs whose guess failed), with holes (kNoPairS) on a board launch
-            const uint32_t nS = min(shared ? ld_l2_u32(my_e + HB_SCNT) : L.qtail, pcap);
+            job_start(wkind);
+            run_job(wkind, nF, ep, (uint32_t)r0, (uint32_t)nk, plist);
+            job_end();
+            // the S list (pairs whose guess failed)
+            const uint32_t nS = min(L.qtail, pcap);
             __syncthreads();
             if (tid == 0) L.pt[1] += wall_clock64() - tp0;  // walks
             if (nS == 0) break;
@@ -2389,28 +1991,18 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
         if (ws.btrace && tid == 0) ws.btrace[kBTraceWords * (size_t)bidx + 9] = L.tk;
 
         // ---------------- per-target latency / reliability / hops (shd-topology.c:561-671) ----
-        // items (source j, target k) of the whole batch: a job (run_job), so idle workgroups take
-        // part; the row minima come back through the board entry (or L.rmin)
-        {
-            const uint32_t ni = (uint32_t)A * (uint32_t)nk;
-            const uint32_t seq = job_publish(kJobEpi, ni, 0u);
-            run_job((uint32_t)slot, seq, kJobEpi, ni, ep, (uint32_t)r0, (uint32_t)nk, 0u);
-            job_finish(ni);
-        }
+        // items (source j, target k) of the whole batch: a job (run_job); row minima in L.rmin
+        job_start(kJobEpi);
+        run_job(kJobEpi, (uint32_t)A * (uint32_t)nk, ep, (uint32_t)r0, (uint32_t)nk, 0u);
+        job_end();
         if ((int)tid < nk) {
-            const unsigned long long rm =
-                shared ? __hip_atomic_load(reinterpret_cast<const unsigned long long*>(my_e + HB_RMIN) + tid,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                       : L.rmin[tid];
+            const unsigned long long rm = L.rmin[tid];
             if (out_rowmin) out_rowmin[ws.rowmap ? (int)ws.rowmap[r0 + tid] : r0 + (int)tid] = bits2d(rm);
             atomicMin(&stats[ST_GLOBAL_MIN], rm);  // shd-topology.c:500-511
         }
         __syncthreads();
         tick(3);
         if (ws.btrace && tid == 0) ws.btrace[kBTraceWords * (size_t)bidx + 10] = L.tk;
-        // the batch's rows are complete (every job's items done): one more finished batch for the
-        // helpers' exit condition
-        if (shared && tid == 0) atomicAdd(ws.board + (size_t)gridDim.x * kBoardWords + HBG_DONE, 1u);
         {
             // the distance lines this batch lowered from +inf back to +inf: only touched tail
             // vertices (their touched bit in D.pt), not the whole [V][K] block (64 MB at K = 8 per
@@ -2449,8 +2041,7 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         const uint32_t v = wv * 32u + ((uint32_t)__ffsll((long long)w) - 1u) / 2u;
                         w &= w - 1ull;
                         wl_count(L, WL_RESET, true, d2 + (size_t)v * G + part);
-                        if (SHD_INIT_NT) __builtin_nontemporal_store(inf2, d2 + (size_t)v * G + part);
-                        else d2[(size_t)v * G + part] = inf2;
+                        __builtin_nontemporal_store(inf2, d2 + (size_t)v * G + part);
                     }
                 }
             }
@@ -2466,137 +2057,6 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
             b[5] = L.ev[2] - b[5];
             b[6] = L.cnt[0] - b[6];
             b[7] = (unsigned long long)nk;
-        }
-    }
-    // ---------------- no batch left for this slot: help the running batches' jobs -------------
-    // A workgroup scans the board for the job with the most unclaimed items, acquires the owner's
-    // data, takes chunks of it (run_job), releases its own stores and adds its items to the job's
-    // done count; it stops when every batch of the launch is finished.  The scan is one wave's
-    // relaxed loads; an idle scan sleeps.
-    if (BOARD && ws.board) {
-        const unsigned long long th0 = wall_clock64();
-        const uint32_t nbat = ws.bstart ? (uint32_t)ws.nbat : (uint32_t)((nsrc + kf - 1) / kf);
-        const uint32_t* const gw = ws.board + (size_t)gridDim.x * kBoardWords;
-        unsigned long long tprog = th0;  // (thread 0) the last progress seen
-        uint32_t lastDone = 0, lastPub = 0xFFFFFFFFu;
-        bool rescan = true;  // (thread 0) scan the entries in the next round
-        for (;;) {
-            // thread 0: finished batches and published jobs (two words); the entries only when a
-            // job was published since the last scan, or after a scan found a job to join
-            if (tid == 0) {
-                L.hjob = kJobNone;
-                const uint32_t dn = ld_l2_u32(gw + HBG_DONE), pb = ld_l2_u32(gw + HBG_PUB);
-                L.hflag = dn >= nbat ? 1u : 0u;
-                if (pb != lastPub) rescan = true;
-                lastPub = pb;
-                const unsigned long long t = wall_clock64();
-                if (dn != lastDone) {
-                    lastDone = dn;
-                    tprog = t;
-                } else if (t - tprog > kHbSpinTicks) {
-                    atomicAdd(&stats[ST_HB_ERR], 1ull);
-                    L.hflag = 1u;
-                }
-                L.hd[7] = rescan ? 1u : 0u;
-            }
-            __syncthreads();
-            if (L.hflag) break;
-            if (L.hd[7] && tid < 64) {
-                // the entry with the most unclaimed items among those with room for a helper
-                uint32_t bo = kJobNone, brem = 0;
-                unsigned long long bc = 0;
-                for (uint32_t o = tid; o < gridDim.x; o += 64) {
-                    if (o == (uint32_t)slot) continue;
-                    const uint32_t* e = ws.board + (size_t)o * kBoardWords;
-                    const unsigned long long c = hb_cur(e);
-                    const uint32_t n = (uint32_t)(c >> 24) & 0xFFFFFFu, x = (uint32_t)c & 0xFFFFFFu;
-                    uint32_t rem = (c >> 48) != 0ull && x < n ? n - x : 0u;
-                    if (rem && ld_l2_u32(e + HB_HELP) >= kMaxHelpers) rem = 0;
-                    if (rem > brem) {
-                        brem = rem;
-                        bo = o;
-                        bc = c;
-                    }
-                }
-#pragma unroll
-                for (int d = 32; d > 0; d >>= 1) {
-                    const uint32_t r2 = __shfl_xor(brem, d, 64), o2 = __shfl_xor(bo, d, 64);
-                    const unsigned long long c2 = __shfl_xor(bc, d, 64);
-                    if (r2 > brem || (r2 == brem && o2 < bo)) {
-                        brem = r2;
-                        bo = o2;
-                        bc = c2;
-                    }
-                }
-                if (tid == 0) {
-                    if (brem) {
-                        // join it unless the helpers' cap was reached meanwhile
-                        uint32_t* e = ws.board + (size_t)bo * kBoardWords;
-                        if (atomicAdd(e + HB_HELP, 1u) < kMaxHelpers) {
-                            L.hjob = bo;
-                            L.hd[0] = (uint32_t)(bc >> 48);
-                            L.hd[2] = (uint32_t)(bc >> 24) & 0xFFFFFFu;
-                        } else {
-                            atomicSub(e + HB_HELP, 1u);
-                        }
-                    }
-                    rescan = brem != 0;  // found one: look again right after it
-                }
-            }
-            __syncthreads();
-            const uint32_t o = L.hjob;
-            if (o == kJobNone) {
-                if (tid == 0) {
-                    __builtin_amdgcn_s_sleep(127);
-                    __builtin_amdgcn_s_sleep(127);
-                }
-                continue;  // (the loop head's barrier)
-            }
-            // acquire the owner's data (its stores precede the cursor store we read), then its
-            // descriptor; a descriptor of another job than the cursor's: scan again
-            uint32_t* const eo = ws.board + (size_t)o * kBoardWords;
-            if (tid == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const uint32_t sq = ld_l2_u32(eo + HB_SEQ);
-                L.hd[1] = ld_l2_u32(eo + HB_KIND);
-                L.hd[3] = ld_l2_u32(eo + HB_EP);
-                L.hd[4] = ld_l2_u32(eo + HB_R0);
-                L.hd[5] = ld_l2_u32(eo + HB_NK);
-                L.hd[6] = ld_l2_u32(eo + HB_LIST);
-                L.hd[7] = sq == L.hd[0] && L.hd[5] >= 1u && L.hd[5] <= (uint32_t)K ? 1u : 0u;
-                L.jtaken = 0;
-                L.lease = 0ull;
-                L.lrefill = 0;
-                L.ljdone = 0;
-            }
-            __syncthreads();
-            const uint32_t hseq = L.hd[0], hkind = L.hd[1], hn = L.hd[2], hep = L.hd[3];
-            const uint32_t hr0 = L.hd[4], hnk = L.hd[5], hlist = L.hd[6];
-            if (L.hd[7]) {
-                if (tid < hnk) L.src[tid] = sources[hr0 + tid];
-                __syncthreads();
-                run_job(o, hseq, hkind, hn, hep, hr0, hnk, hlist);
-            }
-            // release this workgroup's stores (records, S entries, table rows), then count them
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) {
-                if (L.jtaken) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    atomicAdd(eo + HB_DONE, L.jtaken);
-                    L.hitems[hkind == kJobEpi ? 1 : 0] += L.jtaken;
-                }
-                atomicSub(eo + HB_HELP, 1u);
-                tprog = wall_clock64();
-            }
-            __syncthreads();
-        }
-        if (tid == 0) {
-            atomicAdd(&stats[ST_T_HELP], wall_clock64() - th0);
-            atomicAdd(&stats[ST_HELP_ITEMS], L.hitems[0]);
-            atomicAdd(&stats[ST_HELP_ITEMS + 1], L.hitems[1]);
         }
     }
     __syncthreads();
@@ -2944,18 +2404,12 @@ static hipError_t launch_batch_k(const DevCSR& g, const SlotWs& ws, const uint32
     if (kf < 1 || kf > K) return hipErrorInvalidValue;
     // (a layout's batches are checked on the host: each within 1..K positions, covering [0, nsrc))
     const int nb = ws.bstart ? ws.nbat : (nsrc + kf - 1) / kf;
-    // with the help board every slot runs: the ones without a batch help the others' jobs
-    const int grid = ws.board ? ws.slots : (ws.slots < nb ? ws.slots : nb);
+    const int grid = ws.slots < nb ? ws.slots : nb;
     if (grid < 1) return hipSuccess;
     if ((int64_t)plan.H > g.V || plan.P > plan.H || plan.bytes > kBMaxLds ||
         blayout<K>(plan.H, plan.P).bytes != plan.bytes || ws.K != K)
         return hipErrorInvalidValue;
-    // the board-less instantiation exists for the default width only (K != 8: the board code is
-    // compiled in and off at run time when ws.board is null)
-    auto* kern = g.directed ? (ws.board || K != 8 ? sssp_batch_kernel<K, true, true>
-                                                  : sssp_batch_kernel<K, true, K != 8>)
-                            : (ws.board || K != 8 ? sssp_batch_kernel<K, false, true>
-                                                  : sssp_batch_kernel<K, false, K != 8>);
+    auto* kern = g.directed ? sssp_batch_kernel<K, true> : sssp_batch_kernel<K, false>;
     {  // per device (multi-GPU builds launch on several): set before every launch
         hipError_t e = hipFuncSetAttribute((const void*)kern,
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2984,7 +2438,7 @@ hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uin
 
 hipError_t preload_batch_module() {
     hipFuncAttributes a;
-    return hipFuncGetAttributes(&a, (const void*)sssp_batch_kernel<8, false, false>);
+    return hipFuncGetAttributes(&a, (const void*)sssp_batch_kernel<8, false>);
 }
 
 }  // namespace shdtopo

@@ -61,8 +61,6 @@ for rep in range(args.reps):
           tuple(x / rows for x in st["parent_phase_ms"]), flush=True)
     print("   walk steps/src %.0f, walk kinds %s" % (st["walk_steps"] / rows, list(st["walk_kinds"])),
           flush=True)
-    print("   help: %.2f ms summed, items walks %d epilogue %d, board errors %d" % (
-        st["help_ms"], st["help_items"][0], st["help_items"][1], st["help_board_errors"]), flush=True)
     print("   target prep %.2f ms (%d kappa iterations)" % (st["target_prep_ms"],
                                                          st["target_kappa_iters"]), flush=True)
     print("   split ms/src %.2f  far-scan sources %d" % (st["split_ms"] / rows,
