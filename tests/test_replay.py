@@ -11,7 +11,7 @@ import pytest
 
 import oracle
 import shadow_amd as sa
-from helpers import attach_hosts, random_topology_graphml, synthetic_pair
+from helpers import attach_hosts, graphml_doc, random_topology_graphml, synthetic_pair
 
 pytestmark = pytest.mark.gpu
 
@@ -258,3 +258,86 @@ def test_tie_dense_auto_switch():
     assert np.array_equal(outs[0][1], outs[1][1])
     oa, olat, orel, ohops = g.table(verts)
     assert np.array_equal(outs[1][0][..., 0].view(np.uint64), olat.view(np.uint64))
+
+
+def _one_way_regions_graphml(back_lat=5000.0, seed=11, with_back=True):
+    """A directed topology whose two side regions hang off a strongly connected core almost one
+    way: the sink region is entered by many cheap arcs and left by ONE arc of latency `back_lat`,
+    the source region left by many cheap arcs and entered by ONE such arc.  With the two arcs the
+    graph is strongly connected (the reference's requirement, shd-topology.c:134-151); without
+    them it is not.  Poi sit in the core and in both regions."""
+    rng = np.random.default_rng(seed)
+    core, side = 300, 120
+    nodes = [("pop-%d" % i, "pop", 0.0) for i in range(core + 2 * side)]
+    edges = []
+    for i in range(core):  # core: bidirectional cycle + random arcs
+        j = (i + 1) % core
+        edges.append(("pop-%d" % i, "pop-%d" % j, rng.uniform(1, 100), rng.uniform(0, 0.01)))
+        edges.append(("pop-%d" % j, "pop-%d" % i, rng.uniform(1, 100), rng.uniform(0, 0.01)))
+    for _ in range(900):
+        a, b = (int(x) for x in rng.integers(0, core, 2))
+        if a != b:
+            edges.append(("pop-%d" % a, "pop-%d" % b, rng.uniform(1, 100), rng.uniform(0, 0.01)))
+    sink = list(range(core, core + side))
+    src = list(range(core + side, core + 2 * side))
+    for reg in (sink, src):  # each region: a bidirectional chain + random internal arcs
+        for a, b in zip(reg[:-1], reg[1:]):
+            edges.append(("pop-%d" % a, "pop-%d" % b, rng.uniform(1, 100), rng.uniform(0, 0.01)))
+            edges.append(("pop-%d" % b, "pop-%d" % a, rng.uniform(1, 100), rng.uniform(0, 0.01)))
+        for _ in range(200):
+            a, b = (int(x) for x in rng.choice(reg, 2))
+            if a != b:
+                edges.append(("pop-%d" % a, "pop-%d" % b, rng.uniform(1, 100), rng.uniform(0, 0.01)))
+    for _ in range(60):  # cheap one-way arcs: core -> sink region, source region -> core
+        c = int(rng.integers(0, core))
+        edges.append(("pop-%d" % c, "pop-%d" % int(rng.choice(sink)), rng.uniform(1, 100), 0.0))
+        edges.append(("pop-%d" % int(rng.choice(src)), "pop-%d" % c, rng.uniform(1, 100), 0.0))
+    if with_back:  # the only ways back
+        edges.append(("pop-%d" % sink[-1], "pop-0", back_lat, 0.0))
+        edges.append(("pop-0", "pop-%d" % src[0], back_lat, 0.0))
+    n_poi = 45
+    for k in range(n_poi):
+        pool = (range(core), sink, src)[k % 3]
+        r = "pop-%d" % int(rng.choice(list(pool)))
+        nodes.append(("poi-%d" % k, ("client", "relay", "server")[k % 3], rng.uniform(0, 0.05)))
+        edges.append(("poi-%d" % k, r, 5.0, 0.0))
+        edges.append((r, "poi-%d" % k, float(rng.uniform(1, 100)), 0.0))
+        edges.append(("poi-%d" % k, "poi-%d" % k, 1.0, 0.0))
+    order = rng.permutation(len(edges))
+    return graphml_doc(nodes, [edges[i] for i in order], directed=True)
+
+
+def test_one_way_region_topology_rejected():
+    """Without the two arcs back the side regions are one-way: not strongly connected, which the
+    reference refuses at load (critical + NULL, shd-topology.c:134-151) -- so sources that cannot
+    reach the landmark, or targets the landmark cannot reach, never reach the kernels."""
+    top = sa.Topology.from_buffer(_one_way_regions_graphml(with_back=False))
+    assert top is None or not getattr(top, "_h", None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["batch", "replay_all"])
+def test_directed_near_one_way_regions(mode):
+    """a directed fixture with near one-way regions -- a sink region left and a source
+    region entered only through one 5,000 ms arc each -- so d(v, h0) (potSrc) and d(h0, v)
+    (kappa) are huge for one side each, and the two directions of most pairs differ by orders of
+    magnitude.  Batch mode (flagged rows through the replay) and replay_all against the oracle,
+    bit for bit, with no error and no -1 pair."""
+    data = _one_way_regions_graphml()
+    top = sa.Topology.from_buffer(data)
+    g = oracle.OGraph.from_graphml(data)
+    assert top.is_directed and not top.is_complete
+    if mode == "replay_all":
+        top.set_option("replay_all", 1)
+    else:
+        top.set_option("tie_dense", 0)
+    otop, ips, verts = attach_hosts(top, g, 90, geo_hints=None)
+    a, lat, rel, hops = top.table()
+    st = top.stats()
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(a, oa)
+    assert st["errors"] == 0 and np.all(lat > 0) and np.all(rel > 0)
+    assert lat.max() > 5000.0 and lat.min() < 100.0  # the long arcs are on some paths
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
