@@ -269,7 +269,14 @@ def _one_way_regions_graphml(back_lat=5000.0, seed=11, with_back=True):
     rng = np.random.default_rng(seed)
     core, side = 300, 120
     nodes = [("pop-%d" % i, "pop", 0.0) for i in range(core + 2 * side)]
-    edges = []
+    edges, seen = [], set()
+
+    class _Arcs(list):  # no parallel arcs (a multigraph would send every row to the replay)
+        def append(self, e):
+            if (e[0], e[1]) not in seen:
+                seen.add((e[0], e[1]))
+                list.append(self, e)
+    edges = _Arcs()
     for i in range(core):  # core: bidirectional cycle + random arcs
         j = (i + 1) % core
         edges.append(("pop-%d" % i, "pop-%d" % j, rng.uniform(1, 100), rng.uniform(0, 0.01)))
