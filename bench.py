@@ -491,10 +491,12 @@ def main():
     top.synth_packets(SEED, args.hosts, 0, 10**9, window0)
     t_att1 = time.perf_counter()
     attach_phase_s = t_att1 - t_att0
-    # the cold build's window starts here: the table geometry (which waits for the attach-time
-    # preparation, if it is still running) is part of the first build
-    attached = top.attached_vertices()
-    A, V, E = len(attached), top.num_vertices, top.num_edges
+    # the cold build's window starts here.  Library mode: Shadow's first packet calls the getters,
+    # which derive the table geometry themselves (part of the first build); torchrun mode needs the
+    # column count for its shards first.
+    V, E = top.num_vertices, top.num_edges
+    attached = None if library else top.attached_vertices()
+    A = None if library else len(attached)
 
     kernel_ms, replay_ms = [], []
     if library:
@@ -552,6 +554,9 @@ def main():
     cold_s = max_over_ranks(t1 - t_att1)
     attach_to_table_s = max_over_ranks(t1 - t_att0)
     st_cold = top.stats()
+    if attached is None:
+        attached = top.attached_vertices()
+        A = len(attached)
     # the packet window (same seed chain: every host re-attaches to the same vertex, the table
     # stays valid), then the timed steps
     tw0 = time.time()
@@ -668,8 +673,9 @@ def main():
         cs = st_cold
         # the first build's wait for the attach-time preparation: the library's lock wait (build
         # and geometry), at most the part of the preparation the attach phase did not hide
-        cold_wait_ms = max(0.0, min(cs["attach_prep_ms"], cs["first_attach_to_table_ms"] -
-                                    attach_phase_s * 1e3 - cs["build_wall_ms"]))
+        cold_wait_ms = (cs["build_wait_ms"] if library else
+                        max(0.0, min(cs["attach_prep_ms"], cs["first_attach_to_table_ms"] -
+                                     attach_phase_s * 1e3 - cs["build_wall_ms"])))
         host_ms = cs["csr_host_ms"] + cs["csr_copy_ms"] + cs["order_ms"] + cs["replay_prep_ms"]
         cold = dict(
             ms=round(cold_s * 1e3, 2), gteps=round(A * E / cold_s / 1e9, 3),
@@ -691,6 +697,8 @@ def main():
             module_load_ms=round(cs["module_load_ms"], 2),
             build_wait_ms=round(cold_wait_ms, 2),
             attach_prep_ms=round(cs["attach_prep_ms"], 2),
+            prep_trigger={0: "none", 1: "first attach", 2: "topology_new"}.get(
+                int(cs["prep_trigger"]), "?"),
             attach_prep_steps_ms=dict(zip(("device_init", "graph_prep", "edge_scan", "workspace"),
                                           [round(x, 2) for x in cs["attach_prep_step_ms"]])),
             attach_phase_ms=round(attach_phase_s * 1e3, 2),
@@ -710,8 +718,9 @@ def main():
                  "attach -> that answer; getter_beyond_build_ms = its time outside the build and "
                  "the lock wait), made right after the attach phase (attach_phase_ms: "
                  "%d hosts, wall clock); device init, graph preparation and the workspace run "
-                 "from the first attach on in a background thread (attach_prep_ms) that overlaps "
-                 "the attaches, and the build waits build_wait_ms for the rest of it; "
+                 "in a background thread (attach_prep_ms) started by prep_trigger (topology_new "
+                 "after the parse, else the first attach), and the build waits build_wait_ms "
+                 "for the rest of it; "
                  "first_attach_to_table_ms = first attach -> first table installed (wall clock); "
                  "serialised_ms = the preparation and the build one after the other (nothing "
                  "overlapped); host_ms = host work of the cold build (graph preparation copies + "

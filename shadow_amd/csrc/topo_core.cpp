@@ -375,6 +375,16 @@ struct _Topology {
                               // fixpoint is reached: cycles without targets rise forever; every
                               // iterate is exact)
     DevBuf<double> d_pot, d_kfA, d_kfB, d_kfPart;
+    // the target-aware re-sort's scratch (KprimeScratch), kept: the first build's target
+    // preparation allocates nothing (the background preparation sizes it)
+    DevBuf<float> d_kpKey;
+    DevBuf<uint32_t> d_kpIdxIn, d_kpIdxOut;
+    DevBuf<uint4> d_kpRec;
+    DevBuf<uint8_t> d_kpTmp;
+    // the target preparation runs asynchronously (overlapping the host's source order): its
+    // iteration count and event time are read after the build's next stream sync
+    bool tpPending = false;
+    hipEvent_t evp0 = nullptr, evp1 = nullptr;
     // hub rows cut into segments (HubSegs): {row, first entry} and the rows cut in several
     DevBuf<uint2> d_hseg;
     DevBuf<uint4> d_hmulti;
@@ -434,6 +444,10 @@ struct _Topology {
     int xchgCus = 8;           // option "exchange_cus": CUs the last part leaves to the exchange
     int slotCap = 0;           // this launch's workgroups: > 0 at most, < 0 that many fewer
     hipStream_t xstream = nullptr;  // exchange stream of a split build (RCCL / peer copies)
+    // the getters' row copies (snap_row): a few streams shared by the worker threads, made by
+    // dev_init (the background init) so that no query pays a stream creation
+    static constexpr int kCopyStreams = 4;
+    hipStream_t cstream[kCopyStreams] = {};
     int memShareDiv = 1;       // engines of this build sharing this engine's physical device: its
                                // workspaces take that share of the device's free memory
     bool forceRccl = false;    // option "rccl": the RCCL exchange even with one device (tests)
@@ -471,8 +485,14 @@ struct _Topology {
     std::unordered_map<int32_t, std::vector<uint64_t>> matEpochs;  // all epochs (lazyMu)
     std::unordered_map<int32_t, double> matMin;  // the row minimum its latest one offered (lazyMu)
     std::mutex lazyMu;
-    std::unique_ptr<std::atomic<uint64_t>[]> matPair;  // per (column pair) bit (complete branch)
-    size_t matPairWords = 0;
+    // per (column pair) bit of the complete branch, for one geometry; superseded arrays stay
+    // allocated (getters read the current one without a lock)
+    struct PairBits {
+        size_t words = 0;
+        std::unique_ptr<std::atomic<uint64_t>[]> bits;
+    };
+    std::atomic<PairBits*> matPair{nullptr};
+    std::vector<std::unique_ptr<PairBits>> matPairs;
     std::mutex minMu;
     double lazyMin = 0.0;  // top->minimumPathLatency
 
@@ -657,9 +677,20 @@ int dev_init(Topology* top) {
     HIPCHK(hipEventCreate(&top->ev3));
     HIPCHK(hipEventCreate(&top->evr0));
     HIPCHK(hipEventCreate(&top->evr1));
+    HIPCHK(hipEventCreate(&top->evp0));
+    HIPCHK(hipEventCreate(&top->evp1));
     tmark("events");
     HIPCHK(top->d_stats.ensure(ST_COUNT));
     tmark("stats buffer");
+    for (hipStream_t& c : top->cstream) HIPCHK(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
+    {
+        // a pageable copy each way: the runtime sets up its staging buffers here (the background
+        // init) rather than in the first build's or the first getter's copies
+        unsigned long long h[4] = {0, 0, 0, 0};
+        HIPCHK(hipMemcpy(h, top->d_stats.p, sizeof h, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(top->d_stats.p, h, sizeof h, hipMemcpyHostToDevice));
+    }
+    tmark("copy streams + staging");
     // the kernels' code objects, loaded here rather than by the first build's launches
     const auto t0 = std::chrono::steady_clock::now();
     HIPCHK(preload_prep_module());
@@ -683,12 +714,18 @@ void dev_release(Topology* top) {
     if (!top->devInit) return;
     (void)hipSetDevice(top->devId);
     (void)hipStreamSynchronize(top->stream);
-    for (hipEvent_t e : {top->ev0, top->ev1, top->ev2, top->ev3, top->evr0, top->evr1})
+    for (hipEvent_t e : {top->ev0, top->ev1, top->ev2, top->ev3, top->evr0, top->evr1, top->evp0,
+                         top->evp1})
         (void)hipEventDestroy(e);
     (void)hipStreamDestroy(top->stream);
     if (top->xstream) (void)hipStreamDestroy(top->xstream);
+    for (hipStream_t& c : top->cstream) {
+        if (c) (void)hipStreamDestroy(c);
+        c = nullptr;
+    }
     top->stream = top->xstream = nullptr;
     top->ev0 = top->ev1 = top->ev2 = top->ev3 = top->evr0 = top->evr1 = nullptr;
+    top->evp0 = top->evp1 = nullptr;
     top->d_stats.release();
     top->devInit = false;
 }
@@ -1288,10 +1325,15 @@ uint64_t compute_geometry(Topology* top) {
     top->tableValid.store(false);
     // complete-branch materialisation bits are per column pair: a new geometry starts them over
     // (a re-touched pair re-offers a latency >= the running minimum: a no-op, shd-topology.c:501)
-    const size_t words = (size_t)((top->A * top->A + 63) / 64);
-    top->matPairWords = words;
-    top->matPair.reset(new std::atomic<uint64_t>[words ? words : 1]);
-    for (size_t i = 0; i < std::max<size_t>(1, words); i++) top->matPair[i].store(0, std::memory_order_relaxed);
+    // (complete topologies only: the SSSP branch tracks rows, and A x A bits are 12.5 MB at C4)
+    if (top->isComplete) {
+        auto pb = std::make_unique<Topology::PairBits>();
+        pb->words = (size_t)((top->A * top->A + 63) / 64);
+        pb->bits.reset(new std::atomic<uint64_t>[std::max<size_t>(1, pb->words)]);
+        for (size_t i = 0; i < std::max<size_t>(1, pb->words); i++) pb->bits[i].store(0, std::memory_order_relaxed);
+        top->matPair.store(pb.get(), std::memory_order_release);
+        top->matPairs.push_back(std::move(pb));
+    }
     return sg;
 }
 
@@ -1522,6 +1564,28 @@ void reset_build_stats(Topology* top) {
     top->stats.tie_probe_ms = 0.0;
 }
 
+// The target-aware re-sort's scratch for the prepared relaxation copy (allocated once).
+int ensure_kprime_scratch(Topology* top, KprimeScratch* out) {
+    const int64_t nadj = (int64_t)(top->d_adjk.n / 4), V = top->g.V;
+    size_t tb = 0;
+    HIPCHK(kprime_sort_tmp_bytes(top->d_rowptr.p, V, nadj, &tb));
+    const size_t n = (size_t)std::max<int64_t>(1, nadj);
+    HIPCHK(top->d_kpKey.ensure(n));
+    HIPCHK(top->d_kpIdxIn.ensure(n));
+    HIPCHK(top->d_kpIdxOut.ensure(n));
+    HIPCHK(top->d_kpRec.ensure(n));
+    HIPCHK(top->d_kpTmp.ensure(std::max<size_t>(1, tb)));
+    if (out) {
+        out->key = top->d_kpKey.p;
+        out->idx_in = top->d_kpIdxIn.p;
+        out->idx_out = top->d_kpIdxOut.p;
+        out->rec = top->d_kpRec.p;
+        out->tmp = top->d_kpTmp.p;
+        out->tmp_bytes = top->d_kpTmp.n;
+    }
+    return 0;
+}
+
 // Enqueue rows [row0,row1) into out buffers (device pointers) on `st`.
 int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uint16_t* out_hops,
                  double* out_rowmin, hipStream_t st) {
@@ -1616,45 +1680,46 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 top->adjkTargets.clear();
             }
             if (top->targetSkip && top->adjkPlain) {
-                // bit 30 of the relaxation copy's columns: the current target set
-                const auto tp0 = std::chrono::steady_clock::now();
+                // bit 30 of the relaxation copy's columns: the current target set.  Everything
+                // after the bit upload is enqueued without a host sync: the GPU prepares the
+                // target set while the host computes the source order below (the fixpoint always
+                // runs target_kappa iterations -- past its convergence an iteration reproduces its
+                // input bit for bit -- and each iteration's change flag is read afterwards).
                 r = upload_target_bits(top, tgt, st);
                 if (r) return r;
+                HIPCHK(hipEventRecord(top->evp0, st));
                 HIPCHK(launch_mark_targets(top->d_adjk.p, nadjk, top->d_tbits.p, st));
                 // the records' kappa field: the target-aware fixpoint (kappa0 with 0 iterations)
                 const int64_t V = top->g.V;
                 const HubSegs hs = hub_segs(top);
+                const int nit = std::max(0, top->targetKappa);
                 HIPCHK(top->d_kfA.ensure((size_t)V));
                 HIPCHK(top->d_kfB.ensure((size_t)V));
                 HIPCHK(top->d_kfPart.ensure(std::max<size_t>(1, hs.nseg)));
-                HIPCHK(top->d_kfChanged.ensure(1));
+                HIPCHK(top->d_kfChanged.ensure((size_t)nit + 1));
+                HIPCHK(hipMemsetAsync(top->d_kfChanged.p, 0, sizeof(unsigned int) * ((size_t)nit + 1), st));
                 HIPCHK(launch_kfix_step(top->d_rowptr.p, adj_out(top), top->d_pot.p, top->d_tbits.p,
                                         nullptr, top->d_kfA.p, V, hs, top->d_kfPart.p,
                                         top->d_kfChanged.p, st));
                 double* kin = top->d_kfA.p;
                 double* kout = top->d_kfB.p;
-                int it = 0;
-                for (; it < top->targetKappa; it++) {
-                    HIPCHK(hipMemsetAsync(top->d_kfChanged.p, 0, sizeof(unsigned int), st));
+                for (int it = 0; it < nit; it++) {
                     HIPCHK(launch_kfix_step(top->d_rowptr.p, adj_out(top), top->d_pot.p,
                                             top->d_tbits.p, kin, kout, V, hs, top->d_kfPart.p,
-                                            top->d_kfChanged.p, st));
-                    unsigned int ch = 0;
-                    HIPCHK(hipMemcpyAsync(&ch, top->d_kfChanged.p, sizeof(unsigned int),
-                                          hipMemcpyDeviceToHost, st));
-                    HIPCHK(hipStreamSynchronize(st));
+                                            top->d_kfChanged.p + 1 + it, st));
                     std::swap(kin, kout);
-                    if (!ch) break;
                 }
-                if (top->targetResort)
+                if (top->targetResort) {
+                    KprimeScratch sc;
+                    r = ensure_kprime_scratch(top, &sc);
+                    if (r) return r;
                     HIPCHK(launch_kprime_resort(top->d_adjk.p, top->d_kap.p, top->d_ksum.p,
                                                 top->d_kap0.p, top->d_rowptr.p, V, nadjk,
-                                                top->d_pot.p, top->d_tbits.p, kin, st));
+                                                top->d_pot.p, top->d_tbits.p, kin, sc, st));
+                }
                 HIPCHK(launch_kfix_store(top->d_adjk.p, nadjk, kin, st));
-                HIPCHK(hipStreamSynchronize(st));
-                top->stats.target_kappa_iters = it;
-                top->stats.target_prep_ms = std::chrono::duration<double, std::milli>(
-                    std::chrono::steady_clock::now() - tp0).count();
+                HIPCHK(hipEventRecord(top->evp1, st));
+                top->tpPending = true;
                 top->adjkTargets = tgt;
                 top->adjkFlagged = true;
                 top->adjkPlain = false;
@@ -1919,6 +1984,19 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
         }
         HIPCHK(hipEventRecord(top->ev1, st));
         HIPCHK(hipStreamSynchronize(st));
+        if (top->tpPending) {  // the asynchronous target preparation: iterations until the fixpoint
+            top->tpPending = false;
+            const int nit = std::max(0, top->targetKappa);
+            std::vector<unsigned int> ch((size_t)nit + 1);
+            HIPCHK(hipMemcpy(ch.data(), top->d_kfChanged.p, sizeof(unsigned int) * ch.size(),
+                             hipMemcpyDeviceToHost));
+            int it = 0;
+            while (it < nit && ch[(size_t)it + 1]) it++;  // the first iteration that changed nothing
+            top->stats.target_kappa_iters = it;
+            float ms = 0.0f;
+            HIPCHK(hipEventElapsedTime(&ms, top->evp0, top->evp1));
+            top->stats.target_prep_ms = ms;  // its GPU time (overlapped with the source order)
+        }
         // the batch times: the sources' costs (option balance) and the SHD_BATCH_TRACE file -- after
         // ev1, so the copy and the host work stay out of the kernel's event time
         if (!bt.start.empty()) {
@@ -2743,7 +2821,7 @@ int getter_snapshot(Topology* top, const HostTable** out) {
 
 // Row c of a snapshot's table ({latency, reliability} per column), copied from the device table
 // the first time a query reads it: one 16 A-byte copy (C4: 160 KB) instead of the whole table.
-// Copies run in parallel (per-thread HIP streams, tabMu shared); two threads racing for the same
+// Copies run in parallel (the library's copy streams, tabMu shared); two threads racing for the same
 // row both copy it and the first to publish wins.  Returns 0 (*out set), 1 when the device table
 // is no longer the snapshot's (a rebuild ran in between: the caller takes a new snapshot), or a
 // negative error.  Rows already copied are read without a lock (acquire load).
@@ -2759,9 +2837,11 @@ int snap_row(Topology* top, const HostTable& h, int64_t c, const double2** out) 
     const auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipSetDevice(top->devId));  // the table's device, for this (worker) thread
     std::unique_ptr<double2[]> buf(new double2[(size_t)std::max<int64_t>(1, h.A)]);
+    const hipStream_t cs = top->cstream[std::hash<std::thread::id>{}(std::this_thread::get_id()) %
+                                        Topology::kCopyStreams];
     HIPCHK(hipMemcpyAsync(buf.get(), tab_lr(top) + c * h.A, sizeof(double2) * (size_t)h.A,
-                          hipMemcpyDeviceToHost, hipStreamPerThread));
-    HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+                          hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipStreamSynchronize(cs));
     const double2* expect = nullptr;
     if (h.rows[(size_t)c].compare_exchange_strong(expect, buf.get(), std::memory_order_acq_rel)) {
         *out = buf.get();
@@ -2901,12 +2981,13 @@ int lazy_orientation(Topology* top, int32_t s, int32_t d) {
 void lazy_touch_pair(Topology* top, const HostTable& h, int64_t cs, int64_t cd, double lat) {
     const int64_t A = h.A;
     const size_t b1 = (size_t)(cs * A + cd), b2 = (size_t)(cd * A + cs);
-    if (top->matPairWords * 64 < (size_t)(A * A)) return;  // geometry moved on (raced)
-    bool have = (top->matPair[b1 >> 6].load(std::memory_order_relaxed) >> (b1 & 63)) & 1;
+    const Topology::PairBits* pb = top->matPair.load(std::memory_order_acquire);
+    if (!pb || pb->words * 64 < (size_t)(A * A)) return;  // geometry moved on (raced)
+    bool have = (pb->bits[b1 >> 6].load(std::memory_order_relaxed) >> (b1 & 63)) & 1;
     if (!have && !top->isDirected)
-        have = (top->matPair[b2 >> 6].load(std::memory_order_relaxed) >> (b2 & 63)) & 1;
+        have = (pb->bits[b2 >> 6].load(std::memory_order_relaxed) >> (b2 & 63)) & 1;
     if (!have) {
-        uint64_t old = top->matPair[b1 >> 6].fetch_or(1ull << (b1 & 63));
+        uint64_t old = pb->bits[b1 >> 6].fetch_or(1ull << (b1 & 63));
         if (!((old >> (b1 & 63)) & 1) && lat > 0) lazy_store_min(top, lat);
     }
 }
@@ -3094,6 +3175,8 @@ void start_graph_prep(Topology* top, bool onLoad) {
         // the batched SSSP's workspace too, sized for a full table (a build with fewer sources
         // uses a part of it; a different batch width re-allocates)
         if (!r) r = ensure_workspace(top, 1 << 30);
+        if (!r && top->targetSkip && top->targetResort)
+            r = ensure_kprime_scratch(top, nullptr);
         if (!r) r = hipStreamSynchronize(top->stream) == hipSuccess ? 0 : -1;
         step(3);
         top->prepBgRc = r;
@@ -3118,6 +3201,8 @@ void release_prepared(Topology* top) {
     top->d_eu.release(); top->d_ev.release();
     top->d_kap.release(); top->d_ksum.release(); top->d_kap0.release();
     top->d_hseg.release(); top->d_hmulti.release(); top->d_kfChanged.release();
+    top->d_kpKey.release(); top->d_kpIdxIn.release(); top->d_kpIdxOut.release();
+    top->d_kpRec.release(); top->d_kpTmp.release();
     top->hsegRows = top->hsegN = top->hmultiN = 0;
     top->csrUploaded = top->rowsSorted = false;
     top->adjkPlain = top->adjkFlagged = top->adjkResorted = false;
@@ -3244,8 +3329,12 @@ void topology_free(Topology* top) {
         (void)hipEventDestroy(top->ev3);
         (void)hipEventDestroy(top->evr0);
         (void)hipEventDestroy(top->evr1);
+        (void)hipEventDestroy(top->evp0);
+        (void)hipEventDestroy(top->evp1);
         (void)hipStreamDestroy(top->stream);
         if (top->xstream) (void)hipStreamDestroy(top->xstream);
+        for (hipStream_t c : top->cstream)
+            if (c) (void)hipStreamDestroy(c);
     }
     delete top;
 }

@@ -251,10 +251,22 @@ hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const d
                             hipStream_t stream);
 hipError_t launch_kfix_store(uint32_t* adjk, int64_t nadj, const double* K, hipStream_t stream);
 // re-sort every row of the relaxation copy (records, kappa array, probes, kappa0) by the
-// target-aware key kap' of the current target set (tbits) and K
+// target-aware key kap' of the current target set (tbits) and K.  Scratch (KprimeScratch, sized
+// by kprime_scratch_bytes) is the caller's, so the resort allocates nothing and never syncs.
+struct KprimeScratch {
+    float* key = nullptr;       // nadj
+    uint32_t* idx_in = nullptr; // nadj
+    uint32_t* idx_out = nullptr;// nadj
+    uint4* rec = nullptr;       // nadj
+    void* tmp = nullptr;        // tmp_bytes (the segmented radix sort's)
+    size_t tmp_bytes = 0;
+};
+// the sort's temporary bytes for nadj keys in V segments (no device work)
+hipError_t kprime_sort_tmp_bytes(const uint32_t* rowptr, int64_t V, int64_t nadj, size_t* bytes);
 hipError_t launch_kprime_resort(uint32_t* adjk, float* kap, float* ksum, float* kap0,
                                 const uint32_t* rowptr, int64_t V, int64_t nadj, const double* pot,
-                                const uint32_t* tbits, const double* K, hipStream_t stream);
+                                const uint32_t* tbits, const double* K, const KprimeScratch& sc,
+                                hipStream_t stream);
 hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uint32_t* d_sources,
                              const double* d_srcsh, int nsrc, int kf, const uint32_t* d_targets, int A,
                              double delta, const SsspLdsPlan& plan, uint32_t iter_guard,

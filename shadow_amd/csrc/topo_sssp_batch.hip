@@ -2309,40 +2309,36 @@ __global__ void kprime_probe_kernel(const uint32_t* __restrict__ rowptr,
     }
 }
 
-hipError_t launch_kprime_resort(uint32_t* adjk, float* kap, float* ksum, float* kap0,
-                                const uint32_t* rowptr, int64_t V, int64_t nadj, const double* pot,
-                                const uint32_t* tbits, const double* K, hipStream_t stream) {
+hipError_t kprime_sort_tmp_bytes(const uint32_t* rowptr, int64_t V, int64_t nadj, size_t* bytes) {
+    *bytes = 0;
     if (nadj <= 0 || V <= 0) return hipSuccess;
     if (nadj > 0x7FFFFFFF) return hipErrorInvalidValue;
-    float* key_in = nullptr;
-    uint32_t *idx_in = nullptr, *idx_out = nullptr;
-    uint4* rec = nullptr;
-    void* tmp = nullptr;
-    size_t tmp_bytes = 0;
-    hipError_t e = hipMalloc((void**)&key_in, sizeof(float) * (size_t)nadj);
-    if (e == hipSuccess) e = hipMalloc((void**)&idx_in, sizeof(uint32_t) * (size_t)nadj);
-    if (e == hipSuccess) e = hipMalloc((void**)&idx_out, sizeof(uint32_t) * (size_t)nadj);
-    if (e == hipSuccess) e = hipMalloc((void**)&rec, sizeof(uint4) * (size_t)nadj);
+    return hipcub::DeviceSegmentedRadixSort::SortPairs(
+        nullptr, *bytes, (const float*)nullptr, (float*)nullptr, (const uint32_t*)nullptr,
+        (uint32_t*)nullptr, (int)nadj, (int)V, rowptr, rowptr + 1, 0, 32, (hipStream_t)0);
+}
+
+hipError_t launch_kprime_resort(uint32_t* adjk, float* kap, float* ksum, float* kap0,
+                                const uint32_t* rowptr, int64_t V, int64_t nadj, const double* pot,
+                                const uint32_t* tbits, const double* K, const KprimeScratch& sc,
+                                hipStream_t stream) {
+    if (nadj <= 0 || V <= 0) return hipSuccess;
+    if (nadj > 0x7FFFFFFF || !sc.key || !sc.idx_in || !sc.idx_out || !sc.rec || !sc.tmp)
+        return hipErrorInvalidValue;
     const int64_t ge = std::min<int64_t>((nadj + 255) / 256, 256 * 16);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(kprime_key_kernel, dim3((unsigned)ge), dim3(256), 0, stream, adjk, nadj,
-                           pot, tbits, K, key_in, idx_in);
-        e = hipGetLastError();
-    }
+    hipLaunchKernelGGL(kprime_key_kernel, dim3((unsigned)ge), dim3(256), 0, stream, adjk, nadj,
+                       pot, tbits, K, sc.key, sc.idx_in);
+    hipError_t e = hipGetLastError();
+    size_t tb = sc.tmp_bytes;
     if (e == hipSuccess)
         e = hipcub::DeviceSegmentedRadixSort::SortPairs(
-            nullptr, tmp_bytes, key_in, kap, idx_in, idx_out, (int)nadj, (int)V, rowptr,
-            rowptr + 1, 0, 32, stream);
-    if (e == hipSuccess) e = hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 1);
-    if (e == hipSuccess)
-        e = hipcub::DeviceSegmentedRadixSort::SortPairs(
-            tmp, tmp_bytes, key_in, kap, idx_in, idx_out, (int)nadj, (int)V, rowptr, rowptr + 1,
+            sc.tmp, tb, sc.key, kap, sc.idx_in, sc.idx_out, (int)nadj, (int)V, rowptr, rowptr + 1,
             0, 32, stream);
     if (e == hipSuccess)
-        e = hipMemcpyAsync(rec, adjk, sizeof(uint4) * (size_t)nadj, hipMemcpyDeviceToDevice, stream);
+        e = hipMemcpyAsync(sc.rec, adjk, sizeof(uint4) * (size_t)nadj, hipMemcpyDeviceToDevice, stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(kprime_gather_kernel, dim3((unsigned)ge), dim3(256), 0, stream, rec,
-                           reinterpret_cast<uint4*>(adjk), idx_out, nadj);
+        hipLaunchKernelGGL(kprime_gather_kernel, dim3((unsigned)ge), dim3(256), 0, stream, sc.rec,
+                           reinterpret_cast<uint4*>(adjk), sc.idx_out, nadj);
         e = hipGetLastError();
     }
     if (e == hipSuccess) {
@@ -2351,13 +2347,6 @@ hipError_t launch_kprime_resort(uint32_t* adjk, float* kap, float* ksum, float* 
                            kap, ksum, kap0, V);
         e = hipGetLastError();
     }
-    const hipError_t es = hipStreamSynchronize(stream);
-    if (e == hipSuccess) e = es;
-    (void)hipFree(key_in);
-    (void)hipFree(idx_in);
-    (void)hipFree(idx_out);
-    (void)hipFree(rec);
-    (void)hipFree(tmp);
     return e;
 }
 
