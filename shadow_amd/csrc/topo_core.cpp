@@ -446,7 +446,7 @@ struct _Topology {
     hipStream_t xstream = nullptr;  // exchange stream of a split build (RCCL / peer copies)
     // the getters' row copies (snap_row): a few streams shared by the worker threads, made by
     // dev_init (the background init) so that no query pays a stream creation
-    static constexpr int kCopyStreams = 4;
+    static constexpr int kCopyStreams = 16;
     hipStream_t cstream[kCopyStreams] = {};
     int memShareDiv = 1;       // engines of this build sharing this engine's physical device: its
                                // workspaces take that share of the device's free memory
