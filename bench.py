@@ -210,7 +210,7 @@ def complete_table_lines(repeats=20, nthreads=1, devices=1, cpu=True):
         if devices > 1:
             line["device_kernel_ms"] = [round(float(x), 4) for x in np.median(np.asarray(dk), axis=0)]
             line["device_rows"] = list(s_["device_rows"][:min(8, devices)])
-            line["exchange"] = dict(kind={0: "none", 1: "rccl", 2: "peer copies"}.get(
+            line["exchange"] = dict(kind={0: "none", 1: "rccl", 2: "push"}.get(
                 int(s_["exchange_kind"]), "?"), ms=round(float(np.median(xm)), 4),
                 bytes_per_device=int(s_["exchange_bytes"]))
         if cpu:
@@ -809,12 +809,10 @@ def main():
             "complete_tables": complete,
             "directed": directed,
             "ambiguous_pairs": st["ambiguous_pairs"],
-            "exchange": dict(kind={0: "none", 1: "rccl", 2: "peer copies"}.get(
+            "exchange": dict(kind={0: "none", 1: "rccl", 2: "push"}.get(
                 int(st["exchange_kind"]), "?") if library else "torch.distributed",
                              ms=round(st["exchange_ms"], 2),
                              ms_exposed=round(st["exchange_exposed_ms"], 2) if library else None,
-                             split=int(st["exchange_split"]) if library else None,
-                             part0_stream_ms=round(st["exchange_part_ms"][0], 3) if library else None,
                              devices=int(st["devices"]) if library else world,
                              device_kernel_ms=[round(x, 3) for x in
                                                st["device_kernel_ms"][:min(8, int(st["devices"]))]]

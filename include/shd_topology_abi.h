@@ -312,9 +312,11 @@ typedef struct {
                                    geometry + table buffers, preparation up to the SSSP launch
                                    (graph, workspace, target set, order), the SSSP kernel, the tie
                                    replay + rest of the rows, statistics, (unused) x 2 */
-    int64_t exchange_kind;      /* the last build's row exchange: 0 none (one device), 1 RCCL
-                                   all-gather + all-reduce(MIN), 2 device-to-device peer copies
-                                   (engines sharing a device, or RCCL unavailable) */
+    int64_t exchange_kind;      /* the last build's row exchange (option "exchange"): 0 none (one
+                                   device), 1 RCCL all-gather + all-reduce(MIN) after every shard,
+                                   2 push: each shard copied into the other devices' tables (peer
+                                   DMA) as soon as it is done (engines sharing a device, RCCL
+                                   unavailable, or exchange = 2) */
     int64_t walk_kinds[4];      /* of the walk steps: parents certified by the h0-tree guess, by a
                                    tail's recorded improver, by a hub's recorded improver, and pairs
                                    sent to the merged row scans */
@@ -380,13 +382,9 @@ typedef struct {
     int64_t prep_trigger;       /* what started the background graph preparation (attach_prep_ms):
                                    0 none, 1 the first attach, 2 topology_new (right after the
                                    parse; SHDTOPO_NO_LOAD_PREP=1 turns that off) */
-    int64_t exchange_split;     /* parts of the last multi-device build (option "exchange_split"):
-                                   2 = the first part's exchange ran while the devices computed
-                                   the second, 1 = the exchange followed all the rows */
-    double exchange_exposed_ms; /*   wall time from the last part's rows to the end of the exchange
-                                     (the part of exchange_ms not hidden behind kernels) */
-    double exchange_part_ms[2]; /*   event time of part 0's exchange on device 0's exchange stream
-                                     (split builds; [1] unused) */
+    double exchange_exposed_ms; /* the last multi-device build: wall time from the last shard's
+                                   rows to the end of the exchange (the part of exchange_ms no
+                                   kernel hid; exchange_kind 2 overlaps the slower shards) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

@@ -60,8 +60,8 @@ class ShdStats(ctypes.Structure):
                 ("device_rows", i64 * 8), ("dev_inits", i64), ("init_bg_ms", dbl),
                 ("path_seconds_total", dbl), ("paths_computed", i64),
                 ("batch_layout_measured", i64), ("batches", i64), ("rows_to_host", i64),
-                ("rows_to_host_ms", dbl), ("prep_trigger", i64), ("exchange_split", i64),
-                ("exchange_exposed_ms", dbl), ("exchange_part_ms", dbl * 2)]
+                ("rows_to_host_ms", dbl), ("prep_trigger", i64),
+                ("exchange_exposed_ms", dbl)]
 
 
 class ShdSynthParams(ctypes.Structure):

@@ -439,11 +439,9 @@ struct _Topology {
     // rows [d*R, (d+1)*R) with its own stream / workspace (a peer Topology on that device),
     // RCCL all-gathers the rows into every device's table and all-reduces the minimum
     int devicesOpt = 1;        // option "devices"
-    int xchgSplit = 2;         // option "exchange_split": parts per device shard (2: the first
-                               // part's exchange overlaps the second part's kernels; 1: serial)
-    int xchgCus = 8;           // option "exchange_cus": CUs the last part leaves to the exchange
-    int slotCap = 0;           // this launch's workgroups: > 0 at most, < 0 that many fewer
-    hipStream_t xstream = nullptr;  // exchange stream of a split build (RCCL / peer copies)
+    int xchgMode = 0;          // option "exchange": 0 auto (RCCL across distinct devices, else
+                               // push), 1 RCCL all-gather, 2 push (peer DMA as each shard ends)
+    hipStream_t xstream = nullptr;  // exchange stream of a push exchange
     // the getters' row copies (snap_row): a few streams shared by the worker threads, made by
     // dev_init (the background init) so that no query pays a stream creation
     static constexpr int kCopyStreams = 16;
@@ -1661,8 +1659,6 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
             HIPCHK(top->d_rowflag.ensure((size_t)rows));
             HIPCHK(hipMemsetAsync(top->d_rowflag.p, 0, (size_t)rows, st));
             SlotWs ws = slot_ws(top);
-            if (top->slotCap > 0) ws.slots = std::min(ws.slots, top->slotCap);
-            else if (top->slotCap < 0) ws.slots = std::max(1, ws.slots + top->slotCap);
             ws.rowflag = top->d_rowflag.p;
             // The relaxation copy's target-derived content (bit 30 target marks, the records'
             // target-aware kappa field, the rows re-sorted by it) belongs to one target set: a new
@@ -2400,126 +2396,18 @@ int build_multi(Topology* top) {
             top->stats.csr_ms = std::chrono::duration<double, std::milli>(
                 std::chrono::steady_clock::now() - tp).count();
     }
-    // 1) rows, one host thread per device, in P parts.  Part p holds rows [B_p, B_p + N R_p):
-    // device d computes [B_p + d R_p, B_p + (d+1) R_p) of every part, so each part is exchanged
-    // in place by its own all-gather.  P = 2 (option "exchange_split", default): a part's exchange
-    // runs on the engines' exchange streams while the devices compute the next part, and only the
-    // last part's exchange is exposed.
-    const int P = (top->xchgSplit > 1 && N > 1 && A >= 4 * (int64_t)N) ? 2 : 1;
-    int64_t Rp[2] = {R, 0}, Bp[2] = {0, (int64_t)N * R};
-    if (P == 2) {
-        Rp[0] = (A + 2 * N - 1) / (2 * N);
-        Bp[1] = (int64_t)N * Rp[0];
-        Rp[1] = std::max<int64_t>(0, (A - Bp[1] + N - 1) / N);
-    }
-    const int64_t rowsAlloc = std::max<int64_t>(Bp[1] + (int64_t)N * Rp[1], (int64_t)N * R);
-    auto part_rows = [&](int p, int d, int64_t* r0, int64_t* r1) {
-        *r0 = std::min(A, Bp[p] + d * Rp[p]);
-        *r1 = std::min(A, *r0 + Rp[p]);
-    };
-    std::vector<int> rc(N, 0);
-    std::vector<double> dwall((size_t)N, 0.0);
-    std::vector<unsigned long long> dmin((size_t)N, 0x7FF0000000000000ull);
-    std::vector<int64_t> drows((size_t)N, 0);
-    std::mutex pmu;
-    std::condition_variable pcv;
-    int pdone[2] = {0, 0};
-    std::vector<std::thread> th;
-    struct JoinAll {  // every return below joins the device threads first
-        std::vector<std::thread>& t;
-        ~JoinAll() {
-            for (auto& x : t)
-                if (x.joinable()) x.join();
-        }
-    } joinGuard{th};
-    for (int d = 0; d < N; d++)
-        th.emplace_back([&, d]() {
-            Topology* T = slot_engine(top, d);
-            const auto tw = std::chrono::steady_clock::now();
-            ShdStats acc{};
-            auto run = [&](int p) -> int {
-                HIPCHK(hipSetDevice(phys[(size_t)d]));
-                int r = dev_init(T);
-                if (r) return r;
-                HIPCHK(hipSetDevice(phys[(size_t)d]));
-                if (p == 0) {
-                    HIPCHK(T->d_lr.ensure((size_t)(rowsAlloc * A)));
-                    HIPCHK(T->d_hops.ensure((size_t)(rowsAlloc * A)));
-                    HIPCHK(T->d_rowmin.ensure((size_t)rowsAlloc));
-                    if (P == 2 && !T->xstream)
-                        HIPCHK(hipStreamCreateWithFlags(&T->xstream, hipStreamNonBlocking));
-                }
-                int64_t r0, r1;
-                part_rows(p, d, &r0, &r1);
-                if (r1 <= r0) return 0;
-                // the last part leaves CUs to the exchange kernels of the part before it
-                T->slotCap = (P == 2 && p == 1 && top->xchgCus > 0) ? -top->xchgCus : 0;
-                r = enqueue_rows(T, r0, r1, T->d_lr.p + r0 * A, T->d_hops.p + r0 * A,
-                                 T->d_rowmin.p + r0, T->stream);
-                T->slotCap = 0;
-                if (r) return r;
-                r = collect_row_stats(T);
-                if (r) return r;
-                unsigned long long m = 0;
-                HIPCHK(hipMemcpy(&m, T->d_stats.p + ST_GLOBAL_MIN, 8, hipMemcpyDeviceToHost));
-                dmin[(size_t)d] = std::min(dmin[(size_t)d], m);
-                drows[(size_t)d] += r1 - r0;
-                const ShdStats& s = T->stats;  // this part's build, summed over the parts
-                acc.sssp_kernel_ms += s.sssp_kernel_ms;
-                acc.build_ms += s.build_ms;
-                acc.replay_ms += s.replay_ms;
-                acc.target_prep_ms += s.target_prep_ms;
-                acc.order_ms += s.order_ms;
-                acc.replay_prep_ms += s.replay_prep_ms;
-                acc.touched_lines += s.touched_lines;
-                acc.ambiguous_pairs += s.ambiguous_pairs;
-                acc.replay_rows += s.replay_rows;
-                acc.replay_skips += s.replay_skips;
-                acc.errors += s.errors;
-                acc.relaxations += s.relaxations;
-                for (int i = 0; i < 8; i++) acc.events[i] += s.events[i];
-                return 0;
-            };
-            for (int p = 0; p < P; p++) {
-                if (!rc[(size_t)d]) rc[(size_t)d] = run(p);
-                std::lock_guard<std::mutex> g(pmu);
-                pdone[p]++;
-                pcv.notify_all();
-            }
-            if (P == 2 && drows[(size_t)d] > 0) {  // the device's statistics: both parts
-                ShdStats& s = T->stats;
-                s.sssp_kernel_ms = acc.sssp_kernel_ms;
-                s.build_ms = acc.build_ms;
-                s.replay_ms = acc.replay_ms;
-                s.target_prep_ms = acc.target_prep_ms;
-                s.order_ms = acc.order_ms;
-                s.replay_prep_ms = acc.replay_prep_ms;
-                s.touched_lines = acc.touched_lines;
-                s.ambiguous_pairs = acc.ambiguous_pairs;
-                s.replay_rows = acc.replay_rows;
-                s.replay_skips = acc.replay_skips;
-                s.errors = acc.errors;
-                s.relaxations = acc.relaxations;
-                for (int i = 0; i < 8; i++) s.events[i] = acc.events[i];
-                s.sources = drows[(size_t)d];
-            }
-            dwall[(size_t)d] = std::chrono::duration<double, std::milli>(
-                std::chrono::steady_clock::now() - tw).count();
-        });
-    auto join_all = [&]() {
-        for (auto& x : th)
-            if (x.joinable()) x.join();
-    };
-    auto wait_part = [&](int p) {
-        std::unique_lock<std::mutex> g(pmu);
-        pcv.wait(g, [&] { return pdone[p] == N; });
-    };
-    // 2) exchange: per part, every device receives the other devices' rows ({lat, rel} + hops)
-    // and row minima; at the end the minimum is all-reduced (MIN over u64 bits of a
-    // non-negative f64 orders like the values) -> topology_getMinimumLatency / the runahead
-    // (shd-master.c:113-124).  Several slots on one physical device (a test configuration: RCCL
-    // refuses duplicate devices) exchange with device copies instead.
-    bool useRccl = distinct;
+    // 1) rows: device d builds rows [d R, (d+1) R) in its own host thread.
+    // 2) exchange, option "exchange" (VERDICT r05 item 3):
+    //    * push (2; the default for engines sharing a device): each device, as soon as its own rows
+    //      are done, copies them into every other device's table on its exchange stream (peer DMA
+    //      over xGMI) while the slower devices still compute -- only the last shard's copies are
+    //      exposed;
+    //    * rccl (1; the default for distinct devices): ncclAllGather of the rows, hops and row
+    //      minima in place once every shard is done (the north-star exchange).
+    //    The minimum (MIN over u64 bits of a non-negative f64 orders like the values) goes to
+    //    every device -> topology_getMinimumLatency / the runahead (shd-master.c:113-124): an
+    //    ncclAllReduce with RCCL, from the host's per-device minima with push.
+    bool useRccl = distinct && top->xchgMode != 2;
     if (useRccl) {
         RcclApi& api = rccl();
         if (!api.ok) {
@@ -2540,105 +2428,121 @@ int build_multi(Topology* top) {
             }
         }
     }
-    top->stats.exchange_kind = N > 1 || top->forceRccl ? (useRccl ? 1 : 2) : 0;
-    top->stats.exchange_split = P;
-    top->stats.exchange_bytes = (int64_t)(N - 1) * (Rp[0] + Rp[1]) * (A * (int64_t)(sizeof(double2) + 2) + 8);
-    auto xs = [&](Topology* T) { return P == 2 ? T->xstream : T->stream; };
-    auto exchange_part = [&](int p) -> int {
-        if (Rp[p] <= 0) return 0;
-        if (useRccl) {
-            RcclApi& api = rccl();
-            NCCLCHK(api.groupStart());
-            for (int d = 0; d < N; d++) {
-                Topology* T = slot_engine(top, d);
-                ncclComm_t c = top->comms[(size_t)d];
-                const size_t lrB = (size_t)(Rp[p] * A) * sizeof(double2), hB = (size_t)(Rp[p] * A) * 2;
-                char* lr = (char*)(T->d_lr.p + Bp[p] * A);
-                char* hp = (char*)(T->d_hops.p + Bp[p] * A);
-                double* rm = T->d_rowmin.p + Bp[p];
-                NCCLCHK(api.allGather(lr + (size_t)d * lrB, lr, lrB, ncclUint8, c, xs(T)));
-                NCCLCHK(api.allGather(hp + (size_t)d * hB, hp, hB, ncclUint8, c, xs(T)));
-                NCCLCHK(api.allGather(rm + (size_t)d * (size_t)Rp[p], rm, (size_t)Rp[p], ncclFloat64, c, xs(T)));
+    const bool push = !useRccl;
+    // every engine's table buffers first: a device's push may arrive before the peer's own rows
+    for (int d = 0; d < N; d++) {
+        Topology* T = slot_engine(top, d);
+        HIPCHK(hipSetDevice(phys[(size_t)d]));
+        HIPCHK(T->d_lr.ensure((size_t)(R * N * A)));
+        HIPCHK(T->d_hops.ensure((size_t)(R * N * A)));
+        HIPCHK(T->d_rowmin.ensure((size_t)(R * N)));
+        if (push && !T->xstream) HIPCHK(hipStreamCreateWithFlags(&T->xstream, hipStreamNonBlocking));
+        if (push && distinct)
+            for (int e = 0; e < N; e++) {
+                if (e == d) continue;
+                const hipError_t pe = hipDeviceEnablePeerAccess(phys[(size_t)e], 0);
+                if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
+                    (void)hipGetLastError();  // no direct access: the runtime stages the copies
             }
-            NCCLCHK(api.groupEnd());
-        } else {
-            for (int d = 0; d < N; d++) {
-                Topology* T = slot_engine(top, d);
-                HIPCHK(hipSetDevice(phys[(size_t)d]));
-                for (int e = 0; e < N; e++) {
-                    if (e == d) continue;
-                    Topology* S = slot_engine(top, e);
-                    int64_t r0, r1;
-                    part_rows(p, e, &r0, &r1);
-                    if (r1 <= r0) continue;
-                    HIPCHK(hipMemcpyAsync(T->d_lr.p + r0 * A, S->d_lr.p + r0 * A, sizeof(double2) * (size_t)((r1 - r0) * A), hipMemcpyDefault, xs(T)));
-                    HIPCHK(hipMemcpyAsync(T->d_hops.p + r0 * A, S->d_hops.p + r0 * A, 2 * (size_t)((r1 - r0) * A), hipMemcpyDefault, xs(T)));
-                    HIPCHK(hipMemcpyAsync(T->d_rowmin.p + r0, S->d_rowmin.p + r0, 8 * (size_t)(r1 - r0), hipMemcpyDefault, xs(T)));
-                }
-            }
-        }
-        return 0;
-    };
-    std::chrono::steady_clock::time_point tx0, tlast;
-    if (P == 2) {
-        wait_part(0);
-        for (int d = 0; d < N; d++)
-            if (rc[(size_t)d]) return rc[(size_t)d];
-        tx0 = std::chrono::steady_clock::now();
-        HIPCHK(hipSetDevice(phys[0]));
-        HIPCHK(hipEventRecord(top->ev2, top->xstream));
-        const int r = exchange_part(0);  // runs while the devices compute part 1
-        if (r) return r;
-        HIPCHK(hipSetDevice(phys[0]));
-        HIPCHK(hipEventRecord(top->ev3, top->xstream));
     }
-    join_all();
+    using clk = std::chrono::steady_clock;
+    std::vector<int> rc(N, 0);
+    std::vector<double> dwall((size_t)N, 0.0);
+    std::vector<unsigned long long> dmin((size_t)N, 0x7FF0000000000000ull);
+    std::vector<int64_t> drows((size_t)N, 0);
+    std::vector<clk::time_point> tdone((size_t)N), tpushed((size_t)N);
+    const auto tb = clk::now();
+    std::vector<std::thread> th;
+    for (int d = 0; d < N; d++)
+        th.emplace_back([&, d]() {
+            Topology* T = slot_engine(top, d);
+            auto run = [&]() -> int {
+                HIPCHK(hipSetDevice(phys[(size_t)d]));
+                int r = dev_init(T);
+                if (r) return r;
+                HIPCHK(hipSetDevice(phys[(size_t)d]));
+                const int64_t r0 = std::min(A, d * R), r1 = std::min(A, r0 + R);
+                if (r1 > r0) {
+                    r = enqueue_rows(T, r0, r1, T->d_lr.p + r0 * A, T->d_hops.p + r0 * A,
+                                     T->d_rowmin.p + r0, T->stream);
+                    if (r) return r;
+                    r = collect_row_stats(T);
+                    if (r) return r;
+                    HIPCHK(hipMemcpy(&dmin[(size_t)d], T->d_stats.p + ST_GLOBAL_MIN, 8, hipMemcpyDeviceToHost));
+                }
+                drows[(size_t)d] = r1 - r0;
+                tdone[(size_t)d] = clk::now();
+                if (push && r1 > r0) {  // this shard into every other device's table, now
+                    for (int e = 0; e < N; e++) {
+                        if (e == d) continue;
+                        Topology* S = slot_engine(top, e);
+                        const int pd = phys[(size_t)e], ps = phys[(size_t)d];
+                        const size_t n = (size_t)((r1 - r0) * A);
+                        HIPCHK(hipMemcpyPeerAsync(S->d_lr.p + r0 * A, pd, T->d_lr.p + r0 * A, ps, sizeof(double2) * n, T->xstream));
+                        HIPCHK(hipMemcpyPeerAsync(S->d_hops.p + r0 * A, pd, T->d_hops.p + r0 * A, ps, 2 * n, T->xstream));
+                        HIPCHK(hipMemcpyPeerAsync(S->d_rowmin.p + r0, pd, T->d_rowmin.p + r0, ps, 8 * (size_t)(r1 - r0), T->xstream));
+                    }
+                    HIPCHK(hipStreamSynchronize(T->xstream));
+                }
+                tpushed[(size_t)d] = clk::now();
+                return 0;
+            };
+            rc[(size_t)d] = run();
+            dwall[(size_t)d] = std::chrono::duration<double, std::milli>(clk::now() - tb).count();
+        });
+    for (auto& x : th) x.join();
     for (int d = 0; d < N; d++)
         if (rc[(size_t)d]) return rc[(size_t)d];
-    tlast = std::chrono::steady_clock::now();
-    if (P == 1) tx0 = tlast;
-    {
-        const int r = exchange_part(P - 1);
-        if (r) return r;
+    auto tfirst = tdone[0], tlast = tdone[0];
+    for (int d = 1; d < N; d++) {
+        tfirst = std::min(tfirst, tdone[(size_t)d]);
+        tlast = std::max(tlast, tdone[(size_t)d]);
     }
-    // the global minimum: every device's minimum over its rows of all parts, all-reduced
+    top->stats.exchange_kind = N > 1 || top->forceRccl ? (useRccl ? 1 : 2) : 0;
+    top->stats.exchange_bytes = (int64_t)(N - 1) * R * (A * (int64_t)(sizeof(double2) + 2) + 8);
     if (useRccl) {
-        for (int d = 0; d < N; d++) {
-            Topology* T = slot_engine(top, d);
-            HIPCHK(hipSetDevice(phys[(size_t)d]));
-            HIPCHK(hipMemcpyAsync(T->d_stats.p + ST_GLOBAL_MIN, &dmin[(size_t)d], 8, hipMemcpyHostToDevice, xs(T)));
-        }
         RcclApi& api = rccl();
         NCCLCHK(api.groupStart());
         for (int d = 0; d < N; d++) {
             Topology* T = slot_engine(top, d);
-            NCCLCHK(api.allReduce(T->d_stats.p + ST_GLOBAL_MIN, T->d_stats.p + ST_GLOBAL_MIN, 1, ncclUint64, ncclMin, top->comms[(size_t)d], xs(T)));
+            ncclComm_t c = top->comms[(size_t)d];
+            const size_t lrB = (size_t)(R * A) * sizeof(double2), hB = (size_t)(R * A) * 2;
+            NCCLCHK(api.allGather((const char*)T->d_lr.p + (size_t)d * lrB, T->d_lr.p, lrB, ncclUint8, c, T->stream));
+            NCCLCHK(api.allGather((const char*)T->d_hops.p + (size_t)d * hB, T->d_hops.p, hB, ncclUint8, c, T->stream));
+            NCCLCHK(api.allGather(T->d_rowmin.p + (size_t)d * (size_t)R, T->d_rowmin.p, (size_t)R, ncclFloat64, c, T->stream));
         }
         NCCLCHK(api.groupEnd());
-    } else {
-        unsigned long long gmin = 0x7FF0000000000000ull;
-        for (int d = 0; d < N; d++) gmin = std::min(gmin, dmin[(size_t)d]);
-        for (int d = 0; d < N; d++) dmin[(size_t)d] = gmin;  // (kept alive until the syncs below)
         for (int d = 0; d < N; d++) {
             Topology* T = slot_engine(top, d);
             HIPCHK(hipSetDevice(phys[(size_t)d]));
-            HIPCHK(hipMemcpyAsync(T->d_stats.p + ST_GLOBAL_MIN, &dmin[(size_t)d], 8, hipMemcpyHostToDevice, xs(T)));
+            HIPCHK(hipMemcpyAsync(T->d_stats.p + ST_GLOBAL_MIN, &dmin[(size_t)d], 8, hipMemcpyHostToDevice, T->stream));
+        }
+        NCCLCHK(api.groupStart());
+        for (int d = 0; d < N; d++) {
+            Topology* T = slot_engine(top, d);
+            NCCLCHK(api.allReduce(T->d_stats.p + ST_GLOBAL_MIN, T->d_stats.p + ST_GLOBAL_MIN, 1, ncclUint64, ncclMin, top->comms[(size_t)d], T->stream));
+        }
+        NCCLCHK(api.groupEnd());
+        for (int d = 0; d < N; d++) {
+            HIPCHK(hipSetDevice(phys[(size_t)d]));
+            HIPCHK(hipStreamSynchronize(slot_engine(top, d)->stream));
+        }
+    } else {
+        unsigned long long gmin = 0x7FF0000000000000ull;
+        for (int d = 0; d < N; d++) gmin = std::min(gmin, dmin[(size_t)d]);
+        for (int d = 0; d < N; d++) {
+            Topology* T = slot_engine(top, d);
+            HIPCHK(hipSetDevice(phys[(size_t)d]));
+            HIPCHK(hipMemcpy(T->d_stats.p + ST_GLOBAL_MIN, &gmin, 8, hipMemcpyHostToDevice));
         }
     }
-    for (int d = 0; d < N; d++) {
-        HIPCHK(hipSetDevice(phys[(size_t)d]));
-        HIPCHK(hipStreamSynchronize(xs(slot_engine(top, d))));
-    }
     HIPCHK(hipSetDevice(phys[0]));
-    const auto tx1 = std::chrono::steady_clock::now();
-    top->stats.exchange_ms = std::chrono::duration<double, std::milli>(tx1 - tx0).count();
-    top->stats.exchange_exposed_ms = std::chrono::duration<double, std::milli>(tx1 - tlast).count();
-    top->stats.exchange_part_ms[0] = top->stats.exchange_part_ms[1] = 0.0;
-    if (P == 2) {
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, top->ev2, top->ev3));
-        top->stats.exchange_part_ms[0] = ms;  // slot 0's stream time of part 0's exchange
-    }
+    auto tend = clk::now();
+    if (push)
+        for (int d = 0; d < N; d++) tend = std::max(tend, tpushed[(size_t)d]);
+    const auto tx0 = useRccl ? tlast : tfirst;
+    top->stats.exchange_ms = std::chrono::duration<double, std::milli>(tend - tx0).count();
+    top->stats.exchange_exposed_ms = std::chrono::duration<double, std::milli>(tend - tlast).count();
     unsigned long long gm = 0;
     HIPCHK(hipMemcpy(&gm, top->d_stats.p + ST_GLOBAL_MIN, 8, hipMemcpyDeviceToHost));
     double g;
@@ -2704,9 +2608,7 @@ int ensure_table(Topology* top) {
     for (Topology* p : top->peers) runs0 += p->csrHostRuns;
     top->stats.devices = 1;
     top->stats.exchange_ms = top->stats.exchange_exposed_ms = 0.0;
-    top->stats.exchange_part_ms[0] = top->stats.exchange_part_ms[1] = 0.0;
     top->stats.exchange_bytes = 0;
-    top->stats.exchange_split = 0;
     if (A > 0 && (top->devicesOpt > 1 || top->forceRccl)) {
         r = build_multi(top);
         if (r) return r;
@@ -3403,8 +3305,12 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "target_skip") top->targetSkip = value != 0;
     else if (k == "target_kappa") top->targetKappa = (int)value;
     else if (k == "target_resort") top->targetResort = value != 0;
-    else if (k == "exchange_split") top->xchgSplit = std::max(1, std::min(2, (int)value));
-    else if (k == "exchange_cus") top->xchgCus = std::max(0, (int)value);
+    else if (k == "exchange") {
+        const int m = (int)value;
+        if (m < 0 || m > 2) return -1;
+        top->xchgMode = m;
+        top->tableValid.store(false);
+    }
     else if (k == "devices") {
         const int n = (int)value;
         if (n < 1 || n > 64) return -1;

@@ -262,7 +262,7 @@ class Topology:
         out["build_step_ms"] = list(out["build_step_ms"])
         out["walk_kinds"] = list(out["walk_kinds"])
         for k in ("device_kernel_ms", "device_build_ms", "device_rows", "attach_prep_step_ms",
-                  "sweep_events", "write_lines", "read_lines", "exchange_part_ms"):
+                  "sweep_events", "write_lines", "read_lines"):
             out[k] = list(out[k])
         out["events"] = dict(zip(("expanded", "tail_relax", "tail_improve", "window_taken",
                                   "overflow_refilled", "parent_vertices", "tail_settled_relax",

@@ -119,7 +119,7 @@ def test_multi_device_build_prepares_the_graph_once(devices):
     top.build()
     st = top.stats()
     assert st["devices"] == devices and st["csr_host_runs"] == 1 and st["csr_ms"] > 0
-    assert st["exchange_kind"] == 2  # engines sharing the test box's one device: peer copies
+    assert st["exchange_kind"] == 2  # engines sharing the test box's one device: push copies
     top.rebuild()
     st = top.stats()
     assert st["csr_host_runs"] == 0 and st["csr_ms"] == 0
@@ -236,9 +236,9 @@ def test_complete_branch_devices8_equals_oracle(name, devices):
 @pytest.mark.timeout(600)
 def test_full_size_c4_devices8_equals_devices1():
     """BASELINE config 4 at full size (1M vertices / 10M edges, 10,000 x
-    10,000 table) built by 8 engines -- rows sharded in two parts per device, part 0 exchanged on
-    the exchange streams while part 1 computes (option exchange_split, default 2).  On the
-    one-GPU test box the engines share the device and exchange with device copies.  The table
+    10,000 table) built by 8 engines -- rows sharded over them, each shard pushed into the other
+    engines' tables as soon as it is done (exchange_kind 2; on the one-GPU test box the engines
+    share the device, so RCCL is not possible and the push is the exchange).  The table
     must equal the devices = 1 table bit for bit (latency, reliability and hops hashed),
     getMinimumLatency must be equal (the all-reduced minimum, shd-master.c:113-124), and 16 seeded
     rows must equal the oracle's Dijkstra + helper."""
@@ -251,7 +251,7 @@ def test_full_size_c4_devices8_equals_devices1():
     top.set_option("devices", 8)
     a8, lat8, rel8, hop8 = top.table()
     st = top.stats()
-    assert st["devices"] == 8 and st["exchange_split"] == 2 and st["errors"] == 0
+    assert st["devices"] == 8 and st["exchange_kind"] == 2 and st["errors"] == 0
     assert sum(st["device_rows"]) == A and st["exchange_exposed_ms"] <= st["exchange_ms"]
     m8 = top.getMinimumLatency()
     digest = lambda *xs: hashlib.sha256(b"".join(x.tobytes() for x in xs)).hexdigest()
