@@ -9,7 +9,7 @@ OUT=$1; shift
 ROOT=$(pwd)
 mkdir -p "$OUT"
 # (--no-directed: the C4-dir line's kernels would add their dispatches to the same kernel names)
-BENCH_ARGS=(--steps 1 --warmup 0 --no-cpu-baseline --no-graphml --no-complete --no-directed --route-steps 3 "$@")
+BENCH_ARGS=(--steps 1 --warmup 0 --no-cpu-baseline --no-graphml --no-complete --no-directed --route-steps 3 --getter-queries 0 "$@")
 LIMIT=${PROF_LIMIT:-240}
 cd /tmp && export TMPDIR=/tmp
 pass() {
