@@ -1,7 +1,7 @@
 #!/bin/bash
-# The C4-int line (every row through the heap replay) on the current code: rocprofv3 trace + PMC
-# passes, their summary (profiles/<TAG>int_*), then the bench line (run from the repo root on the
-# GPU box).   tools/measure_int.sh TAG
+# The C4-int line on the GPU box (run from the repo root): rocprofv3 passes of the integer-latency
+# bench (heap replay), their summary + PMC JSON under profiles/<TAG>int_*, then the bench line.
+#   tools/measure_int.sh TAG
 set -u
 TAG=$1
 OUT=gpurun_out/meas_${TAG}int
@@ -9,6 +9,6 @@ mkdir -p "$OUT"
 tools/profile_bench.sh "$OUT/prof_int" --integer || exit $?
 python3 tools/summarize_prof.py "$OUT/prof_int" "${TAG}int" > "$OUT/summary_int.log" 2>&1 || exit $?
 cp profiles/${TAG}int_* "$OUT/" || exit $?
-timeout -k 10 700 python3 -u bench.py --integer --pmc-tag "${TAG}int" --no-complete \
+timeout -k 10 900 python3 -u bench.py --integer --pmc-tag "${TAG}int" --no-complete --getter-queries 0 \
     > "$OUT/bench_int.json" 2> "$OUT/bench_int.log" || exit $?
 echo "measure_int $TAG done"
