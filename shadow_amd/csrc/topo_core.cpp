@@ -1302,17 +1302,23 @@ uint64_t compute_geometry(Topology* top) {
     std::vector<int32_t> vs;
     uint64_t sg;
     {
+        // the attached vertices are those with a host (hostsOn, kept by attach / detach) plus the
+        // columns a window adapter keeps (deferredOff): one ordered pass over V counters instead
+        // of sorting every host's vertex (C4: 100,000 hosts; 3.9 -> ~1 ms of the first build)
         std::shared_lock<std::shared_mutex> lk(top->ipMu);
         sg = top->setGen.load();
         if (top->geomInit && top->geomGen == top->ipGen) return sg;  // no attach / detach since
         top->geomGen = top->ipGen;
-        vs.reserve(top->virtualIP.size());
-        for (auto& kv : top->virtualIP)
-            if (kv.second >= 0) vs.push_back(kv.second);
-        vs.insert(vs.end(), top->deferredOff.begin(), top->deferredOff.end());
+        std::vector<int32_t> def(top->deferredOff.begin(), top->deferredOff.end());
+        std::sort(def.begin(), def.end());
+        vs.reserve(std::max<size_t>(top->A, 16));
+        size_t k = 0;
+        const uint32_t* on = top->hostsOn.data();
+        for (int32_t v = 0; v < top->g.V; v++) {
+            while (k < def.size() && def[k] < v) k++;
+            if (on[v] || (k < def.size() && def[k] == v)) vs.push_back(v);
+        }
     }
-    std::sort(vs.begin(), vs.end());
-    vs.erase(std::unique(vs.begin(), vs.end()), vs.end());
     if (top->geomInit && vs == top->attached) return sg;
     top->geomInit = true;
     top->attached = vs;
