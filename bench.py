@@ -43,7 +43,7 @@ from shadow_amd import sharding  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SEED = 20261015
-PROFILE_TAG = "r06a"           # profiles/<tag>_*_pmc.json: the committed counter passes
+PROFILE_TAG = "r06b"           # profiles/<tag>_*_pmc.json: the committed counter passes
 
 
 def log(rank, *a):
@@ -659,6 +659,7 @@ def main():
             roofline["model_batched"] = batched_model(st, rows * A, k_ms, roofline.get("traffic"))
         sssp = dict(kernel=roofline["kernel"], batch=K, lds_hubs=int(st["lds_hubs"]),
                     sweeps=int(st["far_splits"]), slots=st["slots"],
+                    workspace_gb=round(st["workspace_bytes"] / 1e9, 2),
                     batch_fill=int(st["batch_fill"]),
                     phase_ms_per_source=[round(x / max(1, rows), 3) for x in st["phase_ms"]],
                     parent_phase_ms_per_source=[round(x / max(1, rows), 3)

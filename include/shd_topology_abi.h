@@ -106,7 +106,8 @@ Topology* shdtopo_new_from_buffer(const char* graphml, size_t len);
  * gap of min(1 % of delta, half the smallest edge latency) below it; < 0: the round-4 bucket
  * shifts), "slots" (concurrent SSSP
  * workgroups), "device" (HIP device ordinal), "lds_hubs" (cap on LDS-resident hub distances,
- * -1 = fill), "par_hubs" (hubs with SSSP parent hints), "wg_per_cu" (SSSP workgroups sharing a
+ * -1 = fill), "par_hubs" (hubs with SSSP parent hints), "row_scan_chunk" (parent-pass pairs
+ * per row-scan chunk, 64..2^20, default 16384: 16 B x batch of workspace per pair), "wg_per_cu" (SSSP workgroups sharing a
  * CU's LDS), "far_cap" / "near_cap" (entries per window bucket and overflow pile / per near
  * queue, 0 = sized from V; small values force the scanning fallback), "events" (1 = diagnostic
  * kernel with event counters), "tie_replay" (1: rows whose target chains cross a d-tied parent
@@ -385,6 +386,7 @@ typedef struct {
     double exchange_exposed_ms; /* the last multi-device build: wall time from the last shard's
                                    rows to the end of the exchange (the part of exchange_ms no
                                    kernel hid; exchange_kind 2 overlaps the slower shards) */
+    int64_t workspace_bytes;    /* HBM held by the batched SSSP's workspace (all slots) */
 } ShdStats;
 int shdtopo_get_stats(Topology* top, ShdStats* out);
 

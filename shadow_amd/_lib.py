@@ -61,7 +61,7 @@ class ShdStats(ctypes.Structure):
                 ("path_seconds_total", dbl), ("paths_computed", i64),
                 ("batch_layout_measured", i64), ("batches", i64), ("rows_to_host", i64),
                 ("rows_to_host_ms", dbl), ("prep_trigger", i64),
-                ("exchange_exposed_ms", dbl)]
+                ("exchange_exposed_ms", dbl), ("workspace_bytes", i64)]
 
 
 class ShdSynthParams(ctypes.Structure):

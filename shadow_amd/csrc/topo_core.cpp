@@ -211,6 +211,7 @@ struct _Topology {
     int device = 0;
     int64_t hubLimit = -1;  // LDS-cached hub distances (-1 = fill the LDS)
     int64_t parHubs = 2048; // hubs whose parent is hinted during the SSSP (0 = always scan)
+    uint32_t rsChunk = kRowScanCap;  // pairs per parent-pass row-scan chunk
     int batchK = 8;         // sources per SSSP workgroup (sssp_batch_kernel<K>, K in {2,4,8,16})
     uint32_t iterGuard = 4000000u;  // near iterations per batch before the kernel gives up
                                     // (option "iter_guard": a test hook for the -4 error path)
@@ -293,6 +294,7 @@ struct _Topology {
                                 // launch with fewer LDS hubs refills [H, wsHubRows) with +inf
     int64_t wsRing = 0;
     size_t wsHpar = 0;          // hub-hint entries per slot the workspace was sized for
+    uint32_t wsRsChunk = 0;     // row-scan chunk the workspace was sized for
     DevBuf<uint32_t> d_rowptr, d_adj;
     // directed topologies: d_rowptr / d_adjo are the out-rows (relaxation, kappa copy, target
     // fixpoint), d_rowptrIn / d_adj / d_aloss the in-rows (parent pass); undirected ones use
@@ -304,11 +306,12 @@ struct _Topology {
     double minLat = 0.0;  // smallest non-loop edge latency (edge_scan): the landmark's bucket gap
     uint64_t ipGen = 1, geomGen = 0;  // attach/detach generation; compute_geometry's copy  // mean non-loop edge latency (default delta), computed once
     DevBuf<double> d_aloss, d_vloss, d_selfLat, d_selfLoss;
-    DevBuf<unsigned long long> d_dist, d_best, d_qa, d_qb;
+    DevBuf<unsigned long long> d_dist, d_qa, d_qb;
     DevBuf<uint32_t> d_ring;
     DevBuf<uint4> d_prec;  // per (vertex, source) pair records of the parent pass
     DevBuf<double> d_pathbuf;
-    DevBuf<uint32_t> d_cnt, d_bslot, d_counters;
+    DevBuf<uint32_t> d_counters;
+    DevBuf<uint4> d_rscan;  // parent pass row-scan records, rsChunk x K per slot
     int slots = 0;
     DevBuf<double2> d_lr;
     DevBuf<uint16_t> d_hops;
@@ -1035,9 +1038,8 @@ int64_t queue_stride(Topology* top, int K) {  // u64 per slot of each near queue
 // whose builds run only the heap replay: its HBM then holds more replay rows at once).
 void release_workspace(Topology* top) {
     if (top->slots <= 0) return;
-    top->d_dist.release(); top->d_ring.release(); top->d_best.release();
-    top->d_prec.release(); top->d_cnt.release();
-    top->d_bslot.release(); top->d_pathbuf.release();
+    top->d_dist.release(); top->d_ring.release(); top->d_rscan.release();
+    top->d_prec.release(); top->d_pathbuf.release();
     top->d_qa.release(); top->d_qb.release(); top->d_mask.release(); top->d_hpar.release();
     top->slots = 0;
 }
@@ -1057,12 +1059,12 @@ int ensure_workspace(Topology* top, int nsrc) {
     const size_t maskb = 2 * (((size_t)V * (K <= 8 ? 1 : 2) + 255) / 256 * 256);
     const int64_t ringE = ring_entries(top, K);
     const size_t hparN = (size_t)std::min<int64_t>(top->parHubs, 1 << 20) * K;
-    // dist (K words/vertex), per-(vertex, source) pair record 16 B + best/cnt/bslot 16 B, the
-    // queues, the u32 scratch, masks, hub hints, path buffer
+    // dist (K words/vertex), per-(vertex, source) pair record 16 B, the queues, the u32 scratch,
+    // masks, hub hints, path buffer, the row-scan records (16 B per pair of a chunk)
     const int64_t qs = queue_stride(top, K);
-    const size_t per_slot = (size_t)V * (8 * (size_t)K + 32 * (size_t)K) + 16 * (size_t)qs +
+    const size_t per_slot = (size_t)V * (8 * (size_t)K + 16 * (size_t)K) + 16 * (size_t)qs +
                             (size_t)ringE * 4 + maskb + 4 * hparN +
-                            kPathBufPerSlot * 8 + 16;
+                            kPathBufPerSlot * 8 + 16 * (size_t)top->rsChunk * K + 16;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     // memory already held by this workspace counts as available
@@ -1079,20 +1081,21 @@ int ensure_workspace(Topology* top, int nsrc) {
     if (top->balance)
         HIPCHK(top->d_btrace.ensure((size_t)std::max<int64_t>(1, std::min<int64_t>(nsrc, V)) * kBTraceWords));
     // hparN follows par_hubs: the kernel indexes the hints at slot * P * K with the current P
-    if (top->slots >= want && top->wsK == K && top->wsRing == ringE && top->wsHpar >= hparN)
+    if (top->slots >= want && top->wsK == K && top->wsRing == ringE && top->wsHpar >= hparN &&
+        top->wsRsChunk == top->rsChunk) {
+        top->stats.workspace_bytes = (int64_t)((size_t)top->slots * per_slot);
         return 0;
+    }
     const auto tw0 = std::chrono::steady_clock::now();
     release_workspace(top);  // a layout change: released before re-allocating
     const size_t n = (size_t)want * (size_t)V;
     const size_t pn = n * (size_t)K;  // per-(vertex, source) arrays
     HIPCHK(top->d_dist.ensure(pn));
-    HIPCHK(top->d_best.ensure(pn));
     HIPCHK(top->d_prec.ensure(pn));
     HIPCHK(top->d_qa.ensure((size_t)want * (size_t)qs));
     HIPCHK(top->d_qb.ensure((size_t)want * (size_t)qs));
     HIPCHK(top->d_ring.ensure((size_t)want * (size_t)ringE));
-    HIPCHK(top->d_cnt.ensure(pn));
-    HIPCHK(top->d_bslot.ensure(pn));
+    HIPCHK(top->d_rscan.ensure((size_t)want * top->rsChunk * K));
     HIPCHK(top->d_pathbuf.ensure((size_t)want * kPathBufPerSlot));
     HIPCHK(top->d_counters.ensure((size_t)want * 4));
     HIPCHK(top->d_mask.ensure((size_t)want * maskb));
@@ -1112,7 +1115,9 @@ int ensure_workspace(Topology* top, int nsrc) {
     top->wsHubRows = 0;  // every row +inf
     top->wsRing = ringE;
     top->wsHpar = hparN;
+    top->wsRsChunk = top->rsChunk;
     top->stats.slots = want;
+    top->stats.workspace_bytes = (int64_t)((size_t)want * per_slot);
     top->stats.workspace_ms = std::chrono::duration<double, std::milli>(
         std::chrono::steady_clock::now() - tw0).count();
     return 0;
@@ -1137,7 +1142,8 @@ SlotWs slot_ws(Topology* top) {
     w.V = top->g.V;
     w.dist = top->d_dist.p; w.prec = top->d_prec.p;
     w.qa = top->d_qa.p; w.qb = top->d_qb.p; w.ring = top->d_ring.p;
-    w.best = top->d_best.p; w.cnt = top->d_cnt.p; w.bslot = top->d_bslot.p;
+    w.rscan = top->d_rscan.p;
+    w.rs_chunk = top->wsRsChunk;
     w.pathbuf = top->d_pathbuf.p;
     w.counters = top->d_counters.p;
     w.K = top->wsK;
@@ -2241,6 +2247,7 @@ void sync_peer(Topology* top, Topology* p) {
     p->slotsOpt = top->slotsOpt;
     p->hubLimit = top->hubLimit;
     p->parHubs = top->parHubs;
+    p->rsChunk = top->rsChunk;
     p->batchK = top->batchK;
     p->iterGuard = top->iterGuard;
     p->tieReplay = top->tieReplay;
@@ -3286,6 +3293,10 @@ int shdtopo_set_option(Topology* top, const char* key, double value) {
     else if (k == "prepare_on_attach") top->prepOnAttach = value != 0;
     else if (k == "lds_hubs") top->hubLimit = (int64_t)value;
     else if (k == "par_hubs") top->parHubs = (int64_t)value;
+    else if (k == "row_scan_chunk") {
+        if (!(value >= 64 && value <= (double)(1 << 20))) return -1;
+        top->rsChunk = (uint32_t)value;
+    }
     else if (k == "batch") {
         const int b = (int)value;
         if (b != 2 && b != 4 && b != 8 && b != 16) return -1;

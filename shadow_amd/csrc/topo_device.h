@@ -27,6 +27,11 @@ constexpr int kBatchWgPerCu = SHD_BATCH_WGPCU;  // batch-kernel workgroups per C
 constexpr int kMaxHops = 48;      // per-thread path buffer depth (longer paths: O(h^2) walk)
 // doubles of the batch kernel's path buffer per slot: the chain losses [kMaxHops][kSsspBlock]
 constexpr size_t kPathBufPerSlot = (size_t)kMaxHops * kSsspBlock;
+// parent pass: pairs of one row-scan chunk by default (records per slot: chunk x K, one per
+// merged vertex and source; C4 sends ~2.6 k pairs per level of a batch to row scans)
+constexpr uint32_t kRowScanCap = 16384;
+// the candidate count of a row-scan record no pair asked for
+constexpr uint32_t kRsUnreq = 0xFFFFFFFEu;
 #ifndef SHD_KAP_IN_REC
 #define SHD_KAP_IN_REC 1
 #endif
@@ -136,9 +141,10 @@ struct SlotWs {
     unsigned long long* qb = nullptr;
     uint32_t* ring = nullptr;            // ring_entries u32 per slot: parent pair list, vertex
                                          // list, pending bitmap, tie bitmap
-    unsigned long long* best = nullptr;  // parent pass: min d[u] over candidates
-    uint32_t* cnt = nullptr;             // parent pass: candidates at the min
-    uint32_t* bslot = nullptr;           // parent pass: lowest adjacency slot at the min
+    uint4* rscan = nullptr;              // parent pass, rs_chunk x K per slot: per (merged vertex,
+                                         // source) of a row-scan chunk {min d[u] over the candidates
+                                         // (u64), candidates at the min, lowest adjacency slot}
+    uint32_t rs_chunk = kRowScanCap;     // pairs per row-scan chunk (option "row_scan_chunk")
     double* pathbuf = nullptr;           // [slot][kPathBufPerSlot]: edge losses of a path
     uint32_t* counters = nullptr;        // [slot][4]: batch tag, (unused)
     int K = 8;

@@ -139,6 +139,7 @@ struct LdsB {
     unsigned long long rl[16];
     // jobs (a level's walks, the epilogue): the cursor of the current job's items
     uint32_t jcur;
+    uint32_t rsb;  // parent pass: the current row-scan chunk's first R entry
 };
 
 // Write categories of SHD_BATCH_WRCOUNT builds (ShdStats.write_lines): each store / atomic
@@ -156,7 +157,7 @@ enum {
     WL_RESET,        // touched distance lines reset to +inf
     WL_TOUCH_CLR,    // touched words cleared
     WL_PREC,         // pair records (walk puts, tags, hint puts, row-scan results)
-    WL_PSCR,         // parent-pass scratch (best / cnt / bslot, row-scan vertex masks)
+    WL_PSCR,         // parent-pass scratch (row-scan records, row-scan vertex masks)
     WL_OUT,          // table rows, hops, row minima, row flags
     WL_HUB,          // hub rows copied to their dist rows, hub parent hints
     WL_QUEUE,        // queue / list appends (near queues, hub lists, pair lists)
@@ -964,12 +965,10 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
     // parent-pass state per (vertex, source) pair q = v * K + j: the pair record {parent vertex
     // (| amb << 31 | bad << 30), claim tag (the batch that resolved it), f64 loss of the parent
     // edge} -- one 16-B line access per hop of a walk or of the epilogue -- and the row-scan
-    // scratch best / cnt / bslot
+    // (the row scans' records: ws.rscan, rs_chunk K per slot -- round 5 kept [V][K] arrays of
+    // them per slot, 32 GB at C4)
     uint4* prec = ws.prec + (size_t)slot * V * K;
     uint32_t* precw = reinterpret_cast<uint32_t*>(prec);
-    unsigned long long* best = ws.best + (size_t)slot * V * K;
-    uint32_t* cntc = ws.cnt + (size_t)slot * V * K;
-    uint32_t* bslot = ws.bslot + (size_t)slot * V * K;
     D.tpar = precw;
     double* pbuf = ws.pathbuf + (size_t)slot * kPathBufPerSlot;
     uint32_t* ctr = ws.counters + (size_t)slot * 4;
@@ -1821,32 +1820,31 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                         if (bh) atomicAdd(&L.wk[3], (unsigned long long)__popcll(bh));
                         if (bs) atomicAdd(&L.wk[4], (unsigned long long)__popcll(bs));
                     }
-                    if (in && scan[h]) {
-                        wl_count(L, WL_PSCR, true, best + q);
-                        wl_count(L, WL_PSCR, true, cntc + q);
-                        wl_count(L, WL_PSCR, true, bslot + q);
-                        best[q] = kInfBits;
-                        cntc[q] = 0;
-                        bslot[q] = 0xFFFFFFFFu;
-                    }
                     wpush<K>(L, in && scan[h], q, pcur, &L.qtail, pcap, &L.fover, 128u);
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             const uint32_t nR = min(L.qtail, pcap);
-            const uint32_t* rl = pcur;
             __syncthreads();
-            if (nR > 0) {
-                // merge the unresolved pairs by vertex (masks in mA / hdef, zero after the SSSP): a
-                // vertex's row is scanned once for every source whose chain needs it
+            // R in chunks of ws.rs_chunk pairs (C4: ~2.6 k per level of a batch, one chunk)
+            if (tid == 0) L.rsb = 0;
+            __syncthreads();
+            for (;;) {
+                const uint32_t rb = L.rsb;
+                if (rb >= nR) break;
+                const uint32_t nc = min(ws.rs_chunk, nR - rb);
+                const uint32_t* rl = pcur + rb;
+                uint4* const rs = ws.rscan + (size_t)slot * ws.rs_chunk * K;
+                // merge the pairs by vertex (masks in mA / hdef, zero after the SSSP): a vertex's
+                // row is scanned once for every source whose chain needs it
                 if (tid == 0) L.qtail = 0;
                 __syncthreads();
-                for (uint32_t ib = 0; ib < nR; ib += kSsspBlock) {
+                for (uint32_t ib = 0; ib < nc; ib += kSsspBlock) {
                     const uint32_t i = ib + tid;
                     bool first = false;
                     uint32_t v = 0;
-                    if (i < nR) {
+                    if (i < nc) {
                         const uint32_t q = rl[i];
                         v = q / K;
                         wl_count(L, WL_PSCR, v >= H, mA + v);
@@ -1857,6 +1855,31 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 const uint32_t nVs = min(L.qtail, cap);
+                __syncthreads();
+                // one scan record per (merged vertex p, source j): x = p K + j (a pair listed twice
+                // has one); a requested record starts at {+inf, 0 candidates, no slot} and its
+                // index is parked in the pair record's third word (read back by the recount), an
+                // unrequested one is marked kRsUnreq
+                for (uint32_t x = tid; x < nVs * K; x += kSsspBlock) {
+                    const uint32_t v = vscr[x / K];
+                    const uint32_t j = x % K;
+                    const uint32_t m = v < H ? (reinterpret_cast<const uint32_t*>(hdef)[v / MO::kPer] >>
+                                                ((v % MO::kPer) * MO::kBits)) & MO::kFull
+                                             : MO::get_l2(mA, v);
+                    const bool req = (m >> j) & 1u;
+                    wl_count(L, WL_PSCR, true, rs + x);
+                    {  // {best, candidates | lowest slot << 32}
+                        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+                        const u64x2 z = {req ? kInfBits : 0ull,
+                                         0xFFFFFFFF00000000ull | (req ? 0u : kRsUnreq)};
+                        __builtin_nontemporal_store(z, reinterpret_cast<u64x2*>(rs + x));
+                    }
+                    if (req) {
+                        wl_count(L, WL_PREC, true, precw + 4 * ((size_t)v * K + j) + 2);
+                        precw[4 * ((size_t)v * K + j) + 2] = x;
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 // one pass over the merged rows: a lane per edge reads the neighbour's K distances
                 // (one line) and tests every source of the row's mask
@@ -1885,16 +1908,14 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                                 du[2 * q + 1] = x.y;
                             }
                         }
+                        uint4* const rv = rs + (size_t)(base + (uint32_t)lo) * K;
 #pragma unroll
                         for (int q = 0; q < K; q++) {
                             if (((m >> q) & 1u) && __dadd_rn(bits2d(du[q]), wt) == L.val[lo * K + q]) {
-                                const uint32_t pq = L.vx[lo] * K + (uint32_t)q;
-                                wl_count(L, WL_PSCR, true, best + pq);
-                                wl_count(L, WL_PSCR, true, cntc + pq);
-                                wl_count(L, WL_PSCR, true, bslot + pq);
-                                atomicMin(&best[pq], du[q]);
-                                atomicAdd(&cntc[pq], 1u);
-                                atomicMin(&bslot[pq], jr);
+                                wl_count(L, WL_PSCR, true, rv + q);
+                                atomicMin(reinterpret_cast<unsigned long long*>(rv + q), du[q]);
+                                atomicAdd(reinterpret_cast<uint32_t*>(rv + q) + 2, 1u);
+                                atomicMin(reinterpret_cast<uint32_t*>(rv + q) + 3, jr);
                             }
                         }
                     }
@@ -1903,21 +1924,23 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                 }
                 if (tid == 0) L.pt[2] += wall_clock64() - tp0;  // merged row scans
                 tp0 = wall_clock64();
+                // (L1-bypassing reads of the records below: atomics of other waves updated them)
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
                 // pairs with several candidates: recount at the minimum
                 if (tid == 0) L.qtail = 0;
                 __syncthreads();
-                for (uint32_t ib = 0; ib < nR; ib += kSsspBlock) {
-                    const uint32_t i = ib + tid;
+                for (uint32_t xb = 0; xb < nVs * K; xb += kSsspBlock) {
+                    const uint32_t x = xb + tid;
                     bool multi = false;
                     uint32_t q = 0;
-                    if (i < nR) {
-                        q = rl[i];
-                        multi = ld_l2_u32(&cntc[q]) > 1u;
-                        wl_count(L, WL_PSCR, multi, cntc + q);
-                        wl_count(L, WL_PSCR, multi, bslot + q);
+                    if (x < nVs * K) {
+                        const uint32_t c = ld_l2_u32(reinterpret_cast<const uint32_t*>(rs + x) + 2);
+                        multi = c > 1u && c != kRsUnreq;
+                        wl_count(L, WL_PSCR, multi, rs + x);
                         if (multi) {
-                            atomicExch(&cntc[q], 0u);
-                            atomicExch(&bslot[q], 0xFFFFFFFFu);
+                            q = vscr[x / K] * K + x % K;
+                            atomicExch(reinterpret_cast<uint32_t*>(rs + x) + 2, 0u);
+                            atomicExch(reinterpret_cast<uint32_t*>(rs + x) + 3, 0xFFFFFFFFu);
                         }
                     }
                     wpush<K>(L, multi, q, pnxt, &L.qtail, pcap, &L.fover, 128u);
@@ -1934,19 +1957,25 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                             double wt;
                             adj_load(g, jr, u, wt);
                             const unsigned long long du = D.get(u, q % K);
-                            const bool hit = __dadd_rn(bits2d(du), wt) == dv && du == ld_l2_u64(&best[q]);
-                            wl_count(L, WL_PSCR, hit, cntc + q);
-                            wl_count(L, WL_PSCR, hit, bslot + q);
+                            uint4* const r = rs + ld_l2_u32(&precw[4 * (size_t)q + 2]);
+                            const bool hit = __dadd_rn(bits2d(du), wt) == dv &&
+                                             du == ld_l2_u64(reinterpret_cast<const unsigned long long*>(r));
+                            wl_count(L, WL_PSCR, hit, r);
                             if (hit) {
-                                atomicAdd(&cntc[q], 1u);
-                                atomicMin(&bslot[q], jr);
+                                atomicAdd(reinterpret_cast<uint32_t*>(r) + 2, 1u);
+                                atomicMin(reinterpret_cast<uint32_t*>(r) + 3, jr);
                             }
                         });
                 }
-                for (uint32_t i = tid; i < nR; i += kSsspBlock) {
-                    const uint32_t q = rl[i];
-                    const uint32_t jr = ld_l2_u32(&bslot[q]);
-                    const uint32_t c = ld_l2_u32(&cntc[q]);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                // each requested record stores its pair record (once per pair)
+                for (uint32_t x = tid; x < nVs * K; x += kSsspBlock) {
+                    const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rs + x));
+                    if (r.z == kRsUnreq) continue;
+                    const uint32_t q = vscr[x / K] * K + x % K;
+                    const uint32_t jr = r.w;
+                    const uint32_t c = r.z;
                     wl_count(L, WL_PREC, true, prec + q);
                     if (jr == 0xFFFFFFFFu) {  // unreachable (cannot happen on a connected graph)
                         atomicAdd(&stats[ST_ERRORS], 1ull);
@@ -1958,9 +1987,16 @@ sssp_batch_kernel(DevCSR g, SlotWs ws, const uint32_t* __restrict__ sources,
                     }
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) {
+                    L.pt[3] += wall_clock64() - tp0;  // recount + finalize
+                    L.rsb = rb + ws.rs_chunk;
+                }
+                tp0 = wall_clock64();
+                __syncthreads();
             }
             __syncthreads();
-            if (tid == 0) L.pt[3] += wall_clock64() - tp0;  // recount + finalize
+            if (tid == 0) L.pt[3] += wall_clock64() - tp0;
             tp0 = wall_clock64();
             // the scanned pairs' parents continue as walks
             if (tid == 0) L.qtail = 0;

@@ -659,6 +659,40 @@ def test_repeated_one_round_builds_equal_oracle(integer):
 
 
 @pytest.mark.parametrize("integer", [False, True])
+def test_row_scans_in_small_chunks_equal_oracle(integer):
+    """The parent pass scans the rows of the pairs whose recorded parents failed (R) in chunks of
+    row_scan_chunk pairs, with one scan record per (merged vertex, source) of a chunk (round 6:
+    the [V][K] best / cnt / bslot arrays, 32 GB at C4, became 16 B x K per pair of a chunk).
+    With no hub parent hints (par_hubs 0: every hub pair is scanned) and 64-pair chunks, a level
+    takes many chunks and a vertex's sources fall into several; the tables equal the default
+    chunk's and the oracle's, bit for bit."""
+    top, g = synthetic_pair(seed=53, n_routers=20000, n_poi=300, n_edges=200000, integer=integer)
+    top.set_option("tie_dense", 0)
+    top.set_option("par_hubs", 0)
+    otop, ips, verts = attach_hosts(top, g, 900, type_hints=["client", "relay", "server"])
+    a0, lat0, rel0, hops0 = top.table()
+    st = top.stats()
+    assert st["errors"] == 0
+    n_batches = (len(verts) + 7) // 8
+    # pairs sent to row scans: several 64-pair chunks per batch
+    assert st["walk_kinds"][3] > 2 * 64 * n_batches, st["walk_kinds"]
+    with pytest.raises(KeyError):
+        top.set_option("row_scan_chunk", 63)
+    top.set_option("row_scan_chunk", 64)
+    top.rebuild()
+    a, lat, rel, hops = top.table()
+    assert top.stats()["errors"] == 0
+    assert np.array_equal(a, a0)
+    assert np.array_equal(lat.view(np.uint64), lat0.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), rel0.view(np.uint64))
+    assert np.array_equal(hops, hops0)
+    oa, olat, orel, ohops = g.table(verts)
+    assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+    assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+    assert np.array_equal(hops, ohops.astype(np.uint16))
+
+
+@pytest.mark.parametrize("integer", [False, True])
 def test_bucket_width_and_landmark_phase_do_not_change_the_table(integer):
     """Option delta (bucket width) and h0_phase (where the landmark h0 sits in its bucket; < 0 the
     round-4 shifts) change only the order of the label-correcting work, not the fixpoint: tables
