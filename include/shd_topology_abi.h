@@ -304,8 +304,9 @@ typedef struct {
     double csr_step_ms[8];      /* graph preparation steps (wall): upload of the parsed edges,
                                    degrees + relabel, adjacency rows, h0 distances, h0 tree +
                                    record fields, kappa-sorted copy, host copies out, (unused) */
-    double module_load_ms;      /* device init: loading the kernels' code objects (once per
-                                   engine, before its first build) */
+    double module_load_ms;      /* device init: loading the kernels' code objects and the first
+                                   segmented sort's host setup (once per engine, before its
+                                   first build) */
     double build_wall_ms;       /* wall time of the last whole-table build (topology_getLatency's
                                    lazy build, shdtopo_build / shdtopo_rebuild) */
     int64_t walk_steps;         /* parent-pass walk steps (pairs resolved) of the last build */
@@ -399,6 +400,14 @@ int shdtopo_get_stats(Topology* top, ShdStats* out);
  * when no layout applies (the build then keeps the grouping order).  Host-only: no device use. */
 int shdtopo_test_batch_layout(const double* cost, int64_t rows, double fixed, int fill, int slots,
                               int batch, uint32_t* order, uint32_t* starts, int64_t* nbatches);
+
+/* Test hook: the segmented sort of the target-aware re-sort on HIP device 0 -- nseg rows
+ * (rowptr u32[nseg + 1] over n f32 keys) each sorted ascending and stably; keys_out receives the
+ * sorted keys, idx_out their input positions.  reference = 1 runs the whole-adjacency hipcub
+ * segmented radix sort the library's kernels replace (the order they must reproduce).  Returns 0,
+ * -1 on bad arguments, or a HIP error. */
+int shdtopo_test_segsort(const uint32_t* rowptr, int64_t nseg, const float* keys, int64_t n,
+                         int reference, float* keys_out, uint32_t* idx_out);
 
 /* Test hook: run the exact heap replay (igraph_get_shortest_paths_dijkstra restated on the GPU)
  * from vertex `src` over the current attached set.  full = 1 runs to an empty heap instead of

@@ -115,6 +115,7 @@ SIGNATURES = {
     "shdtopo_get_stats": (ctypes.c_int, [P, P]),
     "shdtopo_write_graphml": (ctypes.c_int, [P, cstr]),
     "shdtopo_replay_source": (ctypes.c_int, [P, i32, ctypes.c_int, P, P]),
+    "shdtopo_test_segsort": (ctypes.c_int, [P, i64, P, i64, ctypes.c_int, P, P]),
     "shdtopo_test_batch_layout": (ctypes.c_int, [P, i64, dbl, ctypes.c_int, ctypes.c_int,
                                                  ctypes.c_int, P, P, P]),
     "shdtopo_export_graph": (ctypes.c_int, [P, P, P, P, P, P]),

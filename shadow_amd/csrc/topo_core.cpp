@@ -381,9 +381,15 @@ struct _Topology {
     // the target-aware re-sort's scratch (KprimeScratch), kept: the first build's target
     // preparation allocates nothing (the background preparation sizes it)
     DevBuf<float> d_kpKey;
-    DevBuf<uint32_t> d_kpIdxIn, d_kpIdxOut;
+    DevBuf<uint32_t> d_kpIdx;
     DevBuf<uint4> d_kpRec;
     DevBuf<uint8_t> d_kpTmp;
+    // the rows longer than kSegBlock (SegBig): their entries' positions and row ordinals, the
+    // radix sort's key / value buffers
+    DevBuf<uint32_t> d_kpBigPos, d_kpBigRow, d_kpBigVal;
+    DevBuf<unsigned long long> d_kpBigKey;
+    int64_t kpBig = -1;  // their entries (-1: not listed yet)
+    int kpBigBits = 33;
     // the target preparation runs asynchronously (overlapping the host's source order): its
     // iteration count and event time are read after the build's next stream sync
     bool tpPending = false;
@@ -702,6 +708,8 @@ int dev_init(Topology* top) {
     tmark("kernels module");
     HIPCHK(preload_replay_module());
     tmark("replay module");
+    HIPCHK(preload_kprime_sort(top->stream));
+    tmark("first segmented sort");
     top->stats.module_load_ms = std::chrono::duration<double, std::milli>(
         std::chrono::steady_clock::now() - t0).count();
     top->devInit = true;
@@ -1575,23 +1583,68 @@ void reset_build_stats(Topology* top) {
 }
 
 // The target-aware re-sort's scratch for the prepared relaxation copy (allocated once).
+// The long rows' entries for the segmented sort's device-wide radix sort (SegBig): positions
+// row by row, each entry's row ordinal, and the sort's end bit.
+void plan_long_rows(const uint32_t* rowptr, int64_t V, std::vector<uint32_t>& pos,
+                    std::vector<uint32_t>& row, int* end_bit) {
+    pos.clear();
+    row.clear();
+    uint32_t nrow = 0;
+    for (int64_t v = 0; v < V; v++) {
+        const uint32_t b = rowptr[v], e = rowptr[v + 1];
+        if (e - b <= kSegBlock) continue;
+        for (uint32_t p = b; p < e; p++) {
+            pos.push_back(p);
+            row.push_back(nrow);
+        }
+        nrow++;
+    }
+    int bits = 1;
+    while (bits < 31 && (1u << bits) < nrow) bits++;
+    *end_bit = 32 + bits;
+}
+
 int ensure_kprime_scratch(Topology* top, KprimeScratch* out) {
     const int64_t nadj = (int64_t)(top->d_adjk.n / 4), V = top->g.V;
+    if (top->kpBig < 0) {
+        // the long rows (the graph's rows never change: listed once, in the preparation)
+        std::vector<uint32_t> rp((size_t)V + 1), pos, row;
+        HIPCHK(hipMemcpyAsync(rp.data(), top->d_rowptr.p, 4 * ((size_t)V + 1), hipMemcpyDeviceToHost,
+                              top->stream));
+        HIPCHK(hipStreamSynchronize(top->stream));
+        plan_long_rows(rp.data(), V, pos, row, &top->kpBigBits);
+        const size_t nb = pos.size();
+        HIPCHK(top->d_kpBigPos.ensure(std::max<size_t>(1, nb)));
+        HIPCHK(top->d_kpBigRow.ensure(std::max<size_t>(1, nb)));
+        HIPCHK(top->d_kpBigKey.ensure(std::max<size_t>(1, 2 * nb)));
+        HIPCHK(top->d_kpBigVal.ensure(std::max<size_t>(1, 2 * nb)));
+        if (nb) {
+            HIPCHK(hipMemcpyAsync(top->d_kpBigPos.p, pos.data(), 4 * nb, hipMemcpyHostToDevice, top->stream));
+            HIPCHK(hipMemcpyAsync(top->d_kpBigRow.p, row.data(), 4 * nb, hipMemcpyHostToDevice, top->stream));
+            HIPCHK(hipStreamSynchronize(top->stream));
+        }
+        top->kpBig = (int64_t)nb;
+    }
     size_t tb = 0;
-    HIPCHK(kprime_sort_tmp_bytes(top->d_rowptr.p, V, nadj, &tb));
+    HIPCHK(segsort_big_tmp_bytes(top->kpBig, top->kpBigBits, &tb));
     const size_t n = (size_t)std::max<int64_t>(1, nadj);
     HIPCHK(top->d_kpKey.ensure(n));
-    HIPCHK(top->d_kpIdxIn.ensure(n));
-    HIPCHK(top->d_kpIdxOut.ensure(n));
+    HIPCHK(top->d_kpIdx.ensure(n));
     HIPCHK(top->d_kpRec.ensure(n));
     HIPCHK(top->d_kpTmp.ensure(std::max<size_t>(1, tb)));
     if (out) {
         out->key = top->d_kpKey.p;
-        out->idx_in = top->d_kpIdxIn.p;
-        out->idx_out = top->d_kpIdxOut.p;
+        out->idx = top->d_kpIdx.p;
         out->rec = top->d_kpRec.p;
-        out->tmp = top->d_kpTmp.p;
-        out->tmp_bytes = top->d_kpTmp.n;
+        SegBig& b = out->big;
+        b.pos = top->d_kpBigPos.p;
+        b.row = top->d_kpBigRow.p;
+        b.nitems = top->kpBig;
+        b.end_bit = top->kpBigBits;
+        b.keys = top->d_kpBigKey.p;
+        b.vals = top->d_kpBigVal.p;
+        b.tmp = top->d_kpTmp.p;
+        b.tmp_bytes = top->d_kpTmp.n;
     }
     return 0;
 }
@@ -3116,8 +3169,11 @@ void release_prepared(Topology* top) {
     top->d_eu.release(); top->d_ev.release();
     top->d_kap.release(); top->d_ksum.release(); top->d_kap0.release();
     top->d_hseg.release(); top->d_hmulti.release(); top->d_kfChanged.release();
-    top->d_kpKey.release(); top->d_kpIdxIn.release(); top->d_kpIdxOut.release();
+    top->d_kpKey.release(); top->d_kpIdx.release();
     top->d_kpRec.release(); top->d_kpTmp.release();
+    top->d_kpBigPos.release(); top->d_kpBigRow.release(); top->d_kpBigVal.release();
+    top->d_kpBigKey.release();
+    top->kpBig = -1;
     top->hsegRows = top->hsegN = top->hmultiN = 0;
     top->csrUploaded = top->rowsSorted = false;
     top->adjkPlain = top->adjkFlagged = top->adjkResorted = false;
@@ -3839,6 +3895,71 @@ int shdtopo_test_batch_layout(const double* cost, int64_t rows, double fixed, in
     std::copy(st.begin(), st.end(), starts);
     *nbatches = (int64_t)st.size() - 1;
     return 0;
+}
+
+int shdtopo_test_segsort(const uint32_t* rowptr, int64_t nseg, const float* keys, int64_t n,
+                         int reference, float* keys_out, uint32_t* idx_out) {
+    if (!rowptr || !keys || !keys_out || !idx_out || nseg < 1 || n < 1 || n > 0x7FFFFFFF ||
+        rowptr[0] != 0 || (int64_t)rowptr[nseg] != n)
+        return -1;
+    for (int64_t i = 0; i < nseg; i++)
+        if (rowptr[i + 1] < rowptr[i]) return -1;
+    HIPCHK(hipSetDevice(0));
+    hipStream_t st = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    DevBuf<uint32_t> rp, iin, iout, bpos, brow, bval;
+    DevBuf<unsigned long long> bkey;
+    DevBuf<float> kin, kout;
+    DevBuf<uint8_t> tmp;
+    auto run = [&]() -> int {
+        HIPCHK(rp.ensure((size_t)nseg + 1));
+        HIPCHK(iout.ensure((size_t)n));
+        HIPCHK(kin.ensure((size_t)n));
+        HIPCHK(kout.ensure((size_t)n));
+        HIPCHK(hipMemcpyAsync(rp.p, rowptr, 4 * ((size_t)nseg + 1), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(kin.p, keys, 4 * (size_t)n, hipMemcpyHostToDevice, st));
+        std::vector<uint32_t> iota, pos, row;
+        size_t tb = 0;
+        if (reference) {
+            iota.resize((size_t)n);
+            for (int64_t i = 0; i < n; i++) iota[(size_t)i] = (uint32_t)i;
+            HIPCHK(iin.ensure((size_t)n));
+            HIPCHK(hipMemcpyAsync(iin.p, iota.data(), 4 * (size_t)n, hipMemcpyHostToDevice, st));
+            HIPCHK(segsort_reference(rp.p, nseg, n, kin.p, iin.p, kout.p, iout.p, nullptr, &tb, st));
+            HIPCHK(tmp.ensure(std::max<size_t>(1, tb)));
+            HIPCHK(segsort_reference(rp.p, nseg, n, kin.p, iin.p, kout.p, iout.p, tmp.p, &tb, st));
+        } else {
+            SegBig big;
+            plan_long_rows(rowptr, nseg, pos, row, &big.end_bit);
+            const size_t nb = pos.size();
+            HIPCHK(bpos.ensure(std::max<size_t>(1, nb)));
+            HIPCHK(brow.ensure(std::max<size_t>(1, nb)));
+            HIPCHK(bkey.ensure(std::max<size_t>(1, 2 * nb)));
+            HIPCHK(bval.ensure(std::max<size_t>(1, 2 * nb)));
+            if (nb) {
+                HIPCHK(hipMemcpyAsync(bpos.p, pos.data(), 4 * nb, hipMemcpyHostToDevice, st));
+                HIPCHK(hipMemcpyAsync(brow.p, row.data(), 4 * nb, hipMemcpyHostToDevice, st));
+            }
+            HIPCHK(segsort_big_tmp_bytes((int64_t)nb, big.end_bit, &tb));
+            HIPCHK(tmp.ensure(std::max<size_t>(1, tb)));
+            big.pos = bpos.p;
+            big.row = brow.p;
+            big.nitems = (int64_t)nb;
+            big.keys = bkey.p;
+            big.vals = bval.p;
+            big.tmp = tmp.p;
+            big.tmp_bytes = tmp.n;
+            HIPCHK(launch_segsort(rp.p, nseg, n, kin.p, kout.p, iout.p, big, st));
+        }
+        HIPCHK(hipMemcpyAsync(keys_out, kout.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(idx_out, iout.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return 0;
+    };
+    const int r = run();
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    return r;
 }
 
 int shdtopo_replay_source(Topology* top, int32_t srcv, int full, double* dist, int32_t* parent) {

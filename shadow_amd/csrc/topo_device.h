@@ -259,16 +259,35 @@ hipError_t launch_kfix_store(uint32_t* adjk, int64_t nadj, const double* K, hipS
 // re-sort every row of the relaxation copy (records, kappa array, probes, kappa0) by the
 // target-aware key kap' of the current target set (tbits) and K.  Scratch (KprimeScratch, sized
 // by kprime_scratch_bytes) is the caller's, so the resort allocates nothing and never syncs.
-struct KprimeScratch {
-    float* key = nullptr;       // nadj
-    uint32_t* idx_in = nullptr; // nadj
-    uint32_t* idx_out = nullptr;// nadj
-    uint4* rec = nullptr;       // nadj
-    void* tmp = nullptr;        // tmp_bytes (the segmented radix sort's)
+// rows of at most kSegBlock entries are sorted in LDS; the longer ones' entries, listed once per
+// graph row by row (pos: adjacency position, row: the row's ordinal among the long rows), go
+// through a device-wide radix sort of (ordinal << 32 | key) -- end_bit = 32 + bits of the ordinal
+constexpr uint32_t kSegBlock = 4096;
+struct SegBig {
+    const uint32_t* pos = nullptr;
+    const uint32_t* row = nullptr;
+    int64_t nitems = 0;
+    int end_bit = 33;
+    unsigned long long* keys = nullptr;  // 2 x nitems
+    uint32_t* vals = nullptr;            // 2 x nitems
+    void* tmp = nullptr;
     size_t tmp_bytes = 0;
 };
-// the sort's temporary bytes for nadj keys in V segments (no device work)
-hipError_t kprime_sort_tmp_bytes(const uint32_t* rowptr, int64_t V, int64_t nadj, size_t* bytes);
+struct KprimeScratch {
+    float* key = nullptr;       // nadj
+    uint32_t* idx = nullptr;    // nadj: each sorted entry's source position
+    uint4* rec = nullptr;       // nadj
+    SegBig big;                 // the rows longer than kSegBlock (listed once per graph)
+};
+// segmented sort (ascending f32 keys, stable, hipcub's order): rows <= 64 by waves, <= kSegBlock
+// by workgroups in LDS, the longer rows' entries by one device-wide radix sort
+hipError_t segsort_big_tmp_bytes(int64_t nitems, int end_bit, size_t* bytes);
+hipError_t launch_segsort(const uint32_t* rowptr, int64_t V, int64_t nadj, const float* key,
+                          float* key_out, uint32_t* idx_out, const SegBig& big, hipStream_t stream);
+hipError_t segsort_reference(const uint32_t* rowptr, int64_t V, int64_t nadj, const float* key,
+                             const uint32_t* idx_in, float* key_out, uint32_t* idx_out, void* tmp,
+                             size_t* tmp_bytes, hipStream_t stream);
+hipError_t preload_kprime_sort(hipStream_t stream);
 hipError_t launch_kprime_resort(uint32_t* adjk, float* kap, float* ksum, float* kap0,
                                 const uint32_t* rowptr, int64_t V, int64_t nadj, const double* pot,
                                 const uint32_t* tbits, const double* K, const KprimeScratch& sc,

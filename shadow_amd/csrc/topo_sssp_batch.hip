@@ -2307,7 +2307,7 @@ __device__ __forceinline__ float f32_down(double x) {
 __global__ void kprime_key_kernel(const uint32_t* __restrict__ adjk, int64_t nadj,
                                   const double* __restrict__ pot,
                                   const uint32_t* __restrict__ tbits, const double* __restrict__ K,
-                                  float* __restrict__ key, uint32_t* __restrict__ idx) {
+                                  float* __restrict__ key) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nadj;
          k += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t y = adjk[kAdjWords * k] & 0x3FFFFFFFu;
@@ -2319,7 +2319,6 @@ __global__ void kprime_key_kernel(const uint32_t* __restrict__ adjk, int64_t nad
             t = ky > t ? ky : t;
         }
         key[k] = f32_down(t);
-        idx[k] = (uint32_t)k;
     }
 }
 
@@ -2345,13 +2344,175 @@ __global__ void kprime_probe_kernel(const uint32_t* __restrict__ rowptr,
     }
 }
 
-hipError_t kprime_sort_tmp_bytes(const uint32_t* rowptr, int64_t V, int64_t nadj, size_t* bytes) {
+// ---- segmented sort of the re-sort keys (replaces a whole-adjacency hipcub segmented radix sort:
+// 5.2-5.6 ms at C4 on the first build's critical path, nearly all of it one workgroup per hub row
+// sorting that row alone) ----
+// The order is hipcub's: ascending by the radix image of the f32 key (-0.0 and +0.0 equal), stable
+// (equal keys keep their row positions).  Rows of at most kSegWave entries: one wave per row,
+// each lane ranks its entry against the row's others.  Rows up to kSegBlock: one workgroup per
+// row, a bitonic sort in LDS of (radix image << 32 | position) -- unique, so the result is the
+// stable order; a workgroup takes every G-th row (the long rows are the hubs, at the head of the
+// relabelled ids).  Longer rows: their entries (listed once per graph, row by row) are sorted
+// together by one device-wide radix sort of (row ordinal << 32 | radix image).
+constexpr uint32_t kSegWave = 64;
+constexpr uint32_t kSegThreads = 256;
+
+__device__ __forceinline__ uint32_t radix_f32(float f) {
+    uint32_t b = __float_as_uint(f);
+    b ^= (b & 0x80000000u) ? 0xFFFFFFFFu : 0x80000000u;
+    return b == 0x7FFFFFFFu ? 0x80000000u : b;  // -0.0 sorts as +0.0
+}
+
+__global__ void __launch_bounds__(kSegThreads)
+segsort_wave_kernel(const uint32_t* __restrict__ rowptr, int64_t V, const float* __restrict__ key,
+                    float* __restrict__ key_out, uint32_t* __restrict__ idx_out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const int64_t nw = ((int64_t)gridDim.x * kSegThreads) >> 6;
+    for (int64_t v = ((int64_t)blockIdx.x * kSegThreads + threadIdx.x) >> 6; v < V; v += nw) {
+        const uint32_t b = rowptr[v], n = rowptr[v + 1] - b;
+        if (n > kSegWave) continue;  // wave-uniform
+        float f = 0.0f;
+        uint32_t u = 0xFFFFFFFFu;
+        if (lane < n) {
+            f = key[b + lane];
+            u = radix_f32(f);
+        }
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < n; j++) {
+            const uint32_t uj = (uint32_t)__shfl((int)u, (int)j, 64);
+            rank += (uj < u || (uj == u && j < lane)) ? 1u : 0u;
+        }
+        if (lane < n) {
+            key_out[b + rank] = f;
+            idx_out[b + rank] = b + lane;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kSegThreads)
+segsort_block_kernel(const uint32_t* __restrict__ rowptr, int64_t V, const float* __restrict__ key,
+                     float* __restrict__ key_out, uint32_t* __restrict__ idx_out) {
+    __shared__ unsigned long long s[kSegBlock];
+    __shared__ uint32_t rows[kSegThreads];
+    __shared__ uint32_t nrows;
+    const uint32_t tid = threadIdx.x;
+    const int64_t G = gridDim.x;
+    for (int64_t base = 0; base < V; base += G * kSegThreads) {
+        // this workgroup's rows base + g + G t (t < 256) that need it
+        if (tid == 0) nrows = 0;
+        __syncthreads();
+        const int64_t v = base + blockIdx.x + G * tid;
+        if (v < V) {
+            const uint32_t n = rowptr[v + 1] - rowptr[v];
+            if (n > kSegWave && n <= kSegBlock) rows[atomicAdd(&nrows, 1u)] = (uint32_t)v;
+        }
+        __syncthreads();
+        const uint32_t nr = nrows;
+        __syncthreads();  // every thread has read nrows before the next range resets it
+        for (uint32_t i = 0; i < nr; i++) {
+            const uint32_t row = rows[i];
+            const uint32_t b = rowptr[row], n = rowptr[row + 1] - b;
+            uint32_t P = 128;
+            while (P < n) P <<= 1;
+            for (uint32_t x = tid; x < P; x += kSegThreads)
+                s[x] = x < n ? ((unsigned long long)radix_f32(key[b + x]) << 32) | x : ~0ull;
+            __syncthreads();
+            for (uint32_t k = 2; k <= P; k <<= 1) {
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    for (uint32_t t = tid; t < P / 2; t += kSegThreads) {
+                        const uint32_t lo = 2 * t - (t & (j - 1));
+                        const uint32_t hi = lo + j;
+                        const unsigned long long x = s[lo], y = s[hi];
+                        if ((x > y) == ((lo & k) == 0)) {
+                            s[lo] = y;
+                            s[hi] = x;
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            for (uint32_t x = tid; x < n; x += kSegThreads) {
+                const uint32_t pos = (uint32_t)s[x];
+                key_out[b + x] = key[b + pos];
+                idx_out[b + x] = b + pos;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ void segsort_gather_kernel(const uint32_t* __restrict__ pos, const uint32_t* __restrict__ row,
+                                      int64_t n, const float* __restrict__ key,
+                                      unsigned long long* __restrict__ k, uint32_t* __restrict__ val) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = pos[i];
+        k[i] = ((unsigned long long)row[i] << 32) | radix_f32(key[p]);
+        val[i] = p;
+    }
+}
+
+// sorted entry i of the long rows goes to the i-th listed position (each row keeps its range)
+__global__ void segsort_scatter_kernel(const uint32_t* __restrict__ pos,
+                                       const uint32_t* __restrict__ src, int64_t n,
+                                       const float* __restrict__ key, float* __restrict__ key_out,
+                                       uint32_t* __restrict__ idx_out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = pos[i], q = src[i];
+        key_out[p] = key[q];
+        idx_out[p] = q;
+    }
+}
+
+hipError_t segsort_big_tmp_bytes(int64_t nitems, int end_bit, size_t* bytes) {
     *bytes = 0;
-    if (nadj <= 0 || V <= 0) return hipSuccess;
+    if (nitems <= 0) return hipSuccess;
+    if (nitems > 0x7FFFFFFF || end_bit < 33 || end_bit > 64) return hipErrorInvalidValue;
+    return hipcub::DeviceRadixSort::SortPairs(nullptr, *bytes, (const unsigned long long*)nullptr,
+                                              (unsigned long long*)nullptr, (const uint32_t*)nullptr,
+                                              (uint32_t*)nullptr, (int)nitems, 0, end_bit,
+                                              (hipStream_t)0);
+}
+
+hipError_t launch_segsort(const uint32_t* rowptr, int64_t V, int64_t nadj, const float* key,
+                          float* key_out, uint32_t* idx_out, const SegBig& big, hipStream_t stream) {
+    if (V <= 0 || nadj <= 0) return hipSuccess;
     if (nadj > 0x7FFFFFFF) return hipErrorInvalidValue;
-    return hipcub::DeviceSegmentedRadixSort::SortPairs(
-        nullptr, *bytes, (const float*)nullptr, (float*)nullptr, (const uint32_t*)nullptr,
-        (uint32_t*)nullptr, (int)nadj, (int)V, rowptr, rowptr + 1, 0, 32, (hipStream_t)0);
+    const int64_t gw = std::min<int64_t>((V * 64 + kSegThreads - 1) / kSegThreads, 256 * 32);
+    hipLaunchKernelGGL(segsort_wave_kernel, dim3((unsigned)gw), dim3(kSegThreads), 0, stream, rowptr,
+                       V, key, key_out, idx_out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t gb = std::min<int64_t>((V + kSegThreads - 1) / kSegThreads, 256 * 8);
+    hipLaunchKernelGGL(segsort_block_kernel, dim3((unsigned)gb), dim3(kSegThreads), 0, stream,
+                       rowptr, V, key, key_out, idx_out);
+    e = hipGetLastError();
+    if (e != hipSuccess || big.nitems <= 0) return e;
+    if (!big.pos || !big.row || !big.keys || !big.vals || !big.tmp) return hipErrorInvalidValue;
+    const int64_t gi = std::min<int64_t>((big.nitems + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(segsort_gather_kernel, dim3((unsigned)gi), dim3(256), 0, stream, big.pos,
+                       big.row, big.nitems, key, big.keys, big.vals);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t tb = big.tmp_bytes;
+    e = hipcub::DeviceRadixSort::SortPairs(big.tmp, tb, big.keys, big.keys + big.nitems, big.vals,
+                                           big.vals + big.nitems, (int)big.nitems, 0, big.end_bit,
+                                           stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(segsort_scatter_kernel, dim3((unsigned)gi), dim3(256), 0, stream, big.pos,
+                       big.vals + big.nitems, big.nitems, key, key_out, idx_out);
+    return hipGetLastError();
+}
+
+// the whole-adjacency hipcub sort the kernels above replace (shdtopo_test_segsort's reference)
+hipError_t segsort_reference(const uint32_t* rowptr, int64_t V, int64_t nadj, const float* key,
+                             const uint32_t* idx_in, float* key_out, uint32_t* idx_out, void* tmp,
+                             size_t* tmp_bytes, hipStream_t stream) {
+    if (nadj > 0x7FFFFFFF) return hipErrorInvalidValue;
+    return hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, *tmp_bytes, key, key_out, idx_in, idx_out,
+                                                       (int)nadj, (int)V, rowptr, rowptr + 1, 0, 32,
+                                                       stream);
 }
 
 hipError_t launch_kprime_resort(uint32_t* adjk, float* kap, float* ksum, float* kap0,
@@ -2359,22 +2520,17 @@ hipError_t launch_kprime_resort(uint32_t* adjk, float* kap, float* ksum, float* 
                                 const uint32_t* tbits, const double* K, const KprimeScratch& sc,
                                 hipStream_t stream) {
     if (nadj <= 0 || V <= 0) return hipSuccess;
-    if (nadj > 0x7FFFFFFF || !sc.key || !sc.idx_in || !sc.idx_out || !sc.rec || !sc.tmp)
-        return hipErrorInvalidValue;
+    if (nadj > 0x7FFFFFFF || !sc.key || !sc.idx || !sc.rec) return hipErrorInvalidValue;
     const int64_t ge = std::min<int64_t>((nadj + 255) / 256, 256 * 16);
     hipLaunchKernelGGL(kprime_key_kernel, dim3((unsigned)ge), dim3(256), 0, stream, adjk, nadj,
-                       pot, tbits, K, sc.key, sc.idx_in);
+                       pot, tbits, K, sc.key);
     hipError_t e = hipGetLastError();
-    size_t tb = sc.tmp_bytes;
-    if (e == hipSuccess)
-        e = hipcub::DeviceSegmentedRadixSort::SortPairs(
-            sc.tmp, tb, sc.key, kap, sc.idx_in, sc.idx_out, (int)nadj, (int)V, rowptr, rowptr + 1,
-            0, 32, stream);
+    if (e == hipSuccess) e = launch_segsort(rowptr, V, nadj, sc.key, kap, sc.idx, sc.big, stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(sc.rec, adjk, sizeof(uint4) * (size_t)nadj, hipMemcpyDeviceToDevice, stream);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(kprime_gather_kernel, dim3((unsigned)ge), dim3(256), 0, stream, sc.rec,
-                           reinterpret_cast<uint4*>(adjk), sc.idx_out, nadj);
+                           reinterpret_cast<uint4*>(adjk), sc.idx, nadj);
         e = hipGetLastError();
     }
     if (e == hipSuccess) {
@@ -2464,6 +2620,28 @@ hipError_t launch_sssp_batch(int K, const DevCSR& g, const SlotWs& ws, const uin
 hipError_t preload_batch_module() {
     hipFuncAttributes a;
     return hipFuncGetAttributes(&a, (const void*)sssp_batch_kernel<8, false>);
+}
+
+// The first hipcub sort of a kind in a process spends ~12 ms of host time before its first
+// kernel (measured by tools/sort_warm_probe.cpp for the segmented radix sort: 11.9 ms, then
+// 0.016 ms per call).  The target preparation's re-sort of the long rows is the first one a build
+// runs, so the background init sorts a few keys of that kind first.
+hipError_t preload_kprime_sort(hipStream_t stream) {
+    constexpr int kN = 256;
+    uint8_t* buf = nullptr;
+    size_t tb = 0;
+    hipError_t e = segsort_big_tmp_bytes(kN, 40, &tb);
+    if (e == hipSuccess) e = hipMalloc(&buf, 2 * 12 * (size_t)kN + tb);
+    if (e != hipSuccess) return e;
+    unsigned long long* k = reinterpret_cast<unsigned long long*>(buf);
+    uint32_t* v = reinterpret_cast<uint32_t*>(buf + 16 * (size_t)kN);
+    e = hipMemsetAsync(buf, 0, 2 * 12 * (size_t)kN, stream);
+    if (e == hipSuccess)
+        e = hipcub::DeviceRadixSort::SortPairs(buf + 24 * (size_t)kN, tb, k, k + kN, v, v + kN, kN,
+                                               0, 40, stream);
+    const hipError_t s = hipStreamSynchronize(stream);
+    (void)hipFree(buf);
+    return e != hipSuccess ? e : s;
 }
 
 }  // namespace shdtopo
