@@ -378,6 +378,8 @@ struct _Topology {
                               // fixpoint is reached: cycles without targets rise forever; every
                               // iterate is exact)
     DevBuf<double> d_pot, d_kfA, d_kfB, d_kfPart;
+    DevBuf<double> d_kfKap;   // the out-rows' static w - pi(y) of the kappa fixpoint
+    bool kfKapReady = false;
     // the target-aware re-sort's scratch (KprimeScratch), kept: the first build's target
     // preparation allocates nothing (the background preparation sizes it)
     DevBuf<float> d_kpKey;
@@ -975,6 +977,10 @@ int upload_csr_impl(Topology* top) {
     top->adjkFlagged = false;
     top->adjkTargets.clear();
     top->rowsSorted = true;
+    // the kappa fixpoint's static w - pi per out-row entry (the first target preparation's)
+    HIPCHK(top->d_kfKap.ensure((size_t)std::max<int64_t>(1, nadj)));
+    HIPCHK(launch_kfix_kap(adj_out(top), top->d_pot.p, nadj, top->d_kfKap.p, st));
+    top->kfKapReady = true;
     step_done(5);
     // 5) what the host keeps
     {
@@ -989,6 +995,9 @@ int upload_csr_impl(Topology* top) {
         HIPCHK(hipMemcpyAsync(top->hp->sptPar.data(), top->d_sptPar.p, 4 * (size_t)V, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         copy_ms += ms_since(tc);
+        const auto th = clk::now();
+        tree_order(*top->hp);
+        host_ms += ms_since(th);
     }
     step_done(6);
     MESSAGE("graph preparation: upload %.1f, relabel %.1f, rows %.1f, h0 distances %.1f (%d "
@@ -1754,18 +1763,23 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 const int64_t V = top->g.V;
                 const HubSegs hs = hub_segs(top);
                 const int nit = std::max(0, top->targetKappa);
-                HIPCHK(top->d_kfA.ensure((size_t)V));
-                HIPCHK(top->d_kfB.ensure((size_t)V));
+                HIPCHK(top->d_kfA.ensure(2 * (size_t)V));  // [K | Kt] (launch_kfix_step)
+                HIPCHK(top->d_kfB.ensure(2 * (size_t)V));
                 HIPCHK(top->d_kfPart.ensure(std::max<size_t>(1, hs.nseg)));
                 HIPCHK(top->d_kfChanged.ensure((size_t)nit + 1));
+                if (!top->kfKapReady) {  // the out-rows' static w - pi (once per graph)
+                    HIPCHK(top->d_kfKap.ensure((size_t)std::max<int64_t>(1, nadjk)));
+                    HIPCHK(launch_kfix_kap(adj_out(top), top->d_pot.p, nadjk, top->d_kfKap.p, st));
+                    top->kfKapReady = true;
+                }
                 HIPCHK(hipMemsetAsync(top->d_kfChanged.p, 0, sizeof(unsigned int) * ((size_t)nit + 1), st));
-                HIPCHK(launch_kfix_step(top->d_rowptr.p, adj_out(top), top->d_pot.p, top->d_tbits.p,
+                HIPCHK(launch_kfix_step(top->d_rowptr.p, adj_out(top), top->d_kfKap.p, top->d_tbits.p,
                                         nullptr, top->d_kfA.p, V, hs, top->d_kfPart.p,
                                         top->d_kfChanged.p, st));
                 double* kin = top->d_kfA.p;
                 double* kout = top->d_kfB.p;
                 for (int it = 0; it < nit; it++) {
-                    HIPCHK(launch_kfix_step(top->d_rowptr.p, adj_out(top), top->d_pot.p,
+                    HIPCHK(launch_kfix_step(top->d_rowptr.p, adj_out(top), top->d_kfKap.p,
                                             top->d_tbits.p, kin, kout, V, hs, top->d_kfPart.p,
                                             top->d_kfChanged.p + 1 + it, st));
                     std::swap(kin, kout);
@@ -1882,25 +1896,12 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                 if (top->sourceOrder == 2) {
                     // preorder of the h0 shortest-path tree (children by ascending vertex id):
                     // sources in one subtree (sharing the longest path prefix from h0) are
-                    // adjacent.  Preorder = lexicographic order of the root-first parent paths,
-                    // so only the sources' paths are walked (O(rows x depth), not a DFS of V);
-                    // a vertex outside the tree sorts last.
-                    std::vector<std::vector<uint32_t>> path((size_t)rows);
-                    std::vector<uint8_t> inTree((size_t)rows, 0);
-                    for (int64_t i = 0; i < rows; i++) {
-                        auto& p = path[(size_t)i];
-                        uint32_t v = src[(size_t)i];
-                        while (v != 0xFFFFFFFFu && p.size() <= (size_t)top->g.V) {
-                            p.push_back(v);
-                            v = top->hp->sptPar[v];
-                        }
-                        inTree[(size_t)i] = !p.empty() && p.back() == 0u;
-                        std::reverse(p.begin(), p.end());
-                    }
+                    // adjacent.  Preorder = lexicographic order of the root-first parent paths;
+                    // the forest's preorder (HostPrep::preorder, from the graph preparation)
+                    // numbers h0's tree first, then the other roots' trees
+                    const std::vector<uint32_t>& pre = top->hp->preorder;
                     std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
-                        if (inTree[a] != inTree[b]) return inTree[a] > inTree[b];
-                        return std::lexicographical_compare(path[a].begin(), path[a].end(),
-                                                            path[b].begin(), path[b].end());
+                        return pre[src[a]] < pre[src[b]];
                     });
                 } else if (top->sourceOrder == 1) {
                     const uint32_t Hc = (uint32_t)std::min<int64_t>(kGroupHubs, top->g.V);
@@ -1945,12 +1946,7 @@ int enqueue_rows(Topology* top, int64_t row0, int64_t row1, double2* out_lr, uin
                                     // the source's depth in the h0 shortest-path tree: deeper
                                     // sources relax more pairs (C4: corr 0.59 with the batch's
                                     // duration, against 0.25 for mean pi)
-                                    uint32_t v = s, dep = 0;
-                                    while (dep <= (uint32_t)top->g.V && top->hp->sptPar[v] != 0xFFFFFFFFu) {
-                                        v = top->hp->sptPar[v];
-                                        dep++;
-                                    }
-                                    mp[(size_t)b] += (double)dep;
+                                    mp[(size_t)b] += (double)top->hp->depth[s];
                                 } else {
                                     const double p = top->hp->pot[(size_t)s];
                                     mp[(size_t)b] += std::isfinite(p) ? p : 0.0;
@@ -3164,8 +3160,10 @@ void release_prepared(Topology* top) {
                     &top->d_adjo, &top->d_rowptrIn, &top->d_adjk})
         b->release();
     for (auto* b : {&top->d_elat, &top->d_eloss, &top->d_aloss, &top->d_vloss, &top->d_selfLat,
-                    &top->d_selfLoss, &top->d_pot, &top->d_kfA, &top->d_kfB, &top->d_kfPart})
+                    &top->d_selfLoss, &top->d_pot, &top->d_kfA, &top->d_kfB, &top->d_kfPart,
+                    &top->d_kfKap})
         b->release();
+    top->kfKapReady = false;
     top->d_eu.release(); top->d_ev.release();
     top->d_kap.release(); top->d_ksum.release(); top->d_kap0.release();
     top->d_hseg.release(); top->d_hmulti.release(); top->d_kfChanged.release();

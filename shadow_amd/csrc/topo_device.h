@@ -248,10 +248,13 @@ SsspLdsPlan sssp_batch_lds_plan(int K, int64_t hub_limit, uint32_t par_hubs, int
 // bit 30 of every adjk column word := the column is set in tbits (the attached vertices)
 hipError_t launch_mark_targets(uint32_t* adjk, int64_t nadj, const uint32_t* tbits,
                                hipStream_t stream);
-// target-aware kappa fixpoint (topo_sssp_batch.hip): one step K_out = F(K_in) (K_in nullptr:
-// kappa0), then the f16 kappa field of the relaxation copy's records := K(column)
-// part: scratch of hs.nseg doubles (the per-segment minima of cut rows)
-hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const double* pot,
+// target-aware kappa fixpoint (topo_sssp_batch.hip): kap_e = every out-row entry's w - pi(y)
+// (static: once per graph); one step K_out = F(K_in) (K_in nullptr: kappa0), K buffers of 2 V
+// doubles [K | Kt = target ? -inf : K]; then the f16 kappa field of the relaxation copy's records
+// := K(column).  part: scratch of hs.nseg doubles (the per-segment minima of cut rows)
+hipError_t launch_kfix_kap(const uint32_t* adj, const double* pot, int64_t nadj, double* kap,
+                           hipStream_t stream);
+hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const double* kap_e,
                             const uint32_t* tbits, const double* Kin, double* Kout, int64_t V,
                             const HubSegs& hs, double* part, unsigned int* changed,
                             hipStream_t stream);

@@ -104,6 +104,10 @@ struct HostPrep {
     std::vector<int32_t> inv;       // old -> new
     std::vector<double> pot;        // pi = d(h0, v) from the top hub: bucket shifts, batch order
     std::vector<uint32_t> sptPar;   // h0 shortest-path tree parent (source ordering)
+    // preorder of the parent forest (roots and children by ascending id, so h0 = vertex 0's tree
+    // comes first) and each vertex's depth below its root (tree_order): the source grouping and
+    // the batch order of a cold build read them instead of walking every source's parent path
+    std::vector<uint32_t> preorder, depth;
     double piMax = 0.0;             // largest finite pi
     // directed topologies: d(v, h0) over the in-rows (undirected: empty, pot serves), the bucket
     // shifts' value of d_s(h0), and its largest finite value
@@ -112,6 +116,45 @@ struct HostPrep {
     double to_h0(uint32_t v) const { return potSrc.empty() ? pot[v] : potSrc[v]; }
     double to_h0_max() const { return potSrc.empty() ? piMax : srcMax; }
 };
+
+// HostPrep::preorder / depth from sptPar (O(V); runs with the graph preparation)
+inline void tree_order(HostPrep& hp) {
+    const uint32_t V = (uint32_t)hp.sptPar.size();
+    std::vector<uint32_t> cstart((size_t)V + 1, 0), child, fill;
+    for (uint32_t v = 0; v < V; v++) {
+        const uint32_t p = hp.sptPar[v];
+        if (p < V) cstart[(size_t)p + 1]++;
+    }
+    for (uint32_t v = 0; v < V; v++) cstart[(size_t)v + 1] += cstart[v];
+    child.resize(cstart[V]);
+    fill.assign(cstart.begin(), cstart.end() - 1);
+    for (uint32_t v = 0; v < V; v++) {  // children in ascending id order
+        const uint32_t p = hp.sptPar[v];
+        if (p < V) child[fill[p]++] = v;
+    }
+    hp.preorder.assign(V, 0xFFFFFFFFu);
+    hp.depth.assign(V, 0);
+    std::vector<uint32_t> stack;
+    uint32_t next = 0;
+    for (uint32_t r = 0; r < V; r++) {
+        if (hp.sptPar[r] < V) continue;  // roots in ascending id order: h0's tree first
+        stack.push_back(r);
+        while (!stack.empty()) {
+            const uint32_t v = stack.back();
+            stack.pop_back();
+            hp.preorder[v] = next++;
+            for (uint32_t k = cstart[(size_t)v + 1]; k > cstart[v]; k--) {  // smallest id on top
+                const uint32_t c = child[k - 1];
+                hp.depth[c] = hp.depth[v] + 1;
+                stack.push_back(c);
+            }
+        }
+    }
+    // a vertex on a parent cycle (no root above it) keeps the walk's cap, V + 1 hops, and sorts
+    // last in its input order (preorder stays UINT32_MAX)
+    for (uint32_t v = 0; v < V; v++)
+        if (hp.preorder[v] == 0xFFFFFFFFu) hp.depth[v] = V + 1;
+}
 
 uint32_t string_to_ip(const char* s);  // inet_pton(AF_INET) as shd-address.c:137-144
 

@@ -2160,20 +2160,38 @@ hipError_t launch_mark_targets(uint32_t* adjk, int64_t nadj, const uint32_t* tbi
 // (kap = w - pi(y); K_0 = kappa0) says "y would relax nothing that reaches a target": along a
 // parent chain x -> y -> ... -> t the threshold at y is the one at x minus w (plus 1e-5 w of
 // margin), so K(x) stays under the threshold of every chain vertex at its final distance (every
-// iterate K_k is such a bound; they rise monotonically towards the fixpoint).  One wavefront per
-// vertex; Kin == nullptr computes K_0.
-__device__ __forceinline__ double kfix_term(const uint32_t* adj, const double* pot,
-                                            const uint32_t* tbits, const double* Kin, uint32_t k) {
-    const uint32_t y = adj[kAdjWords * k];
-    const double w = __hiloint2double((int)adj[kAdjWords * k + 3], (int)adj[kAdjWords * k + 2]);
-    const double p = pot[y];
-    const double kap = isfinite(p) ? w - p : -INFINITY;
+// iterate K_k is such a bound; they rise monotonically towards the fixpoint).  Kin == nullptr
+// computes K_0.  An edge's kap is static (kfix_kap_kernel, once per graph) and the target test is
+// folded into a second array Kt = target ? -inf : K (max(kap, -inf) = kap), so an entry costs one
+// random read, Kt[y], instead of three (pi, the target bit and K: 0.52 ms per C4 step).
+__global__ void kfix_kap_kernel(const uint32_t* __restrict__ adj, const double* __restrict__ pot,
+                                int64_t nadj, double* __restrict__ kap) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nadj;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t y = adj[kAdjWords * k];
+        const double w = __hiloint2double((int)adj[kAdjWords * k + 3], (int)adj[kAdjWords * k + 2]);
+        const double p = pot[y];
+        kap[k] = isfinite(p) ? w - p : -INFINITY;
+    }
+}
+
+__device__ __forceinline__ double kfix_term(const uint32_t* adj, const double* kap_e,
+                                            const double* Ktin, uint32_t k) {
+    const double kap = kap_e[k];
     double t = kap;
-    if (Kin && !((tbits[y >> 5] >> (y & 31u)) & 1u)) {
-        const double ky = Kin[y] + w * (1.0 - 2e-5) - 1e-9;
+    if (Ktin) {
+        const uint32_t y = adj[kAdjWords * k];
+        const double w = __hiloint2double((int)adj[kAdjWords * k + 3], (int)adj[kAdjWords * k + 2]);
+        const double ky = Ktin[y] + w * (1.0 - 2e-5) - 1e-9;
         t = ky > kap ? ky : kap;
     }
     return t;
+}
+
+__device__ __forceinline__ void kfix_put(double* Kout, double* Ktout, const uint32_t* tbits,
+                                         uint32_t x, double m) {
+    Kout[x] = m;
+    Ktout[x] = ((tbits[x >> 5] >> (x & 31u)) & 1u) ? -INFINITY : m;
 }
 
 // A wavefront per segment of a hub row (ids < hs.rows: the long rows of the degree order; a row cut
@@ -2181,9 +2199,10 @@ __device__ __forceinline__ double kfix_term(const uint32_t* adj, const double* p
 // wavefront per row left 54 of 64 lanes idle on the C4 tail: 6.2 ms per step; a wavefront per
 // whole hub row left the top hub's 250 k entries on one wavefront: 4.4 ms per step).
 __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
-                                 const uint32_t* __restrict__ adj, const double* __restrict__ pot,
+                                 const uint32_t* __restrict__ adj, const double* __restrict__ kap_e,
                                  const uint32_t* __restrict__ tbits,
-                                 const double* __restrict__ Kin, double* __restrict__ Kout,
+                                 const double* __restrict__ Kin, const double* __restrict__ Ktin,
+                                 double* __restrict__ Kout, double* __restrict__ Ktout,
                                  int64_t V, HubSegs hs, double* __restrict__ part,
                                  unsigned int* __restrict__ changed) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -2196,7 +2215,7 @@ __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
         const uint32_t e = min(sg.y + kHubSeg, r1);
         double m = INFINITY;
         for (uint32_t k = sg.y + lane; k < e; k += 64u) {
-            const double t = kfix_term(adj, pot, tbits, Kin, k);
+            const double t = kfix_term(adj, kap_e, Ktin, k);
             m = t < m ? t : m;
         }
 #pragma unroll
@@ -2207,7 +2226,7 @@ __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
         if (lane == 0) {
             if (sg.y == r0 && e == r1) {
                 ch |= Kin && !(m == Kin[x]);
-                Kout[x] = m;
+                kfix_put(Kout, Ktout, tbits, x, m);
             } else {
                 part[s] = m;
             }
@@ -2215,18 +2234,46 @@ __global__ void kfix_step_kernel(const uint32_t* __restrict__ rowptr,
     }
     for (int64_t x = (int64_t)hs.rows + gt; x < V; x += gs) {
         double m = INFINITY;
-        for (uint32_t k = rowptr[x]; k < rowptr[x + 1]; k++) {
-            const double t = kfix_term(adj, pot, tbits, Kin, k);
+        const uint32_t r1 = rowptr[x + 1];
+        uint32_t k = rowptr[x];
+        // 4 entries at a time: their records and kap, then their neighbours' Kt, all in flight
+        for (; k + 4 <= r1; k += 4) {
+            double t[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) t[i] = kap_e[k + i];
+            if (Ktin) {
+                uint32_t y[4];
+                double w[4], ky[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    y[i] = adj[kAdjWords * (k + i)];
+                    w[i] = __hiloint2double((int)adj[kAdjWords * (k + i) + 3],
+                                            (int)adj[kAdjWords * (k + i) + 2]);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) ky[i] = Ktin[y[i]];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const double kk = ky[i] + w[i] * (1.0 - 2e-5) - 1e-9;
+                    t[i] = kk > t[i] ? kk : t[i];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) m = t[i] < m ? t[i] : m;
+        }
+        for (; k < r1; k++) {
+            const double t = kfix_term(adj, kap_e, Ktin, k);
             m = t < m ? t : m;
         }
         ch |= Kin && !(m == Kin[x]);
-        Kout[x] = m;
+        kfix_put(Kout, Ktout, tbits, (uint32_t)x, m);
     }
     if (__ballot(ch) && lane == 0) atomicOr(changed, 1u);  // one atomic per wave
 }
 
 // the hub rows cut in several segments: a wavefront each takes the minimum of its partials
 __global__ void kfix_multi_kernel(const double* __restrict__ Kin, double* __restrict__ Kout,
+                                  double* __restrict__ Ktout, const uint32_t* __restrict__ tbits,
                                   HubSegs hs, const double* __restrict__ part,
                                   unsigned int* __restrict__ changed) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -2247,7 +2294,7 @@ __global__ void kfix_multi_kernel(const double* __restrict__ Kin, double* __rest
         }
         if (lane == 0) {
             ch |= Kin && !(m == Kin[mr.x]);
-            Kout[mr.x] = m;
+            kfix_put(Kout, Ktout, tbits, mr.x, m);
         }
     }
     if (__ballot(ch) && lane == 0) atomicOr(changed, 1u);
@@ -2278,17 +2325,26 @@ __global__ void kfix_store_kernel(uint32_t* __restrict__ adjk, int64_t nadj,
     }
 }
 
-hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const double* pot,
+hipError_t launch_kfix_kap(const uint32_t* adj, const double* pot, int64_t nadj, double* kap,
+                           hipStream_t stream) {
+    if (nadj <= 0) return hipSuccess;
+    const int64_t g = std::min<int64_t>((nadj + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(kfix_kap_kernel, dim3((unsigned)g), dim3(256), 0, stream, adj, pot, nadj, kap);
+    return hipGetLastError();
+}
+
+hipError_t launch_kfix_step(const uint32_t* rowptr, const uint32_t* adj, const double* kap_e,
                             const uint32_t* tbits, const double* Kin, double* Kout, int64_t V,
                             const HubSegs& hs, double* part, unsigned int* changed,
                             hipStream_t stream) {
     if (V <= 0) return hipSuccess;
     const int64_t g = std::min<int64_t>(std::max<int64_t>((V + 255) / 256, (hs.nseg + 3) / 4), 256 * 32);
+    const double* Ktin = Kin ? Kin + V : nullptr;
     hipLaunchKernelGGL(kfix_step_kernel, dim3((unsigned)g), dim3(256), 0, stream, rowptr, adj,
-                       pot, tbits, Kin, Kout, V, hs, part, changed);
+                       kap_e, tbits, Kin, Ktin, Kout, Kout + V, V, hs, part, changed);
     if (hs.nmulti > 0)
         hipLaunchKernelGGL(kfix_multi_kernel, dim3((hs.nmulti + 3) / 4), dim3(256), 0, stream, Kin,
-                           Kout, hs, part, changed);
+                           Kout, Kout + V, tbits, hs, part, changed);
     return hipGetLastError();
 }
 
