@@ -3917,6 +3917,7 @@ int shdtopo_test_segsort(const uint32_t* rowptr, int64_t nseg, const float* keys
     DevBuf<unsigned long long> bkey;
     DevBuf<float> kin, kout;
     DevBuf<uint8_t> tmp;
+    std::vector<uint32_t> iota, pos, row;  // outlive every copy (synchronised below)
     auto run = [&]() -> int {
         HIPCHK(rp.ensure((size_t)nseg + 1));
         HIPCHK(iout.ensure((size_t)n));
@@ -3924,7 +3925,6 @@ int shdtopo_test_segsort(const uint32_t* rowptr, int64_t nseg, const float* keys
         HIPCHK(kout.ensure((size_t)n));
         HIPCHK(hipMemcpyAsync(rp.p, rowptr, 4 * ((size_t)nseg + 1), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(kin.p, keys, 4 * (size_t)n, hipMemcpyHostToDevice, st));
-        std::vector<uint32_t> iota, pos, row;
         size_t tb = 0;
         if (reference) {
             iota.resize((size_t)n);
