@@ -43,7 +43,7 @@ from shadow_amd import sharding  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SEED = 20261015
-PROFILE_TAG = "r06d"           # profiles/<tag>_*_pmc.json: the committed counter passes
+PROFILE_TAG = "r06e"           # profiles/<tag>_*_pmc.json: the committed counter passes
 
 
 def log(rank, *a):
