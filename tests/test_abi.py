@@ -260,6 +260,12 @@ def test_synthetic_directed_shape_and_bucket_options():
         top.set_option(k, v)
     with pytest.raises(KeyError):
         top.set_option("h0_phase", 1.0)
+    # parent-pass row-scan chunk (records per slot: chunk x batch x 16 B): 64 .. 2^20
+    for v in (64, 16384, 1 << 20):
+        top.set_option("row_scan_chunk", v)
+    for v in (63, 0, -1, (1 << 20) + 1):
+        with pytest.raises(KeyError):
+            top.set_option("row_scan_chunk", v)
 
 
 def _layout(cost, fixed, fill, slots, batch):
