@@ -692,6 +692,28 @@ def test_row_scans_in_small_chunks_equal_oracle(integer):
     assert np.array_equal(hops, ohops.astype(np.uint16))
 
 
+@pytest.mark.parametrize("n_hosts", [1, 2, 9, 17])
+def test_small_and_ragged_attached_sets_equal_oracle(n_hosts):
+    """Edge sizes of the batch launch: one attached host (a 1 x 1 table: the self pair through
+    the self loop), two, and counts that leave a ragged last batch (9 = 8 + 1, 17 = 2 x 8 + 1),
+    under the default options (auto batch fill, measured layout from the second build on) --
+    first build and a rebuild, both bit for bit the oracle's."""
+    top, g = synthetic_pair(seed=59, n_routers=3000, n_poi=150, n_edges=30000)
+    top.set_option("tie_dense", 0)
+    otop, ips, verts = attach_hosts(top, g, n_hosts, type_hints=["client", "relay", "server"])
+    oa, olat, orel, ohops = g.table(verts)
+    for rep in range(2):
+        if rep:
+            top.rebuild()
+        a, lat, rel, hops = top.table()
+        assert top.stats()["errors"] == 0
+        assert np.array_equal(a, oa)
+        assert np.array_equal(lat.view(np.uint64), olat.view(np.uint64))
+        assert np.array_equal(rel.view(np.uint64), orel.view(np.uint64))
+        assert np.array_equal(hops, ohops.astype(np.uint16))
+    assert top.getMinimumLatency() == olat.min()
+
+
 @pytest.mark.parametrize("integer", [False, True])
 def test_bucket_width_and_landmark_phase_do_not_change_the_table(integer):
     """Option delta (bucket width) and h0_phase (where the landmark h0 sits in its bucket; < 0 the
