@@ -473,6 +473,13 @@ def test_sssp_full_size_c4_int_rows():
     assert np.array_equal(glr[..., 0].view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(glr[..., 1].view(np.uint64), orel.view(np.uint64))
     assert np.array_equal(hp.cpu().numpy().view(np.uint16), ohops.astype(np.uint16))
+    # latencies pinned independently of the oracle: with integer edge latencies every shortest
+    # path sums to the same exact value whichever tie igraph's heap picks, so scipy's Dijkstra
+    # (helpers.scipy_rows) gives the reference's latency bit for bit on 8 of the rows (its
+    # reliability and hops follow scipy's own tie choice: not compared)
+    sub = np.arange(0, r1 - r0, 8)
+    slat, _, _ = scipy_rows((V, eu, ev, elat, eloss, vloss), att[r0 + sub], att)
+    assert np.array_equal(glr[sub, :, 0].view(np.uint64), slat.view(np.uint64))
 
 
 def test_sssp_full_size_c4_dir_rows():
