@@ -132,13 +132,14 @@ def random_topology_graphml(n_routers=600, n_poi=60, extra=2400, seed=3, integer
     return graphml_doc(nodes, [edges[i] for i in order], directed)
 
 
-def scipy_rows(graph, srcs, targets):
+def scipy_rows(graph, srcs, targets, directed=False):
     """The per-target helper (shd-topology.c:561-671) over scipy's shortest-path trees, an
     implementation independent of the oracle: scipy.sparse.csgraph.dijkstra with predecessors on
     the undirected non-loop graph.  latency = scipy's distance (the same left-to-right f64 sums
     from the source), hops = the predecessor chain's length, reliability = ((1 * (1 - vloss[s]))
     * (1 - vloss[t])) * prod(1 - loss(e)) in path order from the source; the self pair is the
-    self loop (latency 0 + its latency, reliability (1 - vloss) * (1 - loss), 1 hop)."""
+    self loop (latency 0 + its latency, reliability (1 - vloss) * (1 - loss), 1 hop).  directed:
+    the arcs as given (igraph mode OUT)."""
     import scipy.sparse as sp
     from scipy.sparse.csgraph import dijkstra
     V, eu, ev, elat, eloss, vloss = graph
@@ -146,19 +147,24 @@ def scipy_rows(graph, srcs, targets):
     elat, eloss = np.asarray(elat, np.float64), np.asarray(eloss, np.float64)
     vloss = np.asarray(vloss, np.float64)
     nl = eu != ev
-    r = np.concatenate([eu[nl], ev[nl]])
-    c = np.concatenate([ev[nl], eu[nl]])
-    W = sp.csr_matrix((np.concatenate([elat[nl], elat[nl]]), (r, c)), shape=(V, V))
-    Lm = sp.csr_matrix((np.concatenate([eloss[nl], eloss[nl]]), (r, c)), shape=(V, V))
+    if directed:
+        r, c, wl, wo = eu[nl], ev[nl], elat[nl], eloss[nl]
+    else:
+        r = np.concatenate([eu[nl], ev[nl]])
+        c = np.concatenate([ev[nl], eu[nl]])
+        wl = np.concatenate([elat[nl], elat[nl]])
+        wo = np.concatenate([eloss[nl], eloss[nl]])
+    W = sp.csr_matrix((wl, (r, c)), shape=(V, V))
+    Lm = sp.csr_matrix((wo, (r, c)), shape=(V, V))
     # no parallel edges (the csr would sum them) and no zero latency (scipy drops zeros)
-    assert W.nnz == 2 * int(nl.sum()) and bool((W.data > 0).all())
+    assert W.nnz == len(r) and bool((W.data > 0).all())
     # self loops: the first (lowest edge id) per vertex, as igraph_get_eid
     selfLat = np.full(V, np.nan)
     selfLoss = np.zeros(V)
     li = np.nonzero(~nl)[0][::-1]  # assigned last-to-first: the lowest edge id wins
     selfLat[eu[li]] = elat[li]
     selfLoss[eu[li]] = eloss[li]
-    dist, pred = dijkstra(W, directed=False, indices=np.asarray(srcs), return_predecessors=True)
+    dist, pred = dijkstra(W, directed=directed, indices=np.asarray(srcs), return_predecessors=True)
     targets = np.asarray(targets, np.int64)
     A = len(targets)
     lat = np.empty((len(srcs), A))

@@ -508,7 +508,17 @@ def test_sssp_full_size_c4_dir_rows():
     assert not np.array_equal(glr[:, r0:r1, 0], glr[:, r0:r1, 0].T)  # really directed
     assert np.array_equal(glr[..., 0].view(np.uint64), olat.view(np.uint64))
     assert np.array_equal(glr[..., 1].view(np.uint64), orel.view(np.uint64))
-    assert np.array_equal(hp.cpu().numpy().view(np.uint16), ohops.astype(np.uint16))
+    ghp = hp.cpu().numpy().view(np.uint16)
+    assert np.array_equal(ghp, ohops.astype(np.uint16))
+    # pinned independently of the oracle: continuous latencies, so every shortest path is unique
+    # and scipy's directed predecessor tree is igraph's -- 8 of the rows, latency, reliability and
+    # hops bit for bit (helpers.scipy_rows, directed)
+    sub = np.arange(0, r1 - r0, 8)
+    slat, srel, shops = scipy_rows((V, eu, ev, elat, eloss, vloss), att[r0 + sub], att,
+                                   directed=True)
+    assert np.array_equal(glr[sub, :, 0].view(np.uint64), slat.view(np.uint64))
+    assert np.array_equal(glr[sub, :, 1].view(np.uint64), srel.view(np.uint64))
+    assert np.array_equal(ghp[sub], shops.astype(np.uint16))
 
 
 def _grid_graphml(n=30, n_poi=60, seed=5):
